@@ -1,0 +1,168 @@
+/*
+ * nfec.h -- C ABI of the MI355X-native NORM FEC engine (libnfec.so).
+ *
+ * Drop-in boundary for NORM's FEC plugin layer (reference include/normEncoder.h:38-54):
+ * plain pointers, sizes and integer status codes; no C++ or torch types cross it.
+ * Every compute entry point runs hand-written gfx950 HIP kernels; there is no CPU
+ * compute path behind this header (a missing/failed GPU yields NFEC_EDEVICE).
+ *
+ * Reference interfaces each entry replaces (paths in USNavalResearchLaboratory/norm):
+ *   nfec_codec_create     NormEncoderRS8::Init   src/common/normEncoderRS8.cpp:400-462
+ *                         NormDecoderRS8::Init   src/common/normEncoderRS8.cpp:542-649
+ *                         NormEncoderRS16::Init  src/common/normEncoderRS16.cpp:399-461
+ *                         NormEncoderMDP::Init   src/common/normEncoderMDP.cpp:56-84
+ *   nfec_codec_destroy    NormEncoderXX::Destroy / NormDecoderXX::Destroy (e.g. normEncoderRS8.cpp:464-471)
+ *   nfec_encode           the per-segment NormEncoder::Encode loop as run by
+ *                         NormObject::CalculateBlockParity  src/common/normObject.cpp:2203-2229
+ *                         (NormEncoderRS8::Encode normEncoderRS8.cpp:473-483, RS16 :472-482,
+ *                          MDP normEncoderMDP.cpp:178-211) for many blocks at once
+ *   nfec_decode           NormDecoder::Decode  (RS8 normEncoderRS8.cpp:652-757, RS16 :650-755,
+ *                         MDP normEncoderMDP.cpp:333-430) for many blocks at once, as called
+ *                         from NormObject::HandleObjectMessage src/common/normObject.cpp:1548-1644
+ *   nfec_encode_segment   NormEncoder::Encode(segmentId, dataVector, parityVectorList)
+ *                         (include/normEncoder.h:44), host pointers, exact per-call semantics
+ *   nfec_decode_vectors   NormDecoder::Decode(vectorList, numData, erasureCount, erasureLocs)
+ *                         (include/normEncoder.h:53), host pointers, exact per-call semantics
+ */
+#ifndef NFEC_H
+#define NFEC_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define NFEC_ABI_VERSION 1
+
+/* codec families (NORM fec_id 5/2 -> RS8/RS16, fec_id 129 -> MDP; normSession.cpp:839-875) */
+enum {
+    NFEC_RS8 = 1,  /* GF(2^8) systematic Reed-Solomon, Rizzo Vandermonde generator   */
+    NFEC_RS16 = 2, /* GF(2^16) systematic Reed-Solomon, native-endian 16-bit symbols */
+    NFEC_MDP = 3   /* legacy GF(2^8) LFSR code (fec_id 129)                          */
+};
+
+/* status codes: >= 0 success */
+enum {
+    NFEC_OK = 0,
+    NFEC_EINVAL = -1,   /* bad argument (sizes, alignment, null pointers)            */
+    NFEC_ENOMEM = -2,   /* device or host allocation failed                            */
+    NFEC_EDEVICE = -3,  /* HIP runtime/launch failure or no usable gfx950 device       */
+    NFEC_ERANGE = -4,   /* numData + numParity exceeds the field (Init returns false)  */
+    NFEC_ENOTSUP = -5   /* combination not supported (e.g. accumulate with MDP encode) */
+};
+
+/* batch flags */
+enum {
+    /* XOR results into the existing output bytes, exactly like the reference's
+     * accumulate-into-caller-zeroed-buffer contract (Encode parity, Decode erased
+     * source).  Without it outputs are overwritten, which is byte-identical whenever
+     * the caller zeroed them first (NORM always does: normObject.cpp:1579, :2240-2252). */
+    NFEC_ACCUMULATE = 1u << 0
+};
+
+typedef struct nfec_codec nfec_codec;
+
+typedef struct nfec_codec_info {
+    int32_t kind;         /* NFEC_RS8 / NFEC_RS16 / NFEC_MDP */
+    int32_t device;       /* HIP device ordinal the codec lives on */
+    uint32_t num_data;    /* k (ndata)  */
+    uint32_t num_parity;  /* m (npar)   */
+    uint32_t vector_size; /* bytes per segment vector processed (vectorSize given to Init) */
+    uint32_t symbol_bytes;/* 1 (RS8/MDP) or 2 (RS16) */
+} nfec_codec_info;
+
+/*
+ * A batch of FEC blocks resident in device memory (HBM).
+ * Block b, segment slot s starts at  blocks + b*block_stride + s*seg_stride.
+ * Slot layout per block mirrors NORM's block segment list (normSegment.h:79,
+ * normObject.cpp:1610): slots [0, numData) hold source symbols, slots
+ * [numData, numData + m) hold parity symbols.
+ * Requirements: blocks, seg_stride and block_stride are multiples of 8 bytes
+ * (NORM's segment pool is 8-byte aligned, normSegment.cpp:25-27), and
+ * seg_stride >= vector_size.
+ */
+typedef struct nfec_block_batch {
+    void* blocks;              /* device pointer */
+    uint64_t block_stride;     /* bytes */
+    uint32_t seg_stride;       /* bytes */
+    uint32_t nblocks;
+    const uint16_t* num_data;  /* device [nblocks] per-block numData (<= k), or NULL = k */
+    uint32_t flags;            /* NFEC_ACCUMULATE */
+    uint32_t reserved;
+} nfec_block_batch;
+
+/* ---- version / device ---- */
+int nfec_abi_version(void);
+/* number of visible gfx950 devices (0 when none) */
+int nfec_device_count(void);
+/* human-readable message for the last error on this thread */
+const char* nfec_last_error(void);
+
+/* ---- host-only generator construction (no GPU needed) ----
+ * Writes the m x k parity rows of the systematic generator (RS8/RS16: Rizzo Vandermonde
+ * code, normEncoderRS8.cpp:428-450; MDP: the LFSR block map for k source symbols),
+ * row-major, symbol_bytes per element.  Returns NFEC_ERANGE where Init would return false. */
+int nfec_build_generator(int kind, uint32_t num_data, uint32_t num_parity, void* host_out, size_t bytes);
+
+/* ---- codec lifecycle ---- */
+int nfec_codec_create(int device, int kind, uint32_t num_data, uint32_t num_parity,
+                      uint32_t vector_size, nfec_codec** out);
+void nfec_codec_destroy(nfec_codec* codec);
+int nfec_codec_get_info(const nfec_codec* codec, nfec_codec_info* out);
+/* Copies the m x k parity rows of the systematic generator (row p = generator row k+p),
+ * row-major, elements of symbol_bytes each.  MDP: the m x k matrix of the LFSR code for a
+ * full block of k source symbols.  bytes must be >= m*k*symbol_bytes. */
+int nfec_codec_get_generator(const nfec_codec* codec, void* host_out, size_t bytes);
+
+/* ---- batched device-resident path (the performance path) ----
+ * stream is a hipStream_t (NULL = legacy default stream).  Calls are asynchronous with
+ * respect to the host; results are ready when the stream reaches them. */
+int nfec_encode(nfec_codec* codec, const nfec_block_batch* batch, void* stream);
+
+/* erasure_locs: device [nblocks][erasure_stride] sorted slot indices (source erasures
+ * first, then missing parity, as NormObject builds them); erasure_counts: device
+ * [nblocks]; status: device [nblocks] or NULL -- per block the reference Decode return
+ * value (erasureCount on success, 0 when the block cannot be repaired).
+ * Erased source slots are repaired; parity slots are never written. */
+int nfec_decode(nfec_codec* codec, const nfec_block_batch* batch, const uint16_t* erasure_locs,
+                uint32_t erasure_stride, const uint16_t* erasure_counts, int32_t* status,
+                void* stream);
+
+/* ---- host-resident batched path: same layouts, host pointers (pageable or pinned).
+ * Staged through pinned buffers with H2D / compute / D2H overlapped on streams.
+ * Synchronous: returns when all outputs are back in host memory. */
+int nfec_encode_host(nfec_codec* codec, const nfec_block_batch* host_batch);
+int nfec_decode_host(nfec_codec* codec, const nfec_block_batch* host_batch,
+                     const uint16_t* erasure_locs, uint32_t erasure_stride,
+                     const uint16_t* erasure_counts, int32_t* status);
+
+/* ---- per-call NORM semantics with scattered host vectors (drop-in classes) ---- */
+/* NormEncoder::Encode: parity_vectors[i] ^= G[k+i][segment_id] * data over vector_size
+ * bytes (RS16: vector_size/2 symbols).  MDP: one in-order LFSR step. Synchronous. */
+int nfec_encode_segment(nfec_codec* codec, uint32_t segment_id, const void* data,
+                        void* const* parity_vectors);
+/* NormDecoder::Decode: returns erasure_count on success, 0 when undecodable, <0 on error. */
+int nfec_decode_vectors(nfec_codec* codec, void* const* vector_list, uint32_t num_data,
+                        uint32_t erasure_count, const uint32_t* erasure_locs);
+
+/* ---- synthetic workload utilities (device kernels; SURVEY.md 8d definitions) ----
+ * fill: source slots [0, numData) of every block with the splitmix64 stream
+ *       word w of (block b, slot s) = mix(seed ^ ((b0+b)<<20) ^ s + (w+1)*0x9E3779B97F4A7C15).
+ * erasures: per block `count` sorted distinct indices in [0, range), Fisher-Yates over the
+ *           counter stream mix(seed ^ 0xE7A5E7A500000000 ^ (b0+b) + (i+1)*gamma).
+ * zero: zero the listed slots of every block (the receiver's zero-fill, normObject.cpp:1579). */
+int nfec_util_fill(const nfec_block_batch* batch, uint32_t num_data, uint32_t vector_size,
+                   uint64_t seed, uint64_t first_block, void* stream);
+int nfec_util_erasures(uint16_t* erasure_locs, uint32_t erasure_stride, uint16_t* erasure_counts,
+                       uint32_t nblocks, uint32_t range, uint32_t count, uint64_t seed,
+                       uint64_t first_block, void* stream);
+int nfec_util_zero_slots(const nfec_block_batch* batch, const uint16_t* erasure_locs,
+                         uint32_t erasure_stride, const uint16_t* erasure_counts,
+                         uint32_t vector_size, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* NFEC_H */

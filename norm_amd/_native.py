@@ -1,0 +1,108 @@
+"""ctypes binding of libnfec.so (include/nfec.h).
+
+The library is built in-tree (norm_amd/_lib/libnfec.so, see norm_amd/Makefile and
+__graft_entry__.build()).  There is no fallback: if the library is missing or a call
+fails, an exception is raised.
+"""
+import ctypes
+import os
+import re
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "_lib", "libnfec.so")
+HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "nfec.h")
+
+NFEC_RS8, NFEC_RS16, NFEC_MDP = 1, 2, 3
+NFEC_OK, NFEC_EINVAL, NFEC_ENOMEM, NFEC_EDEVICE, NFEC_ERANGE, NFEC_ENOTSUP = 0, -1, -2, -3, -4, -5
+NFEC_ACCUMULATE = 1
+
+
+class NfecError(RuntimeError):
+    def __init__(self, code, what):
+        super().__init__(f"{what} failed with {code}: {last_error()}")
+        self.code = code
+
+
+class BlockBatch(ctypes.Structure):
+    _fields_ = [
+        ("blocks", ctypes.c_void_p),
+        ("block_stride", ctypes.c_uint64),
+        ("seg_stride", ctypes.c_uint32),
+        ("nblocks", ctypes.c_uint32),
+        ("num_data", ctypes.c_void_p),
+        ("flags", ctypes.c_uint32),
+        ("reserved", ctypes.c_uint32),
+    ]
+
+
+class CodecInfo(ctypes.Structure):
+    _fields_ = [
+        ("kind", ctypes.c_int32),
+        ("device", ctypes.c_int32),
+        ("num_data", ctypes.c_uint32),
+        ("num_parity", ctypes.c_uint32),
+        ("vector_size", ctypes.c_uint32),
+        ("symbol_bytes", ctypes.c_uint32),
+    ]
+
+
+_P = ctypes.c_void_p
+_U32 = ctypes.c_uint32
+_U64 = ctypes.c_uint64
+_I = ctypes.c_int
+_SIGS = {
+    "nfec_abi_version": (_I, []),
+    "nfec_device_count": (_I, []),
+    "nfec_last_error": (ctypes.c_char_p, []),
+    "nfec_build_generator": (_I, [_I, _U32, _U32, _P, ctypes.c_size_t]),
+    "nfec_codec_create": (_I, [_I, _I, _U32, _U32, _U32, ctypes.POINTER(_P)]),
+    "nfec_codec_destroy": (None, [_P]),
+    "nfec_codec_get_info": (_I, [_P, ctypes.POINTER(CodecInfo)]),
+    "nfec_codec_get_generator": (_I, [_P, _P, ctypes.c_size_t]),
+    "nfec_encode": (_I, [_P, ctypes.POINTER(BlockBatch), _P]),
+    "nfec_decode": (_I, [_P, ctypes.POINTER(BlockBatch), _P, _U32, _P, _P, _P]),
+    "nfec_encode_host": (_I, [_P, ctypes.POINTER(BlockBatch)]),
+    "nfec_decode_host": (_I, [_P, ctypes.POINTER(BlockBatch), _P, _U32, _P, _P]),
+    "nfec_encode_segment": (_I, [_P, _U32, _P, _P]),
+    "nfec_decode_vectors": (_I, [_P, _P, _U32, _U32, _P]),
+    "nfec_util_fill": (_I, [ctypes.POINTER(BlockBatch), _U32, _U32, _U64, _U64, _P]),
+    "nfec_util_erasures": (_I, [_P, _U32, _P, _U32, _U32, _U32, _U64, _U64, _P]),
+    "nfec_util_zero_slots": (_I, [ctypes.POINTER(BlockBatch), _P, _U32, _P, _U32, _P]),
+}
+
+_lib = None
+
+
+def lib():
+    """Load libnfec.so (raises if it has not been built)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(f"libnfec.so not built ({LIB_PATH}); run __graft_entry__.build() or make -C norm_amd")
+        L = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in _SIGS.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+def last_error():
+    if _lib is None:
+        return ""
+    msg = _lib.nfec_last_error()
+    return msg.decode() if msg else ""
+
+
+def check(rc, what):
+    if rc < 0:
+        raise NfecError(rc, what)
+    return rc
+
+
+def declared_symbols():
+    """Function names declared in include/nfec.h (used by the ABI export test)."""
+    text = open(HEADER_PATH).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(nfec_[a-z0-9_]+)\s*\(", text)))

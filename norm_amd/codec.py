@@ -1,0 +1,281 @@
+"""Python mirror of NORM's FEC plugin surface, backed by the MI355X kernels.
+
+Class names, method names, argument meaning and return values follow the reference
+classes (include/normEncoder.h:38-54, normEncoderRS8.h, normEncoderRS16.h,
+normEncoderMDP.h) so parity tests read like the reference's own fecTest
+(src/common/fecTest.cpp):
+
+    enc = NormEncoderRS8(); enc.Init(numData, numParity, vectorSize)
+    enc.Encode(segmentId, dataVector, parityVectorList)      # parity ^= G[k+i][seg] * data
+    dec = NormDecoderRS8(); dec.Init(numData, numParity, vectorSize)
+    dec.Decode(vectorList, numData, erasureCount, erasureLocs) -> erasureCount | 0
+
+On top of the per-call surface, `encode_blocks` / `decode_blocks` take a batch of blocks
+resident in HBM (a torch uint8 CUDA tensor shaped [nblocks, k+m, seg_stride]) -- the
+performance path.  Everything runs through libnfec.so; nothing here computes on the CPU.
+"""
+import ctypes
+
+from . import _native as N
+
+
+def _addr_ro(buf):
+    """Address of a read-only byte buffer (bytes, bytearray, numpy array, memoryview)."""
+    if hasattr(buf, "ctypes"):
+        return buf.ctypes.data, buf
+    if isinstance(buf, bytes):
+        keep = ctypes.create_string_buffer(buf, len(buf))
+        return ctypes.addressof(keep), keep
+    mv = memoryview(buf)
+    keep = (ctypes.c_char * mv.nbytes).from_buffer(mv)
+    return ctypes.addressof(keep), keep
+
+
+def _addr_rw(buf):
+    if buf is None:
+        return None, None
+    if hasattr(buf, "ctypes"):
+        return buf.ctypes.data, buf
+    mv = memoryview(buf)
+    keep = (ctypes.c_char * mv.nbytes).from_buffer(mv)
+    return ctypes.addressof(keep), keep
+
+
+def _stream_handle(stream):
+    if stream is not None:
+        return ctypes.c_void_p(int(getattr(stream, "cuda_stream", stream)))
+    import torch
+
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def _tensor_ptr(t, what):
+    if t is None:
+        return None
+    if not t.is_cuda:
+        raise ValueError(f"{what} must be a CUDA (HIP) tensor")
+    if not t.is_contiguous():
+        raise ValueError(f"{what} must be contiguous")
+    return ctypes.c_void_p(t.data_ptr())
+
+
+def device_count():
+    return N.lib().nfec_device_count()
+
+
+def build_generator(kind, num_data, num_parity):
+    """Host-only generator parity rows (m x k) as a numpy array (no GPU needed)."""
+    import numpy as np
+
+    dtype = np.uint16 if kind == N.NFEC_RS16 else np.uint8
+    out = np.zeros((num_parity, num_data), dtype)
+    N.check(N.lib().nfec_build_generator(kind, num_data, num_parity, out.ctypes.data, out.nbytes),
+            "nfec_build_generator")
+    return out
+
+
+class BlockLayout:
+    """Contiguous HBM layout of a batch: block b, slot s at (b*(k+m) + s) * seg_stride."""
+
+    def __init__(self, num_data, num_parity, vector_size, seg_stride=None):
+        self.k, self.m, self.vec = num_data, num_parity, vector_size
+        self.seg_stride = seg_stride or ((vector_size + 7) // 8 * 8)
+
+    def empty(self, nblocks, device="cuda"):
+        import torch
+
+        return torch.zeros((nblocks, self.k + self.m, self.seg_stride), dtype=torch.uint8, device=device)
+
+
+def _batch_struct(blocks, num_data, accumulate):
+    if blocks.dtype.itemsize != 1 or blocks.dim() != 3:
+        raise ValueError("blocks must be a uint8 tensor [nblocks, slots, seg_stride]")
+    b = N.BlockBatch()
+    b.blocks = blocks.data_ptr()
+    b.block_stride = blocks.stride(0)
+    b.seg_stride = blocks.stride(1)
+    b.nblocks = blocks.shape[0]
+    b.num_data = num_data.data_ptr() if num_data is not None else None
+    b.flags = N.NFEC_ACCUMULATE if accumulate else 0
+    if blocks.stride(2) != 1:
+        raise ValueError("segment bytes must be contiguous")
+    return b
+
+
+class _Codec:
+    KIND = None
+
+    def __init__(self, device=0):
+        self.device = device
+        self._h = ctypes.c_void_p()
+        self.ndata = self.npar = self.vector_size = 0
+
+    # -- reference surface --
+    def Init(self, numData, numParity, vectorSize):
+        self.Destroy()
+        rc = N.lib().nfec_codec_create(self.device, self.KIND, numData, numParity, vectorSize, ctypes.byref(self._h))
+        if rc == N.NFEC_ERANGE:
+            return False  # reference: PLOG(PL_FATAL) + return false (normEncoderRS8.cpp:405-409)
+        N.check(rc, "nfec_codec_create")
+        self.ndata, self.npar, self.vector_size = numData, numParity, vectorSize
+        return True
+
+    def Destroy(self):
+        if self._h:
+            N.lib().nfec_codec_destroy(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.Destroy()
+        except Exception:
+            pass
+
+    def GetNumData(self):
+        return self.ndata
+
+    def GetNumParity(self):
+        return self.npar
+
+    def GetVectorSize(self):
+        return self.vector_size
+
+    def generator(self):
+        import numpy as np
+
+        dtype = np.uint16 if self.KIND == N.NFEC_RS16 else np.uint8
+        out = np.zeros((self.npar, self.ndata), dtype)
+        N.check(N.lib().nfec_codec_get_generator(self._h, out.ctypes.data, out.nbytes), "nfec_codec_get_generator")
+        return out
+
+    def _need(self):
+        if not self._h:
+            raise RuntimeError("codec not initialised (call Init)")
+
+
+class _Encoder(_Codec):
+    def Encode(self, segmentId, dataVector, parityVectorList):
+        self._need()
+        daddr, dkeep = _addr_ro(dataVector)
+        keeps = []
+        arr = (ctypes.c_void_p * self.npar)()
+        for i in range(self.npar):
+            a, k = _addr_rw(parityVectorList[i])
+            arr[i] = a
+            keeps.append(k)
+        N.check(N.lib().nfec_encode_segment(self._h, segmentId, daddr, arr), "nfec_encode_segment")
+
+    def encode_blocks(self, blocks, num_data=None, accumulate=False, stream=None):
+        """Parity for every block of a device batch (slots [nd, nd+m) of each block)."""
+        self._need()
+        b = _batch_struct(blocks, num_data, accumulate)
+        N.check(N.lib().nfec_encode(self._h, ctypes.byref(b), _stream_handle(stream)), "nfec_encode")
+
+    def encode_blocks_host(self, blocks, num_data=None, accumulate=False):
+        """Same as encode_blocks for a numpy uint8 array [nblocks, slots, seg_stride] in host memory."""
+        self._need()
+        b = N.BlockBatch()
+        b.blocks = blocks.ctypes.data
+        b.block_stride = blocks.strides[0]
+        b.seg_stride = blocks.strides[1]
+        b.nblocks = blocks.shape[0]
+        b.num_data = num_data.ctypes.data if num_data is not None else None
+        b.flags = N.NFEC_ACCUMULATE if accumulate else 0
+        N.check(N.lib().nfec_encode_host(self._h, ctypes.byref(b)), "nfec_encode_host")
+
+
+class _Decoder(_Codec):
+    def Decode(self, vectorList, numData, erasureCount, erasureLocs):
+        self._need()
+        n = numData + self.npar
+        arr = (ctypes.c_void_p * n)()
+        keeps = []
+        for i in range(n):
+            a, k = _addr_rw(vectorList[i])
+            arr[i] = a
+            keeps.append(k)
+        locs = (ctypes.c_uint32 * max(1, erasureCount))(*list(erasureLocs)[:erasureCount])
+        rc = N.lib().nfec_decode_vectors(self._h, arr, numData, erasureCount, locs)
+        return N.check(rc, "nfec_decode_vectors")
+
+    def decode_blocks(self, blocks, erasure_locs, erasure_counts, num_data=None, status=None, accumulate=False,
+                      stream=None):
+        """Repair every block of a device batch.  erasure_locs: int16/uint16 [nblocks, stride]
+        sorted slot indices; erasure_counts: int16/uint16 [nblocks]; returns int32 status
+        [nblocks] (reference Decode return value per block)."""
+        import torch
+
+        self._need()
+        if status is None:
+            status = torch.empty(blocks.shape[0], dtype=torch.int32, device=blocks.device)
+        b = _batch_struct(blocks, num_data, accumulate)
+        rc = N.lib().nfec_decode(self._h, ctypes.byref(b), _tensor_ptr(erasure_locs, "erasure_locs"),
+                                 erasure_locs.shape[1], _tensor_ptr(erasure_counts, "erasure_counts"),
+                                 _tensor_ptr(status, "status"), _stream_handle(stream))
+        N.check(rc, "nfec_decode")
+        return status
+
+    def decode_blocks_host(self, blocks, erasure_locs, erasure_counts, num_data=None, accumulate=False):
+        import numpy as np
+
+        self._need()
+        status = np.zeros(blocks.shape[0], np.int32)
+        b = N.BlockBatch()
+        b.blocks = blocks.ctypes.data
+        b.block_stride = blocks.strides[0]
+        b.seg_stride = blocks.strides[1]
+        b.nblocks = blocks.shape[0]
+        b.num_data = num_data.ctypes.data if num_data is not None else None
+        b.flags = N.NFEC_ACCUMULATE if accumulate else 0
+        N.check(N.lib().nfec_decode_host(self._h, ctypes.byref(b), erasure_locs.ctypes.data, erasure_locs.shape[1],
+                                         erasure_counts.ctypes.data, status.ctypes.data), "nfec_decode_host")
+        return status
+
+
+class NormEncoderRS8(_Encoder):
+    KIND = N.NFEC_RS8
+
+
+class NormDecoderRS8(_Decoder):
+    KIND = N.NFEC_RS8
+
+
+class NormEncoderRS16(_Encoder):
+    KIND = N.NFEC_RS16
+
+
+class NormDecoderRS16(_Decoder):
+    KIND = N.NFEC_RS16
+
+
+class NormEncoderMDP(_Encoder):
+    KIND = N.NFEC_MDP
+
+
+class NormDecoderMDP(_Decoder):
+    KIND = N.NFEC_MDP
+
+
+# -- synthetic workload helpers (device kernels) --
+def fill_blocks(blocks, num_data, vector_size, seed, first_block=0, per_block_num_data=None, stream=None):
+    b = _batch_struct(blocks, per_block_num_data, False)
+    N.check(N.lib().nfec_util_fill(ctypes.byref(b), num_data, vector_size, seed, first_block, _stream_handle(stream)),
+            "nfec_util_fill")
+
+
+def make_erasures(nblocks, range_, count, seed, stride, first_block=0, device="cuda", stream=None):
+    import torch
+
+    locs = torch.zeros((nblocks, stride), dtype=torch.int16, device=device)
+    counts = torch.zeros(nblocks, dtype=torch.int16, device=device)
+    N.check(N.lib().nfec_util_erasures(ctypes.c_void_p(locs.data_ptr()), stride, ctypes.c_void_p(counts.data_ptr()),
+                                       nblocks, range_, count, seed, first_block, _stream_handle(stream)),
+            "nfec_util_erasures")
+    return locs, counts
+
+
+def zero_erasures(blocks, erasure_locs, erasure_counts, vector_size, stream=None):
+    b = _batch_struct(blocks, None, False)
+    N.check(N.lib().nfec_util_zero_slots(ctypes.byref(b), _tensor_ptr(erasure_locs, "erasure_locs"),
+                                         erasure_locs.shape[1], _tensor_ptr(erasure_counts, "erasure_counts"),
+                                         vector_size, _stream_handle(stream)), "nfec_util_zero_slots")

@@ -1,0 +1,151 @@
+// gf_host.cpp -- host-side field tables, generator construction and kernel tables.
+//
+// Field construction follows generate_gf() (reference src/common/normEncoderRS8.cpp:182-242,
+// normEncoderRS16.cpp:181-241): alpha = x over the primitive polynomials 0x11d / 0x1100B.
+//
+// The systematic generator is built in closed form.  The reference fills an n x k
+// Vandermonde matrix whose row r evaluates the powers of the point p_r (p_0 = 0,
+// p_r = alpha^(r-1)), inverts the top k x k block and multiplies the bottom rows by it
+// (normEncoderRS8.cpp:428-450).  That product is the Lagrange basis of the top points
+// evaluated at the bottom points:
+//     G[k+p][j] = W(y_p) / ((y_p + x_j) * W'(x_j)),   W(z) = prod_l (z + x_l)
+// which is unique, so it is byte-identical to the reference matrix while costing
+// O(k^2 + m k) instead of O(m k^2) (the reference's RS16 Init takes 26 s at k = 4096).
+// tests/ checks it against the oracle's Vandermonde construction.
+#include <cstring>
+#include <mutex>
+
+#include "nfec_internal.hpp"
+
+namespace nfec {
+
+static thread_local std::string g_last_error;
+
+void set_error(const std::string& msg) { g_last_error = msg; }
+int fail(int code, const std::string& msg)
+{
+    set_error(msg);
+    return code;
+}
+int hip_fail(hipError_t e, const char* what)
+{
+    set_error(std::string(what) + ": " + hipGetErrorString(e));
+    return NFEC_EDEVICE;
+}
+const char* last_error_cstr() { return g_last_error.c_str(); }
+
+static void build_field(Field& f, int bits, uint32_t poly)
+{
+    f.bits = bits;
+    f.q = (1u << bits) - 1u;
+    f.exp.assign(2 * f.q, 0);
+    f.log.assign(f.q + 1, 0);
+    uint32_t v = 1;
+    for (uint32_t i = 0; i < f.q; ++i) {
+        f.exp[i] = v;
+        f.log[v] = i;
+        v <<= 1;
+        if (v & (1u << bits)) v ^= poly;
+    }
+    f.log[0] = f.q;
+    for (uint32_t i = 0; i < f.q; ++i) f.exp[i + f.q] = f.exp[i];
+}
+
+const Field& gf8()
+{
+    static Field f;
+    static std::once_flag once;
+    std::call_once(once, [] { build_field(f, 8, 0x11d); });
+    return f;
+}
+
+const Field& gf16()
+{
+    static Field f;
+    static std::once_flag once;
+    std::call_once(once, [] { build_field(f, 16, 0x1100b); });
+    return f;
+}
+
+int rs_generator(int bits, uint32_t k, uint32_t m, std::vector<uint32_t>& rows)
+{
+    const Field& f = bits == 8 ? gf8() : gf16();
+    if (k == 0 || (uint64_t)k + m > f.q) return NFEC_ERANGE;
+    // The reference computes the point exponents as int row*col (normEncoderRS8.cpp:433);
+    // past 2^31 that is undefined behaviour, so such shapes are refused.
+    if (k + m >= 2 && (uint64_t)(k + m - 2) * (k - 1) >= (1ull << 31)) return NFEC_ERANGE;
+    const uint32_t q = f.q;
+    std::vector<uint32_t> x(k);
+    for (uint32_t j = 0; j < k; ++j) x[j] = rs_point(f, j);
+    // log W'(x_j) = sum_{l != j} log(x_j + x_l)
+    std::vector<uint64_t> lwp(k, 0);
+    for (uint32_t j = 0; j < k; ++j) {
+        uint64_t s = 0;
+        for (uint32_t l = 0; l < k; ++l)
+            if (l != j) s += f.log[x[j] ^ x[l]];
+        lwp[j] = s % q;
+    }
+    rows.assign((size_t)m * k, 0);
+    for (uint32_t p = 0; p < m; ++p) {
+        const uint32_t y = rs_point(f, k + p);
+        uint64_t lw = 0;
+        for (uint32_t l = 0; l < k; ++l) lw += f.log[y ^ x[l]];
+        lw %= q;
+        for (uint32_t j = 0; j < k; ++j) {
+            uint64_t e = lw + 2ull * q - f.log[y ^ x[j]] - lwp[j];
+            rows[(size_t)p * k + j] = f.exp[e % q];
+        }
+    }
+    return NFEC_OK;
+}
+
+void mdp_generator_poly(uint32_t m, std::vector<uint8_t>& g)
+{
+    // g(x) = prod_{n=1..m} (x + alpha^n), g[i] = coefficient of x^i
+    const Field& f = gf8();
+    g.assign(m + 1, 0);
+    g[0] = 1;
+    for (uint32_t n = 1; n <= m; ++n) {
+        const uint32_t a = f.exp[n];
+        for (uint32_t i = n; i > 0; --i) g[i] = (uint8_t)(g[i - 1] ^ f.mul(g[i], a));
+        g[0] = (uint8_t)f.mul(g[0], a);
+    }
+}
+
+void mdp_encode_matrix(const std::vector<uint8_t>& g, uint32_t m, uint32_t nd, uint8_t* out)
+{
+    // The MDP encoder (normEncoderMDP.cpp:178-211) is a linear shift register over the
+    // parity vectors: fb = d ^ P[0];  P[i] = P[i+1] ^ g[m-1-i]*fb;  P[m-1] = g[0]*fb.
+    // Column j of the block map is the register after an impulse at step j followed
+    // by nd-1-j zero steps, so all columns come from one impulse response.
+    const Field& f = gf8();
+    std::vector<uint8_t> st(m, 0), nx(m);
+    auto step = [&](uint32_t d) {
+        uint32_t fb = d ^ st[0];
+        for (uint32_t i = 0; i + 1 < m; ++i) nx[i] = (uint8_t)(st[i + 1] ^ f.mul(g[m - 1 - i], fb));
+        nx[m - 1] = (uint8_t)f.mul(g[0], fb);
+        st.swap(nx);
+    };
+    if (nd == 0) return;
+    step(1);
+    for (uint32_t j = nd; j-- > 0;) {
+        for (uint32_t i = 0; i < m; ++i) out[(size_t)i * nd + j] = st[i];
+        if (j) step(0);
+    }
+}
+
+void vperm_table(uint32_t c, uint32_t out[8])
+{
+    const Field& f = gf8();
+    auto pack = [&](uint32_t a, uint32_t b, uint32_t cc, uint32_t d) {
+        return f.mul(c, a) | (f.mul(c, b) << 8) | (f.mul(c, cc) << 16) | (f.mul(c, d) << 24);
+    };
+    out[0] = pack(0, 1, 2, 3);
+    out[1] = pack(4, 5, 6, 7);
+    out[2] = pack(0, 8, 16, 24);
+    out[3] = pack(32, 40, 48, 56);
+    out[4] = pack(0, 64, 128, 192);
+    out[5] = out[6] = out[7] = 0;
+}
+
+}  // namespace nfec

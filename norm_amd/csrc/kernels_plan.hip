@@ -1,0 +1,335 @@
+// kernels_plan.hip -- per-block erasure-decode planning on the GPU.
+//
+// RS (RS8 and RS16): the reference builds a k x k decoding matrix whose erased source
+// rows are replaced by the generator rows of the first surviving parities and inverts it
+// by Gauss-Jordan (src/common/normEncoderRS8.cpp:656-725, 766-889).  Only the rows of
+// the erased symbols are ever used (:727-756) and, with D = [[A, B], [0, I]] in
+// (erased, rest) order, those rows of D^-1 are [A^-1, A^-1 B].  So the repair is
+//     z_t = parity(P_t) ^ sum_{c present} G[P_t][c] * d_c      (stage 1: gather rows of G)
+//     d_E = A^-1 z,   A[t][s] = G[P_t][E_s]                      (stage 2: e x e inverse)
+// which is byte-identical (the inverse is unique) and needs only an e x e inversion per
+// block instead of k x k.  One wavefront plans one block: parity selection follows the
+// reference's ascending scan (:660-718), the e x [A | I] Gauss-Jordan runs lane-parallel
+// over columns in LDS.
+//
+// MDP: the reference decode (src/common/normEncoderMDP.cpp:333-430) is linear in the
+// surviving vectors; the plan evaluates its syndrome / erasure-locator / Omega / Forney
+// chain symbolically into one coefficient per (erased source symbol, surviving vector):
+//   C[r][v] = Dinv_r * gamma_v * sum_{l<m} (gamma_v beta_r)^l Lambda_{m-1-l}(beta_r)
+// with gamma_v = alpha^(nvecs-1-v), beta_r = alpha^((255-k_r) % 255), Lambda_u the prefix
+// sums of the locator evaluated at beta_r and Dinv_r = GINV[lambda'(beta_r)] (GINV[0]=1).
+#include "nfec_internal.hpp"
+
+namespace nfec {
+
+namespace {
+
+constexpr int kWave = 64;
+constexpr uint32_t kPlanLdsMaxE = 64;
+
+__device__ __forceinline__ uint32_t uni(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
+
+template <typename E>
+struct FieldDev {
+    const E* exp;          // 2q entries
+    const uint16_t* log;   // q+1 entries, log[0] = q
+    uint32_t q;
+    __device__ __forceinline__ uint32_t mul(uint32_t a, uint32_t b) const
+    {
+        return (a && b) ? (uint32_t)exp[(uint32_t)log[a] + (uint32_t)log[b]] : 0u;
+    }
+    __device__ __forceinline__ uint32_t inv(uint32_t a) const
+    {
+        return a <= 1 ? a : (uint32_t)exp[q - (uint32_t)log[a]];
+    }
+};
+
+template <typename E>
+__global__ __launch_bounds__(kWave) void rs_plan_kernel(RsPlanArgs a)
+{
+    __shared__ E lds_work[kPlanLdsMaxE * 2 * kPlanLdsMaxE];
+    __shared__ uint16_t lds_E[256], lds_P[256];
+    __shared__ E lds_fac[256];
+    __shared__ uint8_t lds_exp8[512];
+    __shared__ uint16_t lds_log8[256];
+
+    const uint32_t lane = threadIdx.x;
+    const uint32_t b = blockIdx.x;
+    FieldDev<E> f;
+    f.q = sizeof(E) == 1 ? 255u : 65535u;
+    if constexpr (sizeof(E) == 1) {
+        const uint8_t* ge = reinterpret_cast<const uint8_t*>(a.exp_tab);
+        for (uint32_t i = lane; i < 510; i += kWave) lds_exp8[i] = ge[i];
+        for (uint32_t i = lane; i < 256; i += kWave) lds_log8[i] = a.log_tab[i];
+        __syncthreads();
+        f.exp = reinterpret_cast<const E*>(lds_exp8);
+        f.log = lds_log8;
+    } else {
+        f.exp = reinterpret_cast<const E*>(a.exp_tab);
+        f.log = a.log_tab;
+    }
+
+    const uint32_t k = a.k, m = a.m;
+    const uint32_t nd = a.num_data ? uni(a.num_data[b]) : k;
+    const uint32_t ec = uni(a.erasure_counts[b]);
+    const uint16_t* locs = a.erasure_locs + (uint64_t)b * a.erasure_stride;
+    int32_t status = (int32_t)ec;
+
+    // ---- validate and split erasures (sorted: source first, then parity) ----
+    bool ok = nd >= 1 && nd <= k && ec <= a.erasure_stride && ec <= m;
+    uint32_t es = 0;
+    if (ok) {
+        for (uint32_t i = 0; i < ec; ++i) {
+            const uint32_t l = locs[i];
+            if (l >= nd + m || (i > 0 && l <= locs[i - 1])) ok = false;
+            if (l < nd) ++es;
+        }
+    }
+    if (!ok) status = 0;
+    if (ok && es > 0) {
+        // surviving parities in ascending slot order (reference scan :660-718)
+        if (lane == 0) {
+            uint32_t next = es, np = 0;
+            for (uint32_t s = nd; s < nd + m && np < es; ++s) {
+                if (next < ec && locs[next] == s) { ++next; continue; }
+                lds_P[np++] = (uint16_t)s;
+            }
+            for (uint32_t i = 0; i < es; ++i) lds_E[i] = locs[i];
+            if (np < es) lds_P[0] = 0xffff;  // not enough parity
+        }
+        __syncthreads();
+        if (lds_P[0] == 0xffff) { ok = false; status = 0; }
+    }
+    const uint32_t e = ok ? es : 0;
+    if (lane == 0) {
+        if (a.status) a.status[b] = status;
+        a.rows[b] = (int32_t)e;
+        a.cols2[b] = (uint16_t)e;
+    }
+    if (e == 0) return;
+
+    // ---- stage-1 gather matrix and slots ----
+    const E* gp = reinterpret_cast<const E*>(a.gen_parity);
+    const uint32_t cs = a.coef_stride;
+    E* coef1 = reinterpret_cast<E*>(a.coef1) + (uint64_t)b * k * cs;
+    uint16_t* islots = a.in_slots1 + (uint64_t)b * k;
+    for (uint32_t c = lane; c < nd; c += kWave) {
+        // is c erased? (E sorted)
+        int32_t s_idx = -1;
+        for (uint32_t i = 0; i < e; ++i)
+            if (lds_E[i] == c) s_idx = (int32_t)i;
+        islots[c] = s_idx >= 0 ? lds_P[s_idx] : (uint16_t)c;
+        for (uint32_t t = 0; t < cs; ++t) {
+            E v = 0;
+            if (t < e) {
+                if (s_idx >= 0) v = (E)((uint32_t)s_idx == t);
+                else v = gp[(uint64_t)(lds_P[t] - nd) * k + c];
+            }
+            coef1[(uint64_t)c * cs + t] = v;
+        }
+    }
+
+    // ---- stage 2: invert A[t][s] = G[P_t][E_s] via Gauss-Jordan on [A | I] ----
+    const uint32_t w2 = 2 * e;
+    E* work = e <= kPlanLdsMaxE ? lds_work : reinterpret_cast<E*>(a.work) + (uint64_t)b * m * 2 * m;
+    for (uint32_t idx = lane; idx < e * w2; idx += kWave) {
+        const uint32_t t = idx / w2, col = idx % w2;
+        E v;
+        if (col < e) v = gp[(uint64_t)(lds_P[t] - nd) * k + lds_E[col]];
+        else v = (E)(col - e == t);
+        work[idx] = v;
+    }
+    __syncthreads();
+    bool singular = false;
+    for (uint32_t j = 0; j < e; ++j) {
+        // pivot: first row >= j with a non-zero entry in column j
+        uint32_t piv = 0xffffffffu;
+        for (uint32_t base = j; base < e; base += kWave) {
+            const uint32_t r = base + lane;
+            const bool nz = r < e && work[r * w2 + j] != 0;
+            const uint64_t mask = __ballot(nz);
+            if (mask) {
+                piv = base + (uint32_t)__ffsll((unsigned long long)mask) - 1;
+                break;
+            }
+        }
+        if (piv == 0xffffffffu) { singular = true; break; }
+        if (piv != j) {
+            for (uint32_t col = lane; col < w2; col += kWave) {
+                E tmp = work[j * w2 + col];
+                work[j * w2 + col] = work[piv * w2 + col];
+                work[piv * w2 + col] = tmp;
+            }
+            __syncthreads();
+        }
+        const uint32_t pinv = f.inv(work[j * w2 + j]);
+        for (uint32_t col = lane; col < w2; col += kWave) work[j * w2 + col] = (E)f.mul(pinv, work[j * w2 + col]);
+        __syncthreads();
+        // snapshot column j (the elimination factors) before any row is updated
+        for (uint32_t r = lane; r < e; r += kWave) lds_fac[r] = work[r * w2 + j];
+        __syncthreads();
+        for (uint32_t idx = lane; idx < e * w2; idx += kWave) {
+            const uint32_t r = idx / w2, col = idx % w2;
+            if (r == j) continue;
+            const uint32_t factor = lds_fac[r];
+            if (factor) work[idx] ^= (E)f.mul(factor, work[j * w2 + col]);
+        }
+        __syncthreads();
+    }
+    if (singular) {
+        if (lane == 0) {
+            if (a.status) a.status[b] = 0;
+            a.rows[b] = 0;
+            a.cols2[b] = 0;
+        }
+        return;
+    }
+    E* coef2 = reinterpret_cast<E*>(a.coef2) + (uint64_t)b * cs * cs;
+    for (uint32_t idx = lane; idx < cs * cs; idx += kWave) {
+        const uint32_t t = idx / cs, s = idx % cs;  // column t (input z_t), row s (output)
+        E v = 0;
+        if (t < e && s < e) v = work[s * w2 + e + t];
+        coef2[idx] = v;
+    }
+    uint16_t* oslots = a.out_slots2 + (uint64_t)b * k;
+    for (uint32_t s = lane; s < e; s += kWave) oslots[s] = lds_E[s];
+}
+
+
+// ---------------------------------------------------------------------------------
+// MDP plan: one wavefront per block.
+// ---------------------------------------------------------------------------------
+__global__ __launch_bounds__(kWave) void mdp_plan_kernel(MdpPlanArgs a)
+{
+    __shared__ uint8_t ex[512];
+    __shared__ uint16_t lg[256];
+    __shared__ uint8_t lam[512];
+    __shared__ uint8_t lamb[256][256 / 4];  // per erased row: prefix sums Lambda_u(beta_r) (u < m)
+    __shared__ uint16_t surv[256];
+    __shared__ uint16_t eras[256];
+    __shared__ uint8_t dinv_s[256], beta_s[256];
+
+    const uint32_t lane = threadIdx.x;
+    const uint32_t b = blockIdx.x;
+    for (uint32_t i = lane; i < 510; i += kWave) ex[i] = a.exp_tab[i];
+    for (uint32_t i = lane; i < 256; i += kWave) lg[i] = a.log_tab[i];
+    __syncthreads();
+    auto mul = [&](uint32_t x, uint32_t y) -> uint32_t { return (x && y) ? ex[lg[x] + lg[y]] : 0u; };
+
+    const uint32_t m = a.m;
+    const uint32_t nd = a.num_data ? uni(a.num_data[b]) : a.k;
+    const uint32_t ec = uni(a.erasure_counts[b]);
+    const uint16_t* locs = a.erasure_locs + (uint64_t)b * a.erasure_stride;
+    const uint32_t nvecs = nd + m;
+    bool ok = nd >= 1 && nd <= a.k && ec <= m && ec <= a.erasure_stride && m <= 64;
+    uint32_t es = 0;
+    if (ok)
+        for (uint32_t i = 0; i < ec; ++i) {
+            const uint32_t l = locs[i];
+            if (l >= nvecs || (i > 0 && l <= locs[i - 1])) ok = false;
+            if (l < nd) ++es;
+        }
+    if (!ok) {
+        if (lane == 0) {
+            if (a.status) a.status[b] = 0;
+            a.rows[b] = 0;
+            a.cols[b] = 0;
+        }
+        return;
+    }
+    if (lane == 0) {
+        if (a.status) a.status[b] = (int32_t)ec;
+        a.rows[b] = (int32_t)es;
+    }
+    if (es == 0) {
+        if (lane == 0) a.cols[b] = 0;
+        return;
+    }
+    // erasure locator: lambda(x) = prod_i (1 + X_i x), X_i = alpha^(nvecs-1-loc_i), 2m coefficients
+    const uint32_t deg = 2 * m;
+    for (uint32_t j = lane; j < deg; j += kWave) lam[j] = (j == 0);
+    __syncthreads();
+    for (uint32_t i = 0; i < ec; ++i) {
+        const uint32_t X = ex[nvecs - 1 - locs[i]];
+        uint8_t nv[8];
+        uint32_t n = 0;
+        for (uint32_t j = lane; j < deg; j += kWave) nv[n++] = (uint8_t)(j ? (lam[j] ^ mul(X, lam[j - 1])) : lam[0]);
+        __syncthreads();
+        n = 0;
+        for (uint32_t j = lane; j < deg; j += kWave) lam[j] = nv[n++];
+        __syncthreads();
+    }
+    // surviving slots, erased source rows
+    if (lane == 0) {
+        uint32_t nxt = 0, ns = 0;
+        for (uint32_t v = 0; v < nvecs; ++v) {
+            if (nxt < ec && locs[nxt] == v) { ++nxt; continue; }
+            surv[ns++] = (uint16_t)v;
+        }
+        for (uint32_t i = 0; i < es; ++i) eras[i] = locs[i];
+        a.cols[b] = (uint16_t)ns;
+    }
+    __syncthreads();
+    const uint32_t ns = nvecs - ec;
+    // per erased row r: beta, Forney denominator, Lambda prefix sums
+    for (uint32_t r = lane; r < es; r += kWave) {
+        const uint32_t kk = nvecs - 1 - eras[r];
+        const uint32_t lb = (255u - kk) % 255u;  // log beta
+        const uint32_t beta = ex[lb];
+        uint32_t denom = 0;
+        for (uint32_t j = 1; j < deg; j += 2) denom ^= mul(lam[j], ex[(lb * (j - 1)) % 255u]);
+        dinv_s[r] = (uint8_t)(denom ? ex[255u - lg[denom]] : 1u);  // GINV[0] = 1 (galois.cpp:39)
+        beta_s[r] = (uint8_t)beta;
+        uint32_t acc = 0, bp = 1;
+        for (uint32_t u = 0; u < m; ++u) {
+            acc ^= mul(lam[u], bp);
+            bp = mul(bp, beta);
+            lamb[r][u] = (uint8_t)acc;
+        }
+    }
+    __syncthreads();
+    // coefficients: C[r][v] = Dinv_r * gamma_v * Horner_{u}(Lambda_u; w = gamma_v * beta_r)
+    const uint32_t cs = a.coef_stride;
+    uint8_t* coef = a.coef + (uint64_t)b * (a.k + a.m) * cs;
+    uint16_t* isl = a.in_slots + (uint64_t)b * (a.k + a.m);
+    for (uint32_t j = lane; j < ns; j += kWave) {
+        const uint32_t v = surv[j];
+        isl[j] = (uint16_t)v;
+        const uint32_t gamma = ex[nvecs - 1 - v];
+        for (uint32_t r = 0; r < cs; ++r) {
+            uint32_t val = 0;
+            if (r < es) {
+                const uint32_t w = mul(gamma, beta_s[r]);
+                uint32_t h = lamb[r][0];
+                for (uint32_t u = 1; u < m; ++u) h = mul(h, w) ^ lamb[r][u];
+                val = mul(dinv_s[r], mul(gamma, h));
+            }
+            coef[(uint64_t)j * cs + r] = (uint8_t)val;
+        }
+    }
+    uint16_t* osl = a.out_slots + (uint64_t)b * (a.k + a.m);
+    for (uint32_t r = lane; r < es; r += kWave) osl[r] = eras[r];
+}
+
+}  // namespace
+
+int launch_rs_plan(const RsPlanArgs& a, hipStream_t s)
+{
+    if (a.nblocks == 0) return NFEC_OK;
+    if (a.bits == 8) hipLaunchKernelGGL(rs_plan_kernel<uint8_t>, dim3(a.nblocks), dim3(kWave), 0, s, a);
+    else hipLaunchKernelGGL(rs_plan_kernel<uint16_t>, dim3(a.nblocks), dim3(kWave), 0, s, a);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return hip_fail(e, "rs_plan launch");
+    return NFEC_OK;
+}
+
+int launch_mdp_plan(const MdpPlanArgs& a, hipStream_t s)
+{
+    if (a.nblocks == 0) return NFEC_OK;
+    hipLaunchKernelGGL(mdp_plan_kernel, dim3(a.nblocks), dim3(kWave), 0, s, a);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return hip_fail(e, "mdp_plan launch");
+    return NFEC_OK;
+}
+
+}  // namespace nfec

@@ -1,0 +1,146 @@
+// kernels_util.hip -- synthetic-workload and receiver helpers (device side).
+//
+// fill:      splitmix64 counter streams per (block, slot), generated in
+//            HBM so the bench never moves gigabytes over PCIe.
+// erasures:  per-block partial Fisher-Yates over [0, range) with a sparse swap map,
+//            identical to the oracle's full-array shuffle (orc_erasure_pattern).
+// zero:      the receiver's zero-fill of erased segments before Decode
+//            (reference src/common/normObject.cpp:1579).
+#include "nfec_internal.hpp"
+
+namespace nfec {
+
+namespace {
+
+constexpr uint64_t kGamma = 0x9E3779B97F4A7C15ull;
+
+__device__ __forceinline__ uint64_t mix64(uint64_t z)
+{
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+__global__ void fill_kernel(uint8_t* base, uint64_t block_stride, uint32_t seg_stride, uint32_t nblocks,
+                            const uint16_t* num_data, uint32_t k, uint32_t vec, uint64_t seed,
+                            uint64_t first_block)
+{
+    const uint32_t words = (vec + 7) / 8;
+    const uint64_t per_block = (uint64_t)k * words;
+    const uint64_t total = per_block * nblocks;
+    for (uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; g < total;
+         g += (uint64_t)gridDim.x * blockDim.x) {
+        const uint32_t b = (uint32_t)(g / per_block);
+        const uint32_t rem = (uint32_t)(g % per_block);
+        const uint32_t s = rem / words, w = rem % words;
+        const uint32_t nd = num_data ? num_data[b] : k;
+        if (s >= nd) continue;
+        const uint64_t s0 = seed ^ ((first_block + b) << 20) ^ (uint64_t)s;
+        const uint64_t v = mix64(s0 + (uint64_t)(w + 1) * kGamma);
+        uint8_t* p = base + (uint64_t)b * block_stride + (uint64_t)s * seg_stride + (uint64_t)w * 8;
+        const uint32_t nbytes = min(8u, vec - w * 8);
+        if (nbytes == 8) {
+            *reinterpret_cast<uint64_t*>(p) = v;
+        } else {
+            for (uint32_t i = 0; i < nbytes; ++i) p[i] = (uint8_t)(v >> (8 * i));
+        }
+    }
+}
+
+__global__ void erasure_kernel(uint16_t* locs, uint32_t stride, uint16_t* counts, uint32_t nblocks,
+                               uint32_t range, uint32_t count, uint64_t seed, uint64_t first_block)
+{
+    const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= nblocks) return;
+    if (count > range) count = range;
+    if (count > stride) count = stride;
+    // sparse Fisher-Yates: only positions touched by swaps are recorded
+    uint16_t pos[256], val[256];
+    uint32_t n = 0;
+    auto get = [&](uint32_t p) -> uint32_t {
+        for (uint32_t i = 0; i < n; ++i)
+            if (pos[i] == p) return val[i];
+        return p;
+    };
+    auto set = [&](uint32_t p, uint32_t v) {
+        for (uint32_t i = 0; i < n; ++i)
+            if (pos[i] == p) { val[i] = (uint16_t)v; return; }
+        pos[n] = (uint16_t)p;
+        val[n] = (uint16_t)v;
+        ++n;
+    };
+    const uint64_t s0 = seed ^ 0xE7A5E7A500000000ull ^ (first_block + b);
+    uint16_t* out = locs + (uint64_t)b * stride;
+    count = min(count, 128u);
+    for (uint32_t i = 0; i < count; ++i) {
+        const uint64_t r = mix64(s0 + (uint64_t)(i + 1) * kGamma);
+        const uint32_t j = i + (uint32_t)(r % (uint64_t)(range - i));
+        const uint32_t vi = get(i), vj = get(j);
+        set(i, vj);
+        set(j, vi);
+        out[i] = (uint16_t)vj;
+    }
+    for (uint32_t i = 1; i < count; ++i) {
+        const uint16_t v = out[i];
+        int32_t j = (int32_t)i - 1;
+        while (j >= 0 && out[j] > v) { out[j + 1] = out[j]; --j; }
+        out[j + 1] = v;
+    }
+    counts[b] = (uint16_t)count;
+}
+
+__global__ void zero_kernel(uint8_t* base, uint64_t block_stride, uint32_t seg_stride, uint32_t nblocks,
+                            const uint16_t* locs, uint32_t stride, const uint16_t* counts, uint32_t vec)
+{
+    // one workgroup per (block, erasure index) pair
+    const uint32_t b = blockIdx.x / stride;
+    const uint32_t e = blockIdx.x % stride;
+    if (b >= nblocks || e >= counts[b]) return;
+    uint8_t* p = base + (uint64_t)b * block_stride + (uint64_t)locs[(uint64_t)b * stride + e] * seg_stride;
+    for (uint32_t i = threadIdx.x; i * 8 < vec; i += blockDim.x) {
+        if (i * 8 + 8 <= vec) *reinterpret_cast<uint64_t*>(p + i * 8) = 0;
+        else
+            for (uint32_t j = i * 8; j < vec; ++j) p[j] = 0;
+    }
+}
+
+}  // namespace
+
+int launch_fill(uint8_t* base, uint64_t block_stride, uint32_t seg_stride, uint32_t nblocks,
+                const uint16_t* num_data, uint32_t k, uint32_t vec, uint64_t seed, uint64_t first_block,
+                hipStream_t s)
+{
+    if (nblocks == 0 || vec == 0) return NFEC_OK;
+    const uint64_t total = (uint64_t)nblocks * k * ((vec + 7) / 8);
+    const uint32_t grid = (uint32_t)std::min<uint64_t>((total + 255) / 256, 65536);
+    hipLaunchKernelGGL(fill_kernel, dim3(grid), dim3(256), 0, s, base, block_stride, seg_stride, nblocks,
+                       num_data, k, vec, seed, first_block);
+    hipError_t e = hipGetLastError();
+    return e == hipSuccess ? NFEC_OK : hip_fail(e, "fill launch");
+}
+
+int launch_erasures(uint16_t* locs, uint32_t stride, uint16_t* counts, uint32_t nblocks, uint32_t range,
+                    uint32_t count, uint64_t seed, uint64_t first_block, hipStream_t s)
+{
+    if (nblocks == 0) return NFEC_OK;
+    if (count > 128) return fail(NFEC_EINVAL, "erasure generator supports at most 128 erasures per block");
+    hipLaunchKernelGGL(erasure_kernel, dim3((nblocks + 63) / 64), dim3(64), 0, s, locs, stride, counts, nblocks,
+                       range, count, seed, first_block);
+    hipError_t e = hipGetLastError();
+    return e == hipSuccess ? NFEC_OK : hip_fail(e, "erasure launch");
+}
+
+int launch_zero_slots(uint8_t* base, uint64_t block_stride, uint32_t seg_stride, uint32_t nblocks,
+                      const uint16_t* locs, uint32_t stride, const uint16_t* counts, uint32_t vec,
+                      hipStream_t s)
+{
+    if (nblocks == 0 || stride == 0) return NFEC_OK;
+    const uint64_t groups = (uint64_t)nblocks * stride;
+    if (groups >= (1ull << 31)) return fail(NFEC_EINVAL, "zero_slots: too many blocks");
+    hipLaunchKernelGGL(zero_kernel, dim3((uint32_t)groups), dim3(64), 0, s, base, block_stride, seg_stride, nblocks,
+                       locs, stride, counts, vec);
+    hipError_t e = hipGetLastError();
+    return e == hipSuccess ? NFEC_OK : hip_fail(e, "zero launch");
+}
+
+}  // namespace nfec

@@ -1,0 +1,843 @@
+// nfec_api.cpp -- C ABI (include/nfec.h): codec objects and batch orchestration.
+//
+// A codec mirrors one NormEncoder/NormDecoder Init (reference normEncoderRS8.cpp:400-462,
+// :542-649; normEncoderRS16.cpp:399-461; normEncoderMDP.cpp:56-84): it owns the generator
+// (built once on the host, uploaded to HBM) and the per-value kernel tables.  Batched calls
+// only enqueue kernels on the caller's stream; no host<->device traffic on the hot path.
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <memory>
+
+#include "nfec_internal.hpp"
+
+namespace nfec {
+const char* last_error_cstr();
+}
+
+using namespace nfec;
+
+namespace {
+
+struct DeviceGuard {
+    int prev = -1;
+    bool ok = true;
+    explicit DeviceGuard(int dev)
+    {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        if (prev != dev) ok = hipSetDevice(dev) == hipSuccess;
+    }
+    ~DeviceGuard()
+    {
+        int cur = -1;
+        if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+    }
+};
+
+template <typename T>
+struct DevBuf {
+    T* p = nullptr;
+    size_t n = 0;
+    int reserve(size_t count)
+    {
+        if (count <= n) return NFEC_OK;
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        n = 0;
+        if (hipMalloc(reinterpret_cast<void**>(&p), count * sizeof(T)) != hipSuccess) {
+            (void)hipGetLastError();
+            return fail(NFEC_ENOMEM, "hipMalloc failed for workspace");
+        }
+        n = count;
+        return NFEC_OK;
+    }
+    void release()
+    {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        n = 0;
+    }
+};
+
+constexpr uint32_t kRowPad = 32;       // coefficient rows padded (kernel row chunk multiple)
+constexpr uint32_t kSubBatch = 16384;  // decode blocks per planning pass (bounds workspace)
+
+uint32_t round_up(uint32_t v, uint32_t a) { return (v + a - 1) / a * a; }
+
+}  // namespace
+
+struct nfec_codec {
+    int kind = 0;
+    int device = 0;
+    uint32_t k = 0, m = 0, vec = 0, sym = 1;
+    uint32_t cs = 0;  // padded parity-row count
+    std::vector<uint32_t> gen;  // m x k parity rows (RS) / LFSR map for a full block (MDP)
+
+    // device-resident state
+    DevBuf<uint8_t> d_coef;      // encode coefficients, column-major [k][cs] elements
+    DevBuf<uint8_t> d_gen;       // m x k row-major elements (decode plan gathers)
+    DevBuf<uint32_t> d_vtab;     // 256 x 8 dwords (GF(2^8) kernels)
+    DevBuf<uint8_t> d_exp;       // field exp table (2q elements)
+    DevBuf<uint16_t> d_log;      // field log table (q+1)
+    DevBuf<uint8_t> d_mdp_step;  // MDP single LFSR step matrix, column-major [m+1][cs]
+
+    // decode workspace (guarded by mu)
+    std::mutex mu;
+    DevBuf<int32_t> w_status, w_rows;
+    DevBuf<uint16_t> w_islots, w_oslots, w_cols;
+    DevBuf<uint8_t> w_coef1, w_coef2, w_z, w_work;
+    // per-call staging
+    DevBuf<uint8_t> s_block;
+    DevBuf<uint16_t> s_locs;
+
+    ~nfec_codec()
+    {
+        DeviceGuard g(device);
+        for (auto* b : {&d_coef, &d_gen, &d_exp, &w_coef1, &w_coef2, &w_z, &w_work, &s_block, &d_mdp_step})
+            b->release();
+        d_vtab.release();
+        d_log.release();
+        w_status.release();
+        w_rows.release();
+        w_islots.release();
+        w_oslots.release();
+        w_cols.release();
+        s_locs.release();
+    }
+};
+
+namespace {
+
+int upload(DevBuf<uint8_t>& d, const void* src, size_t bytes)
+{
+    int rc = d.reserve(bytes);
+    if (rc) return rc;
+    NFEC_HIP(hipMemcpy(d.p, src, bytes, hipMemcpyHostToDevice));
+    return NFEC_OK;
+}
+
+int check_batch(const nfec_codec* c, const nfec_block_batch* b)
+{
+    if (!c || !b) return fail(NFEC_EINVAL, "null codec or batch");
+    if (b->nblocks == 0) return NFEC_OK;
+    if (!b->blocks) return fail(NFEC_EINVAL, "null blocks pointer");
+    if ((reinterpret_cast<uintptr_t>(b->blocks) & 7) || (b->seg_stride & 7) || (b->block_stride & 7))
+        return fail(NFEC_EINVAL, "blocks, seg_stride and block_stride must be multiples of 8 bytes");
+    if (b->seg_stride < c->vec) return fail(NFEC_EINVAL, "seg_stride < vector_size");
+    if (b->block_stride < (uint64_t)(c->k + c->m) * b->seg_stride && b->nblocks > 1)
+        return fail(NFEC_EINVAL, "block_stride smaller than (k+m)*seg_stride");
+    return NFEC_OK;
+}
+
+// ---- codec construction ----
+int build_codec(nfec_codec* c)
+{
+    const bool wide = c->kind == NFEC_RS16;
+    c->sym = wide ? 2 : 1;
+    c->cs = round_up(std::max(c->m, 1u), kRowPad);
+    const Field& f = wide ? gf16() : gf8();
+    if (c->kind == NFEC_MDP) {
+        if (c->k + c->m > 255 || c->m == 0) return fail(NFEC_ERANGE, "MDP: numData + numParity > 255");
+        std::vector<uint8_t> g;
+        mdp_generator_poly(c->m, g);
+        // encode matrices for every block length nd = 1..k: [nd-1][col][cs]
+        std::vector<uint8_t> coef((size_t)c->k * c->k * c->cs, 0);
+        std::vector<uint8_t> map((size_t)c->m * c->k);
+        for (uint32_t nd = 1; nd <= c->k; ++nd) {
+            mdp_encode_matrix(g, c->m, nd, map.data());
+            for (uint32_t col = 0; col < nd; ++col)
+                for (uint32_t r = 0; r < c->m; ++r)
+                    coef[((size_t)(nd - 1) * c->k + col) * c->cs + r] = map[(size_t)r * nd + col];
+            if (nd == c->k) {
+                c->gen.assign(map.begin(), map.end());
+            }
+        }
+        int rc = upload(c->d_coef, coef.data(), coef.size());
+        if (rc) return rc;
+        // one in-order Encode step: inputs [d, P0..P(m-1)] -> new P (normEncoderMDP.cpp:178-211)
+        std::vector<uint8_t> step((size_t)(c->m + 1) * c->cs, 0);
+        for (uint32_t i = 0; i < c->m; ++i) {
+            const uint8_t gi = (i + 1 < c->m) ? g[c->m - 1 - i] : g[0];
+            step[(size_t)0 * c->cs + i] = gi;              // data
+            step[(size_t)1 * c->cs + i] ^= gi;             // P0 enters the feedback
+            if (i + 1 < c->m) step[(size_t)(i + 2) * c->cs + i] ^= 1;  // shift P(i+1) -> P(i)
+        }
+        rc = upload(c->d_mdp_step, step.data(), step.size());
+        if (rc) return rc;
+    } else {
+        const int bits = wide ? 16 : 8;
+        int rc = rs_generator(bits, c->k, c->m, c->gen);
+        if (rc) return fail(rc, "RS: numData/numParity exceeds code limits");
+        std::vector<uint8_t> coef((size_t)c->k * c->cs * c->sym, 0);
+        std::vector<uint8_t> genb((size_t)c->m * c->k * c->sym);
+        for (uint32_t p = 0; p < c->m; ++p)
+            for (uint32_t j = 0; j < c->k; ++j) {
+                const uint32_t v = c->gen[(size_t)p * c->k + j];
+                if (wide) {
+                    reinterpret_cast<uint16_t*>(coef.data())[(size_t)j * c->cs + p] = (uint16_t)v;
+                    reinterpret_cast<uint16_t*>(genb.data())[(size_t)p * c->k + j] = (uint16_t)v;
+                } else {
+                    coef[(size_t)j * c->cs + p] = (uint8_t)v;
+                    genb[(size_t)p * c->k + j] = (uint8_t)v;
+                }
+            }
+        rc = upload(c->d_coef, coef.data(), coef.size());
+        if (rc) return rc;
+        rc = upload(c->d_gen, genb.data(), genb.size());
+        if (rc) return rc;
+    }
+    // field tables
+    if (wide) {
+        std::vector<uint16_t> ex(2 * f.q), lg(f.q + 1);
+        for (uint32_t i = 0; i < 2 * f.q; ++i) ex[i] = (uint16_t)f.exp[i];
+        for (uint32_t i = 0; i <= f.q; ++i) lg[i] = (uint16_t)f.log[i];
+        int rc = upload(c->d_exp, ex.data(), ex.size() * 2);
+        if (rc) return rc;
+        rc = c->d_log.reserve(lg.size());
+        if (rc) return rc;
+        NFEC_HIP(hipMemcpy(c->d_log.p, lg.data(), lg.size() * 2, hipMemcpyHostToDevice));
+    } else {
+        std::vector<uint8_t> ex(2 * f.q);
+        std::vector<uint16_t> lg(f.q + 1);
+        for (uint32_t i = 0; i < 2 * f.q; ++i) ex[i] = (uint8_t)f.exp[i];
+        for (uint32_t i = 0; i <= f.q; ++i) lg[i] = (uint16_t)f.log[i];
+        int rc = upload(c->d_exp, ex.data(), ex.size());
+        if (rc) return rc;
+        rc = c->d_log.reserve(lg.size());
+        if (rc) return rc;
+        NFEC_HIP(hipMemcpy(c->d_log.p, lg.data(), lg.size() * 2, hipMemcpyHostToDevice));
+        std::vector<uint32_t> vt(256 * 8);
+        for (uint32_t v = 0; v < 256; ++v) vperm_table(v, &vt[v * 8]);
+        rc = c->d_vtab.reserve(vt.size());
+        if (rc) return rc;
+        NFEC_HIP(hipMemcpy(c->d_vtab.p, vt.data(), vt.size() * 4, hipMemcpyHostToDevice));
+    }
+    return NFEC_OK;
+}
+
+// ---- encode on a device batch ----
+int encode_device(nfec_codec* c, const nfec_block_batch* b, hipStream_t s)
+{
+    const bool acc = b->flags & NFEC_ACCUMULATE;
+    if (c->kind == NFEC_RS8) {
+        Gf8MatmulArgs a;
+        a.in_base = static_cast<const uint8_t*>(b->blocks);
+        a.in_block_stride = b->block_stride;
+        a.in_seg_stride = b->seg_stride;
+        a.in_count = b->num_data;
+        a.cols_const = c->k;
+        a.out_base = static_cast<uint8_t*>(b->blocks);
+        a.out_block_stride = b->block_stride;
+        a.out_seg_stride = b->seg_stride;
+        a.out_slot_mode = OUT_SLOT_AFTER_INPUT;
+        a.rows_const = c->m;
+        a.coef = c->d_coef.p;
+        a.coef_col_stride = c->cs;
+        a.vtab = c->d_vtab.p;
+        a.nblocks = b->nblocks;
+        a.vec_bytes = c->vec;
+        a.accumulate = acc;
+        return launch_gf8_matmul(a, true, s);
+    }
+    if (c->kind == NFEC_RS16) {
+        Gf16MatmulArgs a;
+        a.in_base = static_cast<const uint8_t*>(b->blocks);
+        a.in_block_stride = b->block_stride;
+        a.in_seg_stride = b->seg_stride;
+        a.in_count = b->num_data;
+        a.cols_const = c->k;
+        a.out_base = static_cast<uint8_t*>(b->blocks);
+        a.out_block_stride = b->block_stride;
+        a.out_seg_stride = b->seg_stride;
+        a.out_slot_mode = OUT_SLOT_AFTER_INPUT;
+        a.rows_const = c->m;
+        a.coef = reinterpret_cast<const uint16_t*>(c->d_coef.p);
+        a.coef_col_stride = c->cs;
+        a.exp_tab = reinterpret_cast<const uint16_t*>(c->d_exp.p);
+        a.log_tab = c->d_log.p;
+        a.nblocks = b->nblocks;
+        a.vec_bytes = c->vec & ~1u;
+        a.accumulate = acc;
+        return launch_gf16_matmul(a, s);
+    }
+    // MDP: the in-order LFSR is a linear map of the block; the caller's parity buffers are
+    // zeroed at block start by contract, so accumulate has no reference meaning.
+    if (acc) return fail(NFEC_ENOTSUP, "MDP encode does not accumulate (LFSR restarts from zeroed parity)");
+    Gf8MatmulArgs a;
+    a.in_base = static_cast<const uint8_t*>(b->blocks);
+    a.in_block_stride = b->block_stride;
+    a.in_seg_stride = b->seg_stride;
+    a.in_count = b->num_data;
+    a.cols_const = c->k;
+    a.out_base = static_cast<uint8_t*>(b->blocks);
+    a.out_block_stride = b->block_stride;
+    a.out_seg_stride = b->seg_stride;
+    a.out_slot_mode = OUT_SLOT_AFTER_INPUT;
+    a.rows_const = c->m;
+    a.coef = c->d_coef.p;
+    a.coef_block_stride = (uint64_t)c->k * c->cs;
+    a.coef_col_stride = c->cs;
+    a.coef_by_count = 1;
+    a.vtab = c->d_vtab.p;
+    a.nblocks = b->nblocks;
+    a.vec_bytes = c->vec;
+    return launch_gf8_matmul(a, false, s);
+}
+
+// ---- decode on a device batch ----
+int decode_device(nfec_codec* c, const nfec_block_batch* b, const uint16_t* locs, uint32_t lstride,
+                  const uint16_t* counts, int32_t* status, hipStream_t s)
+{
+    if (!locs || !counts) return fail(NFEC_EINVAL, "null erasure arrays");
+    const bool acc = b->flags & NFEC_ACCUMULATE;
+    if (c->kind == NFEC_MDP && acc) return fail(NFEC_ENOTSUP, "MDP decode requires zero-filled erased segments");
+    std::lock_guard<std::mutex> lk(c->mu);
+    const uint32_t sb = std::min(b->nblocks, kSubBatch);
+    const uint32_t n = c->k + c->m;
+    const uint32_t zstride = round_up(c->vec, 8);
+    int rc;
+    if ((rc = c->w_rows.reserve(sb))) return rc;
+    if ((rc = c->w_cols.reserve(sb))) return rc;
+    if (!status && (rc = c->w_status.reserve(sb))) return rc;
+    if ((rc = c->w_islots.reserve((size_t)sb * n))) return rc;
+    if ((rc = c->w_oslots.reserve((size_t)sb * n))) return rc;
+    if (c->kind == NFEC_MDP) {
+        if ((rc = c->w_coef1.reserve((size_t)sb * n * c->cs))) return rc;
+    } else {
+        if ((rc = c->w_coef1.reserve((size_t)sb * c->k * c->cs * c->sym))) return rc;
+        if ((rc = c->w_coef2.reserve((size_t)sb * c->cs * c->cs * c->sym))) return rc;
+        if ((rc = c->w_z.reserve((size_t)sb * c->cs * zstride))) return rc;
+        if (c->m > 64 && (rc = c->w_work.reserve((size_t)sb * c->m * 2 * c->m * c->sym))) return rc;
+    }
+    for (uint32_t b0 = 0; b0 < b->nblocks; b0 += sb) {
+        const uint32_t nb = std::min(sb, b->nblocks - b0);
+        uint8_t* blocks = static_cast<uint8_t*>(b->blocks) + (uint64_t)b0 * b->block_stride;
+        const uint16_t* nd = b->num_data ? b->num_data + b0 : nullptr;
+        const uint16_t* l = locs + (uint64_t)b0 * lstride;
+        const uint16_t* cnt = counts + b0;
+        int32_t* st = status ? status + b0 : c->w_status.p;
+        if (c->kind == NFEC_MDP) {
+            MdpPlanArgs p;
+            p.k = c->k;
+            p.m = c->m;
+            p.nblocks = nb;
+            p.num_data = nd;
+            p.erasure_locs = l;
+            p.erasure_stride = lstride;
+            p.erasure_counts = cnt;
+            p.exp_tab = c->d_exp.p;
+            p.log_tab = c->d_log.p;
+            p.status = st;
+            p.rows = c->w_rows.p;
+            p.cols = c->w_cols.p;
+            p.in_slots = c->w_islots.p;
+            p.out_slots = c->w_oslots.p;
+            p.coef_stride = c->cs;
+            p.coef = c->w_coef1.p;
+            if ((rc = launch_mdp_plan(p, s))) return rc;
+            Gf8MatmulArgs a;
+            a.in_base = blocks;
+            a.in_block_stride = b->block_stride;
+            a.in_seg_stride = b->seg_stride;
+            a.in_slots = c->w_islots.p;
+            a.in_count = c->w_cols.p;
+            a.out_base = blocks;
+            a.out_block_stride = b->block_stride;
+            a.out_seg_stride = b->seg_stride;
+            a.out_slots = c->w_oslots.p;
+            a.out_slot_mode = OUT_SLOT_LIST;
+            a.row_count = c->w_rows.p;
+            a.slots_stride = n;
+            a.coef = c->w_coef1.p;
+            a.coef_block_stride = (uint64_t)n * c->cs;
+            a.coef_col_stride = c->cs;
+            a.vtab = c->d_vtab.p;
+            a.nblocks = nb;
+            a.vec_bytes = c->vec;
+            if ((rc = launch_gf8_matmul(a, false, s))) return rc;
+            continue;
+        }
+        RsPlanArgs p;
+        p.bits = c->kind == NFEC_RS16 ? 16 : 8;
+        p.k = c->k;
+        p.m = c->m;
+        p.nblocks = nb;
+        p.num_data = nd;
+        p.erasure_locs = l;
+        p.erasure_stride = lstride;
+        p.erasure_counts = cnt;
+        p.gen_parity = c->d_gen.p;
+        p.exp_tab = c->d_exp.p;
+        p.log_tab = c->d_log.p;
+        p.status = st;
+        p.rows = c->w_rows.p;
+        p.in_slots1 = c->w_islots.p;
+        p.out_slots2 = c->w_oslots.p;
+        p.cols2 = c->w_cols.p;
+        p.coef_stride = c->cs;
+        p.coef1 = c->w_coef1.p;
+        p.coef2 = c->w_coef2.p;
+        p.work = c->w_work.p;
+        if ((rc = launch_rs_plan(p, s))) return rc;
+        // stage 1: z_t = parity(P_t) ^ sum_{present c} G[P_t][c] d_c  -> scratch rows
+        // stage 2: d_E = A^-1 z                                          -> erased slots
+        if (c->kind == NFEC_RS8) {
+            Gf8MatmulArgs a;
+            a.in_base = blocks;
+            a.in_block_stride = b->block_stride;
+            a.in_seg_stride = b->seg_stride;
+            a.in_slots = c->w_islots.p;
+            a.in_count = nd;
+            a.cols_const = c->k;
+            a.out_base = c->w_z.p;
+            a.out_block_stride = (uint64_t)c->cs * zstride;
+            a.out_seg_stride = zstride;
+            a.out_slot_mode = OUT_SLOT_ROW;
+            a.row_count = c->w_rows.p;
+            a.slots_stride = c->k;
+            a.coef = c->w_coef1.p;
+            a.coef_block_stride = (uint64_t)c->k * c->cs;
+            a.coef_col_stride = c->cs;
+            a.vtab = c->d_vtab.p;
+            a.nblocks = nb;
+            a.vec_bytes = c->vec;
+            if ((rc = launch_gf8_matmul(a, false, s))) return rc;
+            Gf8MatmulArgs a2;
+            a2.in_base = c->w_z.p;
+            a2.in_block_stride = (uint64_t)c->cs * zstride;
+            a2.in_seg_stride = zstride;
+            a2.in_count = c->w_cols.p;
+            a2.out_base = blocks;
+            a2.out_block_stride = b->block_stride;
+            a2.out_seg_stride = b->seg_stride;
+            a2.out_slots = c->w_oslots.p;
+            a2.out_slot_mode = OUT_SLOT_LIST;
+            a2.row_count = c->w_rows.p;
+            a2.slots_stride = c->k;
+            a2.coef = c->w_coef2.p;
+            a2.coef_block_stride = (uint64_t)c->cs * c->cs;
+            a2.coef_col_stride = c->cs;
+            a2.vtab = c->d_vtab.p;
+            a2.nblocks = nb;
+            a2.vec_bytes = c->vec;
+            a2.accumulate = acc;
+            if ((rc = launch_gf8_matmul(a2, false, s))) return rc;
+        } else {
+            const uint32_t vb = c->vec & ~1u;
+            Gf16MatmulArgs a;
+            a.in_base = blocks;
+            a.in_block_stride = b->block_stride;
+            a.in_seg_stride = b->seg_stride;
+            a.in_slots = c->w_islots.p;
+            a.in_count = nd;
+            a.cols_const = c->k;
+            a.out_base = c->w_z.p;
+            a.out_block_stride = (uint64_t)c->cs * zstride;
+            a.out_seg_stride = zstride;
+            a.out_slot_mode = OUT_SLOT_ROW;
+            a.row_count = c->w_rows.p;
+            a.slots_stride = c->k;
+            a.coef = reinterpret_cast<const uint16_t*>(c->w_coef1.p);
+            a.coef_block_stride = (uint64_t)c->k * c->cs;
+            a.coef_col_stride = c->cs;
+            a.exp_tab = reinterpret_cast<const uint16_t*>(c->d_exp.p);
+            a.log_tab = c->d_log.p;
+            a.nblocks = nb;
+            a.vec_bytes = vb;
+            if ((rc = launch_gf16_matmul(a, s))) return rc;
+            Gf16MatmulArgs a2 = a;
+            a2.in_base = c->w_z.p;
+            a2.in_block_stride = (uint64_t)c->cs * zstride;
+            a2.in_seg_stride = zstride;
+            a2.in_slots = nullptr;
+            a2.in_count = c->w_cols.p;
+            a2.out_base = blocks;
+            a2.out_block_stride = b->block_stride;
+            a2.out_seg_stride = b->seg_stride;
+            a2.out_slots = c->w_oslots.p;
+            a2.out_slot_mode = OUT_SLOT_LIST;
+            a2.coef = reinterpret_cast<const uint16_t*>(c->w_coef2.p);
+            a2.coef_block_stride = (uint64_t)c->cs * c->cs;
+            a2.accumulate = acc;
+            if ((rc = launch_gf16_matmul(a2, s))) return rc;
+        }
+    }
+    return NFEC_OK;
+}
+
+}  // namespace
+
+// =====================================================================================
+// C ABI
+// =====================================================================================
+extern "C" {
+
+int nfec_abi_version(void) { return NFEC_ABI_VERSION; }
+
+const char* nfec_last_error(void) { return last_error_cstr(); }
+
+int nfec_device_count(void)
+{
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) {
+        (void)hipGetLastError();
+        return 0;
+    }
+    int good = 0;
+    for (int d = 0; d < n; ++d) {
+        hipDeviceProp_t prop;
+        if (hipGetDeviceProperties(&prop, d) == hipSuccess && std::strncmp(prop.gcnArchName, "gfx950", 6) == 0)
+            ++good;
+    }
+    return good;
+}
+
+int nfec_codec_create(int device, int kind, uint32_t num_data, uint32_t num_parity, uint32_t vector_size,
+                      nfec_codec** out)
+{
+    if (!out) return fail(NFEC_EINVAL, "null output pointer");
+    *out = nullptr;
+    if (kind != NFEC_RS8 && kind != NFEC_RS16 && kind != NFEC_MDP) return fail(NFEC_EINVAL, "unknown codec kind");
+    if (num_data == 0 || num_parity == 0) return fail(NFEC_EINVAL, "numData and numParity must be > 0");
+    if (vector_size == 0 || vector_size > 65535) return fail(NFEC_EINVAL, "vectorSize must be in [1, 65535]");
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev) {
+        (void)hipGetLastError();
+        return fail(NFEC_EDEVICE, "no such HIP device (the MI355X path needs a GPU)");
+    }
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) != hipSuccess || std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+        return fail(NFEC_EDEVICE, "device is not gfx950 (MI355X)");
+    DeviceGuard g(device);
+    if (!g.ok) return fail(NFEC_EDEVICE, "hipSetDevice failed");
+    std::unique_ptr<nfec_codec> c(new nfec_codec);
+    c->kind = kind;
+    c->device = device;
+    c->k = num_data;
+    c->m = num_parity;
+    c->vec = vector_size;
+    int rc = build_codec(c.get());
+    if (rc) return rc;
+    *out = c.release();
+    return NFEC_OK;
+}
+
+void nfec_codec_destroy(nfec_codec* codec) { delete codec; }
+
+int nfec_build_generator(int kind, uint32_t num_data, uint32_t num_parity, void* host_out, size_t bytes)
+{
+    if (!host_out || num_data == 0 || num_parity == 0) return fail(NFEC_EINVAL, "bad argument");
+    const size_t cnt = (size_t)num_data * num_parity;
+    if (kind == NFEC_MDP) {
+        if (num_data + num_parity > 255) return fail(NFEC_ERANGE, "MDP: numData + numParity > 255");
+        if (bytes < cnt) return fail(NFEC_EINVAL, "output buffer too small");
+        std::vector<uint8_t> g;
+        mdp_generator_poly(num_parity, g);
+        mdp_encode_matrix(g, num_parity, num_data, static_cast<uint8_t*>(host_out));
+        return NFEC_OK;
+    }
+    if (kind != NFEC_RS8 && kind != NFEC_RS16) return fail(NFEC_EINVAL, "unknown codec kind");
+    const size_t sym = kind == NFEC_RS16 ? 2 : 1;
+    if (bytes < cnt * sym) return fail(NFEC_EINVAL, "output buffer too small");
+    std::vector<uint32_t> rows;
+    int rc = rs_generator(kind == NFEC_RS16 ? 16 : 8, num_data, num_parity, rows);
+    if (rc) return fail(rc, "numData/numParity exceeds code limits");
+    for (size_t i = 0; i < cnt; ++i) {
+        if (sym == 2) static_cast<uint16_t*>(host_out)[i] = (uint16_t)rows[i];
+        else static_cast<uint8_t*>(host_out)[i] = (uint8_t)rows[i];
+    }
+    return NFEC_OK;
+}
+
+int nfec_codec_get_info(const nfec_codec* c, nfec_codec_info* out)
+{
+    if (!c || !out) return fail(NFEC_EINVAL, "null argument");
+    out->kind = c->kind;
+    out->device = c->device;
+    out->num_data = c->k;
+    out->num_parity = c->m;
+    out->vector_size = c->vec;
+    out->symbol_bytes = c->sym;
+    return NFEC_OK;
+}
+
+int nfec_codec_get_generator(const nfec_codec* c, void* host_out, size_t bytes)
+{
+    if (!c || !host_out) return fail(NFEC_EINVAL, "null argument");
+    const size_t need = (size_t)c->m * c->k * c->sym;
+    if (bytes < need) return fail(NFEC_EINVAL, "output buffer too small");
+    for (size_t i = 0; i < (size_t)c->m * c->k; ++i) {
+        if (c->sym == 2) static_cast<uint16_t*>(host_out)[i] = (uint16_t)c->gen[i];
+        else static_cast<uint8_t*>(host_out)[i] = (uint8_t)c->gen[i];
+    }
+    return NFEC_OK;
+}
+
+int nfec_encode(nfec_codec* codec, const nfec_block_batch* batch, void* stream)
+{
+    int rc = check_batch(codec, batch);
+    if (rc || batch->nblocks == 0) return rc;
+    DeviceGuard g(codec->device);
+    return encode_device(codec, batch, static_cast<hipStream_t>(stream));
+}
+
+int nfec_decode(nfec_codec* codec, const nfec_block_batch* batch, const uint16_t* erasure_locs,
+                uint32_t erasure_stride, const uint16_t* erasure_counts, int32_t* status, void* stream)
+{
+    int rc = check_batch(codec, batch);
+    if (rc || batch->nblocks == 0) return rc;
+    if (erasure_stride == 0) return fail(NFEC_EINVAL, "erasure_stride must be > 0");
+    DeviceGuard g(codec->device);
+    return decode_device(codec, batch, erasure_locs, erasure_stride, erasure_counts, status,
+                         static_cast<hipStream_t>(stream));
+}
+
+// ---- per-call NORM semantics (synchronous, host vectors) ----
+int nfec_encode_segment(nfec_codec* c, uint32_t segment_id, const void* data, void* const* parity)
+{
+    if (!c || !data || !parity) return fail(NFEC_EINVAL, "null argument");
+    if (segment_id >= c->k) return fail(NFEC_EINVAL, "segmentId >= numData");
+    DeviceGuard g(c->device);
+    std::lock_guard<std::mutex> lk(c->mu);
+    const uint32_t stride = round_up(c->vec, 8);
+    const uint32_t nslots = 2 * c->m + 1;
+    int rc = c->s_block.reserve((size_t)nslots * stride);
+    if (rc) return rc;
+    uint8_t* d = c->s_block.p;
+    NFEC_HIP(hipMemcpy(d, data, c->vec, hipMemcpyHostToDevice));
+    for (uint32_t i = 0; i < c->m; ++i)
+        NFEC_HIP(hipMemcpy(d + (size_t)(1 + i) * stride, parity[i], c->vec, hipMemcpyHostToDevice));
+    uint32_t out_first = 1;
+    if (c->kind == NFEC_RS8 || c->kind == NFEC_MDP) {
+        Gf8MatmulArgs a;
+        a.in_base = d;
+        a.in_seg_stride = stride;
+        a.out_base = d;
+        a.out_seg_stride = stride;
+        a.out_slot_mode = OUT_SLOT_AFTER_INPUT;
+        a.rows_const = c->m;
+        a.coef_col_stride = c->cs;
+        a.vtab = c->d_vtab.p;
+        a.nblocks = 1;
+        a.vec_bytes = c->vec;
+        if (c->kind == NFEC_RS8) {
+            a.cols_const = 1;  // data in slot 0, column segment_id of the generator
+            a.coef = c->d_coef.p + (size_t)segment_id * c->cs;
+            a.accumulate = 1;  // parity[i] ^= G[k+i][segment_id] * data  (normEncoderRS8.cpp:473-483)
+        } else {
+            a.cols_const = c->m + 1;  // [d, P0..P(m-1)] -> new P in slots m+1..2m
+            a.coef = c->d_mdp_step.p;
+            out_first = c->m + 1;
+        }
+        if ((rc = launch_gf8_matmul(a, false, nullptr))) return rc;
+    } else {
+        Gf16MatmulArgs a;
+        a.in_base = d;
+        a.in_seg_stride = stride;
+        a.cols_const = 1;
+        a.out_base = d;
+        a.out_seg_stride = stride;
+        a.out_slot_mode = OUT_SLOT_AFTER_INPUT;
+        a.rows_const = c->m;
+        a.coef = reinterpret_cast<const uint16_t*>(c->d_coef.p) + (size_t)segment_id * c->cs;
+        a.coef_col_stride = c->cs;
+        a.exp_tab = reinterpret_cast<const uint16_t*>(c->d_exp.p);
+        a.log_tab = c->d_log.p;
+        a.nblocks = 1;
+        a.vec_bytes = c->vec & ~1u;
+        a.accumulate = 1;
+        if ((rc = launch_gf16_matmul(a, nullptr))) return rc;
+    }
+    for (uint32_t i = 0; i < c->m; ++i)
+        NFEC_HIP(hipMemcpy(parity[i], d + (size_t)(out_first + i) * stride, c->vec, hipMemcpyDeviceToHost));
+    return NFEC_OK;
+}
+
+int nfec_decode_vectors(nfec_codec* c, void* const* vectors, uint32_t num_data, uint32_t erasure_count,
+                        const uint32_t* erasure_locs)
+{
+    if (!c || !vectors || (erasure_count && !erasure_locs)) return fail(NFEC_EINVAL, "null argument");
+    if (num_data == 0 || num_data > c->k) return fail(NFEC_EINVAL, "numData out of range");
+    if (erasure_count > c->m) return 0;
+    DeviceGuard g(c->device);
+    const uint32_t stride = round_up(c->vec, 8);
+    const uint32_t nslots = num_data + c->m;
+    uint8_t* d = nullptr;
+    uint16_t* dl = nullptr;
+    {
+        std::lock_guard<std::mutex> lk(c->mu);
+        int rc = c->s_block.reserve((size_t)(c->k + c->m) * stride + 64);
+        if (rc) return rc;
+        rc = c->s_locs.reserve(c->m + 8);
+        if (rc) return rc;
+        d = c->s_block.p;
+        dl = c->s_locs.p;
+    }
+    NFEC_HIP(hipMemset(d, 0, (size_t)nslots * stride));
+    for (uint32_t s = 0; s < nslots; ++s)
+        if (vectors[s]) NFEC_HIP(hipMemcpy(d + (size_t)s * stride, vectors[s], c->vec, hipMemcpyHostToDevice));
+    std::vector<uint16_t> hl(c->m + 4, 0);
+    for (uint32_t i = 0; i < erasure_count; ++i) hl[i] = (uint16_t)erasure_locs[i];
+    hl[c->m] = (uint16_t)erasure_count;
+    hl[c->m + 1] = (uint16_t)num_data;
+    NFEC_HIP(hipMemcpy(dl, hl.data(), hl.size() * 2, hipMemcpyHostToDevice));
+    int32_t* dstatus = nullptr;
+    NFEC_HIP(hipMalloc(reinterpret_cast<void**>(&dstatus), sizeof(int32_t)));
+    nfec_block_batch b{};
+    b.blocks = d;
+    b.block_stride = (uint64_t)(c->k + c->m) * stride;
+    b.seg_stride = stride;
+    b.nblocks = 1;
+    b.num_data = dl + c->m + 1;
+    b.flags = c->kind == NFEC_MDP ? 0 : NFEC_ACCUMULATE;
+    int rc = decode_device(c, &b, dl, c->m, dl + c->m, dstatus, nullptr);
+    int32_t st = 0;
+    if (rc == NFEC_OK) {
+        hipError_t e = hipMemcpy(&st, dstatus, sizeof(st), hipMemcpyDeviceToHost);
+        if (e != hipSuccess) rc = hip_fail(e, "decode status copy");
+    }
+    (void)hipFree(dstatus);
+    if (rc) return rc;
+    if (st > 0) {
+        for (uint32_t i = 0; i < erasure_count; ++i) {
+            const uint32_t s = erasure_locs[i];
+            if (s >= num_data) break;  // parity is never filled (normEncoderRS8.cpp:732)
+            NFEC_HIP(hipMemcpy(vectors[s], d + (size_t)s * stride, c->vec, hipMemcpyDeviceToHost));
+        }
+    }
+    return st;
+}
+
+// ---- host-resident batches: pinned staging, H2D || compute || D2H over two slots ----
+static int run_host_batch(nfec_codec* c, const nfec_block_batch* hb, const uint16_t* locs, uint32_t lstride,
+                      const uint16_t* counts, int32_t* status, bool decode)
+{
+    int rc = check_batch(c, hb);
+    if (rc || hb->nblocks == 0) return rc;
+    DeviceGuard g(c->device);
+    const uint64_t bs = hb->block_stride;
+    const uint32_t chunk = std::max<uint32_t>(1, std::min<uint32_t>(hb->nblocks, (uint32_t)std::max<uint64_t>(1, (64ull << 20) / std::max<uint64_t>(bs, 1))));
+    const uint32_t nslot = 2;
+    struct Slot {
+        uint8_t* dev = nullptr;
+        uint8_t* pin = nullptr;
+        uint16_t* dmeta = nullptr;  // num_data, locs, counts
+        int32_t* dstat = nullptr;
+        hipStream_t st = nullptr;
+        hipEvent_t done = nullptr;
+        uint32_t b0 = 0, nb = 0;
+        bool busy = false;
+    } slots[2];
+    const size_t meta = (size_t)chunk * (1 + lstride + 1);
+    auto cleanup = [&]() {
+        for (auto& s : slots) {
+            if (s.st) (void)hipStreamSynchronize(s.st);
+            if (s.dev) (void)hipFree(s.dev);
+            if (s.pin) (void)hipHostFree(s.pin);
+            if (s.dmeta) (void)hipFree(s.dmeta);
+            if (s.dstat) (void)hipFree(s.dstat);
+            if (s.done) (void)hipEventDestroy(s.done);
+            if (s.st) (void)hipStreamDestroy(s.st);
+        }
+    };
+    for (auto& s : slots) {
+        if (hipMalloc(reinterpret_cast<void**>(&s.dev), (size_t)chunk * bs) != hipSuccess ||
+            hipHostMalloc(reinterpret_cast<void**>(&s.pin), (size_t)chunk * bs, hipHostMallocDefault) != hipSuccess ||
+            hipMalloc(reinterpret_cast<void**>(&s.dmeta), meta * 2 + 16) != hipSuccess ||
+            hipMalloc(reinterpret_cast<void**>(&s.dstat), (size_t)chunk * 4 + 16) != hipSuccess ||
+            hipStreamCreateWithFlags(&s.st, hipStreamNonBlocking) != hipSuccess ||
+            hipEventCreateWithFlags(&s.done, hipEventDisableTiming) != hipSuccess) {
+            cleanup();
+            return fail(NFEC_ENOMEM, "host batch staging allocation failed");
+        }
+    }
+    std::vector<int32_t> hstat(chunk);
+    auto finish = [&](Slot& s) -> int {
+        if (!s.busy) return NFEC_OK;
+        NFEC_HIP(hipEventSynchronize(s.done));
+        std::memcpy(static_cast<uint8_t*>(hb->blocks) + (uint64_t)s.b0 * bs, s.pin, (size_t)s.nb * bs);
+        if (decode && status) {
+            NFEC_HIP(hipMemcpy(hstat.data(), s.dstat, (size_t)s.nb * 4, hipMemcpyDeviceToHost));
+            std::memcpy(status + s.b0, hstat.data(), (size_t)s.nb * 4);
+        }
+        s.busy = false;
+        return NFEC_OK;
+    };
+    uint32_t idx = 0;
+    for (uint32_t b0 = 0; b0 < hb->nblocks; b0 += chunk, ++idx) {
+        Slot& s = slots[idx % nslot];
+        if ((rc = finish(s))) { cleanup(); return rc; }
+        s.b0 = b0;
+        s.nb = std::min(chunk, hb->nblocks - b0);
+        std::memcpy(s.pin, static_cast<const uint8_t*>(hb->blocks) + (uint64_t)b0 * bs, (size_t)s.nb * bs);
+        hipError_t ae = hipMemcpyAsync(s.dev, s.pin, (size_t)s.nb * bs, hipMemcpyHostToDevice, s.st);
+        uint16_t* dnd = nullptr;
+        if (hb->num_data) {
+            dnd = s.dmeta;
+            if (ae == hipSuccess) ae = hipMemcpyAsync(dnd, hb->num_data + b0, (size_t)s.nb * 2, hipMemcpyHostToDevice, s.st);
+        }
+        nfec_block_batch db = *hb;
+        db.blocks = s.dev;
+        db.nblocks = s.nb;
+        db.num_data = dnd;
+        if (decode) {
+            uint16_t* dl = s.dmeta + chunk;
+            uint16_t* dc = dl + (size_t)chunk * lstride;
+            if (ae == hipSuccess) ae = hipMemcpyAsync(dl, locs + (uint64_t)b0 * lstride, (size_t)s.nb * lstride * 2, hipMemcpyHostToDevice, s.st);
+            if (ae == hipSuccess) ae = hipMemcpyAsync(dc, counts + b0, (size_t)s.nb * 2, hipMemcpyHostToDevice, s.st);
+            rc = decode_device(c, &db, dl, lstride, dc, s.dstat, s.st);
+        } else {
+            rc = encode_device(c, &db, s.st);
+        }
+        if (rc) { cleanup(); return rc; }
+        if (ae == hipSuccess) ae = hipMemcpyAsync(s.pin, s.dev, (size_t)s.nb * bs, hipMemcpyDeviceToHost, s.st);
+        if (ae == hipSuccess) ae = hipEventRecord(s.done, s.st);
+        if (ae != hipSuccess) { cleanup(); return hip_fail(ae, "host batch copy"); }
+        s.busy = true;
+    }
+    for (auto& s : slots)
+        if ((rc = finish(s))) { cleanup(); return rc; }
+    hipError_t e = hipGetLastError();
+    cleanup();
+    if (e != hipSuccess) return hip_fail(e, "host batch");
+    return NFEC_OK;
+}
+
+int nfec_encode_host(nfec_codec* codec, const nfec_block_batch* host_batch)
+{
+    return run_host_batch(codec, host_batch, nullptr, 0, nullptr, nullptr, false);
+}
+
+int nfec_decode_host(nfec_codec* codec, const nfec_block_batch* host_batch, const uint16_t* erasure_locs,
+                     uint32_t erasure_stride, const uint16_t* erasure_counts, int32_t* status)
+{
+    if (!erasure_locs || !erasure_counts || erasure_stride == 0) return fail(NFEC_EINVAL, "bad erasure arrays");
+    return run_host_batch(codec, host_batch, erasure_locs, erasure_stride, erasure_counts, status, true);
+}
+
+// ---- synthetic workload utilities ----
+int nfec_util_fill(const nfec_block_batch* b, uint32_t num_data, uint32_t vector_size, uint64_t seed,
+                   uint64_t first_block, void* stream)
+{
+    if (!b || !b->blocks) return fail(NFEC_EINVAL, "null batch");
+    return launch_fill(static_cast<uint8_t*>(b->blocks), b->block_stride, b->seg_stride, b->nblocks, b->num_data,
+                       num_data, vector_size, seed, first_block, static_cast<hipStream_t>(stream));
+}
+
+int nfec_util_erasures(uint16_t* locs, uint32_t stride, uint16_t* counts, uint32_t nblocks, uint32_t range,
+                       uint32_t count, uint64_t seed, uint64_t first_block, void* stream)
+{
+    if (!locs || !counts || stride == 0) return fail(NFEC_EINVAL, "bad erasure arrays");
+    return launch_erasures(locs, stride, counts, nblocks, range, count, seed, first_block,
+                           static_cast<hipStream_t>(stream));
+}
+
+int nfec_util_zero_slots(const nfec_block_batch* b, const uint16_t* locs, uint32_t stride, const uint16_t* counts,
+                         uint32_t vector_size, void* stream)
+{
+    if (!b || !b->blocks || !locs || !counts) return fail(NFEC_EINVAL, "null argument");
+    return launch_zero_slots(static_cast<uint8_t*>(b->blocks), b->block_stride, b->seg_stride, b->nblocks, locs,
+                             stride, counts, vector_size, static_cast<hipStream_t>(stream));
+}
+
+}  // extern "C"

@@ -1,0 +1,183 @@
+// nfec_internal.hpp -- shared declarations of the MI355X FEC engine (not part of the ABI).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstddef>
+#include <cstdint>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/nfec.h"
+
+namespace nfec {
+
+// ---------------------------------------------------------------------------------
+// Error plumbing: the ABI never throws; failures set a thread-local message.
+// ---------------------------------------------------------------------------------
+void set_error(const std::string& msg);
+int fail(int code, const std::string& msg);
+int hip_fail(hipError_t e, const char* what);
+
+#define NFEC_HIP(call)                                    \
+    do {                                                  \
+        hipError_t e_ = (call);                           \
+        if (e_ != hipSuccess) return ::nfec::hip_fail(e_, #call); \
+    } while (0)
+
+// ---------------------------------------------------------------------------------
+// Host field arithmetic (gf_host.cpp).  GF(2^8) on 0x11d and GF(2^16) on 0x1100B with
+// alpha = x, exactly the fields of normEncoderRS8.cpp:81 / normEncoderRS16.cpp:88.
+// ---------------------------------------------------------------------------------
+struct Field {
+    int bits = 0;
+    uint32_t q = 0;                 // 2^bits - 1
+    std::vector<uint32_t> exp;      // 2q entries (exp[i] = alpha^(i mod q))
+    std::vector<uint32_t> log;      // q+1 entries, log[0] = q
+    uint32_t mul(uint32_t a, uint32_t b) const { return (a && b) ? exp[log[a] + log[b]] : 0; }
+    uint32_t inv(uint32_t a) const { return a <= 1 ? a : exp[q - log[a]]; }
+    uint32_t div(uint32_t a, uint32_t b) const { return a ? exp[log[a] + q - log[b]] : 0; }
+};
+const Field& gf8();
+const Field& gf16();
+
+// Systematic generator parity rows (m x k, row-major) of the reference's Rizzo code, built
+// in closed (Lagrange) form; identical to Vandermonde-invert-and-multiply because the
+// systematic matrix is unique for the reference's evaluation points.
+int rs_generator(int bits, uint32_t k, uint32_t m, std::vector<uint32_t>& parity_rows);
+// Evaluation point of generator row r (0 -> 0, r >= 1 -> alpha^(r-1)).
+inline uint32_t rs_point(const Field& f, uint32_t row) { return row == 0 ? 0u : f.exp[(row - 1) % f.q]; }
+
+// MDP: generator polynomial (normEncoderMDP.cpp:102-170) and the linear map of the
+// in-order LFSR encoder for a block of nd source symbols (m x nd, row-major).
+void mdp_generator_poly(uint32_t m, std::vector<uint8_t>& g);
+void mdp_encode_matrix(const std::vector<uint8_t>& g, uint32_t m, uint32_t nd, uint8_t* out);
+
+// v_perm product tables for one GF(2^8) constant c: 8 dwords (32 bytes)
+//   t0 = c*{0,1,2,3}   t1 = c*{4,5,6,7}       (low 3 bits)
+//   t2 = c*{0,8,16,24} t3 = c*{32,40,48,56}   (middle 3 bits)
+//   t4 = c*{0,64,128,192}                     (top 2 bits), t5..t7 = 0
+void vperm_table(uint32_t c, uint32_t out[8]);
+
+// ---------------------------------------------------------------------------------
+// Device kernels (launchers live next to the kernels).
+// ---------------------------------------------------------------------------------
+enum OutSlotMode : uint32_t {
+    OUT_SLOT_LIST = 0,      // slot = out_slots[b][r]
+    OUT_SLOT_AFTER_INPUT = 1,// slot = in_count(b) + r   (parity after the block's numData sources)
+    OUT_SLOT_ROW = 2        // slot = r
+};
+
+// Generic batched GF(2^8) matrix product over segment vectors:
+//   out[b][slot_out(r)] (^)= sum_c coef[b][c][r] * in[b][slot_in(c)]   for r < rows(b), c < cols(b)
+struct Gf8MatmulArgs {
+    const uint8_t* in_base = nullptr;
+    uint64_t in_block_stride = 0;
+    uint32_t in_seg_stride = 0;
+    const uint16_t* in_slots = nullptr;  // [b*slots_stride + c] or null (identity)
+    const uint16_t* in_count = nullptr;  // per block column count or null (cols_const)
+    uint32_t cols_const = 0;
+    uint8_t* out_base = nullptr;
+    uint64_t out_block_stride = 0;
+    uint32_t out_seg_stride = 0;
+    const uint16_t* out_slots = nullptr; // [b*slots_stride + r]
+    uint32_t out_slot_mode = OUT_SLOT_AFTER_INPUT;
+    const int32_t* row_count = nullptr;  // per block rows (<=0: skip block) or null (rows_const)
+    uint32_t rows_const = 0;
+    uint32_t slots_stride = 0;
+    const uint8_t* coef = nullptr;       // coef[b*coef_block_stride + c*coef_col_stride + r]
+    uint64_t coef_block_stride = 0;
+    uint32_t coef_col_stride = 0;
+    const uint32_t* vtab = nullptr;      // 256 x 8 dword v_perm tables (device)
+    uint32_t coef_by_count = 0;          // coef block = coef + (cols(b)-1)*coef_block_stride (MDP encode)
+    uint32_t nblocks = 0;
+    uint32_t vec_bytes = 0;
+    uint32_t accumulate = 0;
+};
+int launch_gf8_matmul(const Gf8MatmulArgs& a, bool shared_coef, hipStream_t s);
+
+// GF(2^16) variant (log/exp); coef holds generator elements (uint16) at the same indexing.
+struct Gf16MatmulArgs {
+    const uint8_t* in_base = nullptr;
+    uint64_t in_block_stride = 0;
+    uint32_t in_seg_stride = 0;
+    const uint16_t* in_slots = nullptr;
+    const uint16_t* in_count = nullptr;
+    uint32_t cols_const = 0;
+    uint8_t* out_base = nullptr;
+    uint64_t out_block_stride = 0;
+    uint32_t out_seg_stride = 0;
+    const uint16_t* out_slots = nullptr;
+    uint32_t out_slot_mode = OUT_SLOT_AFTER_INPUT;
+    const int32_t* row_count = nullptr;
+    uint32_t rows_const = 0;
+    uint32_t slots_stride = 0;
+    const uint16_t* coef = nullptr;      // element values (0 allowed)
+    uint32_t coef_by_count = 0;
+    uint64_t coef_block_stride = 0;
+    uint32_t coef_col_stride = 0;
+    const uint16_t* exp_tab = nullptr;   // device exp table, 2q entries
+    const uint16_t* log_tab = nullptr;   // device log table, q+1 entries (log 0 = q)
+    uint32_t nblocks = 0;
+    uint32_t vec_bytes = 0;              // even number of bytes processed
+    uint32_t accumulate = 0;
+};
+int launch_gf16_matmul(const Gf16MatmulArgs& a, hipStream_t s);
+
+// RS decode planning (per block): pick parities, invert the e x e system, emit the
+// stage-1 (gather) and stage-2 (inverse) matrices and slot lists.
+struct RsPlanArgs {
+    int bits = 8;
+    uint32_t k = 0, m = 0;
+    uint32_t nblocks = 0;
+    const uint16_t* num_data = nullptr;      // per block or null (k)
+    const uint16_t* erasure_locs = nullptr;
+    uint32_t erasure_stride = 0;
+    const uint16_t* erasure_counts = nullptr;
+    const void* gen_parity = nullptr;        // device m x k generator parity rows (elements)
+    const void* exp_tab = nullptr;           // device exp (2q) table of the field (elements)
+    const uint16_t* log_tab = nullptr;       // device log table (q+1 entries)
+    // outputs
+    int32_t* status = nullptr;               // per block decode return value
+    int32_t* rows = nullptr;                 // per block source-erasure count e_s (0: nothing to do)
+    uint16_t* in_slots1 = nullptr;           // [b][k]   stage-1 input slots
+    uint16_t* out_slots2 = nullptr;          // [b][k]   stage-2 output slots (erased source)
+    uint16_t* cols2 = nullptr;               // per block stage-2 column count (= e_s)
+    uint32_t coef_stride = 0;                // padded row count of coef1/coef2 (multiple of 16)
+    void* coef1 = nullptr;                   // [b][k][cs] gathered generator / unit columns
+    void* coef2 = nullptr;                   // [b][cs][cs] inverse (column-major: [t][s])
+    void* work = nullptr;                    // [b][m][2m] scratch
+};
+int launch_rs_plan(const RsPlanArgs& a, hipStream_t s);
+
+// MDP decode planning: per block one-stage coefficient matrix over the surviving slots.
+struct MdpPlanArgs {
+    uint32_t k = 0, m = 0, nblocks = 0;
+    const uint16_t* num_data = nullptr;
+    const uint16_t* erasure_locs = nullptr;
+    uint32_t erasure_stride = 0;
+    const uint16_t* erasure_counts = nullptr;
+    const uint8_t* exp_tab = nullptr;        // 510-entry GF(2^8) exp table (device)
+    const uint16_t* log_tab = nullptr;       // 256-entry log table (device)
+    int32_t* status = nullptr;
+    int32_t* rows = nullptr;
+    uint16_t* cols = nullptr;                // number of surviving input slots
+    uint16_t* in_slots = nullptr;            // [b][k+m]
+    uint16_t* out_slots = nullptr;           // [b][k+m]
+    uint32_t coef_stride = 0;                // padded row count (multiple of 16)
+    uint8_t* coef = nullptr;                 // [b][k+m][cs]
+};
+int launch_mdp_plan(const MdpPlanArgs& a, hipStream_t s);
+
+// utilities
+int launch_fill(uint8_t* base, uint64_t block_stride, uint32_t seg_stride, uint32_t nblocks,
+                const uint16_t* num_data, uint32_t k, uint32_t vec, uint64_t seed, uint64_t first_block,
+                hipStream_t s);
+int launch_erasures(uint16_t* locs, uint32_t stride, uint16_t* counts, uint32_t nblocks, uint32_t range,
+                    uint32_t count, uint64_t seed, uint64_t first_block, hipStream_t s);
+int launch_zero_slots(uint8_t* base, uint64_t block_stride, uint32_t seg_stride, uint32_t nblocks,
+                      const uint16_t* locs, uint32_t stride, const uint16_t* counts, uint32_t vec,
+                      hipStream_t s);
+
+}  // namespace nfec

@@ -1,0 +1,88 @@
+// norm_codecs.cpp -- NormEncoder/NormDecoder drop-in classes over the nfec C ABI.
+#include "../../include/norm_fec/nfecCodecs.h"
+
+#include <cstdio>
+
+NormEncoder::~NormEncoder() {}
+NormDecoder::~NormDecoder() {}
+
+int NfecCodecBase::default_device = 0;
+
+bool NfecCodecBase::InitCodec(int kind, unsigned int numData, unsigned int numParity, UINT16 vectorSize)
+{
+    DestroyCodec();
+    nfec_codec* c = 0;
+    int rc = nfec_codec_create(default_device, kind, numData, numParity, vectorSize, &c);
+    if (rc != NFEC_OK) {
+        // the reference logs PL_FATAL and returns false (normEncoderRS8.cpp:405-409)
+        std::fprintf(stderr, "nfec: Init(%u, %u, %u) failed: %s\n", numData, numParity, (unsigned)vectorSize,
+                     nfec_last_error());
+        return false;
+    }
+    codec = c;
+    ndata = numData;
+    npar = numParity;
+    vector_size = vectorSize;
+    return true;
+}
+
+void NfecCodecBase::DestroyCodec()
+{
+    if (codec) nfec_codec_destroy(codec);
+    codec = 0;
+}
+
+int NfecCodecBase::EncodeBlocks(const nfec_block_batch* batch, void* stream)
+{
+    return codec ? nfec_encode(codec, batch, stream) : NFEC_EINVAL;
+}
+
+int NfecCodecBase::DecodeBlocks(const nfec_block_batch* batch, const uint16_t* erasureLocs, uint32_t erasureStride,
+                                const uint16_t* erasureCounts, int32_t* status, void* stream)
+{
+    return codec ? nfec_decode(codec, batch, erasureLocs, erasureStride, erasureCounts, status, stream)
+                 : NFEC_EINVAL;
+}
+
+#define NFEC_DEFINE_ENCODER(NAME, KIND)                                                          \
+    NAME::NAME() {}                                                                              \
+    NAME::~NAME() { DestroyCodec(); }                                                            \
+    bool NAME::Init(unsigned int numData, unsigned int numParity, UINT16 vectorSize)             \
+    {                                                                                            \
+        return InitCodec(KIND, numData, numParity, vectorSize);                                  \
+    }                                                                                            \
+    void NAME::Destroy() { DestroyCodec(); }                                                     \
+    void NAME::Encode(unsigned int segmentId, const char* dataVector, char** parityVectorList)   \
+    {                                                                                            \
+        if (!codec) return;                                                                      \
+        int rc = nfec_encode_segment(codec, segmentId, dataVector, (void* const*)parityVectorList); \
+        if (rc != NFEC_OK) std::fprintf(stderr, "nfec: Encode failed: %s\n", nfec_last_error()); \
+    }
+
+#define NFEC_DEFINE_DECODER(NAME, KIND)                                                          \
+    NAME::NAME() {}                                                                              \
+    NAME::~NAME() { DestroyCodec(); }                                                            \
+    bool NAME::Init(unsigned int numData, unsigned int numParity, UINT16 vectorSize)             \
+    {                                                                                            \
+        return InitCodec(KIND, numData, numParity, vectorSize);                                  \
+    }                                                                                            \
+    void NAME::Destroy() { DestroyCodec(); }                                                     \
+    int NAME::Decode(char** vectorList, unsigned int numData, unsigned int erasureCount,         \
+                     unsigned int* erasureLocs)                                                  \
+    {                                                                                            \
+        if (!codec) return 0;                                                                    \
+        int rc = nfec_decode_vectors(codec, (void* const*)vectorList, numData, erasureCount,     \
+                                     (const uint32_t*)erasureLocs);                              \
+        if (rc < 0) {                                                                            \
+            std::fprintf(stderr, "nfec: Decode failed: %s\n", nfec_last_error());                \
+            return 0;                                                                            \
+        }                                                                                        \
+        return rc;                                                                               \
+    }
+
+NFEC_DEFINE_ENCODER(NormEncoderRS8, NFEC_RS8)
+NFEC_DEFINE_DECODER(NormDecoderRS8, NFEC_RS8)
+NFEC_DEFINE_ENCODER(NormEncoderRS16, NFEC_RS16)
+NFEC_DEFINE_DECODER(NormDecoderRS16, NFEC_RS16)
+NFEC_DEFINE_ENCODER(NormEncoderMDP, NFEC_MDP)
+NFEC_DEFINE_DECODER(NormDecoderMDP, NFEC_MDP)

@@ -1,0 +1,286 @@
+"""Parity of the HIP path (through the C ABI) against the oracle, on the GPU.
+
+Bar: bit-exact for every byte of every block (parity slots, repaired source slots, and
+the untouched bytes), same per-block Decode return values as the reference algorithm.
+Small cases are checked byte-for-byte against the oracle; the BASELINE full size is
+checked by the encode -> erase -> decode round trip plus sampled blocks against the oracle.
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+from norm_amd import (NFEC_RS8, NFEC_RS16, NFEC_MDP, NormDecoderMDP, NormDecoderRS8, NormDecoderRS16,  # noqa: E402
+                      NormEncoderMDP, NormEncoderRS8, NormEncoderRS16, fill_blocks, make_erasures, zero_erasures)
+
+ENC = {NFEC_RS8: NormEncoderRS8, NFEC_RS16: NormEncoderRS16, NFEC_MDP: NormEncoderMDP}
+DEC = {NFEC_RS8: NormDecoderRS8, NFEC_RS16: NormDecoderRS16, NFEC_MDP: NormDecoderMDP}
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu():
+    from norm_amd import device_count
+
+    assert torch.cuda.is_available(), "GPU tests need a HIP device"
+    assert device_count() >= 1, "no gfx950 device visible to libnfec"
+
+
+def _codecs(kind, k, m, vec):
+    e, d = ENC[kind](), DEC[kind]()
+    assert e.Init(k, m, vec) and d.Init(k, m, vec)
+    return e, d
+
+
+def _erasures(orc, kind, k, m, nblocks, n_src, n_par, num_data=None, seed_off=0):
+    locs = np.zeros((nblocks, m), np.uint16)
+    counts = np.zeros(nblocks, np.uint16)
+    for b in range(nblocks):
+        nd = k if num_data is None else int(num_data[b])
+        src = orc.erasure_pattern(b + seed_off, nd, min(n_src, nd))
+        par = (nd + orc.erasure_pattern(b + 9000 + seed_off, m, n_par)).astype(np.uint16)
+        allp = np.concatenate([src, par])[:m]
+        counts[b] = len(allp)
+        locs[b, : len(allp)] = allp
+    return locs, counts
+
+
+def _erase(blocks, locs, counts):
+    for b in range(blocks.shape[0]):
+        for s in locs[b, : counts[b]]:
+            blocks[b, s, :] = 0
+
+
+ENC_CASES = [
+    # kind, k, m, vec, seg_stride, nblocks
+    (NFEC_RS8, 64, 32, 1400, 1400, 37),
+    (NFEC_RS8, 64, 32, 1400, 1408, 5),
+    (NFEC_RS8, 64, 16, 1400, 1400, 9),
+    (NFEC_RS8, 1, 1, 17, 24, 3),
+    (NFEC_RS8, 16, 4, 64, 64, 11),
+    (NFEC_RS8, 200, 55, 100, 104, 3),
+    (NFEC_RS8, 128, 127, 64, 64, 2),
+    (NFEC_RS8, 8, 40, 1401, 1408, 3),
+    (NFEC_RS8, 64, 32, 8, 8, 300),
+    (NFEC_RS16, 40, 10, 65, 72, 3),
+    (NFEC_RS16, 400, 100, 64, 64, 2),
+    (NFEC_RS16, 100, 20, 1400, 1400, 3),
+    (NFEC_MDP, 64, 32, 1400, 1400, 4),
+    (NFEC_MDP, 16, 4, 33, 40, 5),
+]
+
+
+@pytest.mark.parametrize("kind,k,m,vec,stride,nb", ENC_CASES)
+def test_encode_matches_oracle(orc, kind, k, m, vec, stride, nb):
+    enc, _ = _codecs(kind, k, m, vec)
+    host = orc.make_blocks(k, m, vec, nb, seg_stride=stride)
+    ref = orc.encode_blocks(kind, k, m, vec, host.copy())
+    dev = torch.from_numpy(host).cuda()
+    enc.encode_blocks(dev)
+    torch.cuda.synchronize()
+    assert np.array_equal(dev.cpu().numpy(), ref)
+
+
+@pytest.mark.parametrize("kind", [NFEC_RS8, NFEC_RS16, NFEC_MDP])
+def test_encode_shortened_blocks(orc, kind):
+    k, m, vec, nb = 64, 16, 200, 7
+    nd = np.array([64, 40, 1, 63, 17, 64, 2], np.uint16)
+    enc, _ = _codecs(kind, k, m, vec)
+    host = orc.make_blocks(k, m, vec, nb, num_data=nd)
+    ref = orc.encode_blocks(kind, k, m, vec, host.copy(), nd)
+    dev = torch.from_numpy(host).cuda()
+    enc.encode_blocks(dev, num_data=torch.from_numpy(nd.astype(np.int16)).cuda())
+    torch.cuda.synchronize()
+    assert np.array_equal(dev.cpu().numpy(), ref)
+
+
+@pytest.mark.parametrize("kind", [NFEC_RS8, NFEC_RS16])
+def test_encode_accumulates_like_reference(orc, kind):
+    """Encode XORs into the parity buffers (reference contract: caller zeroes them)."""
+    k, m, vec, nb = 32, 8, 96, 4
+    enc, _ = _codecs(kind, k, m, vec)
+    host = orc.make_blocks(k, m, vec, nb)
+    junk = np.random.default_rng(1).integers(0, 256, (nb, m, vec), dtype=np.uint8)
+    ref = orc.encode_blocks(kind, k, m, vec, host.copy())
+    host[:, k:, :] = junk
+    expect = ref.copy()
+    nbytes = vec if kind == NFEC_RS8 else vec // 2 * 2
+    expect[:, k:, :nbytes] ^= junk[:, :, :nbytes]
+    expect[:, k:, nbytes:] = junk[:, :, nbytes:]
+    dev = torch.from_numpy(host).cuda()
+    enc.encode_blocks(dev, accumulate=True)
+    torch.cuda.synchronize()
+    assert np.array_equal(dev.cpu().numpy(), expect)
+
+
+DEC_CASES = [
+    # kind, k, m, vec, nblocks, source erasures, parity erasures
+    (NFEC_RS8, 64, 32, 1400, 23, 16, 0),
+    (NFEC_RS8, 64, 32, 1400, 9, 32, 0),
+    (NFEC_RS8, 64, 32, 1400, 9, 20, 12),
+    (NFEC_RS8, 64, 32, 1400, 5, 0, 7),
+    (NFEC_RS8, 16, 4, 64, 13, 3, 1),
+    (NFEC_RS8, 1, 1, 24, 4, 1, 0),
+    (NFEC_RS8, 128, 127, 64, 2, 100, 27),
+    (NFEC_RS8, 200, 55, 100, 3, 40, 10),
+    (NFEC_RS16, 40, 10, 65, 3, 7, 3),
+    (NFEC_RS16, 400, 100, 64, 2, 2, 0),
+    (NFEC_RS16, 400, 100, 64, 1, 90, 10),
+    (NFEC_MDP, 64, 32, 1400, 4, 16, 0),
+    (NFEC_MDP, 64, 32, 200, 4, 20, 12),
+    (NFEC_MDP, 16, 4, 33, 6, 2, 2),
+]
+
+
+@pytest.mark.parametrize("kind,k,m,vec,nb,es,ep", DEC_CASES)
+def test_decode_matches_oracle(orc, kind, k, m, vec, nb, es, ep):
+    enc, dec = _codecs(kind, k, m, vec)
+    host = orc.encode_blocks(kind, k, m, vec, orc.make_blocks(k, m, vec, nb))
+    locs, counts = _erasures(orc, kind, k, m, nb, es, ep)
+    _erase(host, locs, counts)
+    ref = host.copy()
+    st_ref = orc.decode_blocks(kind, k, m, vec, ref, locs, counts)
+    dev = torch.from_numpy(host).cuda()
+    st = dec.decode_blocks(dev, torch.from_numpy(locs.astype(np.int16)).cuda(),
+                           torch.from_numpy(counts.astype(np.int16)).cuda())
+    torch.cuda.synchronize()
+    assert np.array_equal(st.cpu().numpy(), st_ref)
+    assert np.array_equal(dev.cpu().numpy(), ref)
+
+
+@pytest.mark.parametrize("kind", [NFEC_RS8, NFEC_RS16, NFEC_MDP])
+def test_decode_shortened_blocks(orc, kind):
+    k, m, vec, nb = 64, 16, 120, 6
+    nd = np.array([40, 64, 1, 17, 63, 5], np.uint16)
+    enc, dec = _codecs(kind, k, m, vec)
+    host = orc.encode_blocks(kind, k, m, vec, orc.make_blocks(k, m, vec, nb, num_data=nd), nd)
+    locs, counts = _erasures(orc, kind, k, m, nb, 12, 3, num_data=nd)
+    _erase(host, locs, counts)
+    ref = host.copy()
+    st_ref = orc.decode_blocks(kind, k, m, vec, ref, locs, counts, nd)
+    dev = torch.from_numpy(host).cuda()
+    st = dec.decode_blocks(dev, torch.from_numpy(locs.astype(np.int16)).cuda(),
+                           torch.from_numpy(counts.astype(np.int16)).cuda(),
+                           num_data=torch.from_numpy(nd.astype(np.int16)).cuda())
+    torch.cuda.synchronize()
+    assert np.array_equal(st.cpu().numpy(), st_ref)
+    assert np.array_equal(dev.cpu().numpy(), ref)
+
+
+@pytest.mark.parametrize("kind", [NFEC_RS8, NFEC_RS16])
+def test_decode_accumulates_into_nonzero_erased_buffers(orc, kind):
+    """Reference Decode XORs the repair into the erased buffer; with a non-zeroed buffer
+    the output is junk ^ data, and the accumulate flag reproduces it byte for byte."""
+    k, m, vec, nb = 32, 8, 96, 3
+    enc, dec = _codecs(kind, k, m, vec)
+    host = orc.encode_blocks(kind, k, m, vec, orc.make_blocks(k, m, vec, nb))
+    locs, counts = _erasures(orc, kind, k, m, nb, 6, 1)
+    rng = np.random.default_rng(7)
+    for b in range(nb):
+        for s in locs[b, : counts[b]]:
+            host[b, s, :] = rng.integers(0, 256, vec, dtype=np.uint8)
+    ref = host.copy()
+    orc.decode_blocks(kind, k, m, vec, ref, locs, counts)
+    dev = torch.from_numpy(host).cuda()
+    dec.decode_blocks(dev, torch.from_numpy(locs.astype(np.int16)).cuda(),
+                      torch.from_numpy(counts.astype(np.int16)).cuda(), accumulate=True)
+    torch.cuda.synchronize()
+    assert np.array_equal(dev.cpu().numpy(), ref)
+
+
+def test_decode_rejects_undecodable_blocks(orc):
+    """More erasures than parity, unsorted or out-of-range lists: status 0, block untouched."""
+    k, m, vec = 16, 4, 64
+    enc, dec = _codecs(NFEC_RS8, k, m, vec)
+    host = orc.encode_blocks(NFEC_RS8, k, m, vec, orc.make_blocks(k, m, vec, 4))
+    locs = np.zeros((4, 8), np.uint16)
+    counts = np.array([5, 2, 2, 4], np.uint16)
+    locs[0, :5] = [0, 1, 2, 3, 4]          # 5 erasures > 4 parity
+    locs[1, :2] = [5, 3]                   # unsorted
+    locs[2, :2] = [1, 30]                  # out of range slot
+    locs[3, :4] = [0, 1, 16, 17]           # 2 source + 2 parity lost: decodable
+    before = host.copy()
+    dev = torch.from_numpy(host).cuda()
+    st = dec.decode_blocks(dev, torch.from_numpy(locs.astype(np.int16)).cuda(),
+                           torch.from_numpy(counts.astype(np.int16)).cuda())
+    torch.cuda.synchronize()
+    st = st.cpu().numpy()
+    assert list(st[:3]) == [0, 0, 0] and st[3] == 4
+    out = dev.cpu().numpy()
+    assert np.array_equal(out[:3], before[:3])
+    assert np.array_equal(out[3], before[3])  # nothing was erased, the repair rewrites the same bytes
+
+
+@pytest.mark.parametrize("kind", [NFEC_RS8, NFEC_RS16, NFEC_MDP])
+def test_per_call_reference_surface(orc, kind):
+    """Encode()/Decode() with scattered host vectors, exactly as fecTest drives them."""
+    k, m, vec = 20, 6, 64
+    enc, dec = _codecs(kind, k, m, vec)
+    blk = orc.make_blocks(k, m, vec, 1)[0]
+    ref = orc.encode_blocks(kind, k, m, vec, blk[None].copy())[0]
+    data = [bytearray(blk[s].tobytes()) for s in range(k)]
+    parity = [bytearray(vec) for _ in range(m)]
+    for s in range(k):
+        enc.Encode(s, bytes(data[s]), parity)
+    assert all(bytes(parity[i]) == ref[k + i].tobytes() for i in range(m))
+    vecs = [bytearray(ref[s].tobytes()) for s in range(k + m)]
+    erased = [1, 5, 6, k + 2]
+    for s in erased:
+        vecs[s] = bytearray(vec)
+    vlist = list(vecs)
+    vlist[k + 2] = None  # missing parity passed as NULL like NormObject
+    assert dec.Decode(vlist, k, len(erased), erased) == len(erased)
+    for s in range(k):
+        assert bytes(vlist[s]) == ref[s].tobytes()
+
+
+def test_host_batch_paths_match_device(orc):
+    k, m, vec, nb = 64, 32, 1400, 40
+    enc, dec = _codecs(NFEC_RS8, k, m, vec)
+    host = orc.make_blocks(k, m, vec, nb)
+    ref = orc.encode_blocks(NFEC_RS8, k, m, vec, host.copy())
+    enc.encode_blocks_host(host)
+    assert np.array_equal(host, ref)
+    locs, counts = _erasures(orc, NFEC_RS8, k, m, nb, 16, 2)
+    _erase(host, locs, counts)
+    st = dec.decode_blocks_host(host, locs, counts)
+    assert np.all(st == counts)
+    assert np.array_equal(host[:, :k], ref[:, :k])
+
+
+def test_device_workload_generators_match_oracle(orc):
+    k, m, vec, nb = 64, 32, 1400, 9
+    dev = torch.zeros((nb, k + m, 1400), dtype=torch.uint8, device="cuda")
+    fill_blocks(dev, k, vec, orc.SEED, first_block=100)
+    locs, counts = make_erasures(nb, k, 16, orc.SEED, m, first_block=100)
+    torch.cuda.synchronize()
+    host = orc.make_blocks(k, m, vec, nb, first_block=100)
+    assert np.array_equal(dev.cpu().numpy(), host)
+    for b in range(nb):
+        assert counts[b].item() == 16
+        assert np.array_equal(locs[b, :16].cpu().numpy().astype(np.uint16), orc.erasure_pattern(100 + b, k, 16))
+
+
+def test_full_size_roundtrip_c2_c3(orc):
+    """BASELINE C2/C3 at full size: 65,536 blocks of RS8(64,32) x 1400 B in HBM.
+    Size-independent properties: erase 16 random source symbols per block, decode, and every
+    byte of every block must equal the pre-erasure bytes; sampled blocks' parity must equal
+    the oracle's."""
+    k, m, vec, nb = 64, 32, 1400, 65536
+    enc, dec = _codecs(NFEC_RS8, k, m, vec)
+    blocks = torch.zeros((nb, k + m, vec), dtype=torch.uint8, device="cuda")
+    fill_blocks(blocks, k, vec, orc.SEED)
+    enc.encode_blocks(blocks)
+    torch.cuda.synchronize()
+    for b in (0, 1, 4097, 65535):
+        ref = orc.encode_blocks(NFEC_RS8, k, m, vec, orc.make_blocks(k, m, vec, 1, first_block=b))
+        assert np.array_equal(blocks[b].cpu().numpy(), ref[0])
+    keep = blocks.clone()
+    locs, counts = make_erasures(nb, k, 16, orc.SEED, m)
+    zero_erasures(blocks, locs, counts, vec)
+    assert not torch.equal(blocks, keep)
+    st = dec.decode_blocks(blocks, locs, counts)
+    torch.cuda.synchronize()
+    assert bool((st == 16).all())
+    assert torch.equal(blocks, keep)
