@@ -1,0 +1,133 @@
+// bitslice.hpp -- device helpers for the bit-sliced GF(2^8) kernels (generated code).
+//
+// A lane owns 32 byte positions of a segment (4 items of 8 bytes, each item index
+// = item_base + i*64 + lane so every wave-wide load is one contiguous 512-byte run).
+// The 32 bytes are held as 8 dwords w[0..7] and transposed into 8 bit-planes X[0..7]
+// (per byte column q: an 8x8 bit transpose of the bytes of the 8 dwords), so that plane
+// X_b bit (8q+d) = bit b of byte q of dword d.  Multiplying every byte by a constant c is
+// then the GF(2) 8x8 matrix of c applied to the planes (XORs only); the transpose is an
+// involution, so the same network maps parity planes back to bytes.
+#pragma once
+
+#include "nfec_internal.hpp"
+
+namespace nfec {
+namespace bs {
+
+__device__ __forceinline__ uint32_t x3(uint32_t a, uint32_t b, uint32_t c)
+{
+    return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+}
+
+// accumulator XOR as an opaque op: keeps LLVM's reassociation from regrouping the long
+// per-accumulator XOR chains across source columns (that blows up register pressure)
+__device__ __forceinline__ uint32_t x2(uint32_t a, uint32_t b)
+{
+    uint32_t r;
+    asm("v_xor_b32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+
+// bit-select: (m & a) | (~m & b)
+__device__ __forceinline__ uint32_t sel(uint32_t m, uint32_t a, uint32_t b)
+{
+    return __builtin_amdgcn_bitop3_b32(m, a, b, 0xca);
+}
+
+// swap M[r][c+s] <-> M[r+s][c] for the bit columns selected by mask (per byte)
+template <int S, uint32_t MASK>
+__device__ __forceinline__ void swapmove(uint32_t& lo, uint32_t& hi)
+{
+    const uint32_t u = lo >> S;   // lo's high columns moved down
+    const uint32_t v = hi << S;   // hi's low columns moved up
+    hi = sel(MASK, u, hi);
+    lo = sel(MASK << S, v, lo);
+}
+
+// 8x8 bit transpose in each of the 4 byte columns of w[0..7] (involution).
+__device__ __forceinline__ void transpose8(uint32_t& w0, uint32_t& w1, uint32_t& w2, uint32_t& w3, uint32_t& w4,
+                                           uint32_t& w5, uint32_t& w6, uint32_t& w7)
+{
+    swapmove<4, 0x0F0F0F0Fu>(w0, w4);
+    swapmove<4, 0x0F0F0F0Fu>(w1, w5);
+    swapmove<4, 0x0F0F0F0Fu>(w2, w6);
+    swapmove<4, 0x0F0F0F0Fu>(w3, w7);
+    swapmove<2, 0x33333333u>(w0, w2);
+    swapmove<2, 0x33333333u>(w1, w3);
+    swapmove<2, 0x33333333u>(w4, w6);
+    swapmove<2, 0x33333333u>(w5, w7);
+    swapmove<1, 0x55555555u>(w0, w1);
+    swapmove<1, 0x55555555u>(w2, w3);
+    swapmove<1, 0x55555555u>(w4, w5);
+    swapmove<1, 0x55555555u>(w6, w7);
+}
+
+struct EncArgs {
+    const uint8_t* base = nullptr;   // block 0 slot 0
+    uint8_t* out = nullptr;          // parity destination base (== base for in-place encode)
+    uint64_t block_stride = 0;
+    uint32_t seg_stride = 0;
+    uint32_t nblocks = 0;
+    uint32_t vec = 0;
+    const uint16_t* num_data = nullptr;  // per block (null: k)
+    uint32_t accumulate = 0;
+};
+
+// per-lane item geometry for the 4 items of a lane (all blocks hold k source symbols; the
+// bit-sliced kernels are only used for unshortened batches).  Addresses are a wave-uniform
+// base (the first block the wave touches) plus 32-bit per-lane offsets, so every load is a
+// global_load with an SGPR base: no 64-bit per-lane pointer arithmetic per column.
+struct Items {
+    const uint8_t* wbase;   // uniform: slot 0 of the wave's first block
+    uint8_t* obase;         // uniform: same block in the output batch
+    uint32_t off[4];        // per lane: byte offset of item i (clamped to a valid item)
+    uint32_t nbytes[4];     // valid bytes in the item (0 if out of range, <8 for the tail)
+};
+
+__device__ __forceinline__ void make_items(const EncArgs& a, uint32_t item_base, uint32_t lane, Items& it)
+{
+    const uint32_t ips = (a.vec + 7) >> 3;
+    const uint32_t total = a.nblocks * ips;  // launcher guarantees < 2^31
+    const uint32_t b0 = __builtin_amdgcn_readfirstlane(min(item_base, total - 1) / ips);
+    it.wbase = a.base + (uint64_t)b0 * a.block_stride;
+    it.obase = a.out + (uint64_t)b0 * a.block_stride;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const uint32_t g = item_base + (uint32_t)i * 64u + lane;
+        const bool ok = g < total;
+        const uint32_t gg = ok ? g : item_base;
+        const uint32_t b = gg / ips;
+        const uint32_t o = gg - b * ips;
+        it.off[i] = (uint32_t)((b - b0) * a.block_stride) + o * 8u;
+        it.nbytes[i] = ok ? min(8u, a.vec - o * 8u) : 0u;
+    }
+}
+
+__device__ __forceinline__ uint2 ld8(const uint8_t* base, uint32_t off)
+{
+    return *reinterpret_cast<const uint2*>(base + off);
+}
+
+__device__ __forceinline__ void st8(uint8_t* p, uint32_t x, uint32_t y, uint32_t nbytes, uint32_t accumulate)
+{
+    if (nbytes == 0) return;
+    if (accumulate) {
+        const uint2 o = *reinterpret_cast<const uint2*>(p);
+        x ^= o.x;
+        y ^= o.y;
+    }
+    if (nbytes >= 8) {
+        *reinterpret_cast<uint2*>(p) = make_uint2(x, y);
+    } else {
+        for (uint32_t i = 0; i < nbytes; ++i) p[i] = (uint8_t)((i < 4 ? x : y) >> (8 * (i & 3)));
+    }
+}
+
+}  // namespace bs
+
+// generated (gen_rs8_bitsliced.hip): NFEC_ENOTSUP when (k, m) has no specialised kernel or
+// the batch is shortened (per-block numData)
+int launch_rs8_bitsliced_encode(uint32_t k, uint32_t m, const bs::EncArgs& a, hipStream_t s);
+int bitsliced_encode_generator(uint32_t k, uint32_t m, uint8_t* out);
+
+}  // namespace nfec

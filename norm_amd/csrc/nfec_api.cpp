@@ -6,9 +6,11 @@
 // only enqueue kernels on the caller's stream; no host<->device traffic on the hot path.
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 
+#include "bitslice.hpp"
 #include "nfec_internal.hpp"
 
 namespace nfec {
@@ -215,10 +217,34 @@ int build_codec(nfec_codec* c)
     return NFEC_OK;
 }
 
+// NFEC_FORCE_GENERIC=1 disables the generated bit-sliced kernels (A/B measurements)
+bool force_generic()
+{
+    static const bool v = [] {
+        const char* e = std::getenv("NFEC_FORCE_GENERIC");
+        return e && *e && *e != '0';
+    }();
+    return v;
+}
+
 // ---- encode on a device batch ----
 int encode_device(nfec_codec* c, const nfec_block_batch* b, hipStream_t s)
 {
     const bool acc = b->flags & NFEC_ACCUMULATE;
+    if (c->kind == NFEC_RS8 && !force_generic()) {
+        // bit-sliced kernel specialised to this (k, m) generator, when one was generated
+        bs::EncArgs e;
+        e.base = static_cast<const uint8_t*>(b->blocks);
+        e.out = static_cast<uint8_t*>(b->blocks);
+        e.block_stride = b->block_stride;
+        e.seg_stride = b->seg_stride;
+        e.nblocks = b->nblocks;
+        e.vec = c->vec;
+        e.num_data = b->num_data;
+        e.accumulate = acc;
+        const int rc = launch_rs8_bitsliced_encode(c->k, c->m, e, s);
+        if (rc != NFEC_ENOTSUP) return rc == NFEC_OK ? NFEC_OK : fail(rc, "bit-sliced encode launch failed");
+    }
     if (c->kind == NFEC_RS8) {
         Gf8MatmulArgs a;
         a.in_base = static_cast<const uint8_t*>(b->blocks);

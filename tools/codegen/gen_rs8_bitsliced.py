@@ -1,0 +1,249 @@
+#!/usr/bin/env python3
+"""Generate norm_amd/csrc/gen_rs8_bitsliced.hip: bit-sliced RS8 encode kernels specialised
+to the reference generator of fixed (k, m) shapes.
+
+Why generate code: the encode matrix of NormEncoderRS8 (src/common/normEncoderRS8.cpp:400-462)
+is a constant of (k, m).  Over GF(2) the map parity = G * data is a (8m x 8k) bit matrix; with
+the data bit-sliced (bitslice.hpp) every parity bit-plane is an XOR of data bit-planes, i.e.
+pure v_bitop3/v_xor work with the constants folded into the instruction stream -- no table
+lookups and no v_perm (which gfx950 issues at half the rate of v_bitop3, measured in
+profiles/r01/ubench_valu_rates.jsonl).  Per source column j the 8 data planes are combined
+four at a time (method of four Russians): T_lo[a] = XOR of planes {b<4 : a_b}, T_hi likewise
+(22 XORs), then each parity plane row (p, i) takes one 3-input XOR:
+    acc[p][i] ^= T_lo[R & 15] ^ T_hi[R >> 4],   R = row i of the 8x8 matrix of G[p][j].
+The code is straight-line (~100 KiB per role); measurements showed no instruction-cache
+penalty for streams of that size.
+
+Parity rows are split into roles of ROWS_PER_ROLE rows; each role is one wavefront that keeps
+ROWS_PER_ROLE x 8 accumulators, so two waves per SIMD stay resident.
+
+Usage: gen_rs8_bitsliced.py OUT.hip [k,m ...]
+"""
+import sys
+
+POLY = 0x11D
+ROWS_PER_ROLE = 16
+DEFAULT_SHAPES = [(64, 32), (64, 16), (64, 8)]
+
+
+def gf_tables():
+    exp = [0] * 510
+    log = [0] * 256
+    v = 1
+    for i in range(255):
+        exp[i] = v
+        log[v] = i
+        v <<= 1
+        if v & 0x100:
+            v ^= POLY
+    for i in range(255, 510):
+        exp[i] = exp[i - 255]
+    log[0] = 255
+    return exp, log
+
+
+EXP, LOG = gf_tables()
+
+
+def mul(a, b):
+    return EXP[LOG[a] + LOG[b]] if a and b else 0
+
+
+def inv(a):
+    return EXP[255 - LOG[a]] if a > 1 else a
+
+
+def point(row):
+    return 0 if row == 0 else EXP[(row - 1) % 255]
+
+
+def generator(k, m):
+    """Parity rows (m x k) of the reference's systematic Rizzo generator, Lagrange form."""
+    x = [point(j) for j in range(k)]
+    G = []
+    for p in range(m):
+        y = point(k + p)
+        row = []
+        for j in range(k):
+            num, den = 1, 1
+            for l in range(k):
+                if l != j:
+                    num = mul(num, y ^ x[l])
+                    den = mul(den, x[j] ^ x[l])
+            row.append(mul(num, inv(den)))
+        G.append(row)
+    return G
+
+
+def bitmatrix_rows(c):
+    """R_i for i in 0..7: bit b of R_i = bit i of c * 2^b  ((c*x)_i = parity(R_i & x))."""
+    cols = [mul(c, 1 << b) for b in range(8)]
+    return [sum(((cols[b] >> i) & 1) << b for b in range(8)) for i in range(8)]
+
+
+def table_expr(prefix, base, a):
+    """Expression for the XOR of planes base+b over the set bits b of a (a in 1..15)."""
+    bits = [b for b in range(4) if (a >> b) & 1]
+    if len(bits) == 1:
+        return f"w{base + bits[0]}"
+    return f"{prefix}{a}"
+
+
+def table_defs(prefix, base, needed):
+    """Definitions of the multi-plane combinations actually used."""
+    out = []
+    defs = {}
+    for a in sorted(needed):
+        bits = [b for b in range(4) if (a >> b) & 1]
+        if len(bits) < 2:
+            continue
+        ws = [f"w{base + b}" for b in bits]
+        if len(ws) == 2:
+            out.append(f"const uint32_t {prefix}{a} = {ws[0]} ^ {ws[1]};")
+        elif len(ws) == 3:
+            out.append(f"const uint32_t {prefix}{a} = bs::x3({ws[0]}, {ws[1]}, {ws[2]});")
+        else:
+            out.append(f"const uint32_t {prefix}{a} = bs::x3({ws[0]}, {ws[1]}, {ws[2]}) ^ {ws[3]};")
+        defs[a] = True
+    return out
+
+
+def gen_role(k, m, role, rows):
+    """Device function computing parity rows [r0, r0+rows) of one lane's 4 items."""
+    G = generator(k, m)
+    r0 = role * ROWS_PER_ROLE
+    L = []
+    fn = f"enc_k{k}_m{m}_role{role}"
+    L.append(f"__device__ __forceinline__ void {fn}(const bs::EncArgs& a, const bs::Items& it)")
+    L.append("{")
+    L.append("    const uint64_t stride = a.seg_stride;")
+    L.append("    const uint32_t o0 = it.off[0], o1 = it.off[1], o2 = it.off[2], o3 = it.off[3];")
+    L.append("    const uint8_t* col = it.wbase;")
+    for r in range(rows):
+        L.append("    uint32_t " + ", ".join(f"a{r}_{i} = 0" for i in range(8)) + ";")
+    L.append("    uint32_t w0, w1, w2, w3, w4, w5, w6, w7;")
+    L.append("    uint2 n0, n1, n2, n3;")
+    L.append("    n0 = bs::ld8(col, o0); n1 = bs::ld8(col, o1); n2 = bs::ld8(col, o2); n3 = bs::ld8(col, o3);")
+    for j in range(k):
+        L.append(f"    // ---- source column {j} ----")
+        L.append("    w0 = n0.x; w1 = n0.y; w2 = n1.x; w3 = n1.y; w4 = n2.x; w5 = n2.y; w6 = n3.x; w7 = n3.y;")
+        if j + 1 < k:
+            L.append("    col += stride;")
+            L.append("    n0 = bs::ld8(col, o0); n1 = bs::ld8(col, o1); n2 = bs::ld8(col, o2); n3 = bs::ld8(col, o3);")
+        # keep the scheduler from hoisting every column's loads to the top (register blow-up)
+        L.append("    __builtin_amdgcn_sched_barrier(0);")
+        L.append("    bs::transpose8(w0, w1, w2, w3, w4, w5, w6, w7);")
+        mats = [bitmatrix_rows(G[r0 + r][j]) for r in range(rows)]
+        need_lo = {R & 15 for rr in mats for R in rr if R & 15}
+        need_hi = {R >> 4 for rr in mats for R in rr if R >> 4}
+        L.append("    {")
+        for d in table_defs("L", 0, need_lo) + table_defs("H", 4, need_hi):
+            L.append("        " + d)
+        for r in range(rows):
+            for i in range(8):
+                R = mats[r][i]
+                lo, hi = R & 15, R >> 4
+                acc = f"a{r}_{i}"
+                if lo and hi:
+                    L.append(f"        {acc} = bs::x3({acc}, {table_expr('L', 0, lo)}, {table_expr('H', 4, hi)});")
+                elif lo:
+                    L.append(f"        {acc} = bs::x2({acc}, {table_expr('L', 0, lo)});")
+                elif hi:
+                    L.append(f"        {acc} = bs::x2({acc}, {table_expr('H', 4, hi)});")
+        L.append("    }")
+        # Pin the accumulators at the end of every column: SelectionDAG linearises pure
+        # arithmetic freely across sched_barrier, sinking accumulator updates to the end of
+        # the kernel and keeping every column's tables alive (spills).  An empty volatile asm
+        # that reads and redefines them forces column-by-column evaluation at zero cost.
+        accs = [f"a{r}_{i}" for r in range(rows) for i in range(8)]
+        for c0 in range(0, len(accs), 16):
+            grp = accs[c0:c0 + 16]
+            L.append('    asm volatile("" : ' + ", ".join(f'"+v"({x})' for x in grp) + ' :: "memory");')
+    L.append("    // ---- parity planes back to bytes, store ----")
+    for r in range(rows):
+        p = r0 + r
+        L.append(f"    bs::transpose8(a{r}_0, a{r}_1, a{r}_2, a{r}_3, a{r}_4, a{r}_5, a{r}_6, a{r}_7);")
+        for i in range(4):
+            L.append(f"    bs::st8(it.obase + {k + p} * stride + o{i}, a{r}_{2 * i}, a{r}_{2 * i + 1}, it.nbytes[{i}], a.accumulate);")
+    L.append("}")
+    return "\n".join(L)
+
+
+def gen_kernel(k, m):
+    roles = (m + ROWS_PER_ROLE - 1) // ROWS_PER_ROLE
+    assert 4 % roles == 0 or roles > 4, "roles must divide the 4 waves of a workgroup"
+    out = []
+    for role in range(roles):
+        rows = min(ROWS_PER_ROLE, m - role * ROWS_PER_ROLE)
+        out.append(gen_role(k, m, role, rows))
+    groups = max(1, 4 // roles)
+    K = f"rs8_enc_k{k}_m{m}"
+    body = [f"__global__ __launch_bounds__(256, 2) void {K}(bs::EncArgs a)", "{"]
+    body.append("    const uint32_t lane = threadIdx.x & 63;")
+    body.append("    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);")
+    body.append(f"    const uint32_t role = wave % {roles};")
+    body.append(f"    const uint64_t group = (uint64_t)blockIdx.x * {groups} + wave / {roles};")
+    body.append("    bs::Items it;")
+    body.append("    bs::make_items(a, (uint32_t)group * 256u, lane, it);")
+    for role in range(roles):
+        kw = "if" if role == 0 else "else if"
+        body.append(f"    {kw} (role == {role}) enc_k{k}_m{m}_role{role}(a, it);")
+    body.append("}")
+    out.append("\n".join(body))
+    launcher = f"""
+static int launch_{K}(const bs::EncArgs& a, hipStream_t s)
+{{
+    const uint64_t items = (uint64_t)a.nblocks * ((a.vec + 7) / 8);
+    if (a.num_data || items >= (1ull << 31)) return NFEC_ENOTSUP;  // shortened / huge batches: generic kernel
+    const uint64_t groups = (items + 255) / 256;
+    const uint64_t wgs = (groups + {groups} - 1) / {groups};
+    hipLaunchKernelGGL({K}, dim3((uint32_t)wgs), dim3(256), 0, s, a);
+    return hipGetLastError() == hipSuccess ? NFEC_OK : NFEC_EDEVICE;
+}}"""
+    out.append(launcher)
+    return "\n\n".join(out)
+
+
+def main():
+    path = sys.argv[1]
+    shapes = DEFAULT_SHAPES
+    if len(sys.argv) > 2:
+        shapes = [tuple(int(v) for v in s.split(",")) for s in sys.argv[2:]]
+    parts = [
+        "// GENERATED by tools/codegen/gen_rs8_bitsliced.py -- do not edit by hand.",
+        "// Bit-sliced RS8 encode kernels specialised to the reference generator of each (k, m):",
+        "// " + ", ".join(f"({k},{m})" for k, m in shapes),
+        '#include "bitslice.hpp"',
+        "",
+        "namespace nfec {",
+        "namespace {",
+    ]
+    for k, m in shapes:
+        parts.append(gen_kernel(k, m))
+    parts.append("}  // namespace")
+    parts.append("")
+    parts.append("// Returns NFEC_ENOTSUP when no specialised kernel exists for (k, m).")
+    parts.append("int launch_rs8_bitsliced_encode(uint32_t k, uint32_t m, const bs::EncArgs& a, hipStream_t s)")
+    parts.append("{")
+    for k, m in shapes:
+        parts.append(f"    if (k == {k} && m == {m}) return launch_rs8_enc_k{k}_m{m}(a, s);")
+    parts.append("    return NFEC_ENOTSUP;")
+    parts.append("}")
+    parts.append("")
+    parts.append("// generator parity rows compiled into the kernels (checked against the host build in tests)")
+    parts.append("int bitsliced_encode_generator(uint32_t k, uint32_t m, uint8_t* out)")
+    parts.append("{")
+    for k, m in shapes:
+        G = generator(k, m)
+        flat = ",".join(str(v) for row in G for v in row)
+        parts.append(f"    if (k == {k} && m == {m}) {{ static const uint8_t g[] = {{{flat}}};")
+        parts.append(f"        for (uint32_t i = 0; i < {k * m}; ++i) out[i] = g[i]; return NFEC_OK; }}")
+    parts.append("    return NFEC_ENOTSUP;")
+    parts.append("}")
+    parts.append("")
+    parts.append("}  // namespace nfec")
+    open(path, "w").write("\n".join(parts) + "\n")
+
+
+if __name__ == "__main__":
+    main()
