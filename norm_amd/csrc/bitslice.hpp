@@ -103,6 +103,62 @@ __device__ __forceinline__ void make_items(const EncArgs& a, uint32_t item_base,
     }
 }
 
+// decode stage 1 (re-encode of the surviving source with the erased columns masked out)
+struct DecArgs {
+    const uint8_t* base = nullptr;
+    uint64_t block_stride = 0;
+    uint32_t seg_stride = 0;
+    uint32_t nblocks = 0;
+    uint32_t vec = 0;
+    const uint32_t* emask = nullptr;  // [b][2] erased source columns
+    const uint32_t* psel = nullptr;   // [b][2] parity rows used
+    const uint8_t* pmap = nullptr;    // [b][m] row -> index t in P
+    uint8_t* z = nullptr;             // [b][cs][z_stride] stage-1 output z_t
+    uint64_t z_block_stride = 0;
+    uint32_t z_stride = 0;
+};
+
+struct DecItems {
+    const uint8_t* wbase;   // uniform: slot 0 of the wave's first block
+    uint32_t off[4];        // per lane: byte offset of item i from wbase (slot 0)
+    uint32_t blk[4];        // absolute block index of item i
+    uint32_t ib[4];         // byte offset of item i inside a segment
+    uint32_t nbytes[4];
+    uint32_t em0[4], em1[4];
+    uint32_t sel[4];        // parity rows used by item i's block (m <= 32)
+};
+
+__device__ __forceinline__ void make_dec_items(const DecArgs& a, uint32_t item_base, uint32_t lane, DecItems& it)
+{
+    const uint32_t ips = (a.vec + 7) >> 3;
+    const uint32_t total = a.nblocks * ips;
+    const uint32_t b0 = __builtin_amdgcn_readfirstlane(min(item_base, total - 1) / ips);
+    it.wbase = a.base + (uint64_t)b0 * a.block_stride;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const uint32_t g = item_base + (uint32_t)i * 64u + lane;
+        const bool ok = g < total;
+        const uint32_t gg = ok ? g : item_base;
+        const uint32_t b = gg / ips;
+        const uint32_t o = gg - b * ips;
+        it.off[i] = (uint32_t)((b - b0) * a.block_stride) + o * 8u;
+        it.blk[i] = b;
+        it.ib[i] = o * 8u;
+        it.nbytes[i] = ok ? min(8u, a.vec - o * 8u) : 0u;
+        it.em0[i] = a.emask[2 * (uint64_t)b];
+        it.em1[i] = a.emask[2 * (uint64_t)b + 1];
+        it.sel[i] = ok ? a.psel[2 * (uint64_t)b] : 0u;
+    }
+}
+
+// zero the 8 bytes of an item whose source column j is erased: keep = bit j clear
+__device__ __forceinline__ void mask_item(uint32_t& x, uint32_t& y, uint32_t emw, uint32_t bit)
+{
+    const uint32_t m = (uint32_t)__builtin_amdgcn_sbfe((int32_t)emw, bit, 1);  // 0 or ~0
+    x = __builtin_amdgcn_bitop3_b32(x, m, 0u, 0x30);  // x & ~m
+    y = __builtin_amdgcn_bitop3_b32(y, m, 0u, 0x30);
+}
+
 __device__ __forceinline__ uint2 ld8(const uint8_t* base, uint32_t off)
 {
     return *reinterpret_cast<const uint2*>(base + off);
@@ -128,6 +184,7 @@ __device__ __forceinline__ void st8(uint8_t* p, uint32_t x, uint32_t y, uint32_t
 // generated (gen_rs8_bitsliced.hip): NFEC_ENOTSUP when (k, m) has no specialised kernel or
 // the batch is shortened (per-block numData)
 int launch_rs8_bitsliced_encode(uint32_t k, uint32_t m, const bs::EncArgs& a, hipStream_t s);
+int launch_rs8_bitsliced_reencode(uint32_t k, uint32_t m, const bs::DecArgs& a, hipStream_t s);
 int bitsliced_encode_generator(uint32_t k, uint32_t m, uint8_t* out);
 
 }  // namespace nfec

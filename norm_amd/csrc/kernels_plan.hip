@@ -333,3 +333,132 @@ int launch_mdp_plan(const MdpPlanArgs& a, hipStream_t s)
 }
 
 }  // namespace nfec
+
+// ---------------------------------------------------------------------------------
+// Closed-form RS8 plan (see RsPlan2Args): one wavefront per block, m <= 64.
+// ---------------------------------------------------------------------------------
+namespace nfec {
+namespace {
+
+__global__ __launch_bounds__(64) void rs_plan2_kernel(RsPlan2Args a)
+{
+    __shared__ uint8_t ex[512];
+    __shared__ uint16_t lg[256];
+    __shared__ uint8_t xs[64], yt[64];             // points of E and P
+    __shared__ uint16_t sP[64], sE[64];
+    __shared__ int32_t lA[64], lB[64];             // per-s and per-t log factors
+    const uint32_t lane = threadIdx.x;
+    const uint32_t b = blockIdx.x;
+    for (uint32_t i = lane; i < 510; i += 64) ex[i] = a.exp_tab[i];
+    for (uint32_t i = lane; i < 256; i += 64) lg[i] = a.log_tab[i];
+    __syncthreads();
+
+    const uint32_t k = a.k, m = a.m;
+    const uint32_t ec = uni(a.erasure_counts[b]);
+    const uint16_t* locs = a.erasure_locs + (uint64_t)b * a.erasure_stride;
+    bool ok = ec <= m && ec <= a.erasure_stride;
+    uint32_t es = 0;
+    // lane-parallel validation: sorted, in range; count source erasures
+    if (ok) {
+        bool bad = false;
+        uint32_t nsrc = 0;
+        for (uint32_t i = lane; i < ec; i += 64) {
+            const uint32_t l = locs[i];
+            if (l >= k + m || (i > 0 && l <= locs[i - 1])) bad = true;
+            if (l < k) ++nsrc;
+        }
+        bad = __any(bad);
+        // es = number of entries < k (sorted list => prefix)
+        for (int off = 32; off > 0; off >>= 1) nsrc += __shfl_xor(nsrc, off);
+        ok = !bad;
+        es = nsrc;
+    }
+    // surviving parity rows: lane p tests slot k+p against the parity erasures
+    uint64_t surv = 0;
+    if (ok) {
+        bool alive = lane < m;
+        for (uint32_t i = es; i < ec; ++i)
+            if (locs[i] == k + lane) alive = false;
+        surv = __ballot(alive);
+        if ((uint32_t)__popcll(surv) < es) ok = false;
+    }
+    const uint32_t e = ok ? es : 0;
+    const uint32_t cs = a.coef_stride;
+    uint32_t* emask = a.emask + (uint64_t)b * 2;
+    uint32_t* psel = a.psel + (uint64_t)b * 2;
+    if (lane == 0) {
+        if (a.status) a.status[b] = ok ? (int32_t)ec : 0;
+        a.rows[b] = (int32_t)e;
+        a.cols2[b] = (uint16_t)e;
+    }
+    // parity map: rank of each surviving row among the first e
+    uint32_t rank = (uint32_t)__popcll(surv & ((1ull << lane) - 1ull));
+    const bool used = e > 0 && lane < m && ((surv >> lane) & 1ull) && rank < e;
+    const uint64_t pused = __ballot(used);
+    if (lane < m) a.pmap[(uint64_t)b * m + lane] = used ? (uint8_t)rank : (uint8_t)0xff;
+    uint64_t em = 0;
+    {
+        // erased-source bitmap (k <= 64 for the specialised kernels; others ignore it)
+        bool er = false;
+        for (uint32_t i = 0; i < e; ++i)
+            if (locs[i] == lane) er = true;
+        em = __ballot(er && lane < k);
+    }
+    if (lane == 0) {
+        emask[0] = (uint32_t)em;
+        emask[1] = (uint32_t)(em >> 32);
+        psel[0] = (uint32_t)pused;
+        psel[1] = (uint32_t)(pused >> 32);
+    }
+    if (e == 0) return;
+    if (used) {
+        sP[rank] = (uint16_t)lane;
+        const uint32_t row = k + lane;  // generator row of parity p; point alpha^(row-1)
+        yt[rank] = ex[(row - 1) % 255u];
+    }
+    if (lane < e) {
+        const uint32_t s = locs[lane];
+        sE[lane] = (uint16_t)s;
+        xs[lane] = s == 0 ? 0 : ex[(s - 1) % 255u];
+    }
+    __syncthreads();
+    // per-s: lA[s] = lWp(x_s) + lPP(s) - lQp(s);  per-t: lB[t] = lQ(t) - lW(t) - lD(t)
+    if (lane < e) {
+        const uint32_t x = xs[lane];
+        int32_t acc = (int32_t)a.lwp[sE[lane]];
+        for (uint32_t t = 0; t < e; ++t) acc += lg[x ^ yt[t]];
+        for (uint32_t s2 = 0; s2 < e; ++s2)
+            if (s2 != lane) acc -= lg[x ^ xs[s2]];
+        lA[lane] = acc;
+        const uint32_t y = yt[lane];
+        int32_t bcc = -(int32_t)a.lw[sP[lane]];
+        for (uint32_t s2 = 0; s2 < e; ++s2) bcc += lg[y ^ xs[s2]];
+        for (uint32_t t2 = 0; t2 < e; ++t2)
+            if (t2 != lane) bcc -= lg[y ^ yt[t2]];
+        lB[lane] = bcc;
+    }
+    __syncthreads();
+    uint8_t* coef = a.coef2 + (uint64_t)b * cs * cs;
+    for (uint32_t idx = lane; idx < e * e; idx += 64) {
+        const uint32_t t = idx / e, s = idx % e;
+        int32_t l = lA[s] + lB[t] - (int32_t)lg[xs[s] ^ yt[t]];
+        l %= 255;
+        if (l < 0) l += 255;
+        coef[(uint64_t)t * cs + s] = ex[l];
+    }
+    if (lane < e) a.out_slots2[(uint64_t)b * k + lane] = sE[lane];
+}
+
+}  // namespace
+
+int launch_rs_plan2(const RsPlan2Args& a, hipStream_t s)
+{
+    if (a.nblocks == 0) return NFEC_OK;
+    if (a.m > 64 || a.k + a.m > 255) return NFEC_ENOTSUP;
+    hipLaunchKernelGGL(rs_plan2_kernel, dim3(a.nblocks), dim3(64), 0, s, a);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return hip_fail(e, "rs_plan2 launch");
+    return NFEC_OK;
+}
+
+}  // namespace nfec

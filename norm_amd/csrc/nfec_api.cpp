@@ -82,12 +82,14 @@ struct nfec_codec {
     DevBuf<uint8_t> d_exp;       // field exp table (2q elements)
     DevBuf<uint16_t> d_log;      // field log table (q+1)
     DevBuf<uint8_t> d_mdp_step;  // MDP single LFSR step matrix, column-major [m+1][cs]
+    DevBuf<uint16_t> d_lwp, d_lw;  // RS8 closed-form plan constants: log W'(x_j), log W(y_p)
 
     // decode workspace (guarded by mu)
     std::mutex mu;
     DevBuf<int32_t> w_status, w_rows;
     DevBuf<uint16_t> w_islots, w_oslots, w_cols;
-    DevBuf<uint8_t> w_coef1, w_coef2, w_z, w_work;
+    DevBuf<uint8_t> w_coef1, w_coef2, w_z, w_work, w_pmap;
+    DevBuf<uint32_t> w_emask, w_psel;
     // per-call staging
     DevBuf<uint8_t> s_block;
     DevBuf<uint16_t> s_locs;
@@ -99,6 +101,11 @@ struct nfec_codec {
             b->release();
         d_vtab.release();
         d_log.release();
+        d_lwp.release();
+        d_lw.release();
+        w_pmap.release();
+        w_emask.release();
+        w_psel.release();
         w_status.release();
         w_rows.release();
         w_islots.release();
@@ -187,6 +194,25 @@ int build_codec(nfec_codec* c)
         if (rc) return rc;
         rc = upload(c->d_gen, genb.data(), genb.size());
         if (rc) return rc;
+        if (!wide) {
+            // log W'(x_j) over the k source points and log W(y_p) at the parity points
+            std::vector<uint16_t> lwp(c->k), lw(c->m);
+            for (uint32_t j = 0; j < c->k; ++j) {
+                uint64_t acc = 0;
+                for (uint32_t l = 0; l < c->k; ++l)
+                    if (l != j) acc += f.log[rs_point(f, j) ^ rs_point(f, l)];
+                lwp[j] = (uint16_t)(acc % f.q);
+            }
+            for (uint32_t p = 0; p < c->m; ++p) {
+                uint64_t acc = 0;
+                for (uint32_t l = 0; l < c->k; ++l) acc += f.log[rs_point(f, c->k + p) ^ rs_point(f, l)];
+                lw[p] = (uint16_t)(acc % f.q);
+            }
+            if ((rc = c->d_lwp.reserve(c->k))) return rc;
+            if ((rc = c->d_lw.reserve(c->m))) return rc;
+            NFEC_HIP(hipMemcpy(c->d_lwp.p, lwp.data(), lwp.size() * 2, hipMemcpyHostToDevice));
+            NFEC_HIP(hipMemcpy(c->d_lw.p, lw.data(), lw.size() * 2, hipMemcpyHostToDevice));
+        }
     }
     // field tables
     if (wide) {
@@ -225,6 +251,13 @@ bool force_generic()
         return e && *e && *e != '0';
     }();
     return v;
+}
+
+// whether the generated bit-sliced kernels cover this RS8 shape
+bool has_bitsliced(uint32_t k, uint32_t m)
+{
+    static std::vector<uint8_t> scratch(256 * 256);
+    return bitsliced_encode_generator(k, m, scratch.data()) == NFEC_OK;
 }
 
 // ---- encode on a device batch ----
@@ -335,6 +368,13 @@ int decode_device(nfec_codec* c, const nfec_block_batch* b, const uint16_t* locs
         if ((rc = c->w_z.reserve((size_t)sb * c->cs * zstride))) return rc;
         if (c->m > 64 && (rc = c->w_work.reserve((size_t)sb * c->m * 2 * c->m * c->sym))) return rc;
     }
+    const bool fast = c->kind == NFEC_RS8 && !b->num_data && c->m <= 32 && c->k <= 64 && !force_generic() &&
+                      has_bitsliced(c->k, c->m);
+    if (fast) {
+        if ((rc = c->w_emask.reserve((size_t)sb * 2))) return rc;
+        if ((rc = c->w_psel.reserve((size_t)sb * 2))) return rc;
+        if ((rc = c->w_pmap.reserve((size_t)sb * c->m))) return rc;
+    }
     for (uint32_t b0 = 0; b0 < b->nblocks; b0 += sb) {
         const uint32_t nb = std::min(sb, b->nblocks - b0);
         uint8_t* blocks = static_cast<uint8_t*>(b->blocks) + (uint64_t)b0 * b->block_stride;
@@ -381,6 +421,64 @@ int decode_device(nfec_codec* c, const nfec_block_batch* b, const uint16_t* locs
             a.nblocks = nb;
             a.vec_bytes = c->vec;
             if ((rc = launch_gf8_matmul(a, false, s))) return rc;
+            continue;
+        }
+        if (fast) {
+            // closed-form plan -> bit-sliced re-encode (z) -> e x e inverse (generic kernel)
+            RsPlan2Args p2;
+            p2.k = c->k;
+            p2.m = c->m;
+            p2.nblocks = nb;
+            p2.erasure_locs = l;
+            p2.erasure_stride = lstride;
+            p2.erasure_counts = cnt;
+            p2.exp_tab = c->d_exp.p;
+            p2.log_tab = c->d_log.p;
+            p2.lwp = c->d_lwp.p;
+            p2.lw = c->d_lw.p;
+            p2.status = st;
+            p2.rows = c->w_rows.p;
+            p2.cols2 = c->w_cols.p;
+            p2.out_slots2 = c->w_oslots.p;
+            p2.emask = c->w_emask.p;
+            p2.psel = c->w_psel.p;
+            p2.pmap = c->w_pmap.p;
+            p2.coef_stride = c->cs;
+            p2.coef2 = c->w_coef2.p;
+            if ((rc = launch_rs_plan2(p2, s))) return rc;
+            bs::DecArgs d;
+            d.base = blocks;
+            d.block_stride = b->block_stride;
+            d.seg_stride = b->seg_stride;
+            d.nblocks = nb;
+            d.vec = c->vec;
+            d.emask = c->w_emask.p;
+            d.psel = c->w_psel.p;
+            d.pmap = c->w_pmap.p;
+            d.z = c->w_z.p;
+            d.z_block_stride = (uint64_t)c->cs * zstride;
+            d.z_stride = zstride;
+            if ((rc = launch_rs8_bitsliced_reencode(c->k, c->m, d, s))) return fail(rc, "bit-sliced re-encode launch failed");
+            Gf8MatmulArgs a2;
+            a2.in_base = c->w_z.p;
+            a2.in_block_stride = (uint64_t)c->cs * zstride;
+            a2.in_seg_stride = zstride;
+            a2.in_count = c->w_cols.p;
+            a2.out_base = blocks;
+            a2.out_block_stride = b->block_stride;
+            a2.out_seg_stride = b->seg_stride;
+            a2.out_slots = c->w_oslots.p;
+            a2.out_slot_mode = OUT_SLOT_LIST;
+            a2.row_count = c->w_rows.p;
+            a2.slots_stride = c->k;
+            a2.coef = c->w_coef2.p;
+            a2.coef_block_stride = (uint64_t)c->cs * c->cs;
+            a2.coef_col_stride = c->cs;
+            a2.vtab = c->d_vtab.p;
+            a2.nblocks = nb;
+            a2.vec_bytes = c->vec;
+            a2.accumulate = acc;
+            if ((rc = launch_gf8_matmul(a2, false, s))) return rc;
             continue;
         }
         RsPlanArgs p;

@@ -151,6 +151,35 @@ struct RsPlanArgs {
 };
 int launch_rs_plan(const RsPlanArgs& a, hipStream_t s);
 
+// RS decode planning, closed form (RS8, m <= 64): the systematic generator is the Lagrange
+// basis of the points x_j = point(j) evaluated at y_p = point(k+p), so the e x e system
+// A[t][s] = G[P_t][E_s] is a row/column-scaled Cauchy matrix with the explicit inverse
+//   Ainv[s][t] = W'(x_s) Q(y_t) M_t(x_s) / (W(y_t) Q'(x_s))
+// (W over all k points, Q over the erased points, M_t the Lagrange basis of the parity
+// points).  Per block this is O(e^2) log-domain additions instead of a Gauss-Jordan
+// elimination; the inverse is unique, so the bytes equal the reference's.
+struct RsPlan2Args {
+    uint32_t k = 0, m = 0, nblocks = 0;
+    const uint16_t* erasure_locs = nullptr;
+    uint32_t erasure_stride = 0;
+    const uint16_t* erasure_counts = nullptr;
+    const uint8_t* exp_tab = nullptr;   // 510-entry GF(2^8) exp table (device)
+    const uint16_t* log_tab = nullptr;  // 256-entry log table (device)
+    const uint16_t* lwp = nullptr;      // [k] log W'(x_j)   (codec constant)
+    const uint16_t* lw = nullptr;       // [m] log W(y_p)    (codec constant)
+    // outputs
+    int32_t* status = nullptr;
+    int32_t* rows = nullptr;            // e_s per block (0: nothing to repair)
+    uint16_t* cols2 = nullptr;          // e_s per block
+    uint16_t* out_slots2 = nullptr;     // [b][k]: erased source slots E_s
+    uint32_t* emask = nullptr;          // [b][2]: bit j set = source column j erased
+    uint32_t* psel = nullptr;           // [b][2]: bit p set = parity row p used (P)
+    uint8_t* pmap = nullptr;            // [b][m]: index t of parity row p in P
+    uint32_t coef_stride = 0;
+    uint8_t* coef2 = nullptr;           // [b][cs][cs]: Ainv column-major ([t][s])
+};
+int launch_rs_plan2(const RsPlan2Args& a, hipStream_t s);
+
 // MDP decode planning: per block one-stage coefficient matrix over the surviving slots.
 struct MdpPlanArgs {
     uint32_t k = 0, m = 0, nblocks = 0;

@@ -57,6 +57,8 @@ ENC_CASES = [
     (NFEC_RS8, 64, 32, 1400, 1400, 37),
     (NFEC_RS8, 64, 32, 1400, 1408, 5),
     (NFEC_RS8, 64, 16, 1400, 1400, 9),
+    (NFEC_RS8, 64, 8, 1400, 1400, 7),
+    (NFEC_RS8, 64, 32, 1401, 1408, 5),
     (NFEC_RS8, 1, 1, 17, 24, 3),
     (NFEC_RS8, 16, 4, 64, 64, 11),
     (NFEC_RS8, 200, 55, 100, 104, 3),
@@ -120,6 +122,10 @@ DEC_CASES = [
     (NFEC_RS8, 64, 32, 1400, 9, 32, 0),
     (NFEC_RS8, 64, 32, 1400, 9, 20, 12),
     (NFEC_RS8, 64, 32, 1400, 5, 0, 7),
+    (NFEC_RS8, 64, 32, 1400, 7, 1, 31),
+    (NFEC_RS8, 64, 16, 1400, 7, 12, 4),
+    (NFEC_RS8, 64, 8, 200, 9, 8, 0),
+    (NFEC_RS8, 64, 8, 203, 9, 5, 3),
     (NFEC_RS8, 16, 4, 64, 13, 3, 1),
     (NFEC_RS8, 1, 1, 24, 4, 1, 0),
     (NFEC_RS8, 128, 127, 64, 2, 100, 27),

@@ -108,6 +108,117 @@ def table_defs(prefix, base, needed):
     return out
 
 
+def column_body(L, G, k, r0, rows, j, masked):
+    """Code for source column j: rotate prefetch, (mask erased), transpose, M4RM update."""
+    L.append(f"    // ---- source column {j} ----")
+    L.append("    w0 = n0.x; w1 = n0.y; w2 = n1.x; w3 = n1.y; w4 = n2.x; w5 = n2.y; w6 = n3.x; w7 = n3.y;")
+    if j + 1 < k:
+        L.append("    col += stride;")
+        L.append("    n0 = bs::ld8(col, o0); n1 = bs::ld8(col, o1); n2 = bs::ld8(col, o2); n3 = bs::ld8(col, o3);")
+    L.append("    __builtin_amdgcn_sched_barrier(0);")
+    if masked:
+        word = "em0" if j < 32 else "em1"
+        bit = j % 32
+        for i in range(4):
+            L.append(f"    bs::mask_item(w{2 * i}, w{2 * i + 1}, it.{word}[{i}], {bit});")
+    L.append("    bs::transpose8(w0, w1, w2, w3, w4, w5, w6, w7);")
+    mats = [bitmatrix_rows(G[r0 + r][j]) for r in range(rows)]
+    need_lo = {R & 15 for rr in mats for R in rr if R & 15}
+    need_hi = {R >> 4 for rr in mats for R in rr if R >> 4}
+    L.append("    {")
+    for d in table_defs("L", 0, need_lo) + table_defs("H", 4, need_hi):
+        L.append("        " + d)
+    for r in range(rows):
+        for i in range(8):
+            R = mats[r][i]
+            lo, hi = R & 15, R >> 4
+            acc = f"a{r}_{i}"
+            if lo and hi:
+                L.append(f"        {acc} = bs::x3({acc}, {table_expr('L', 0, lo)}, {table_expr('H', 4, hi)});")
+            elif lo:
+                L.append(f"        {acc} = bs::x2({acc}, {table_expr('L', 0, lo)});")
+            elif hi:
+                L.append(f"        {acc} = bs::x2({acc}, {table_expr('H', 4, hi)});")
+    L.append("    }")
+    accs = [f"a{r}_{i}" for r in range(rows) for i in range(8)]
+    for c0 in range(0, len(accs), 16):
+        grp = accs[c0:c0 + 16]
+        L.append('    asm volatile("" : ' + ", ".join(f'"+v"({x})' for x in grp) + ' :: "memory");')
+
+
+def gen_dec_role(k, m, role, rows):
+    """Decode stage 1 for parity rows [r0, r0+rows): z_t = parity_p ^ G[p][present] * data."""
+    G = generator(k, m)
+    r0 = role * ROWS_PER_ROLE
+    L = []
+    L.append(f"__device__ __forceinline__ void dec_k{k}_m{m}_role{role}(const bs::DecArgs& a, const bs::DecItems& it)")
+    L.append("{")
+    L.append("    const uint64_t stride = a.seg_stride;")
+    L.append("    const uint32_t o0 = it.off[0], o1 = it.off[1], o2 = it.off[2], o3 = it.off[3];")
+    L.append("    const uint8_t* col = it.wbase;")
+    for r in range(rows):
+        L.append("    uint32_t " + ", ".join(f"a{r}_{i} = 0" for i in range(8)) + ";")
+    L.append("    uint32_t w0, w1, w2, w3, w4, w5, w6, w7;")
+    L.append("    uint2 n0, n1, n2, n3;")
+    L.append("    n0 = bs::ld8(col, o0); n1 = bs::ld8(col, o1); n2 = bs::ld8(col, o2); n3 = bs::ld8(col, o3);")
+    for j in range(k):
+        column_body(L, G, k, r0, rows, j, masked=True)
+    L.append("    // ---- z_t = received parity p ^ re-encoded row p, for the rows P uses ----")
+    L.append(f"    const uint8_t* par = it.wbase + {k} * stride;")
+    for r in range(rows):
+        p = r0 + r
+        L.append(f"    if (__any(((it.sel[0] | it.sel[1] | it.sel[2] | it.sel[3]) >> {p}) & 1u)) {{")
+        L.append(f"        bs::transpose8(a{r}_0, a{r}_1, a{r}_2, a{r}_3, a{r}_4, a{r}_5, a{r}_6, a{r}_7);")
+        for i in range(4):
+            L.append(f"        if ((it.sel[{i}] >> {p}) & 1u) {{")
+            L.append(f"            const uint2 q = bs::ld8(par + {p} * stride, it.off[{i}]);")
+            L.append(f"            const uint32_t t = a.pmap[(uint64_t)it.blk[{i}] * {m} + {p}];")
+            L.append(f"            bs::st8(a.z + (uint64_t)it.blk[{i}] * a.z_block_stride + (uint64_t)t * a.z_stride + it.ib[{i}],")
+            L.append(f"                    a{r}_{2 * i} ^ q.x, a{r}_{2 * i + 1} ^ q.y, it.nbytes[{i}], 0u);")
+            L.append("        }")
+        L.append("    }")
+    L.append("}")
+    return "\n".join(L)
+
+
+def gen_dec_kernel(k, m):
+    roles = (m + ROWS_PER_ROLE - 1) // ROWS_PER_ROLE
+    out = []
+    for role in range(roles):
+        rows = min(ROWS_PER_ROLE, m - role * ROWS_PER_ROLE)
+        out.append(gen_dec_role(k, m, role, rows))
+    groups = max(1, 4 // roles)
+    K = f"rs8_dec_k{k}_m{m}"
+    body = [f"__global__ __launch_bounds__(256, 2) void {K}(bs::DecArgs a)", "{"]
+    body.append("    const uint32_t lane = threadIdx.x & 63;")
+    body.append("    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);")
+    body.append(f"    const uint32_t role = wave % {roles};")
+    body.append(f"    const uint64_t group = (uint64_t)blockIdx.x * {groups} + wave / {roles};")
+    body.append("    bs::DecItems it;")
+    body.append("    bs::make_dec_items(a, (uint32_t)group * 256u, lane, it);")
+    body.append("    const uint32_t need = it.sel[0] | it.sel[1] | it.sel[2] | it.sel[3];")
+    for role in range(roles):
+        lo = role * ROWS_PER_ROLE
+        rows = min(ROWS_PER_ROLE, m - lo)
+        rmask = ((1 << rows) - 1) << lo
+        kw = "if" if role == 0 else "else if"
+        # a role whose parity rows no block of the wave uses is skipped (uniform branch)
+        body.append(f"    {kw} (role == {role}) {{ if (__any(need & 0x{rmask:08x}u)) dec_k{k}_m{m}_role{role}(a, it); }}")
+    body.append("}")
+    out.append("\n".join(body))
+    out.append(f"""
+static int launch_{K}(const bs::DecArgs& a, hipStream_t s)
+{{
+    const uint64_t items = (uint64_t)a.nblocks * ((a.vec + 7) / 8);
+    if (items >= (1ull << 31)) return NFEC_ENOTSUP;
+    const uint64_t groups = (items + 255) / 256;
+    const uint64_t wgs = (groups + {groups} - 1) / {groups};
+    hipLaunchKernelGGL({K}, dim3((uint32_t)wgs), dim3(256), 0, s, a);
+    return hipGetLastError() == hipSuccess ? NFEC_OK : NFEC_EDEVICE;
+}}""")
+    return "\n\n".join(out)
+
+
 def gen_role(k, m, role, rows):
     """Device function computing parity rows [r0, r0+rows) of one lane's 4 items."""
     G = generator(k, m)
@@ -125,40 +236,7 @@ def gen_role(k, m, role, rows):
     L.append("    uint2 n0, n1, n2, n3;")
     L.append("    n0 = bs::ld8(col, o0); n1 = bs::ld8(col, o1); n2 = bs::ld8(col, o2); n3 = bs::ld8(col, o3);")
     for j in range(k):
-        L.append(f"    // ---- source column {j} ----")
-        L.append("    w0 = n0.x; w1 = n0.y; w2 = n1.x; w3 = n1.y; w4 = n2.x; w5 = n2.y; w6 = n3.x; w7 = n3.y;")
-        if j + 1 < k:
-            L.append("    col += stride;")
-            L.append("    n0 = bs::ld8(col, o0); n1 = bs::ld8(col, o1); n2 = bs::ld8(col, o2); n3 = bs::ld8(col, o3);")
-        # keep the scheduler from hoisting every column's loads to the top (register blow-up)
-        L.append("    __builtin_amdgcn_sched_barrier(0);")
-        L.append("    bs::transpose8(w0, w1, w2, w3, w4, w5, w6, w7);")
-        mats = [bitmatrix_rows(G[r0 + r][j]) for r in range(rows)]
-        need_lo = {R & 15 for rr in mats for R in rr if R & 15}
-        need_hi = {R >> 4 for rr in mats for R in rr if R >> 4}
-        L.append("    {")
-        for d in table_defs("L", 0, need_lo) + table_defs("H", 4, need_hi):
-            L.append("        " + d)
-        for r in range(rows):
-            for i in range(8):
-                R = mats[r][i]
-                lo, hi = R & 15, R >> 4
-                acc = f"a{r}_{i}"
-                if lo and hi:
-                    L.append(f"        {acc} = bs::x3({acc}, {table_expr('L', 0, lo)}, {table_expr('H', 4, hi)});")
-                elif lo:
-                    L.append(f"        {acc} = bs::x2({acc}, {table_expr('L', 0, lo)});")
-                elif hi:
-                    L.append(f"        {acc} = bs::x2({acc}, {table_expr('H', 4, hi)});")
-        L.append("    }")
-        # Pin the accumulators at the end of every column: SelectionDAG linearises pure
-        # arithmetic freely across sched_barrier, sinking accumulator updates to the end of
-        # the kernel and keeping every column's tables alive (spills).  An empty volatile asm
-        # that reads and redefines them forces column-by-column evaluation at zero cost.
-        accs = [f"a{r}_{i}" for r in range(rows) for i in range(8)]
-        for c0 in range(0, len(accs), 16):
-            grp = accs[c0:c0 + 16]
-            L.append('    asm volatile("" : ' + ", ".join(f'"+v"({x})' for x in grp) + ' :: "memory");')
+        column_body(L, G, k, r0, rows, j, masked=False)
     L.append("    // ---- parity planes back to bytes, store ----")
     for r in range(rows):
         p = r0 + r
@@ -220,6 +298,8 @@ def main():
     ]
     for k, m in shapes:
         parts.append(gen_kernel(k, m))
+        if m <= 32:
+            parts.append(gen_dec_kernel(k, m))
     parts.append("}  // namespace")
     parts.append("")
     parts.append("// Returns NFEC_ENOTSUP when no specialised kernel exists for (k, m).")
@@ -227,6 +307,14 @@ def main():
     parts.append("{")
     for k, m in shapes:
         parts.append(f"    if (k == {k} && m == {m}) return launch_rs8_enc_k{k}_m{m}(a, s);")
+    parts.append("    return NFEC_ENOTSUP;")
+    parts.append("}")
+    parts.append("")
+    parts.append("int launch_rs8_bitsliced_reencode(uint32_t k, uint32_t m, const bs::DecArgs& a, hipStream_t s)")
+    parts.append("{")
+    for k, m in shapes:
+        if m <= 32:
+            parts.append(f"    if (k == {k} && m == {m}) return launch_rs8_dec_k{k}_m{m}(a, s);")
     parts.append("    return NFEC_ENOTSUP;")
     parts.append("}")
     parts.append("")
