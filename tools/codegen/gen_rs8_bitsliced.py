@@ -23,6 +23,7 @@ import sys
 
 POLY = 0x11D
 ROWS_PER_ROLE = 16
+PF = 3  # source columns in flight per wave (prefetch depth)
 DEFAULT_SHAPES = [(64, 32), (64, 16), (64, 8)]
 
 
@@ -108,13 +109,25 @@ def table_defs(prefix, base, needed):
     return out
 
 
+def prologue_loads(L, k):
+    L.append("    uint32_t w0, w1, w2, w3, w4, w5, w6, w7;")
+    for r in range(PF):
+        L.append(f"    uint2 n{r}_0, n{r}_1, n{r}_2, n{r}_3;")
+    for r in range(min(PF, k)):
+        L.append(f"    {{ const uint8_t* c = it.wbase + {r} * stride; n{r}_0 = bs::ld8(c, o0); n{r}_1 = bs::ld8(c, o1); "
+                 f"n{r}_2 = bs::ld8(c, o2); n{r}_3 = bs::ld8(c, o3); }}")
+
+
 def column_body(L, G, k, r0, rows, j, masked):
-    """Code for source column j: rotate prefetch, (mask erased), transpose, M4RM update."""
+    """Code for source column j: take it from the prefetch ring, refill the ring slot with
+    column j+PF, (mask erased), transpose, M4RM update."""
     L.append(f"    // ---- source column {j} ----")
-    L.append("    w0 = n0.x; w1 = n0.y; w2 = n1.x; w3 = n1.y; w4 = n2.x; w5 = n2.y; w6 = n3.x; w7 = n3.y;")
-    if j + 1 < k:
-        L.append("    col += stride;")
-        L.append("    n0 = bs::ld8(col, o0); n1 = bs::ld8(col, o1); n2 = bs::ld8(col, o2); n3 = bs::ld8(col, o3);")
+    q = j % PF
+    L.append(f"    w0 = n{q}_0.x; w1 = n{q}_0.y; w2 = n{q}_1.x; w3 = n{q}_1.y; w4 = n{q}_2.x; w5 = n{q}_2.y; "
+             f"w6 = n{q}_3.x; w7 = n{q}_3.y;")
+    if j + PF < k:
+        L.append(f"    {{ const uint8_t* c = it.wbase + {j + PF} * stride; n{q}_0 = bs::ld8(c, o0); n{q}_1 = bs::ld8(c, o1); "
+                 f"n{q}_2 = bs::ld8(c, o2); n{q}_3 = bs::ld8(c, o3); }}")
     L.append("    __builtin_amdgcn_sched_barrier(0);")
     if masked:
         word = "em0" if j < 32 else "em1"
@@ -155,12 +168,9 @@ def gen_dec_role(k, m, role, rows):
     L.append("{")
     L.append("    const uint64_t stride = a.seg_stride;")
     L.append("    const uint32_t o0 = it.off[0], o1 = it.off[1], o2 = it.off[2], o3 = it.off[3];")
-    L.append("    const uint8_t* col = it.wbase;")
     for r in range(rows):
         L.append("    uint32_t " + ", ".join(f"a{r}_{i} = 0" for i in range(8)) + ";")
-    L.append("    uint32_t w0, w1, w2, w3, w4, w5, w6, w7;")
-    L.append("    uint2 n0, n1, n2, n3;")
-    L.append("    n0 = bs::ld8(col, o0); n1 = bs::ld8(col, o1); n2 = bs::ld8(col, o2); n3 = bs::ld8(col, o3);")
+    prologue_loads(L, k)
     for j in range(k):
         column_body(L, G, k, r0, rows, j, masked=True)
     L.append("    // ---- z_t = received parity p ^ re-encoded row p, for the rows P uses ----")
@@ -187,13 +197,12 @@ def gen_dec_kernel(k, m):
     for role in range(roles):
         rows = min(ROWS_PER_ROLE, m - role * ROWS_PER_ROLE)
         out.append(gen_dec_role(k, m, role, rows))
-    groups = max(1, 4 // roles)
+    groups = 4
     K = f"rs8_dec_k{k}_m{m}"
     body = [f"__global__ __launch_bounds__(256, 2) void {K}(bs::DecArgs a)", "{"]
     body.append("    const uint32_t lane = threadIdx.x & 63;")
     body.append("    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);")
-    body.append(f"    const uint32_t role = wave % {roles};")
-    body.append(f"    const uint64_t group = (uint64_t)blockIdx.x * {groups} + wave / {roles};")
+    body.append(f"    const uint64_t group = (uint64_t)blockIdx.x * {groups} + wave;")
     body.append("    bs::DecItems it;")
     body.append("    bs::make_dec_items(a, (uint32_t)group * 256u, lane, it);")
     body.append("    const uint32_t need = it.sel[0] | it.sel[1] | it.sel[2] | it.sel[3];")
@@ -201,9 +210,9 @@ def gen_dec_kernel(k, m):
         lo = role * ROWS_PER_ROLE
         rows = min(ROWS_PER_ROLE, m - lo)
         rmask = ((1 << rows) - 1) << lo
-        kw = "if" if role == 0 else "else if"
-        # a role whose parity rows no block of the wave uses is skipped (uniform branch)
-        body.append(f"    {kw} (role == {role}) {{ if (__any(need & 0x{rmask:08x}u)) dec_k{k}_m{m}_role{role}(a, it); }}")
+        # every wave handles all roles its blocks need (usually only the first: P is the
+        # first e surviving parity rows); unused roles cost nothing
+        body.append(f"    if (__any(need & 0x{rmask:08x}u)) dec_k{k}_m{m}_role{role}(a, it);")
     body.append("}")
     out.append("\n".join(body))
     out.append(f"""
@@ -229,12 +238,9 @@ def gen_role(k, m, role, rows):
     L.append("{")
     L.append("    const uint64_t stride = a.seg_stride;")
     L.append("    const uint32_t o0 = it.off[0], o1 = it.off[1], o2 = it.off[2], o3 = it.off[3];")
-    L.append("    const uint8_t* col = it.wbase;")
     for r in range(rows):
         L.append("    uint32_t " + ", ".join(f"a{r}_{i} = 0" for i in range(8)) + ";")
-    L.append("    uint32_t w0, w1, w2, w3, w4, w5, w6, w7;")
-    L.append("    uint2 n0, n1, n2, n3;")
-    L.append("    n0 = bs::ld8(col, o0); n1 = bs::ld8(col, o1); n2 = bs::ld8(col, o2); n3 = bs::ld8(col, o3);")
+    prologue_loads(L, k)
     for j in range(k):
         column_body(L, G, k, r0, rows, j, masked=False)
     L.append("    // ---- parity planes back to bytes, store ----")
