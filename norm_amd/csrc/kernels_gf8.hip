@@ -67,6 +67,10 @@ template <int NI, int RC, bool FLAT>
 __global__ __launch_bounds__(kThreads) void gf8_matmul_kernel(Gf8MatmulArgs a)
 {
     __shared__ uint4 lds_tab[256 * 2];  // 256 x 32 bytes
+    // !FLAT: the wave's per-block coefficient matrix, staged once so the per-column
+    // coefficient reads are LDS broadcasts instead of dependent global loads
+    constexpr uint32_t kCoefLds = FLAT ? 1u : 1024u;  // dwords per wave
+    __shared__ uint32_t lds_coef[kWavesPerGroup][kCoefLds];
     {
         const uint4* g = reinterpret_cast<const uint4*>(a.vtab);
         for (int i = threadIdx.x; i < 512; i += kThreads) lds_tab[i] = g[i];
@@ -129,6 +133,19 @@ __global__ __launch_bounds__(kThreads) void gf8_matmul_kernel(Gf8MatmulArgs a)
         const uint8_t* coef_blk = a.coef;
         if constexpr (!FLAT)
             coef_blk += (uint64_t)(a.coef_by_count ? (cols ? cols - 1 : 0) : wblock) * a.coef_block_stride;
+        bool staged = false;
+        if constexpr (!FLAT) {
+            const uint32_t cdw = (cols * a.coef_col_stride + 3) / 4;
+            if (grp == 0 && cdw <= kCoefLds && (reinterpret_cast<uintptr_t>(coef_blk) & 3) == 0) {
+                const uint32_t* src = reinterpret_cast<const uint32_t*>(coef_blk);
+                uint32_t* dst = lds_coef[threadIdx.x >> 6];
+                for (uint32_t i = lane; i < cdw; i += kWave) dst[i] = src[i];
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            }
+            staged = cdw <= kCoefLds && (reinterpret_cast<uintptr_t>(coef_blk) & 3) == 0;
+        }
         const uint16_t* islots = (!FLAT && a.in_slots) ? a.in_slots + (uint64_t)wblock * a.slots_stride : nullptr;
 
         for (int32_t r0 = 0; r0 < rows; r0 += RC) {
@@ -159,7 +176,9 @@ __global__ __launch_bounds__(kThreads) void gf8_matmul_kernel(Gf8MatmulArgs a)
                     sel[2 * j] = selectors(cur[j].x);
                     sel[2 * j + 1] = selectors(cur[j].y);
                 }
-                const uint32_t* cw = reinterpret_cast<const uint32_t*>(coef_blk + (uint64_t)c * a.coef_col_stride + r0);
+                const uint32_t* cw =
+                    staged ? &lds_coef[threadIdx.x >> 6][((uint64_t)c * a.coef_col_stride + r0) >> 2]
+                           : reinterpret_cast<const uint32_t*>(coef_blk + (uint64_t)c * a.coef_col_stride + r0);
 #pragma unroll
                 for (int r4 = 0; r4 < RC / 4; ++r4) {
                     const uint32_t word = cw[r4];

@@ -174,17 +174,29 @@ def gen_dec_role(k, m, role, rows):
     for j in range(k):
         column_body(L, G, k, r0, rows, j, masked=True)
     L.append("    // ---- z_t = received parity p ^ re-encoded row p, for the rows P uses ----")
+    L.append("    // t = rank of row p among the used rows (P is the first e surviving parity rows in")
+    L.append("    // ascending order), so no table lookup; received parity is prefetched 4 rows ahead.")
     L.append(f"    const uint8_t* par = it.wbase + {k} * stride;")
+    AHEAD = min(4, rows)
+    for r in range(AHEAD):
+        p = r0 + r
+        L.append(f"    uint2 q{r}_0 = bs::ld8(par + {p} * stride, o0), q{r}_1 = bs::ld8(par + {p} * stride, o1), "
+                 f"q{r}_2 = bs::ld8(par + {p} * stride, o2), q{r}_3 = bs::ld8(par + {p} * stride, o3);")
     for r in range(rows):
         p = r0 + r
-        L.append(f"    if (__any(((it.sel[0] | it.sel[1] | it.sel[2] | it.sel[3]) >> {p}) & 1u)) {{")
+        q = r % AHEAD
+        L.append(f"    {{")
+        L.append(f"        const uint2 c0 = q{q}_0, c1 = q{q}_1, c2 = q{q}_2, c3 = q{q}_3;")
+        if r + AHEAD < rows:
+            pn = r0 + r + AHEAD
+            L.append(f"        q{q}_0 = bs::ld8(par + {pn} * stride, o0); q{q}_1 = bs::ld8(par + {pn} * stride, o1); "
+                     f"q{q}_2 = bs::ld8(par + {pn} * stride, o2); q{q}_3 = bs::ld8(par + {pn} * stride, o3);")
         L.append(f"        bs::transpose8(a{r}_0, a{r}_1, a{r}_2, a{r}_3, a{r}_4, a{r}_5, a{r}_6, a{r}_7);")
         for i in range(4):
             L.append(f"        if ((it.sel[{i}] >> {p}) & 1u) {{")
-            L.append(f"            const uint2 q = bs::ld8(par + {p} * stride, it.off[{i}]);")
-            L.append(f"            const uint32_t t = a.pmap[(uint64_t)it.blk[{i}] * {m} + {p}];")
+            L.append(f"            const uint32_t t = __builtin_popcount(it.sel[{i}] & 0x{(1 << p) - 1:08x}u);")
             L.append(f"            bs::st8(a.z + (uint64_t)it.blk[{i}] * a.z_block_stride + (uint64_t)t * a.z_stride + it.ib[{i}],")
-            L.append(f"                    a{r}_{2 * i} ^ q.x, a{r}_{2 * i + 1} ^ q.y, it.nbytes[{i}], 0u);")
+            L.append(f"                    a{r}_{2 * i} ^ c{i}.x, a{r}_{2 * i + 1} ^ c{i}.y, it.nbytes[{i}], 0u);")
             L.append("        }")
         L.append("    }")
     L.append("}")

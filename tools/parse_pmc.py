@@ -25,7 +25,7 @@ def main(root):
             per[name][cname].append(val)
     out = {}
     for name, ctrs in per.items():
-        short = name.split("(")[0].replace("nfec::(anonymous namespace)::", "").replace("void ", "")
+        short = name.replace("(anonymous namespace)::", "").replace("void ", "").split("(")[0]
         d = {c: sum(v) / len(v) for c, v in ctrs.items()}
         d["dispatches"] = max(len(v) for v in ctrs.values())
         if "FETCH_SIZE" in d:
