@@ -159,6 +159,30 @@ __device__ __forceinline__ void mask_item(uint32_t& x, uint32_t& y, uint32_t emw
     y = __builtin_amdgcn_bitop3_b32(y, m, 0u, 0x30);
 }
 
+// LDS-DMA: each lane copies 4 bytes from gbase + off into LDS at lds_base + 4*lane.  Issued
+// through inline asm because LLVM does not model the builtin's LDS write (it dropped the
+// subsequent LDS reads in a probe); completion is tracked by hand with s_waitcnt vmcnt.
+__device__ __forceinline__ void dma4(const uint8_t* gbase, uint32_t off, uint32_t lds_base)
+{
+    asm volatile("s_mov_b32 m0, %0\n\tglobal_load_lds_dword %1, %2"
+                 :
+                 : "s"(lds_base), "v"(off), "s"(gbase)
+                 : "memory", "m0");
+}
+
+// wait until at most N vector-memory ops of this wave are outstanding, then workgroup barrier
+template <int N>
+__device__ __forceinline__ void wait_barrier()
+{
+    asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" : : "n"(N) : "memory");
+}
+
+__device__ __forceinline__ uint2 lds_item(const uint32_t* slot, uint32_t item, uint32_t lane)
+{
+    // the two dwords of an 8-byte item were written by two 256-byte DMA pieces
+    return make_uint2(slot[item * 128 + lane], slot[item * 128 + 64 + lane]);
+}
+
 __device__ __forceinline__ uint2 ld8(const uint8_t* base, uint32_t off)
 {
     return *reinterpret_cast<const uint2*>(base + off);

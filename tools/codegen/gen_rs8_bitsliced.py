@@ -23,7 +23,8 @@ import sys
 
 POLY = 0x11D
 ROWS_PER_ROLE = 16
-PF = 3  # source columns in flight per wave (prefetch depth)
+PF = 3  # source columns in flight per wave (prefetch depth, register ring)
+RING = 8  # LDS ring depth (columns in flight per workgroup) for the LDS-staged encode
 DEFAULT_SHAPES = [(64, 32), (64, 16), (64, 8)]
 
 
@@ -265,6 +266,112 @@ def gen_role(k, m, role, rows):
     return "\n".join(L)
 
 
+def gen_lds_role(k, m, role, rows, roles):
+    """Encode role with the source staged through an LDS ring shared by the role-waves of a
+    group: each wave DMAs its share of a column's 8 dword pieces, one barrier per column."""
+    G = generator(k, m)
+    r0 = role * ROWS_PER_ROLE
+    pieces = [(i, h) for i in range(4) for h in range(2)]
+    mine = [pc for n, pc in enumerate(pieces) if n % roles == role]
+    L = []
+    L.append(f"__device__ __forceinline__ void lenc_k{k}_m{m}_role{role}(const bs::EncArgs& a, const bs::Items& it, "
+             f"uint32_t* ring, uint32_t lane)")
+    L.append("{")
+    L.append("    const uint64_t stride = a.seg_stride;")
+    L.append("    const uint32_t o0 = it.off[0], o1 = it.off[1], o2 = it.off[2], o3 = it.off[3];")
+    L.append("    const uint32_t ring_base = (uint32_t)(uintptr_t)ring;")
+    for r in range(rows):
+        L.append("    uint32_t " + ", ".join(f"a{r}_{i} = 0" for i in range(8)) + ";")
+    L.append("    uint32_t w0, w1, w2, w3, w4, w5, w6, w7;")
+
+    def issue(col, indent="    "):
+        slot = col % RING
+        out = [f"{indent}{{ const uint8_t* c = it.wbase + {col} * stride;"]
+        for (i, h) in mine:
+            out.append(f"{indent}  bs::dma4(c, o{i} + {4 * h}, ring_base + {slot * 2048 + (2 * i + h) * 256}u);")
+        out.append(f"{indent}}}")
+        return out
+
+    for col in range(min(RING - 1, k)):
+        L.extend(issue(col))
+    per = len(mine)
+    for j in range(k):
+        L.append(f"    // ---- source column {j} ----")
+        issued_after = min(j + RING - 2, k - 1) - j  # columns issued after column j so far
+        L.append(f"    bs::wait_barrier<{per * issued_after}>();")
+        if j + RING - 1 < k:
+            L.extend(issue(j + RING - 1))
+        slot = j % RING
+        L.append(f"    {{ const uint32_t* sl = ring + {slot * 512};")
+        for i in range(4):
+            L.append(f"      const uint2 v{i} = bs::lds_item(sl, {i}, lane);")
+        L.append("      w0 = v0.x; w1 = v0.y; w2 = v1.x; w3 = v1.y; w4 = v2.x; w5 = v2.y; w6 = v3.x; w7 = v3.y; }")
+        L.append("    bs::transpose8(w0, w1, w2, w3, w4, w5, w6, w7);")
+        mats = [bitmatrix_rows(G[r0 + r][j]) for r in range(rows)]
+        need_lo = {R & 15 for rr in mats for R in rr if R & 15}
+        need_hi = {R >> 4 for rr in mats for R in rr if R >> 4}
+        L.append("    {")
+        for d in table_defs("L", 0, need_lo) + table_defs("H", 4, need_hi):
+            L.append("        " + d)
+        for r in range(rows):
+            for i in range(8):
+                R = mats[r][i]
+                lo, hi = R & 15, R >> 4
+                acc = f"a{r}_{i}"
+                if lo and hi:
+                    L.append(f"        {acc} = bs::x3({acc}, {table_expr('L', 0, lo)}, {table_expr('H', 4, hi)});")
+                elif lo:
+                    L.append(f"        {acc} = bs::x2({acc}, {table_expr('L', 0, lo)});")
+                elif hi:
+                    L.append(f"        {acc} = bs::x2({acc}, {table_expr('H', 4, hi)});")
+        L.append("    }")
+        accs = [f"a{r}_{i}" for r in range(rows) for i in range(8)]
+        for c0 in range(0, len(accs), 16):
+            grp = accs[c0:c0 + 16]
+            L.append('    asm volatile("" : ' + ", ".join(f'"+v"({x})' for x in grp) + ' :: "memory");')
+    L.append("    // ---- parity planes back to bytes, store ----")
+    for r in range(rows):
+        p = r0 + r
+        L.append(f"    bs::transpose8(a{r}_0, a{r}_1, a{r}_2, a{r}_3, a{r}_4, a{r}_5, a{r}_6, a{r}_7);")
+        for i in range(4):
+            L.append(f"    bs::st8(it.obase + {k + p} * stride + o{i}, a{r}_{2 * i}, a{r}_{2 * i + 1}, it.nbytes[{i}], a.accumulate);")
+    L.append("}")
+    return "\n".join(L)
+
+
+def gen_lds_kernel(k, m):
+    roles = (m + ROWS_PER_ROLE - 1) // ROWS_PER_ROLE
+    assert roles in (1, 2)
+    out = []
+    for role in range(roles):
+        rows = min(ROWS_PER_ROLE, m - role * ROWS_PER_ROLE)
+        out.append(gen_lds_role(k, m, role, rows, roles))
+    K = f"rs8_lenc_k{k}_m{m}"
+    threads = 64 * roles
+    body = [f"__global__ __launch_bounds__({threads}, 2) void {K}(bs::EncArgs a)", "{"]
+    body.append(f"    __shared__ __attribute__((aligned(16))) uint32_t ring[{RING} * 512];  // {RING} columns x 2 KiB")
+    body.append("    const uint32_t lane = threadIdx.x & 63;")
+    body.append("    const uint32_t role = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);")
+    body.append("    bs::Items it;")
+    body.append("    bs::make_items(a, (uint32_t)blockIdx.x * 256u, lane, it);")
+    for role in range(roles):
+        kw = "if" if role == 0 else "else"
+        body.append(f"    {kw} {{ lenc_k{k}_m{m}_role{role}(a, it, ring, lane); }}" if role else
+                    f"    if (role == 0) {{ lenc_k{k}_m{m}_role0(a, it, ring, lane); }}")
+    body.append("}")
+    out.append("\n".join(body))
+    out.append(f"""
+static int launch_{K}(const bs::EncArgs& a, hipStream_t s)
+{{
+    const uint64_t items = (uint64_t)a.nblocks * ((a.vec + 7) / 8);
+    if (a.num_data || items >= (1ull << 31)) return NFEC_ENOTSUP;
+    const uint64_t groups = (items + 255) / 256;
+    hipLaunchKernelGGL({K}, dim3((uint32_t)groups), dim3({threads}), 0, s, a);
+    return hipGetLastError() == hipSuccess ? NFEC_OK : NFEC_EDEVICE;
+}}""")
+    return "\n\n".join(out)
+
+
 def gen_kernel(k, m):
     roles = (m + ROWS_PER_ROLE - 1) // ROWS_PER_ROLE
     assert 4 % roles == 0 or roles > 4, "roles must divide the 4 waves of a workgroup"
@@ -309,6 +416,7 @@ def main():
         "// GENERATED by tools/codegen/gen_rs8_bitsliced.py -- do not edit by hand.",
         "// Bit-sliced RS8 encode kernels specialised to the reference generator of each (k, m):",
         "// " + ", ".join(f"({k},{m})" for k, m in shapes),
+        '#include <cstdlib>',
         '#include "bitslice.hpp"',
         "",
         "namespace nfec {",
@@ -317,13 +425,17 @@ def main():
     for k, m in shapes:
         parts.append(gen_kernel(k, m))
         if m <= 32:
+            parts.append(gen_lds_kernel(k, m))
             parts.append(gen_dec_kernel(k, m))
     parts.append("}  // namespace")
     parts.append("")
     parts.append("// Returns NFEC_ENOTSUP when no specialised kernel exists for (k, m).")
     parts.append("int launch_rs8_bitsliced_encode(uint32_t k, uint32_t m, const bs::EncArgs& a, hipStream_t s)")
     parts.append("{")
+    parts.append("    static const int variant = [] { const char* e = std::getenv(\"NFEC_BS_VARIANT\"); return e ? std::atoi(e) : 1; }();")
     for k, m in shapes:
+        if m <= 32:
+            parts.append(f"    if (k == {k} && m == {m} && variant == 1) return launch_rs8_lenc_k{k}_m{m}(a, s);")
         parts.append(f"    if (k == {k} && m == {m}) return launch_rs8_enc_k{k}_m{m}(a, s);")
     parts.append("    return NFEC_ENOTSUP;")
     parts.append("}")
