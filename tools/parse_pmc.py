@@ -35,6 +35,22 @@ def main(root):
         out[short] = d
     json.dump(out, sys.stdout, indent=1, sort_keys=True)
     print()
+    # traffic summary for bench.py (encode kernel, bench workload)
+    enc = [v for k_, v in out.items() if ("rs8_lenc_k64_m32" in k_ or "rs8_enc_k64_m32" in k_) and "FETCH_SIZE" in v]
+    if enc and len(sys.argv) > 2:
+        e = enc[0]
+        traffic = {
+            "blocks": 65536, "k": 64, "m": 32, "vec": 1400,
+            "kernel": [k_ for k_, v in out.items() if v is e][0],
+            "encode_hbm_bytes_per_launch": round(e["hbm_read_bytes_corrected"] + e["hbm_write_bytes"]),
+            "read_bytes_corrected": round(e["hbm_read_bytes_corrected"]),
+            "write_bytes": round(e["hbm_write_bytes"]),
+            "method": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE in separate passes; read = 2 x FETCH_SIZE KiB "
+                      "(gfx950 correction, MI355X_MICROARCH.md HBM), write = WRITE_SIZE KiB",
+        }
+        with open(sys.argv[2], "w") as f:
+            json.dump(traffic, f, indent=1)
+            f.write("\n")
 
 
 if __name__ == "__main__":

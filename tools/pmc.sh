@@ -12,4 +12,4 @@ for grp in "FETCH_SIZE" "WRITE_SIZE" "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_IN
   i=$((i+1))
   timeout -k 10 300 rocprofv3 --pmc $grp --output-format csv -d $OUT/p$i -o pmc -- python3 bench.py $ARGS > $OUT/p$i.log 2>&1 || { echo "pmc pass $i ($grp) failed"; tail -5 $OUT/p$i.log; exit 1; }
 done
-python3 tools/parse_pmc.py $OUT > $OUT/summary.json && cat $OUT/summary.json
+python3 tools/parse_pmc.py $OUT $OUT/pmc_traffic.json > $OUT/summary.json && cat $OUT/pmc_traffic.json
