@@ -9,6 +9,8 @@
 #include <cstdlib>
 #include <cstring>
 #include <memory>
+#include <thread>
+#include <vector>
 
 #include "bitslice.hpp"
 #include "nfec_internal.hpp"
@@ -833,40 +835,131 @@ int nfec_decode_vectors(nfec_codec* c, void* const* vectors, uint32_t num_data, 
 }
 
 // ---- host-resident batches: pinned staging, H2D || compute || D2H over two slots ----
+// Host-resident batches: a pipeline of device slots, each on its own stream, with the H2D
+// copy, the kernels and the D2H copy of chunk i overlapping chunk i+1's.  Only the bytes the
+// operation reads are uploaded and only the bytes it writes are downloaded:
+//   encode  (unshortened, overwrite): up source slots [0,k), down parity slots [k,k+m)
+//   encode  (shortened or accumulate): up/down the whole block span
+//   decode: up the whole block span, down source slots [0,k) (unerased bytes come back
+//           unchanged; parity slots are never written).
+// A pinned (page-locked / hipHostRegister'ed) caller buffer is DMA'd directly; a pageable one
+// goes through pinned staging with the copy split over host threads.
+namespace {
+
+bool host_is_pinned(const void* p)
+{
+    hipPointerAttribute_t at;
+    std::memset(&at, 0, sizeof(at));
+    const hipError_t e = hipPointerGetAttributes(&at, p);
+    if (e != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    return at.type == hipMemoryTypeHost;
+}
+
+unsigned host_copy_threads()
+{
+    static const unsigned n = [] {
+        unsigned t = 8;
+        if (const char* v = std::getenv("NFEC_HOST_THREADS")) t = (unsigned)std::max(1, std::atoi(v));
+        return std::min<unsigned>(t, 64);
+    }();
+    return n;
+}
+
+// rows x width bytes, strided on both sides, split over host threads for large copies
+void copy2d(uint8_t* dst, uint64_t dpitch, const uint8_t* src, uint64_t spitch, uint64_t width, uint32_t rows)
+{
+    if (rows == 0 || width == 0) return;
+    auto run = [=](uint32_t r0, uint32_t r1) {
+        if (dpitch == width && spitch == width) {
+            std::memcpy(dst + r0 * width, src + r0 * width, (size_t)(r1 - r0) * width);
+            return;
+        }
+        for (uint32_t r = r0; r < r1; ++r) std::memcpy(dst + r * dpitch, src + r * spitch, (size_t)width);
+    };
+    const uint64_t bytes = width * rows;
+    const unsigned nt = (unsigned)std::min<uint64_t>(std::min<uint64_t>(host_copy_threads(), rows),
+                                                      std::max<uint64_t>(1, bytes >> 22));
+    if (nt <= 1) {
+        run(0, rows);
+        return;
+    }
+    std::vector<std::thread> th;
+    th.reserve(nt - 1);
+    const uint32_t per = (rows + nt - 1) / nt;
+    for (unsigned t = 1; t < nt; ++t) {
+        const uint32_t r0 = std::min<uint32_t>(rows, t * per), r1 = std::min<uint32_t>(rows, r0 + per);
+        if (r0 < r1) th.emplace_back(run, r0, r1);
+    }
+    run(0, std::min(per, rows));
+    for (auto& t : th) t.join();
+}
+
+}  // namespace
+
 static int run_host_batch(nfec_codec* c, const nfec_block_batch* hb, const uint16_t* locs, uint32_t lstride,
-                      const uint16_t* counts, int32_t* status, bool decode)
+                          const uint16_t* counts, int32_t* status, bool decode)
 {
     int rc = check_batch(c, hb);
     if (rc || hb->nblocks == 0) return rc;
     DeviceGuard g(c->device);
-    const uint64_t bs = hb->block_stride;
-    const uint32_t chunk = std::max<uint32_t>(1, std::min<uint32_t>(hb->nblocks, (uint32_t)std::max<uint64_t>(1, (64ull << 20) / std::max<uint64_t>(bs, 1))));
-    const uint32_t nslot = 2;
+    const uint64_t hbs = hb->block_stride;
+    const uint64_t ss = hb->seg_stride;
+    const uint64_t dbs = (uint64_t)(c->k + c->m) * ss;       // compact device pitch
+    const uint64_t span = (uint64_t)(c->k + c->m - 1) * ss + c->vec;  // bytes a block op can touch
+    const bool acc = (hb->flags & NFEC_ACCUMULATE) != 0;
+    const bool partial_enc = !decode && !acc && !hb->num_data;
+    const uint64_t up_off = 0;
+    const uint64_t up_len = partial_enc ? (uint64_t)(c->k - 1) * ss + c->vec : span;
+    const uint64_t dn_off = partial_enc ? (uint64_t)c->k * ss : 0;
+    const uint64_t dn_len = partial_enc ? (uint64_t)(c->m - 1) * ss + c->vec
+                                        : (decode ? (uint64_t)(c->k - 1) * ss + c->vec : span);
+    // download pieces: parity slots one by one when slots carry padding (so the caller's
+    // bytes between vec and seg_stride are never overwritten)
+    std::vector<std::pair<uint64_t, uint64_t>> dn;
+    if (partial_enc && ss != c->vec)
+        for (uint32_t p = 0; p < c->m; ++p) dn.emplace_back((uint64_t)(c->k + p) * ss, (uint64_t)c->vec);
+    else
+        dn.emplace_back(dn_off, dn_len);
+    const bool pinned = host_is_pinned(hb->blocks);
+    uint8_t* const hbase = static_cast<uint8_t*>(hb->blocks);
+
+    const uint32_t chunk = (uint32_t)std::max<uint64_t>(
+        1, std::min<uint64_t>(hb->nblocks, (64ull << 20) / std::max<uint64_t>(dbs, 1)));
+    constexpr uint32_t nslot = 3;
     struct Slot {
         uint8_t* dev = nullptr;
-        uint8_t* pin = nullptr;
+        uint8_t* pin = nullptr;     // staging (pageable caller buffers only), pitch dbs
         uint16_t* dmeta = nullptr;  // num_data, locs, counts
         int32_t* dstat = nullptr;
+        int32_t* hstat = nullptr;   // pinned status readback
         hipStream_t st = nullptr;
         hipEvent_t done = nullptr;
         uint32_t b0 = 0, nb = 0;
         bool busy = false;
-    } slots[2];
+    } slots[nslot];
     const size_t meta = (size_t)chunk * (1 + lstride + 1);
     auto cleanup = [&]() {
         for (auto& s : slots) {
             if (s.st) (void)hipStreamSynchronize(s.st);
             if (s.dev) (void)hipFree(s.dev);
             if (s.pin) (void)hipHostFree(s.pin);
+            if (s.hstat) (void)hipHostFree(s.hstat);
             if (s.dmeta) (void)hipFree(s.dmeta);
             if (s.dstat) (void)hipFree(s.dstat);
             if (s.done) (void)hipEventDestroy(s.done);
             if (s.st) (void)hipStreamDestroy(s.st);
         }
     };
-    for (auto& s : slots) {
-        if (hipMalloc(reinterpret_cast<void**>(&s.dev), (size_t)chunk * bs) != hipSuccess ||
-            hipHostMalloc(reinterpret_cast<void**>(&s.pin), (size_t)chunk * bs, hipHostMallocDefault) != hipSuccess ||
+    const uint32_t used = std::min<uint32_t>(nslot, (hb->nblocks + chunk - 1) / chunk);
+    for (uint32_t i = 0; i < used; ++i) {
+        Slot& s = slots[i];
+        if (hipMalloc(reinterpret_cast<void**>(&s.dev), (size_t)chunk * dbs) != hipSuccess ||
+            (!pinned && hipHostMalloc(reinterpret_cast<void**>(&s.pin), (size_t)chunk * dbs, hipHostMallocDefault) !=
+                            hipSuccess) ||
+            hipHostMalloc(reinterpret_cast<void**>(&s.hstat), (size_t)chunk * 4 + 16, hipHostMallocDefault) != hipSuccess ||
             hipMalloc(reinterpret_cast<void**>(&s.dmeta), meta * 2 + 16) != hipSuccess ||
             hipMalloc(reinterpret_cast<void**>(&s.dstat), (size_t)chunk * 4 + 16) != hipSuccess ||
             hipStreamCreateWithFlags(&s.st, hipStreamNonBlocking) != hipSuccess ||
@@ -875,26 +968,29 @@ static int run_host_batch(nfec_codec* c, const nfec_block_batch* hb, const uint1
             return fail(NFEC_ENOMEM, "host batch staging allocation failed");
         }
     }
-    std::vector<int32_t> hstat(chunk);
     auto finish = [&](Slot& s) -> int {
         if (!s.busy) return NFEC_OK;
-        NFEC_HIP(hipEventSynchronize(s.done));
-        std::memcpy(static_cast<uint8_t*>(hb->blocks) + (uint64_t)s.b0 * bs, s.pin, (size_t)s.nb * bs);
-        if (decode && status) {
-            NFEC_HIP(hipMemcpy(hstat.data(), s.dstat, (size_t)s.nb * 4, hipMemcpyDeviceToHost));
-            std::memcpy(status + s.b0, hstat.data(), (size_t)s.nb * 4);
-        }
         s.busy = false;
+        NFEC_HIP(hipEventSynchronize(s.done));
+        if (!pinned)
+            for (const auto& pc : dn) copy2d(hbase + (uint64_t)s.b0 * hbs + pc.first, hbs, s.pin + pc.first, dbs, pc.second, s.nb);
+        if (decode && status) std::memcpy(status + s.b0, s.hstat, (size_t)s.nb * 4);
         return NFEC_OK;
     };
     uint32_t idx = 0;
     for (uint32_t b0 = 0; b0 < hb->nblocks; b0 += chunk, ++idx) {
-        Slot& s = slots[idx % nslot];
+        Slot& s = slots[idx % used];
         if ((rc = finish(s))) { cleanup(); return rc; }
         s.b0 = b0;
         s.nb = std::min(chunk, hb->nblocks - b0);
-        std::memcpy(s.pin, static_cast<const uint8_t*>(hb->blocks) + (uint64_t)b0 * bs, (size_t)s.nb * bs);
-        hipError_t ae = hipMemcpyAsync(s.dev, s.pin, (size_t)s.nb * bs, hipMemcpyHostToDevice, s.st);
+        uint8_t* hsrc = hbase + (uint64_t)b0 * hbs;
+        hipError_t ae;
+        if (pinned) {
+            ae = hipMemcpy2DAsync(s.dev + up_off, dbs, hsrc + up_off, hbs, up_len, s.nb, hipMemcpyHostToDevice, s.st);
+        } else {
+            copy2d(s.pin + up_off, dbs, hsrc + up_off, hbs, up_len, s.nb);
+            ae = hipMemcpyAsync(s.dev, s.pin, (size_t)(s.nb - 1) * dbs + up_off + up_len, hipMemcpyHostToDevice, s.st);
+        }
         uint16_t* dnd = nullptr;
         if (hb->num_data) {
             dnd = s.dmeta;
@@ -902,25 +998,36 @@ static int run_host_batch(nfec_codec* c, const nfec_block_batch* hb, const uint1
         }
         nfec_block_batch db = *hb;
         db.blocks = s.dev;
+        db.block_stride = dbs;
         db.nblocks = s.nb;
         db.num_data = dnd;
+        if (ae != hipSuccess) { cleanup(); return hip_fail(ae, "host batch upload"); }
         if (decode) {
             uint16_t* dl = s.dmeta + chunk;
             uint16_t* dc = dl + (size_t)chunk * lstride;
-            if (ae == hipSuccess) ae = hipMemcpyAsync(dl, locs + (uint64_t)b0 * lstride, (size_t)s.nb * lstride * 2, hipMemcpyHostToDevice, s.st);
+            ae = hipMemcpyAsync(dl, locs + (uint64_t)b0 * lstride, (size_t)s.nb * lstride * 2, hipMemcpyHostToDevice, s.st);
             if (ae == hipSuccess) ae = hipMemcpyAsync(dc, counts + b0, (size_t)s.nb * 2, hipMemcpyHostToDevice, s.st);
+            if (ae != hipSuccess) { cleanup(); return hip_fail(ae, "host batch upload"); }
             rc = decode_device(c, &db, dl, lstride, dc, s.dstat, s.st);
         } else {
             rc = encode_device(c, &db, s.st);
         }
         if (rc) { cleanup(); return rc; }
-        if (ae == hipSuccess) ae = hipMemcpyAsync(s.pin, s.dev, (size_t)s.nb * bs, hipMemcpyDeviceToHost, s.st);
+        if (pinned)
+            for (size_t i = 0; i < dn.size() && ae == hipSuccess; ++i)
+                ae = hipMemcpy2DAsync(hsrc + dn[i].first, hbs, s.dev + dn[i].first, dbs, dn[i].second, s.nb,
+                                      hipMemcpyDeviceToHost, s.st);
+        else
+            ae = hipMemcpyAsync(s.pin + dn_off, s.dev + dn_off, (size_t)(s.nb - 1) * dbs + dn_len, hipMemcpyDeviceToHost,
+                                s.st);
+        if (ae == hipSuccess && decode && status)
+            ae = hipMemcpyAsync(s.hstat, s.dstat, (size_t)s.nb * 4, hipMemcpyDeviceToHost, s.st);
         if (ae == hipSuccess) ae = hipEventRecord(s.done, s.st);
         if (ae != hipSuccess) { cleanup(); return hip_fail(ae, "host batch copy"); }
         s.busy = true;
     }
-    for (auto& s : slots)
-        if ((rc = finish(s))) { cleanup(); return rc; }
+    for (uint32_t i = 0; i < used; ++i)
+        if ((rc = finish(slots[(idx + i) % used]))) { cleanup(); return rc; }
     hipError_t e = hipGetLastError();
     cleanup();
     if (e != hipSuccess) return hip_fail(e, "host batch");

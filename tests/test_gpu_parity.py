@@ -255,6 +255,38 @@ def test_host_batch_paths_match_device(orc):
     assert np.array_equal(host[:, :k], ref[:, :k])
 
 
+@pytest.mark.parametrize("pinned", [False, True])
+@pytest.mark.parametrize("kind,k,m,vec,stride,nb", [
+    (NFEC_RS8, 64, 32, 1400, 1408, 1100),   # several pipeline chunks, padded slots
+    (NFEC_RS8, 20, 12, 1000, 1000, 70),
+    (NFEC_RS16, 30, 10, 998, 1000, 33),
+    (NFEC_MDP, 24, 8, 600, 608, 50),
+])
+def test_host_batch_pipeline(orc, kind, k, m, vec, stride, nb, pinned):
+    """nfec_encode_host/nfec_decode_host over multi-chunk batches, pinned and pageable caller
+    buffers: parity and repaired source match the oracle and slot padding is never written."""
+    enc, dec = _codecs(kind, k, m, vec)
+    base = orc.make_blocks(k, m, vec, nb, seg_stride=stride)
+    base[:, :, vec:] = 0xA5
+    ref = orc.encode_blocks(kind, k, m, vec, base.copy())
+    if pinned:
+        host = torch.empty(base.shape, dtype=torch.uint8).pin_memory().numpy()
+        host[...] = base
+    else:
+        host = base.copy()
+    host[:, k:, :vec] = 0x3C   # stale parity must be overwritten
+    enc.encode_blocks_host(host)
+    assert np.array_equal(host, ref)
+    locs, counts = _erasures(orc, kind, k, m, nb, m - 3, 3)
+    for b in range(nb):
+        for s in locs[b, : counts[b]]:
+            host[b, s, :vec] = 0
+    st = dec.decode_blocks_host(host, locs, counts)
+    assert np.all(st == counts)
+    assert np.array_equal(host[:, :k], ref[:, :k])
+    assert np.all(host[:, :, vec:] == 0xA5)
+
+
 def test_device_workload_generators_match_oracle(orc):
     k, m, vec, nb = 64, 32, 1400, 9
     dev = torch.zeros((nb, k + m, 1400), dtype=torch.uint8, device="cuda")
