@@ -40,6 +40,9 @@ def parse():
     p.add_argument("--cpu-threads", type=int, default=16)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--verify", action="store_true", help="check the round trip after timing")
+    p.add_argument("--host-steps", type=int, default=0,
+                   help="also time K steps with the batch in pinned host memory (PCIe-inclusive, reported "
+                        "under 'host_resident'; never the headline value)")
     return p.parse_args()
 
 
@@ -114,6 +117,42 @@ def main():
     enc_ms = timed(lambda: enc.encode_blocks(blocks, stream=stream), n_k)
     dec_ms = timed(lambda: dec.decode_blocks(blocks, locs, counts, status=status, stream=stream), n_k)
     torch.cuda.synchronize(dev)
+
+    host = None
+    if a.host_steps > 0:
+        import numpy as np
+
+        hblocks = torch.empty(blocks.shape, dtype=torch.uint8, pin_memory=True)
+        hblocks.copy_(blocks)
+        hnp = hblocks.numpy()
+        hlocs = locs.cpu().numpy().view(np.uint16)
+        hcounts = counts.cpu().numpy().view(np.uint16)
+
+        def hstep():
+            enc.encode_blocks_host(hnp)
+            dec.decode_blocks_host(hnp, hlocs, hcounts)
+
+        hstep()
+        barrier()
+        h0 = time.perf_counter()
+        for _ in range(a.host_steps):
+            hstep()
+        h1 = time.perf_counter()
+        barrier()
+        he = h1 - h0
+        if dist is not None:
+            t = torch.tensor([he], dtype=torch.float64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            he = float(t.item())
+        host = {
+            "value": round(k * vec * nb * world / (he / a.host_steps) / 2**30, 2),
+            "unit": "GiB/s",
+            "steps": a.host_steps,
+            "ms_per_step": round(he / a.host_steps * 1e3, 2),
+            "note": "same workload with the blocks in pinned host memory: nfec_encode_host + nfec_decode_host "
+                    "(H2D of the bytes read, D2H of the bytes written, overlapped with the kernels)",
+        }
+        del hblocks, hnp
 
     ok = None
     if a.verify:
@@ -190,12 +229,16 @@ def main():
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4),
             "traffic": traffic,
-            "kernel": "gf8_matmul_kernel<2,32,FLAT> (RS8 encode)",
+            "kernel": f"nfec::{'rs8_enc' if os.environ.get('NFEC_BS_VARIANT', '0') == '0' else 'rs8_lenc'}_k{k}_m{m} (RS8 encode)"
+            if (k, m) in ((64, 32), (64, 16), (64, 8)) and not os.environ.get("NFEC_FORCE_GENERIC")
+            else "gf8_matmul_kernel (RS8 encode)",
             "algorithmic_bytes_per_launch": enc_bytes,
         },
         "kernels_ms": {"encode": round(enc_ms, 4), "decode": round(dec_ms, 4)},
         "cpu_baseline": cpu,
     }
+    if host is not None:
+        out["host_resident"] = host
     if ok is not None:
         out["verified"] = ok
     print(json.dumps(out))

@@ -241,7 +241,148 @@ hipError_t launch_one(const Gf8MatmulArgs& a, hipStream_t s)
     return hipGetLastError();
 }
 
+// ---- per-block square solve (decode stage 2 of the fast RS8 path) ----
+// out[b][out_slots[b][r]] (^)= XOR_t coef[b][t][r] (x) z[b][t]   for r < rows(b) <= RC, t < cols(b).
+// One wave per block.  The block's RC x cols coefficient tables (5 dwords each) are expanded
+// into LDS once, zero-padded to RC rows and an even column count, so the main loop is
+// branch-free: per column pair the wave issues the next pair's z loads, then for each of
+// the RC rows reads its table with uniform (broadcast) LDS loads whose addresses do not
+// depend on data, and applies 3 v_perm + 1 bitop3 + 1 xor per output dword.
+template <int NI, int RC>
+__global__ __launch_bounds__(kThreads) void gf8_solve_kernel(Gf8SolveArgs a)
+{
+    constexpr int kMaxCols = 32;
+    __shared__ uint4 lds_t4[kWavesPerGroup][kMaxCols * RC + 1];  // +1: pipelined read past the end
+    __shared__ uint32_t lds_t1[kWavesPerGroup][kMaxCols * RC + 1];
+    const uint32_t lane = threadIdx.x & (kWave - 1);
+    const uint32_t w = threadIdx.x >> 6;
+    const uint32_t blk = uni(blockIdx.x * kWavesPerGroup + w);
+    if (blk >= a.nblocks) return;
+    const int32_t rows = (int32_t)uni((uint32_t)a.rows[blk]);
+    if (rows <= 0) return;
+    const uint32_t cols = min(uni((uint32_t)a.cols[blk]), (uint32_t)kMaxCols);
+    const uint32_t cols2 = (cols + 1) & ~1u;
+
+    for (int32_t r0 = 0; r0 < rows; r0 += RC) {
+    // expand the tables of rows [r0, r0+RC): entry (t, r) for t < cols2
+    {
+        const uint8_t* cb = a.coef + (uint64_t)blk * a.coef_block_stride + r0;
+        __builtin_amdgcn_wave_barrier();
+        for (uint32_t e = lane; e < cols2 * RC; e += kWave) {
+            const uint32_t t = e / RC, r = e % RC;
+            const uint32_t cv = (t < cols && r0 + (int32_t)r < rows) ? cb[(uint64_t)t * a.coef_col_stride + r] : 0u;
+            const uint32_t* src = a.vtab + cv * 8;
+            lds_t4[w][e] = make_uint4(src[0], src[1], src[2], src[3]);
+            lds_t1[w][e] = src[4];
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+    const uint32_t ips = (a.vec_bytes + 7) >> 3;
+    const uint8_t* zb = a.z + (uint64_t)blk * a.z_block_stride;
+    const uint16_t* oslots = a.out_slots + (uint64_t)blk * a.slots_stride;
+    for (uint32_t g0 = 0; g0 < ips; g0 += NI * kWave) {
+        uint32_t zoff[NI];
+        bool valid[NI];
+#pragma unroll
+        for (int j = 0; j < NI; ++j) {
+            const uint32_t it = g0 + (uint32_t)j * kWave + lane;
+            valid[j] = it < ips;
+            zoff[j] = (valid[j] ? it : g0) * 8u;
+        }
+        uint32_t acc[RC][2 * NI];
+#pragma unroll
+        for (int r = 0; r < RC; ++r)
+#pragma unroll
+            for (int d = 0; d < 2 * NI; ++d) acc[r][d] = 0;
+
+        auto load_pair = [&](uint32_t t, uint2 (&dst)[2][NI]) {
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                const uint32_t tt = min(t + (uint32_t)u, cols - 1);
+                const uint8_t* zr = zb + (uint64_t)tt * a.z_stride;
+#pragma unroll
+                for (int j = 0; j < NI; ++j) dst[u][j] = load8(zr + zoff[j]);
+            }
+        };
+        uint2 cur[2][NI], nxt[2][NI];
+        load_pair(0, cur);
+        // tables are software-pipelined one row ahead (LDS latency off the VALU chain)
+        const uint4* t4 = lds_t4[w];
+        const uint32_t* t1 = lds_t1[w];
+        uint4 tb = t4[0];
+        uint32_t tc = t1[0];
+        for (uint32_t t = 0; t < cols2; t += 2) {
+            load_pair(min(t + 2, cols2 - 2), nxt);
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                Sel sel[2 * NI];
+#pragma unroll
+                for (int j = 0; j < NI; ++j) {
+                    sel[2 * j] = selectors(cur[u][j].x);
+                    sel[2 * j + 1] = selectors(cur[u][j].y);
+                }
+                const uint32_t e0 = (t + u) * RC;
+#pragma unroll
+                for (int r = 0; r < RC; ++r) {
+                    const uint4 tbn = t4[e0 + r + 1];
+                    const uint32_t tcn = t1[e0 + r + 1];
+                    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                    for (int d = 0; d < 2 * NI; ++d) acc[r][d] ^= gfmul4(tb, tc, sel[d]);
+                    __builtin_amdgcn_sched_barrier(0);
+                    tb = tbn;
+                    tc = tcn;
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < 2; ++u)
+#pragma unroll
+                for (int j = 0; j < NI; ++j) cur[u][j] = nxt[u][j];
+        }
+#pragma unroll
+        for (int r = 0; r < RC; ++r) {
+            if (r0 + (int32_t)r >= rows) continue;
+            uint8_t* orow = a.out + (uint64_t)blk * a.out_block_stride + (uint64_t)oslots[r0 + r] * a.out_seg_stride;
+#pragma unroll
+            for (int j = 0; j < NI; ++j) {
+                if (!valid[j]) continue;
+                uint8_t* p = orow + zoff[j];
+                uint2 v = make_uint2(acc[r][2 * j], acc[r][2 * j + 1]);
+                if (a.accumulate) {
+                    const uint2 o = load8(p);
+                    v.x ^= o.x;
+                    v.y ^= o.y;
+                }
+                store_bytes(p, v, a.vec_bytes - zoff[j]);
+            }
+        }
+    }
+    }
+}
+
+template <int NI, int RC>
+hipError_t launch_solve(const Gf8SolveArgs& a, hipStream_t s)
+{
+    const uint32_t groups = (a.nblocks + kWavesPerGroup - 1) / kWavesPerGroup;
+    hipLaunchKernelGGL((gf8_solve_kernel<NI, RC>), dim3(groups), dim3(kThreads), 0, s, a);
+    return hipGetLastError();
+}
+
 }  // namespace
+
+int launch_gf8_solve(const Gf8SolveArgs& a, uint32_t max_rows, uint32_t max_cols, hipStream_t s)
+{
+    if (a.nblocks == 0 || a.vec_bytes == 0) return NFEC_OK;
+    if (max_cols > 32) return NFEC_ENOTSUP;
+    const uint32_t ni = (((a.vec_bytes + 7) / 8) + kWave - 1) / kWave;
+    hipError_t e;
+    if (max_rows <= 8) e = ni <= 2 ? launch_solve<2, 8>(a, s) : launch_solve<3, 8>(a, s);
+    else e = ni <= 2 ? launch_solve<2, 16>(a, s) : launch_solve<3, 16>(a, s);
+    if (e != hipSuccess) return hip_fail(e, "gf8_solve launch");
+    return NFEC_OK;
+}
 
 int launch_gf8_matmul(const Gf8MatmulArgs& a, bool shared_coef, hipStream_t s)
 {

@@ -461,18 +461,44 @@ int decode_device(nfec_codec* c, const nfec_block_batch* b, const uint16_t* locs
             d.z_block_stride = (uint64_t)c->cs * zstride;
             d.z_stride = zstride;
             if ((rc = launch_rs8_bitsliced_reencode(c->k, c->m, d, s))) return fail(rc, "bit-sliced re-encode launch failed");
-            Gf8MatmulArgs a2;
-            a2.in_base = c->w_z.p;
-            a2.in_block_stride = (uint64_t)c->cs * zstride;
-            a2.in_seg_stride = zstride;
-            a2.in_count = c->w_cols.p;
-            a2.out_base = blocks;
+            static const bool use_solve = [] {
+                const char* e = std::getenv("NFEC_SOLVE");
+                return !(e && e[0] == '0');
+            }();
+            if (!use_solve) {
+                Gf8MatmulArgs g2;
+                g2.in_base = c->w_z.p;
+                g2.in_block_stride = (uint64_t)c->cs * zstride;
+                g2.in_seg_stride = zstride;
+                g2.in_count = c->w_cols.p;
+                g2.out_base = blocks;
+                g2.out_block_stride = b->block_stride;
+                g2.out_seg_stride = b->seg_stride;
+                g2.out_slots = c->w_oslots.p;
+                g2.out_slot_mode = OUT_SLOT_LIST;
+                g2.row_count = c->w_rows.p;
+                g2.slots_stride = c->k;
+                g2.coef = c->w_coef2.p;
+                g2.coef_block_stride = (uint64_t)c->cs * c->cs;
+                g2.coef_col_stride = c->cs;
+                g2.vtab = c->d_vtab.p;
+                g2.nblocks = nb;
+                g2.vec_bytes = c->vec;
+                g2.accumulate = acc;
+                if ((rc = launch_gf8_matmul(g2, false, s))) return rc;
+                continue;
+            }
+            Gf8SolveArgs a2;
+            a2.z = c->w_z.p;
+            a2.z_block_stride = (uint64_t)c->cs * zstride;
+            a2.z_stride = zstride;
+            a2.cols = c->w_cols.p;
+            a2.rows = c->w_rows.p;
+            a2.out_slots = c->w_oslots.p;
+            a2.slots_stride = c->k;
+            a2.out = blocks;
             a2.out_block_stride = b->block_stride;
             a2.out_seg_stride = b->seg_stride;
-            a2.out_slots = c->w_oslots.p;
-            a2.out_slot_mode = OUT_SLOT_LIST;
-            a2.row_count = c->w_rows.p;
-            a2.slots_stride = c->k;
             a2.coef = c->w_coef2.p;
             a2.coef_block_stride = (uint64_t)c->cs * c->cs;
             a2.coef_col_stride = c->cs;
@@ -480,7 +506,7 @@ int decode_device(nfec_codec* c, const nfec_block_batch* b, const uint16_t* locs
             a2.nblocks = nb;
             a2.vec_bytes = c->vec;
             a2.accumulate = acc;
-            if ((rc = launch_gf8_matmul(a2, false, s))) return rc;
+            if ((rc = launch_gf8_solve(a2, std::min(c->m, c->k), c->m, s))) return rc;
             continue;
         }
         RsPlanArgs p;

@@ -97,6 +97,29 @@ struct Gf8MatmulArgs {
 };
 int launch_gf8_matmul(const Gf8MatmulArgs& a, bool shared_coef, hipStream_t s);
 
+// per-block square solve: out[b][out_slots[b][r]] (^)= XOR_t coef[b][t][r] (x) z[b][t]
+// (rows(b) <= 16, cols(b) <= 32; NFEC_ENOTSUP beyond)
+struct Gf8SolveArgs {
+    const uint8_t* z = nullptr;
+    uint64_t z_block_stride = 0;
+    uint32_t z_stride = 0;
+    const uint16_t* cols = nullptr;      // per block: z rows used
+    const int32_t* rows = nullptr;       // per block: outputs (<= 0: skip block)
+    const uint16_t* out_slots = nullptr; // [b*slots_stride + r]
+    uint32_t slots_stride = 0;
+    uint8_t* out = nullptr;
+    uint64_t out_block_stride = 0;
+    uint32_t out_seg_stride = 0;
+    const uint8_t* coef = nullptr;       // coef[b*coef_block_stride + t*coef_col_stride + r]
+    uint64_t coef_block_stride = 0;
+    uint32_t coef_col_stride = 0;
+    const uint32_t* vtab = nullptr;
+    uint32_t nblocks = 0;
+    uint32_t vec_bytes = 0;
+    uint32_t accumulate = 0;
+};
+int launch_gf8_solve(const Gf8SolveArgs& a, uint32_t max_rows, uint32_t max_cols, hipStream_t s);
+
 // GF(2^16) variant (log/exp); coef holds generator elements (uint16) at the same indexing.
 struct Gf16MatmulArgs {
     const uint8_t* in_base = nullptr;

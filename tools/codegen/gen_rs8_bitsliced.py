@@ -432,7 +432,7 @@ def main():
     parts.append("// Returns NFEC_ENOTSUP when no specialised kernel exists for (k, m).")
     parts.append("int launch_rs8_bitsliced_encode(uint32_t k, uint32_t m, const bs::EncArgs& a, hipStream_t s)")
     parts.append("{")
-    parts.append("    static const int variant = [] { const char* e = std::getenv(\"NFEC_BS_VARIANT\"); return e ? std::atoi(e) : 1; }();")
+    parts.append("    static const int variant = [] { const char* e = std::getenv(\"NFEC_BS_VARIANT\"); return e ? std::atoi(e) : 0; }();")
     for k, m in shapes:
         if m <= 32:
             parts.append(f"    if (k == {k} && m == {m} && variant == 1) return launch_rs8_lenc_k{k}_m{m}(a, s);")
