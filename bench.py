@@ -159,8 +159,10 @@ def main():
         keep = blocks.clone()
         from norm_amd import zero_erasures
 
+        # erase, repair with the parity the timed encodes produced: a wrong encode or a
+        # wrong decode both break the round trip
         zero_erasures(blocks, locs, counts, vec, stream=stream)
-        step()
+        dec.decode_blocks(blocks, locs, counts, status=status, stream=stream)
         torch.cuda.synchronize(dev)
         ok = bool(torch.equal(blocks, keep)) and bool((status == a.erasures).all())
 

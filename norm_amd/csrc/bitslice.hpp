@@ -62,6 +62,28 @@ __device__ __forceinline__ void transpose8(uint32_t& w0, uint32_t& w1, uint32_t&
     swapmove<1, 0x55555555u>(w6, w7);
 }
 
+// Buffer descriptor over a wave-uniform base: loads/stores then take a 32-bit VGPR offset
+// (the item) plus an SGPR offset (the slot), so no 64-bit address arithmetic per column.
+// num_records = 2^32-1: the launchers keep every offset a wave uses below 2^31.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* base)
+{
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, -1, 0x00020000);
+}
+
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+
+// a wave's items span at most 3 blocks and 256 slots: every buffer offset stays < 2^31
+inline bool offsets_fit(uint64_t block_stride, uint64_t seg_stride)
+{
+    return 3 * block_stride + 256 * seg_stride < (1ull << 31);
+}
+
+__device__ __forceinline__ uint2 bld8(__amdgpu_buffer_rsrc_t rs, uint32_t voff, uint32_t soff)
+{
+    const u32x2 v = __builtin_amdgcn_raw_buffer_load_b64(rs, voff, soff, 0);
+    return make_uint2(v.x, v.y);
+}
+
 struct EncArgs {
     const uint8_t* base = nullptr;   // block 0 slot 0
     uint8_t* out = nullptr;          // parity destination base (== base for in-place encode)
@@ -71,6 +93,8 @@ struct EncArgs {
     uint32_t vec = 0;
     const uint16_t* num_data = nullptr;  // per block (null: k)
     uint32_t accumulate = 0;
+    uint32_t xcd_remap = 0;   // nonzero: give each XCD a contiguous range of workgroups
+    uint32_t nt_store = 0;    // nonzero: nontemporal parity stores
 };
 
 // per-lane item geometry for the 4 items of a lane (all blocks hold k source symbols; the
@@ -80,6 +104,8 @@ struct EncArgs {
 struct Items {
     const uint8_t* wbase;   // uniform: slot 0 of the wave's first block
     uint8_t* obase;         // uniform: same block in the output batch
+    __amdgpu_buffer_rsrc_t rs;   // buffer descriptors over wbase / obase (32-bit offsets)
+    __amdgpu_buffer_rsrc_t ors;
     uint32_t off[4];        // per lane: byte offset of item i (clamped to a valid item)
     uint32_t nbytes[4];     // valid bytes in the item (0 if out of range, <8 for the tail)
 };
@@ -91,6 +117,8 @@ __device__ __forceinline__ void make_items(const EncArgs& a, uint32_t item_base,
     const uint32_t b0 = __builtin_amdgcn_readfirstlane(min(item_base, total - 1) / ips);
     it.wbase = a.base + (uint64_t)b0 * a.block_stride;
     it.obase = a.out + (uint64_t)b0 * a.block_stride;
+    it.rs = rsrc(it.wbase);
+    it.ors = rsrc(it.obase);
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
         const uint32_t g = item_base + (uint32_t)i * 64u + lane;
@@ -116,10 +144,26 @@ struct DecArgs {
     uint8_t* z = nullptr;             // [b][cs][z_stride] stage-1 output z_t
     uint64_t z_block_stride = 0;
     uint32_t z_stride = 0;
+    uint32_t xcd_remap = 0;
 };
+
+// Workgroup -> work index.  The dispatcher deals workgroups round-robin over the 8 XCDs
+// (each with its own L2); with remap on, XCD x gets the contiguous index range
+// [x*q + min(x, r), ...) so neighbouring items (which share 128-byte lines at their
+// boundaries) are fetched through one L2 instead of two.
+__device__ __forceinline__ uint32_t wg_index(uint32_t remap)
+{
+    const uint32_t bid = blockIdx.x;
+    if (!remap) return bid;
+    constexpr uint32_t kXcd = 8;
+    const uint32_t n = gridDim.x, q = n / kXcd, r = n % kXcd;
+    const uint32_t x = bid % kXcd, i = bid / kXcd;
+    return x < r ? x * (q + 1) + i : r * (q + 1) + (x - r) * q + i;
+}
 
 struct DecItems {
     const uint8_t* wbase;   // uniform: slot 0 of the wave's first block
+    __amdgpu_buffer_rsrc_t rs;
     uint32_t off[4];        // per lane: byte offset of item i from wbase (slot 0)
     uint32_t blk[4];        // absolute block index of item i
     uint32_t ib[4];         // byte offset of item i inside a segment
@@ -134,6 +178,7 @@ __device__ __forceinline__ void make_dec_items(const DecArgs& a, uint32_t item_b
     const uint32_t total = a.nblocks * ips;
     const uint32_t b0 = __builtin_amdgcn_readfirstlane(min(item_base, total - 1) / ips);
     it.wbase = a.base + (uint64_t)b0 * a.block_stride;
+    it.rs = rsrc(it.wbase);
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
         const uint32_t g = item_base + (uint32_t)i * 64u + lane;
@@ -159,30 +204,6 @@ __device__ __forceinline__ void mask_item(uint32_t& x, uint32_t& y, uint32_t emw
     y = __builtin_amdgcn_bitop3_b32(y, m, 0u, 0x30);
 }
 
-// LDS-DMA: each lane copies 4 bytes from gbase + off into LDS at lds_base + 4*lane.  Issued
-// through inline asm because LLVM does not model the builtin's LDS write (it dropped the
-// subsequent LDS reads in a probe); completion is tracked by hand with s_waitcnt vmcnt.
-__device__ __forceinline__ void dma4(const uint8_t* gbase, uint32_t off, uint32_t lds_base)
-{
-    asm volatile("s_mov_b32 m0, %0\n\tglobal_load_lds_dword %1, %2"
-                 :
-                 : "s"(lds_base), "v"(off), "s"(gbase)
-                 : "memory", "m0");
-}
-
-// wait until at most N vector-memory ops of this wave are outstanding, then workgroup barrier
-template <int N>
-__device__ __forceinline__ void wait_barrier()
-{
-    asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" : : "n"(N) : "memory");
-}
-
-__device__ __forceinline__ uint2 lds_item(const uint32_t* slot, uint32_t item, uint32_t lane)
-{
-    // the two dwords of an 8-byte item were written by two 256-byte DMA pieces
-    return make_uint2(slot[item * 128 + lane], slot[item * 128 + 64 + lane]);
-}
-
 __device__ __forceinline__ uint2 ld8(const uint8_t* base, uint32_t off)
 {
     return *reinterpret_cast<const uint2*>(base + off);
@@ -201,6 +222,21 @@ __device__ __forceinline__ void st8(uint8_t* p, uint32_t x, uint32_t y, uint32_t
     } else {
         for (uint32_t i = 0; i < nbytes; ++i) p[i] = (uint8_t)((i < 4 ? x : y) >> (8 * (i & 3)));
     }
+}
+
+// parity store through the output descriptor (full items), byte stores for the tail
+__device__ __forceinline__ void bst8(const Items& it, uint32_t voff, uint32_t soff, uint32_t x, uint32_t y,
+                                     uint32_t nbytes, uint32_t accumulate, uint32_t nt)
+{
+    if (nbytes >= 8 && !accumulate) {
+        u32x2 v;
+        v.x = x;
+        v.y = y;
+        if (nt) __builtin_amdgcn_raw_buffer_store_b64(v, it.ors, voff, soff, 2);
+        else __builtin_amdgcn_raw_buffer_store_b64(v, it.ors, voff, soff, 0);
+        return;
+    }
+    st8(it.obase + soff + voff, x, y, nbytes, accumulate);
 }
 
 }  // namespace bs

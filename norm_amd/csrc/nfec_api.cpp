@@ -262,6 +262,17 @@ bool has_bitsliced(uint32_t k, uint32_t m)
     return bitsliced_encode_generator(k, m, scratch.data()) == NFEC_OK;
 }
 
+// tuning knobs of the bit-sliced kernels (A/B runs): bit 0 XCD-contiguous workgroup
+// mapping, bit 1 nontemporal parity stores
+static uint32_t bs_flags()
+{
+    static const uint32_t f = [] {
+        const char* e = std::getenv("NFEC_BS_FLAGS");
+        return e ? (uint32_t)std::strtoul(e, nullptr, 0) : 0u;
+    }();
+    return f;
+}
+
 // ---- encode on a device batch ----
 int encode_device(nfec_codec* c, const nfec_block_batch* b, hipStream_t s)
 {
@@ -277,6 +288,8 @@ int encode_device(nfec_codec* c, const nfec_block_batch* b, hipStream_t s)
         e.vec = c->vec;
         e.num_data = b->num_data;
         e.accumulate = acc;
+        e.xcd_remap = bs_flags() & 1u;
+        e.nt_store = (bs_flags() >> 1) & 1u;
         const int rc = launch_rs8_bitsliced_encode(c->k, c->m, e, s);
         if (rc != NFEC_ENOTSUP) return rc == NFEC_OK ? NFEC_OK : fail(rc, "bit-sliced encode launch failed");
     }
@@ -371,7 +384,7 @@ int decode_device(nfec_codec* c, const nfec_block_batch* b, const uint16_t* locs
         if (c->m > 64 && (rc = c->w_work.reserve((size_t)sb * c->m * 2 * c->m * c->sym))) return rc;
     }
     const bool fast = c->kind == NFEC_RS8 && !b->num_data && c->m <= 32 && c->k <= 64 && !force_generic() &&
-                      has_bitsliced(c->k, c->m);
+                      has_bitsliced(c->k, c->m) && bs::offsets_fit(b->block_stride, b->seg_stride);
     if (fast) {
         if ((rc = c->w_emask.reserve((size_t)sb * 2))) return rc;
         if ((rc = c->w_psel.reserve((size_t)sb * 2))) return rc;
@@ -460,6 +473,7 @@ int decode_device(nfec_codec* c, const nfec_block_batch* b, const uint16_t* locs
             d.z = c->w_z.p;
             d.z_block_stride = (uint64_t)c->cs * zstride;
             d.z_stride = zstride;
+            d.xcd_remap = bs_flags() & 1u;
             if ((rc = launch_rs8_bitsliced_reencode(c->k, c->m, d, s))) return fail(rc, "bit-sliced re-encode launch failed");
             static const bool use_solve = [] {
                 const char* e = std::getenv("NFEC_SOLVE");

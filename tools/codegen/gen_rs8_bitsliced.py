@@ -14,18 +14,38 @@ four at a time (method of four Russians): T_lo[a] = XOR of planes {b<4 : a_b}, T
 The code is straight-line (~100 KiB per role); measurements showed no instruction-cache
 penalty for streams of that size.
 
-Parity rows are split into roles of ROWS_PER_ROLE rows; each role is one wavefront that keeps
-ROWS_PER_ROLE x 8 accumulators, so two waves per SIMD stay resident.
+Parity rows are split into roles of Cfg.rows rows; each role is one wavefront that keeps
+rows x 8 plane accumulators in VGPRs (the register budget, hence the occupancy, is set by
+the role size; see Cfg).
 
 Usage: gen_rs8_bitsliced.py OUT.hip [k,m ...]
 """
 import sys
 
 POLY = 0x11D
-ROWS_PER_ROLE = 16
-PF = 3  # source columns in flight per wave (prefetch depth, register ring)
-RING = 8  # LDS ring depth (columns in flight per workgroup) for the LDS-staged encode
 DEFAULT_SHAPES = [(64, 32), (64, 16), (64, 8)]
+
+
+class Cfg:
+    """Code shape of one kernel build.
+    rows: parity rows per role (one wavefront keeps rows x 8 plane accumulators)
+    pf:   source columns in flight per wave (register prefetch ring)
+    wpe:  occupancy target (waves per SIMD) handed to the register allocator, or None
+    lazy: emit the plane updates grouped by low-table entry, so at most one low entry is
+          live at a time (shorter live ranges; lets higher occupancy targets fit)"""
+
+    def __init__(self, rows=16, pf=3, wpe=None, lazy=False, suffix=""):
+        self.rows, self.pf, self.wpe, self.lazy, self.suffix = rows, pf, wpe, lazy, suffix
+
+
+DEFAULT = Cfg(rows=16, pf=3, lazy=True)
+DEC_DEFAULT = Cfg(rows=16, pf=3, lazy=False)
+# extra (64,32) encode builds selectable with NFEC_BS_VARIANT=<id> for A/B runs
+VARIANTS_64_32 = {
+    2: Cfg(rows=12, pf=3, wpe=3, lazy=True, suffix="_v2"),
+    3: Cfg(rows=8, pf=3, wpe=4, lazy=True, suffix="_v3"),
+    4: Cfg(rows=16, pf=4, lazy=True, suffix="_v4"),
+}
 
 
 def gf_tables():
@@ -94,7 +114,6 @@ def table_expr(prefix, base, a):
 def table_defs(prefix, base, needed):
     """Definitions of the multi-plane combinations actually used."""
     out = []
-    defs = {}
     for a in sorted(needed):
         bits = [b for b in range(4) if (a >> b) & 1]
         if len(bits) < 2:
@@ -106,29 +125,43 @@ def table_defs(prefix, base, needed):
             out.append(f"const uint32_t {prefix}{a} = bs::x3({ws[0]}, {ws[1]}, {ws[2]});")
         else:
             out.append(f"const uint32_t {prefix}{a} = bs::x3({ws[0]}, {ws[1]}, {ws[2]}) ^ {ws[3]};")
-        defs[a] = True
     return out
 
 
-def prologue_loads(L, k):
+def acc_update(acc, R):
+    lo, hi = R & 15, R >> 4
+    if lo and hi:
+        return f"{acc} = bs::x3({acc}, {table_expr('L', 0, lo)}, {table_expr('H', 4, hi)});"
+    if lo:
+        return f"{acc} = bs::x2({acc}, {table_expr('L', 0, lo)});"
+    if hi:
+        return f"{acc} = bs::x2({acc}, {table_expr('H', 4, hi)});"
+    return None
+
+
+def col_loads(q, col):
+    """Refill prefetch slot q with source column col (buffer loads: VGPR item offset + SGPR slot offset)."""
+    return "; ".join(f"n{q}_{i} = bs::bld8(it.rs, o{i}, {col}u * sstride)" for i in range(4)) + ";"
+
+
+def prologue_loads(L, k, cfg):
     L.append("    uint32_t w0, w1, w2, w3, w4, w5, w6, w7;")
-    for r in range(PF):
+    for r in range(cfg.pf):
         L.append(f"    uint2 n{r}_0, n{r}_1, n{r}_2, n{r}_3;")
-    for r in range(min(PF, k)):
-        L.append(f"    {{ const uint8_t* c = it.wbase + {r} * stride; n{r}_0 = bs::ld8(c, o0); n{r}_1 = bs::ld8(c, o1); "
-                 f"n{r}_2 = bs::ld8(c, o2); n{r}_3 = bs::ld8(c, o3); }}")
+    for r in range(min(cfg.pf, k)):
+        L.append(f"    " + col_loads(r, r))
 
 
-def column_body(L, G, k, r0, rows, j, masked):
+def column_body(L, G, k, r0, rows, j, masked, cfg):
     """Code for source column j: take it from the prefetch ring, refill the ring slot with
-    column j+PF, (mask erased), transpose, M4RM update."""
+    column j+pf, (mask erased), transpose, M4RM update."""
+    pf = cfg.pf
     L.append(f"    // ---- source column {j} ----")
-    q = j % PF
+    q = j % pf
     L.append(f"    w0 = n{q}_0.x; w1 = n{q}_0.y; w2 = n{q}_1.x; w3 = n{q}_1.y; w4 = n{q}_2.x; w5 = n{q}_2.y; "
              f"w6 = n{q}_3.x; w7 = n{q}_3.y;")
-    if j + PF < k:
-        L.append(f"    {{ const uint8_t* c = it.wbase + {j + PF} * stride; n{q}_0 = bs::ld8(c, o0); n{q}_1 = bs::ld8(c, o1); "
-                 f"n{q}_2 = bs::ld8(c, o2); n{q}_3 = bs::ld8(c, o3); }}")
+    if j + pf < k:
+        L.append("    " + col_loads(q, j + pf))
     L.append("    __builtin_amdgcn_sched_barrier(0);")
     if masked:
         word = "em0" if j < 32 else "em1"
@@ -137,61 +170,81 @@ def column_body(L, G, k, r0, rows, j, masked):
             L.append(f"    bs::mask_item(w{2 * i}, w{2 * i + 1}, it.{word}[{i}], {bit});")
     L.append("    bs::transpose8(w0, w1, w2, w3, w4, w5, w6, w7);")
     mats = [bitmatrix_rows(G[r0 + r][j]) for r in range(rows)]
-    need_lo = {R & 15 for rr in mats for R in rr if R & 15}
-    need_hi = {R >> 4 for rr in mats for R in rr if R >> 4}
+    outs = [(f"a{r}_{i}", mats[r][i]) for r in range(rows) for i in range(8)]
+    need_lo = {R & 15 for _, R in outs if R & 15}
+    need_hi = {R >> 4 for _, R in outs if R >> 4}
     L.append("    {")
-    for d in table_defs("L", 0, need_lo) + table_defs("H", 4, need_hi):
-        L.append("        " + d)
-    for r in range(rows):
-        for i in range(8):
-            R = mats[r][i]
-            lo, hi = R & 15, R >> 4
-            acc = f"a{r}_{i}"
-            if lo and hi:
-                L.append(f"        {acc} = bs::x3({acc}, {table_expr('L', 0, lo)}, {table_expr('H', 4, hi)});")
-            elif lo:
-                L.append(f"        {acc} = bs::x2({acc}, {table_expr('L', 0, lo)});")
-            elif hi:
-                L.append(f"        {acc} = bs::x2({acc}, {table_expr('H', 4, hi)});")
+    if not cfg.lazy:
+        for d in table_defs("L", 0, need_lo) + table_defs("H", 4, need_hi):
+            L.append("        " + d)
+        for acc, R in outs:
+            u = acc_update(acc, R)
+            if u:
+                L.append("        " + u)
+    else:
+        # high entries first (<= 11 multi-plane ones live), then one low entry at a time
+        # together with all of its users
+        for d in table_defs("H", 4, need_hi):
+            L.append("        " + d)
+        for acc, R in outs:
+            if not R & 15 and R >> 4:
+                L.append("        " + acc_update(acc, R))
+        for lo in sorted(need_lo):
+            L.append("        {")
+            for d in table_defs("L", 0, {lo}):
+                L.append("            " + d)
+            for acc, R in outs:
+                if R & 15 == lo:
+                    L.append("            " + acc_update(acc, R))
+            L.append("        }")
     L.append("    }")
-    accs = [f"a{r}_{i}" for r in range(rows) for i in range(8)]
+    accs = [a for a, _ in outs]
     for c0 in range(0, len(accs), 16):
         grp = accs[c0:c0 + 16]
         L.append('    asm volatile("" : ' + ", ".join(f'"+v"({x})' for x in grp) + ' :: "memory");')
 
 
-def gen_dec_role(k, m, role, rows):
+def kernel_attrs(cfg, threads=256):
+    a = f"__launch_bounds__({threads}, 2)"
+    if cfg.wpe:
+        a += f" __attribute__((amdgpu_waves_per_eu({cfg.wpe}, {cfg.wpe})))"
+    return a
+
+
+def role_split(m, cfg):
+    roles = (m + cfg.rows - 1) // cfg.rows
+    return [(r * cfg.rows, min(cfg.rows, m - r * cfg.rows)) for r in range(roles)]
+
+
+def gen_dec_role(k, m, role, r0, rows, cfg):
     """Decode stage 1 for parity rows [r0, r0+rows): z_t = parity_p ^ G[p][present] * data."""
     G = generator(k, m)
-    r0 = role * ROWS_PER_ROLE
     L = []
-    L.append(f"__device__ __forceinline__ void dec_k{k}_m{m}_role{role}(const bs::DecArgs& a, const bs::DecItems& it)")
+    L.append(f"__device__ __forceinline__ void dec{cfg.suffix}_k{k}_m{m}_role{role}(const bs::DecArgs& a, "
+             f"const bs::DecItems& it)")
     L.append("{")
-    L.append("    const uint64_t stride = a.seg_stride;")
+    L.append("    const uint32_t sstride = a.seg_stride;")
     L.append("    const uint32_t o0 = it.off[0], o1 = it.off[1], o2 = it.off[2], o3 = it.off[3];")
     for r in range(rows):
         L.append("    uint32_t " + ", ".join(f"a{r}_{i} = 0" for i in range(8)) + ";")
-    prologue_loads(L, k)
+    prologue_loads(L, k, cfg)
     for j in range(k):
-        column_body(L, G, k, r0, rows, j, masked=True)
+        column_body(L, G, k, r0, rows, j, True, cfg)
     L.append("    // ---- z_t = received parity p ^ re-encoded row p, for the rows P uses ----")
     L.append("    // t = rank of row p among the used rows (P is the first e surviving parity rows in")
     L.append("    // ascending order), so no table lookup; received parity is prefetched 4 rows ahead.")
-    L.append(f"    const uint8_t* par = it.wbase + {k} * stride;")
-    AHEAD = min(4, rows)
-    for r in range(AHEAD):
+    ahead = min(4, rows)
+    for r in range(ahead):
         p = r0 + r
-        L.append(f"    uint2 q{r}_0 = bs::ld8(par + {p} * stride, o0), q{r}_1 = bs::ld8(par + {p} * stride, o1), "
-                 f"q{r}_2 = bs::ld8(par + {p} * stride, o2), q{r}_3 = bs::ld8(par + {p} * stride, o3);")
+        L.append(f"    uint2 " + ", ".join(f"q{r}_{i} = bs::bld8(it.rs, o{i}, {k + p}u * sstride)" for i in range(4)) + ";")
     for r in range(rows):
         p = r0 + r
-        q = r % AHEAD
-        L.append(f"    {{")
+        q = r % ahead
+        L.append("    {")
         L.append(f"        const uint2 c0 = q{q}_0, c1 = q{q}_1, c2 = q{q}_2, c3 = q{q}_3;")
-        if r + AHEAD < rows:
-            pn = r0 + r + AHEAD
-            L.append(f"        q{q}_0 = bs::ld8(par + {pn} * stride, o0); q{q}_1 = bs::ld8(par + {pn} * stride, o1); "
-                     f"q{q}_2 = bs::ld8(par + {pn} * stride, o2); q{q}_3 = bs::ld8(par + {pn} * stride, o3);")
+        if r + ahead < rows:
+            pn = r0 + r + ahead
+            L.append("        " + "; ".join(f"q{q}_{i} = bs::bld8(it.rs, o{i}, {k + pn}u * sstride)" for i in range(4)) + ";")
         L.append(f"        bs::transpose8(a{r}_0, a{r}_1, a{r}_2, a{r}_3, a{r}_4, a{r}_5, a{r}_6, a{r}_7);")
         for i in range(4):
             L.append(f"        if ((it.sel[{i}] >> {p}) & 1u) {{")
@@ -204,35 +257,30 @@ def gen_dec_role(k, m, role, rows):
     return "\n".join(L)
 
 
-def gen_dec_kernel(k, m):
-    roles = (m + ROWS_PER_ROLE - 1) // ROWS_PER_ROLE
-    out = []
-    for role in range(roles):
-        rows = min(ROWS_PER_ROLE, m - role * ROWS_PER_ROLE)
-        out.append(gen_dec_role(k, m, role, rows))
+def gen_dec_kernel(k, m, cfg):
+    split = role_split(m, cfg)
+    out = [gen_dec_role(k, m, role, r0, rows, cfg) for role, (r0, rows) in enumerate(split)]
     groups = 4
-    K = f"rs8_dec_k{k}_m{m}"
-    body = [f"__global__ __launch_bounds__(256, 2) void {K}(bs::DecArgs a)", "{"]
+    K = f"rs8_dec{cfg.suffix}_k{k}_m{m}"
+    body = [f"__global__ {kernel_attrs(cfg)} void {K}(bs::DecArgs a)", "{"]
     body.append("    const uint32_t lane = threadIdx.x & 63;")
     body.append("    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);")
-    body.append(f"    const uint64_t group = (uint64_t)blockIdx.x * {groups} + wave;")
+    body.append(f"    const uint64_t group = (uint64_t)bs::wg_index(a.xcd_remap) * {groups} + wave;")
     body.append("    bs::DecItems it;")
     body.append("    bs::make_dec_items(a, (uint32_t)group * 256u, lane, it);")
     body.append("    const uint32_t need = it.sel[0] | it.sel[1] | it.sel[2] | it.sel[3];")
-    for role in range(roles):
-        lo = role * ROWS_PER_ROLE
-        rows = min(ROWS_PER_ROLE, m - lo)
-        rmask = ((1 << rows) - 1) << lo
-        # every wave handles all roles its blocks need (usually only the first: P is the
-        # first e surviving parity rows); unused roles cost nothing
-        body.append(f"    if (__any(need & 0x{rmask:08x}u)) dec_k{k}_m{m}_role{role}(a, it);")
+    for role, (r0, rows) in enumerate(split):
+        rmask = ((1 << rows) - 1) << r0
+        # every wave handles all roles its blocks need (usually only the first ones: P is
+        # the first e surviving parity rows); unused roles cost nothing
+        body.append(f"    if (__any(need & 0x{rmask:08x}u)) dec{cfg.suffix}_k{k}_m{m}_role{role}(a, it);")
     body.append("}")
     out.append("\n".join(body))
     out.append(f"""
 static int launch_{K}(const bs::DecArgs& a, hipStream_t s)
 {{
     const uint64_t items = (uint64_t)a.nblocks * ((a.vec + 7) / 8);
-    if (items >= (1ull << 31)) return NFEC_ENOTSUP;
+    if (items >= (1ull << 31) || !bs::offsets_fit(a.block_stride, a.seg_stride)) return NFEC_ENOTSUP;
     const uint64_t groups = (items + 255) / 256;
     const uint64_t wgs = (groups + {groups} - 1) / {groups};
     hipLaunchKernelGGL({K}, dim3((uint32_t)wgs), dim3(256), 0, s, a);
@@ -241,169 +289,62 @@ static int launch_{K}(const bs::DecArgs& a, hipStream_t s)
     return "\n\n".join(out)
 
 
-def gen_role(k, m, role, rows):
+def gen_role(k, m, role, r0, rows, cfg):
     """Device function computing parity rows [r0, r0+rows) of one lane's 4 items."""
     G = generator(k, m)
-    r0 = role * ROWS_PER_ROLE
     L = []
-    fn = f"enc_k{k}_m{m}_role{role}"
-    L.append(f"__device__ __forceinline__ void {fn}(const bs::EncArgs& a, const bs::Items& it)")
+    L.append(f"__device__ __forceinline__ void enc{cfg.suffix}_k{k}_m{m}_role{role}(const bs::EncArgs& a, "
+             f"const bs::Items& it)")
     L.append("{")
-    L.append("    const uint64_t stride = a.seg_stride;")
+    L.append("    const uint32_t sstride = a.seg_stride;")
     L.append("    const uint32_t o0 = it.off[0], o1 = it.off[1], o2 = it.off[2], o3 = it.off[3];")
     for r in range(rows):
         L.append("    uint32_t " + ", ".join(f"a{r}_{i} = 0" for i in range(8)) + ";")
-    prologue_loads(L, k)
+    prologue_loads(L, k, cfg)
     for j in range(k):
-        column_body(L, G, k, r0, rows, j, masked=False)
+        column_body(L, G, k, r0, rows, j, False, cfg)
     L.append("    // ---- parity planes back to bytes, store ----")
     for r in range(rows):
         p = r0 + r
         L.append(f"    bs::transpose8(a{r}_0, a{r}_1, a{r}_2, a{r}_3, a{r}_4, a{r}_5, a{r}_6, a{r}_7);")
         for i in range(4):
-            L.append(f"    bs::st8(it.obase + {k + p} * stride + o{i}, a{r}_{2 * i}, a{r}_{2 * i + 1}, it.nbytes[{i}], a.accumulate);")
+            L.append(f"    bs::bst8(it, o{i}, {k + p}u * sstride, a{r}_{2 * i}, a{r}_{2 * i + 1}, "
+                     f"it.nbytes[{i}], a.accumulate, a.nt_store);")
     L.append("}")
     return "\n".join(L)
 
 
-def gen_lds_role(k, m, role, rows, roles):
-    """Encode role with the source staged through an LDS ring shared by the role-waves of a
-    group: each wave DMAs its share of a column's 8 dword pieces, one barrier per column."""
-    G = generator(k, m)
-    r0 = role * ROWS_PER_ROLE
-    pieces = [(i, h) for i in range(4) for h in range(2)]
-    mine = [pc for n, pc in enumerate(pieces) if n % roles == role]
-    L = []
-    L.append(f"__device__ __forceinline__ void lenc_k{k}_m{m}_role{role}(const bs::EncArgs& a, const bs::Items& it, "
-             f"uint32_t* ring, uint32_t lane)")
-    L.append("{")
-    L.append("    const uint64_t stride = a.seg_stride;")
-    L.append("    const uint32_t o0 = it.off[0], o1 = it.off[1], o2 = it.off[2], o3 = it.off[3];")
-    L.append("    const uint32_t ring_base = (uint32_t)(uintptr_t)ring;")
-    for r in range(rows):
-        L.append("    uint32_t " + ", ".join(f"a{r}_{i} = 0" for i in range(8)) + ";")
-    L.append("    uint32_t w0, w1, w2, w3, w4, w5, w6, w7;")
-
-    def issue(col, indent="    "):
-        slot = col % RING
-        out = [f"{indent}{{ const uint8_t* c = it.wbase + {col} * stride;"]
-        for (i, h) in mine:
-            out.append(f"{indent}  bs::dma4(c, o{i} + {4 * h}, ring_base + {slot * 2048 + (2 * i + h) * 256}u);")
-        out.append(f"{indent}}}")
-        return out
-
-    for col in range(min(RING - 1, k)):
-        L.extend(issue(col))
-    per = len(mine)
-    for j in range(k):
-        L.append(f"    // ---- source column {j} ----")
-        issued_after = min(j + RING - 2, k - 1) - j  # columns issued after column j so far
-        L.append(f"    bs::wait_barrier<{per * issued_after}>();")
-        if j + RING - 1 < k:
-            L.extend(issue(j + RING - 1))
-        slot = j % RING
-        L.append(f"    {{ const uint32_t* sl = ring + {slot * 512};")
-        for i in range(4):
-            L.append(f"      const uint2 v{i} = bs::lds_item(sl, {i}, lane);")
-        L.append("      w0 = v0.x; w1 = v0.y; w2 = v1.x; w3 = v1.y; w4 = v2.x; w5 = v2.y; w6 = v3.x; w7 = v3.y; }")
-        L.append("    bs::transpose8(w0, w1, w2, w3, w4, w5, w6, w7);")
-        mats = [bitmatrix_rows(G[r0 + r][j]) for r in range(rows)]
-        need_lo = {R & 15 for rr in mats for R in rr if R & 15}
-        need_hi = {R >> 4 for rr in mats for R in rr if R >> 4}
-        L.append("    {")
-        for d in table_defs("L", 0, need_lo) + table_defs("H", 4, need_hi):
-            L.append("        " + d)
-        for r in range(rows):
-            for i in range(8):
-                R = mats[r][i]
-                lo, hi = R & 15, R >> 4
-                acc = f"a{r}_{i}"
-                if lo and hi:
-                    L.append(f"        {acc} = bs::x3({acc}, {table_expr('L', 0, lo)}, {table_expr('H', 4, hi)});")
-                elif lo:
-                    L.append(f"        {acc} = bs::x2({acc}, {table_expr('L', 0, lo)});")
-                elif hi:
-                    L.append(f"        {acc} = bs::x2({acc}, {table_expr('H', 4, hi)});")
-        L.append("    }")
-        accs = [f"a{r}_{i}" for r in range(rows) for i in range(8)]
-        for c0 in range(0, len(accs), 16):
-            grp = accs[c0:c0 + 16]
-            L.append('    asm volatile("" : ' + ", ".join(f'"+v"({x})' for x in grp) + ' :: "memory");')
-    L.append("    // ---- parity planes back to bytes, store ----")
-    for r in range(rows):
-        p = r0 + r
-        L.append(f"    bs::transpose8(a{r}_0, a{r}_1, a{r}_2, a{r}_3, a{r}_4, a{r}_5, a{r}_6, a{r}_7);")
-        for i in range(4):
-            L.append(f"    bs::st8(it.obase + {k + p} * stride + o{i}, a{r}_{2 * i}, a{r}_{2 * i + 1}, it.nbytes[{i}], a.accumulate);")
-    L.append("}")
-    return "\n".join(L)
-
-
-def gen_lds_kernel(k, m):
-    roles = (m + ROWS_PER_ROLE - 1) // ROWS_PER_ROLE
-    assert roles in (1, 2)
-    out = []
-    for role in range(roles):
-        rows = min(ROWS_PER_ROLE, m - role * ROWS_PER_ROLE)
-        out.append(gen_lds_role(k, m, role, rows, roles))
-    K = f"rs8_lenc_k{k}_m{m}"
-    threads = 64 * roles
-    body = [f"__global__ __launch_bounds__({threads}, 2) void {K}(bs::EncArgs a)", "{"]
-    body.append(f"    __shared__ __attribute__((aligned(16))) uint32_t ring[{RING} * 512];  // {RING} columns x 2 KiB")
+def gen_kernel(k, m, cfg):
+    """One workgroup = `groups` item groups x `roles` role-waves (<= 4 waves)."""
+    split = role_split(m, cfg)
+    roles = len(split)
+    groups = max(1, 4 // roles)
+    threads = 64 * roles * groups
+    out = [gen_role(k, m, role, r0, rows, cfg) for role, (r0, rows) in enumerate(split)]
+    K = f"rs8_enc{cfg.suffix}_k{k}_m{m}"
+    body = [f"__global__ {kernel_attrs(cfg, threads)} void {K}(bs::EncArgs a)", "{"]
     body.append("    const uint32_t lane = threadIdx.x & 63;")
-    body.append("    const uint32_t role = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);")
+    body.append("    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);")
+    body.append(f"    const uint32_t role = wave % {roles};")
+    body.append(f"    const uint64_t group = (uint64_t)bs::wg_index(a.xcd_remap) * {groups} + wave / {roles};")
     body.append("    bs::Items it;")
-    body.append("    bs::make_items(a, (uint32_t)blockIdx.x * 256u, lane, it);")
+    body.append("    bs::make_items(a, (uint32_t)group * 256u, lane, it);")
     for role in range(roles):
-        kw = "if" if role == 0 else "else"
-        body.append(f"    {kw} {{ lenc_k{k}_m{m}_role{role}(a, it, ring, lane); }}" if role else
-                    f"    if (role == 0) {{ lenc_k{k}_m{m}_role0(a, it, ring, lane); }}")
+        kw = "if" if role == 0 else "else if"
+        body.append(f"    {kw} (role == {role}) enc{cfg.suffix}_k{k}_m{m}_role{role}(a, it);")
     body.append("}")
     out.append("\n".join(body))
     out.append(f"""
 static int launch_{K}(const bs::EncArgs& a, hipStream_t s)
 {{
     const uint64_t items = (uint64_t)a.nblocks * ((a.vec + 7) / 8);
-    if (a.num_data || items >= (1ull << 31)) return NFEC_ENOTSUP;
-    const uint64_t groups = (items + 255) / 256;
-    hipLaunchKernelGGL({K}, dim3((uint32_t)groups), dim3({threads}), 0, s, a);
-    return hipGetLastError() == hipSuccess ? NFEC_OK : NFEC_EDEVICE;
-}}""")
-    return "\n\n".join(out)
-
-
-def gen_kernel(k, m):
-    roles = (m + ROWS_PER_ROLE - 1) // ROWS_PER_ROLE
-    assert 4 % roles == 0 or roles > 4, "roles must divide the 4 waves of a workgroup"
-    out = []
-    for role in range(roles):
-        rows = min(ROWS_PER_ROLE, m - role * ROWS_PER_ROLE)
-        out.append(gen_role(k, m, role, rows))
-    groups = max(1, 4 // roles)
-    K = f"rs8_enc_k{k}_m{m}"
-    body = [f"__global__ __launch_bounds__(256, 2) void {K}(bs::EncArgs a)", "{"]
-    body.append("    const uint32_t lane = threadIdx.x & 63;")
-    body.append("    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);")
-    body.append(f"    const uint32_t role = wave % {roles};")
-    body.append(f"    const uint64_t group = (uint64_t)blockIdx.x * {groups} + wave / {roles};")
-    body.append("    bs::Items it;")
-    body.append("    bs::make_items(a, (uint32_t)group * 256u, lane, it);")
-    for role in range(roles):
-        kw = "if" if role == 0 else "else if"
-        body.append(f"    {kw} (role == {role}) enc_k{k}_m{m}_role{role}(a, it);")
-    body.append("}")
-    out.append("\n".join(body))
-    launcher = f"""
-static int launch_{K}(const bs::EncArgs& a, hipStream_t s)
-{{
-    const uint64_t items = (uint64_t)a.nblocks * ((a.vec + 7) / 8);
-    if (a.num_data || items >= (1ull << 31)) return NFEC_ENOTSUP;  // shortened / huge batches: generic kernel
+    // shortened batches, huge batches or strides beyond 32-bit buffer offsets: generic kernel
+    if (a.num_data || items >= (1ull << 31) || !bs::offsets_fit(a.block_stride, a.seg_stride)) return NFEC_ENOTSUP;
     const uint64_t groups = (items + 255) / 256;
     const uint64_t wgs = (groups + {groups} - 1) / {groups};
-    hipLaunchKernelGGL({K}, dim3((uint32_t)wgs), dim3(256), 0, s, a);
+    hipLaunchKernelGGL({K}, dim3((uint32_t)wgs), dim3({threads}), 0, s, a);
     return hipGetLastError() == hipSuccess ? NFEC_OK : NFEC_EDEVICE;
-}}"""
-    out.append(launcher)
+}}""")
     return "\n\n".join(out)
 
 
@@ -414,28 +355,37 @@ def main():
         shapes = [tuple(int(v) for v in s.split(",")) for s in sys.argv[2:]]
     parts = [
         "// GENERATED by tools/codegen/gen_rs8_bitsliced.py -- do not edit by hand.",
-        "// Bit-sliced RS8 encode kernels specialised to the reference generator of each (k, m):",
-        "// " + ", ".join(f"({k},{m})" for k, m in shapes),
+        "// Bit-sliced RS8 encode / decode-stage-1 kernels specialised to the reference generator",
+        "// of each (k, m): " + ", ".join(f"({k},{m})" for k, m in shapes),
         '#include <cstdlib>',
         '#include "bitslice.hpp"',
         "",
         "namespace nfec {",
         "namespace {",
     ]
+    extra = {}
     for k, m in shapes:
-        parts.append(gen_kernel(k, m))
+        parts.append(gen_kernel(k, m, DEFAULT))
         if m <= 32:
-            parts.append(gen_lds_kernel(k, m))
-            parts.append(gen_dec_kernel(k, m))
+            parts.append(gen_dec_kernel(k, m, DEC_DEFAULT))
+        if (k, m) == (64, 32):
+            extra[(k, m)] = VARIANTS_64_32
+            for v, cfg in VARIANTS_64_32.items():
+                parts.append(gen_kernel(k, m, cfg))
     parts.append("}  // namespace")
+    parts.append("")
+    parts.append("static int bs_variant()")
+    parts.append("{")
+    parts.append("    static const int v = [] { const char* e = std::getenv(\"NFEC_BS_VARIANT\"); return e ? std::atoi(e) : 0; }();")
+    parts.append("    return v;")
+    parts.append("}")
     parts.append("")
     parts.append("// Returns NFEC_ENOTSUP when no specialised kernel exists for (k, m).")
     parts.append("int launch_rs8_bitsliced_encode(uint32_t k, uint32_t m, const bs::EncArgs& a, hipStream_t s)")
     parts.append("{")
-    parts.append("    static const int variant = [] { const char* e = std::getenv(\"NFEC_BS_VARIANT\"); return e ? std::atoi(e) : 0; }();")
     for k, m in shapes:
-        if m <= 32:
-            parts.append(f"    if (k == {k} && m == {m} && variant == 1) return launch_rs8_lenc_k{k}_m{m}(a, s);")
+        for v, cfg in extra.get((k, m), {}).items():
+            parts.append(f"    if (k == {k} && m == {m} && bs_variant() == {v}) return launch_rs8_enc{cfg.suffix}_k{k}_m{m}(a, s);")
         parts.append(f"    if (k == {k} && m == {m}) return launch_rs8_enc_k{k}_m{m}(a, s);")
     parts.append("    return NFEC_ENOTSUP;")
     parts.append("}")
