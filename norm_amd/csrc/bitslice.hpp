@@ -163,12 +163,19 @@ __device__ __forceinline__ uint32_t wg_index(uint32_t remap)
 
 struct DecItems {
     const uint8_t* wbase;   // uniform: slot 0 of the wave's first block
-    __amdgpu_buffer_rsrc_t rs;
+    __amdgpu_buffer_rsrc_t rs;   // num_records = 2^31: offsets with bit 31 set read as zero
+    uint32_t item_base;     // uniform
     uint32_t off[4];        // per lane: byte offset of item i from wbase (slot 0)
+    uint32_t em0[4], em1[4];  // erased source columns of item i's block
+    uint32_t need;          // OR of the used parity rows of the lane's blocks
+};
+
+// per-item data only the z stores need: rebuilt after the column loop so it is not live
+// across it
+struct DecTail {
     uint32_t blk[4];        // absolute block index of item i
     uint32_t ib[4];         // byte offset of item i inside a segment
     uint32_t nbytes[4];
-    uint32_t em0[4], em1[4];
     uint32_t sel[4];        // parity rows used by item i's block (m <= 32)
 };
 
@@ -178,7 +185,9 @@ __device__ __forceinline__ void make_dec_items(const DecArgs& a, uint32_t item_b
     const uint32_t total = a.nblocks * ips;
     const uint32_t b0 = __builtin_amdgcn_readfirstlane(min(item_base, total - 1) / ips);
     it.wbase = a.base + (uint64_t)b0 * a.block_stride;
-    it.rs = rsrc(it.wbase);
+    it.rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(it.wbase), (short)0, (int)0x80000000u, 0x00020000);
+    it.item_base = item_base;
+    it.need = 0;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
         const uint32_t g = item_base + (uint32_t)i * 64u + lane;
@@ -187,21 +196,39 @@ __device__ __forceinline__ void make_dec_items(const DecArgs& a, uint32_t item_b
         const uint32_t b = gg / ips;
         const uint32_t o = gg - b * ips;
         it.off[i] = (uint32_t)((b - b0) * a.block_stride) + o * 8u;
-        it.blk[i] = b;
-        it.ib[i] = o * 8u;
-        it.nbytes[i] = ok ? min(8u, a.vec - o * 8u) : 0u;
         it.em0[i] = a.emask[2 * (uint64_t)b];
         it.em1[i] = a.emask[2 * (uint64_t)b + 1];
-        it.sel[i] = ok ? a.psel[2 * (uint64_t)b] : 0u;
+        it.need |= ok ? a.psel[2 * (uint64_t)b] : 0u;
     }
 }
 
-// zero the 8 bytes of an item whose source column j is erased: keep = bit j clear
-__device__ __forceinline__ void mask_item(uint32_t& x, uint32_t& y, uint32_t emw, uint32_t bit)
+__device__ __forceinline__ void make_dec_tail(const DecArgs& a, const DecItems& it, DecTail& tl)
 {
-    const uint32_t m = (uint32_t)__builtin_amdgcn_sbfe((int32_t)emw, bit, 1);  // 0 or ~0
-    x = __builtin_amdgcn_bitop3_b32(x, m, 0u, 0x30);  // x & ~m
-    y = __builtin_amdgcn_bitop3_b32(y, m, 0u, 0x30);
+    const uint32_t lane = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+    const uint32_t ips = (a.vec + 7) >> 3;
+    const uint32_t total = a.nblocks * ips;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const uint32_t g = it.item_base + (uint32_t)i * 64u + lane;
+        const bool ok = g < total;
+        const uint32_t gg = ok ? g : it.item_base;
+        const uint32_t b = gg / ips;
+        const uint32_t o = gg - b * ips;
+        tl.blk[i] = b;
+        tl.ib[i] = o * 8u;
+        tl.nbytes[i] = ok ? min(8u, a.vec - o * 8u) : 0u;
+        tl.sel[i] = ok ? a.psel[2 * (uint64_t)b] : 0u;
+    }
+}
+
+// Load offset of item (offset o) in source column j: erased columns get bit 31 set, which
+// puts the access past the decode descriptor's num_records (2^31), so the buffer load
+// returns zeros without touching memory -- masking and skipping in one VALU op.
+template <int J>
+__device__ __forceinline__ uint32_t dec_off(uint32_t o, uint32_t em0, uint32_t em1)
+{
+    const uint32_t t = J < 32 ? (em0 << (31 - J)) : (em1 << (63 - J));
+    return __builtin_amdgcn_bitop3_b32(t, 0x80000000u, o, 0xEA);  // (t & bit31) | o
 }
 
 __device__ __forceinline__ uint2 ld8(const uint8_t* base, uint32_t off)

@@ -139,17 +139,21 @@ def acc_update(acc, R):
     return None
 
 
-def col_loads(q, col):
-    """Refill prefetch slot q with source column col (buffer loads: VGPR item offset + SGPR slot offset)."""
+def col_loads(q, col, masked=False):
+    """Refill prefetch slot q with source column col (buffer loads: VGPR item offset + SGPR
+    slot offset).  masked (decode): erased columns read as zeros (bs::dec_off)."""
+    if masked:
+        return "; ".join(f"n{q}_{i} = bs::bld8(it.rs, bs::dec_off<{col}>(o{i}, it.em0[{i}], it.em1[{i}]), {col}u * sstride)"
+                         for i in range(4)) + ";"
     return "; ".join(f"n{q}_{i} = bs::bld8(it.rs, o{i}, {col}u * sstride)" for i in range(4)) + ";"
 
 
-def prologue_loads(L, k, cfg):
+def prologue_loads(L, k, cfg, masked=False):
     L.append("    uint32_t w0, w1, w2, w3, w4, w5, w6, w7;")
     for r in range(cfg.pf):
         L.append(f"    uint2 n{r}_0, n{r}_1, n{r}_2, n{r}_3;")
     for r in range(min(cfg.pf, k)):
-        L.append(f"    " + col_loads(r, r))
+        L.append(f"    " + col_loads(r, r, masked))
 
 
 def column_body(L, G, k, r0, rows, j, masked, cfg):
@@ -161,13 +165,8 @@ def column_body(L, G, k, r0, rows, j, masked, cfg):
     L.append(f"    w0 = n{q}_0.x; w1 = n{q}_0.y; w2 = n{q}_1.x; w3 = n{q}_1.y; w4 = n{q}_2.x; w5 = n{q}_2.y; "
              f"w6 = n{q}_3.x; w7 = n{q}_3.y;")
     if j + pf < k:
-        L.append("    " + col_loads(q, j + pf))
+        L.append("    " + col_loads(q, j + pf, masked))
     L.append("    __builtin_amdgcn_sched_barrier(0);")
-    if masked:
-        word = "em0" if j < 32 else "em1"
-        bit = j % 32
-        for i in range(4):
-            L.append(f"    bs::mask_item(w{2 * i}, w{2 * i + 1}, it.{word}[{i}], {bit});")
     L.append("    bs::transpose8(w0, w1, w2, w3, w4, w5, w6, w7);")
     mats = [bitmatrix_rows(G[r0 + r][j]) for r in range(rows)]
     outs = [(f"a{r}_{i}", mats[r][i]) for r in range(rows) for i in range(8)]
@@ -227,10 +226,12 @@ def gen_dec_role(k, m, role, r0, rows, cfg):
     L.append("    const uint32_t o0 = it.off[0], o1 = it.off[1], o2 = it.off[2], o3 = it.off[3];")
     for r in range(rows):
         L.append("    uint32_t " + ", ".join(f"a{r}_{i} = 0" for i in range(8)) + ";")
-    prologue_loads(L, k, cfg)
+    prologue_loads(L, k, cfg, masked=True)
     for j in range(k):
         column_body(L, G, k, r0, rows, j, True, cfg)
     L.append("    // ---- z_t = received parity p ^ re-encoded row p, for the rows P uses ----")
+    L.append("    bs::DecTail tl;")
+    L.append("    bs::make_dec_tail(a, it, tl);")
     L.append("    // t = rank of row p among the used rows (P is the first e surviving parity rows in")
     L.append("    // ascending order), so no table lookup; received parity is prefetched 4 rows ahead.")
     ahead = min(4, rows)
@@ -247,10 +248,10 @@ def gen_dec_role(k, m, role, r0, rows, cfg):
             L.append("        " + "; ".join(f"q{q}_{i} = bs::bld8(it.rs, o{i}, {k + pn}u * sstride)" for i in range(4)) + ";")
         L.append(f"        bs::transpose8(a{r}_0, a{r}_1, a{r}_2, a{r}_3, a{r}_4, a{r}_5, a{r}_6, a{r}_7);")
         for i in range(4):
-            L.append(f"        if ((it.sel[{i}] >> {p}) & 1u) {{")
-            L.append(f"            const uint32_t t = __builtin_popcount(it.sel[{i}] & 0x{(1 << p) - 1:08x}u);")
-            L.append(f"            bs::st8(a.z + (uint64_t)it.blk[{i}] * a.z_block_stride + (uint64_t)t * a.z_stride + it.ib[{i}],")
-            L.append(f"                    a{r}_{2 * i} ^ c{i}.x, a{r}_{2 * i + 1} ^ c{i}.y, it.nbytes[{i}], 0u);")
+            L.append(f"        if ((tl.sel[{i}] >> {p}) & 1u) {{")
+            L.append(f"            const uint32_t t = __builtin_popcount(tl.sel[{i}] & 0x{(1 << p) - 1:08x}u);")
+            L.append(f"            bs::st8(a.z + (uint64_t)tl.blk[{i}] * a.z_block_stride + (uint64_t)t * a.z_stride + tl.ib[{i}],")
+            L.append(f"                    a{r}_{2 * i} ^ c{i}.x, a{r}_{2 * i + 1} ^ c{i}.y, tl.nbytes[{i}], 0u);")
             L.append("        }")
         L.append("    }")
     L.append("}")
@@ -268,7 +269,7 @@ def gen_dec_kernel(k, m, cfg):
     body.append(f"    const uint64_t group = (uint64_t)bs::wg_index(a.xcd_remap) * {groups} + wave;")
     body.append("    bs::DecItems it;")
     body.append("    bs::make_dec_items(a, (uint32_t)group * 256u, lane, it);")
-    body.append("    const uint32_t need = it.sel[0] | it.sel[1] | it.sel[2] | it.sel[3];")
+    body.append("    const uint32_t need = it.need;")
     for role, (r0, rows) in enumerate(split):
         rmask = ((1 << rows) - 1) << r0
         # every wave handles all roles its blocks need (usually only the first ones: P is
