@@ -26,7 +26,21 @@ __device__ __forceinline__ uint32_t dlog(const uint16_t* __restrict__ log_tab, u
     return x ? 2u * (uint32_t)log_tab[x] : kZeroLog;
 }
 
-// one wave per block; NI dwords (2 symbols each) per lane per group; RC rows per pass
+// exp-table byte offset of (doubled) log a + log b: the sum mod 2q, or the zero entry when
+// either operand is the zero sentinel.  lcm = a - 2q (wraps for a < 2q), so one v_min3.
+__device__ __forceinline__ uint32_t eidx(uint32_t lc, uint32_t lcm, uint32_t l)
+{
+    return min(min(lc + l, lcm + l), kQ2);  // v_min3_u32
+}
+
+// One wave per block.  NI dwords (2 symbols) per lane per item group, RC output rows per
+// pass, accumulators packed (low symbol | high symbol << 16).  Per source column the wave
+//  - already holds the column's data and its doubled logs (computed one column earlier),
+//  - holds the column's RC coefficient logs distributed over lanes 0..RC-1 (also one column
+//    earlier), read back with v_readlane into SGPRs,
+//  - issues the next column's data load, its log gathers and its coefficient logs,
+//  - and does RC x NI x 2 exp lookups in LDS.
+// No dependent global load sits on the per-row path.
 template <int NI, int RC>
 __global__ __launch_bounds__(kThreads) void gf16_matmul_kernel(Gf16MatmulArgs a)
 {
@@ -59,37 +73,60 @@ __global__ __launch_bounds__(kThreads) void gf16_matmul_kernel(Gf16MatmulArgs a)
             valid[j] = dw[j] < dws;
         }
         for (int32_t r0 = 0; r0 < rows; r0 += RC) {
-            uint32_t acc_lo[RC][NI], acc_hi[RC][NI];
+            uint32_t acc[RC][NI];
 #pragma unroll
             for (int r = 0; r < RC; ++r)
 #pragma unroll
-                for (int j = 0; j < NI; ++j) acc_lo[r][j] = acc_hi[r][j] = 0;
-            for (uint32_t c = 0; c < cols; ++c) {
+                for (int j = 0; j < NI; ++j) acc[r][j] = 0;
+
+            // column c's inputs: data x, its logs (l0 low, l1 high), coefficient logs (lane r)
+            auto col_data = [&](uint32_t c, uint32_t (&x)[NI]) {
                 const uint32_t slot = islots ? uni(islots[c]) : c;
-                uint32_t l0[NI], l1[NI];
+                const uint8_t* src = in_blk + (uint64_t)slot * a.in_seg_stride;
+#pragma unroll
+                for (int j = 0; j < NI; ++j)
+                    x[j] = valid[j] ? *reinterpret_cast<const uint32_t*>(src + dw[j] * 4u) : 0u;
+            };
+            auto col_clog = [&](uint32_t c) -> uint32_t {
+                const int32_t r = r0 + (int32_t)lane;
+                const uint32_t cv = (lane < (uint32_t)RC && r < rows)
+                                        ? (uint32_t)coef_blk[(uint64_t)c * a.coef_col_stride + r] : 0u;
+                return dlog(a.log_tab, cv);
+            };
+            uint32_t x[NI], l0[NI], l1[NI];
+            uint32_t clog = 0;
+            if (cols > 0) {
+                col_data(0, x);
+                clog = col_clog(0);
 #pragma unroll
                 for (int j = 0; j < NI; ++j) {
-                    uint32_t x = 0;
-                    if (valid[j]) x = *reinterpret_cast<const uint32_t*>(in_blk + (uint64_t)slot * a.in_seg_stride + dw[j] * 4u);
-                    l0[j] = dlog(a.log_tab, x & 0xffffu);
-                    l1[j] = dlog(a.log_tab, x >> 16);
+                    l0[j] = dlog(a.log_tab, x[j] & 0xffffu);
+                    l1[j] = dlog(a.log_tab, x[j] >> 16);
                 }
-                const uint16_t* cc = coef_blk + (uint64_t)c * a.coef_col_stride + r0;
+            }
+            for (uint32_t c = 0; c < cols; ++c) {
+                // next column's loads and gathers first, then this column's lookups
+                uint32_t xn[NI], clogn = 0;
+                const uint32_t cn = min(c + 1, cols - 1);
+                col_data(cn, xn);
+                clogn = col_clog(cn);
 #pragma unroll
                 for (int r = 0; r < RC; ++r) {
-                    const uint32_t cv = (r0 + r < rows) ? uni(cc[r]) : 0u;
-                    if (cv != 0) {
-                        const uint32_t lc = 2u * (uint32_t)a.log_tab[cv];
-                        const uint32_t lcm = lc - kQ2;
+                    const uint32_t lc = (uint32_t)__builtin_amdgcn_readlane((int)clog, r);
+                    const uint32_t lcm = lc - kQ2;
 #pragma unroll
-                        for (int j = 0; j < NI; ++j) {
-                            const uint32_t i0 = min(min(lc + l0[j], lcm + l0[j]), kQ2);
-                            const uint32_t i1 = min(min(lc + l1[j], lcm + l1[j]), kQ2);
-                            acc_lo[r][j] ^= *reinterpret_cast<const uint16_t*>(lds_bytes + i0);
-                            acc_hi[r][j] ^= *reinterpret_cast<const uint16_t*>(lds_bytes + i1);
-                        }
+                    for (int j = 0; j < NI; ++j) {
+                        const uint32_t lo = *reinterpret_cast<const uint16_t*>(lds_bytes + eidx(lc, lcm, l0[j]));
+                        const uint32_t hi = *reinterpret_cast<const uint16_t*>(lds_bytes + eidx(lc, lcm, l1[j]));
+                        acc[r][j] ^= lo | (hi << 16);
                     }
                 }
+#pragma unroll
+                for (int j = 0; j < NI; ++j) {
+                    l0[j] = dlog(a.log_tab, xn[j] & 0xffffu);
+                    l1[j] = dlog(a.log_tab, xn[j] >> 16);
+                }
+                clog = clogn;
             }
 #pragma unroll
             for (int r = 0; r < RC; ++r) {
@@ -102,7 +139,7 @@ __global__ __launch_bounds__(kThreads) void gf16_matmul_kernel(Gf16MatmulArgs a)
 #pragma unroll
                 for (int j = 0; j < NI; ++j) {
                     if (!valid[j]) continue;
-                    uint32_t v = acc_lo[r][j] | (acc_hi[r][j] << 16);
+                    uint32_t v = acc[r][j];
                     const uint32_t byte0 = dw[j] * 4u;
                     if (byte0 + 4u <= a.vec_bytes) {
                         uint32_t* p = reinterpret_cast<uint32_t*>(o + byte0);
@@ -127,27 +164,18 @@ int launch_gf16_matmul(const Gf16MatmulArgs& a, hipStream_t s)
 {
     if (a.nblocks == 0 || a.vec_bytes < 2) return NFEC_OK;
     if (a.vec_bytes & 1) return fail(NFEC_EINVAL, "gf16 matmul: odd byte count");
-    const uint32_t dws = (a.vec_bytes + 3) / 4;
     const uint32_t groups = (a.nblocks + kWaves - 1) / kWaves;
     const size_t lds = 65536 * sizeof(uint16_t);
-    hipError_t e;
-    if (dws <= kWave) {
-        static bool attr1 = false;
-        if (!attr1) {
-            (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&gf16_matmul_kernel<1, 16>),
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-            attr1 = true;
-        }
-        hipLaunchKernelGGL((gf16_matmul_kernel<1, 16>), dim3(groups), dim3(kThreads), lds, s, a);
-    } else {
-        static bool attr2 = false;
-        if (!attr2) {
-            (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&gf16_matmul_kernel<2, 16>),
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-            attr2 = true;
-        }
-        hipLaunchKernelGGL((gf16_matmul_kernel<2, 16>), dim3(groups), dim3(kThreads), lds, s, a);
+    // one dword (2 symbols) per lane per item group, 32 rows per pass: the LDS lookups are
+    // the same for any split, the log gathers scale with the number of row passes
+    static bool attr = false;
+    if (!attr) {
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&gf16_matmul_kernel<1, 32>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        attr = true;
     }
+    hipError_t e;
+    hipLaunchKernelGGL((gf16_matmul_kernel<1, 32>), dim3(groups), dim3(kThreads), lds, s, a);
     e = hipGetLastError();
     if (e != hipSuccess) return hip_fail(e, "gf16_matmul launch");
     return NFEC_OK;

@@ -12,6 +12,8 @@
 // tables held in 5 dwords, so one v_perm_b32 performs four byte lookups.  Per (row,
 // column, dword) that is 3 v_perm + ~1.5 v_bitop3/xor; the per-value tables (256 x 32 B)
 // sit in LDS and are read with uniform (broadcast) ds_read_b128/_b32.
+#include <cstdlib>
+
 #include "nfec_internal.hpp"
 
 namespace nfec {
@@ -248,12 +250,12 @@ hipError_t launch_one(const Gf8MatmulArgs& a, hipStream_t s)
 // branch-free: per column pair the wave issues the next pair's z loads, then for each of
 // the RC rows reads its table with uniform (broadcast) LDS loads whose addresses do not
 // depend on data, and applies 3 v_perm + 1 bitop3 + 1 xor per output dword.
-template <int NI, int RC>
+template <int NI, int RC, int LA>
 __global__ __launch_bounds__(kThreads) void gf8_solve_kernel(Gf8SolveArgs a)
 {
     constexpr int kMaxCols = 32;
-    __shared__ uint4 lds_t4[kWavesPerGroup][kMaxCols * RC + 1];  // +1: pipelined read past the end
-    __shared__ uint32_t lds_t1[kWavesPerGroup][kMaxCols * RC + 1];
+    __shared__ uint4 lds_t4[kWavesPerGroup][kMaxCols * RC + LA];  // +LA: pipelined reads past the end
+    __shared__ uint32_t lds_t1[kWavesPerGroup][kMaxCols * RC + LA];
     const uint32_t lane = threadIdx.x & (kWave - 1);
     const uint32_t w = threadIdx.x >> 6;
     const uint32_t blk = uni(blockIdx.x * kWavesPerGroup + w);
@@ -308,11 +310,16 @@ __global__ __launch_bounds__(kThreads) void gf8_solve_kernel(Gf8SolveArgs a)
         };
         uint2 cur[2][NI], nxt[2][NI];
         load_pair(0, cur);
-        // tables are software-pipelined one row ahead (LDS latency off the VALU chain)
+        // tables are software-pipelined LA rows ahead (LDS latency off the VALU chain)
         const uint4* t4 = lds_t4[w];
         const uint32_t* t1 = lds_t1[w];
-        uint4 tb = t4[0];
-        uint32_t tc = t1[0];
+        uint4 tb[LA + 1];
+        uint32_t tc[LA + 1];
+#pragma unroll
+        for (int q = 0; q < LA; ++q) {
+            tb[q] = t4[q];
+            tc[q] = t1[q];
+        }
         for (uint32_t t = 0; t < cols2; t += 2) {
             load_pair(min(t + 2, cols2 - 2), nxt);
 #pragma unroll
@@ -326,14 +333,17 @@ __global__ __launch_bounds__(kThreads) void gf8_solve_kernel(Gf8SolveArgs a)
                 const uint32_t e0 = (t + u) * RC;
 #pragma unroll
                 for (int r = 0; r < RC; ++r) {
-                    const uint4 tbn = t4[e0 + r + 1];
-                    const uint32_t tcn = t1[e0 + r + 1];
+                    tb[LA] = t4[e0 + r + LA];
+                    tc[LA] = t1[e0 + r + LA];
                     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-                    for (int d = 0; d < 2 * NI; ++d) acc[r][d] ^= gfmul4(tb, tc, sel[d]);
+                    for (int d = 0; d < 2 * NI; ++d) acc[r][d] ^= gfmul4(tb[0], tc[0], sel[d]);
                     __builtin_amdgcn_sched_barrier(0);
-                    tb = tbn;
-                    tc = tcn;
+#pragma unroll
+                    for (int q = 0; q < LA; ++q) {
+                        tb[q] = tb[q + 1];
+                        tc[q] = tc[q + 1];
+                    }
                 }
             }
 #pragma unroll
@@ -362,11 +372,11 @@ __global__ __launch_bounds__(kThreads) void gf8_solve_kernel(Gf8SolveArgs a)
     }
 }
 
-template <int NI, int RC>
+template <int NI, int RC, int LA = 1>
 hipError_t launch_solve(const Gf8SolveArgs& a, hipStream_t s)
 {
     const uint32_t groups = (a.nblocks + kWavesPerGroup - 1) / kWavesPerGroup;
-    hipLaunchKernelGGL((gf8_solve_kernel<NI, RC>), dim3(groups), dim3(kThreads), 0, s, a);
+    hipLaunchKernelGGL((gf8_solve_kernel<NI, RC, LA>), dim3(groups), dim3(kThreads), 0, s, a);
     return hipGetLastError();
 }
 
@@ -377,8 +387,14 @@ int launch_gf8_solve(const Gf8SolveArgs& a, uint32_t max_rows, uint32_t max_cols
     if (a.nblocks == 0 || a.vec_bytes == 0) return NFEC_OK;
     if (max_cols > 32) return NFEC_ENOTSUP;
     const uint32_t ni = (((a.vec_bytes + 7) / 8) + kWave - 1) / kWave;
+    // NFEC_SOLVE_CFG (A/B runs): 1 = 8-row bands, 2 = tables two rows ahead
+    static const int cfg = [] {
+        const char* v = std::getenv("NFEC_SOLVE_CFG");
+        return v ? std::atoi(v) : 0;
+    }();
     hipError_t e;
-    if (max_rows <= 8) e = ni <= 2 ? launch_solve<2, 8>(a, s) : launch_solve<3, 8>(a, s);
+    if (max_rows <= 8 || cfg == 1) e = ni <= 2 ? launch_solve<2, 8>(a, s) : launch_solve<3, 8>(a, s);
+    else if (cfg == 2) e = ni <= 2 ? launch_solve<2, 16, 2>(a, s) : launch_solve<3, 16, 2>(a, s);
     else e = ni <= 2 ? launch_solve<2, 16>(a, s) : launch_solve<3, 16>(a, s);
     if (e != hipSuccess) return hip_fail(e, "gf8_solve launch");
     return NFEC_OK;

@@ -1,0 +1,106 @@
+"""Secondary workloads (not the headline bench line): one JSON line per workload.
+
+    python tools/bench_extra.py [--workload c4|rs16|mdp|rs8] [--blocks N] [--steps K]
+
+c4    RS16 k=4096 m=256 vec=1400 encode (BASELINE C4), default 4096 blocks in HBM
+rs16  RS16 k=400 m=100 vec=1400 encode + 50-erasure decode (the C5 RS16 block type)
+mdp   MDP k=64 m=32 vec=1400 encode + 16-erasure decode
+rs8   RS8 with --k/--m/--erasures (other shapes than the headline)
+
+Inputs are synthetic (splitmix64 segments generated on the GPU); GiB/s counts source bytes
+(k * vec per block) per pass, like the headline metric.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    p = argparse.ArgumentParser()
+    p.add_argument("--workload", default="c4")
+    p.add_argument("--blocks", type=int, default=0)
+    p.add_argument("--steps", type=int, default=3)
+    p.add_argument("--warmup", type=int, default=1)
+    p.add_argument("--k", type=int, default=0)
+    p.add_argument("--m", type=int, default=0)
+    p.add_argument("--vec", type=int, default=1400)
+    p.add_argument("--erasures", type=int, default=-1)
+    a = p.parse_args()
+    import torch
+    import norm_amd as na
+
+    shapes = {  # kind, k, m, blocks, erasures (0: encode only)
+        "c4": (na.NFEC_RS16, 4096, 256, 4096, 0),
+        "rs16": (na.NFEC_RS16, 400, 100, 16384, 50),
+        "mdp": (na.NFEC_MDP, 64, 32, 65536, 16),
+        "rs8": (na.NFEC_RS8, 64, 32, 65536, 16),
+    }
+    kind, k, m, nb, er = shapes[a.workload]
+    k = a.k or k
+    m = a.m or m
+    nb = a.blocks or nb
+    er = er if a.erasures < 0 else a.erasures
+    vec = a.vec
+    enc_cls = {na.NFEC_RS8: na.NormEncoderRS8, na.NFEC_RS16: na.NormEncoderRS16, na.NFEC_MDP: na.NormEncoderMDP}[kind]
+    dec_cls = {na.NFEC_RS8: na.NormDecoderRS8, na.NFEC_RS16: na.NormDecoderRS16, na.NFEC_MDP: na.NormDecoderMDP}[kind]
+    torch.cuda.set_device(0)
+    t0 = time.perf_counter()
+    enc = enc_cls()
+    assert enc.Init(k, m, vec)
+    init_s = time.perf_counter() - t0
+    dec = None
+    if er:
+        dec = dec_cls()
+        assert dec.Init(k, m, vec)
+    blocks = torch.zeros((nb, k + m, vec), dtype=torch.uint8, device="cuda")
+    na.fill_blocks(blocks, k, vec, 0x4E4F524D)
+    if er:
+        locs, counts = na.make_erasures(nb, k, er, 0x4E4F524D, m)
+        status = torch.empty(nb, dtype=torch.int32, device="cuda")
+    stream = torch.cuda.current_stream()
+
+    def timed(fn, n):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for _ in range(n):
+            fn()
+        e1.record(stream)
+        e1.synchronize()
+        return e0.elapsed_time(e1) / n
+
+    for _ in range(a.warmup):
+        enc.encode_blocks(blocks, stream=stream)
+        if er:
+            dec.decode_blocks(blocks, locs, counts, status=status, stream=stream)
+    torch.cuda.synchronize()
+    enc_ms = timed(lambda: enc.encode_blocks(blocks, stream=stream), a.steps)
+    out = {
+        "workload": a.workload,
+        "codec": {na.NFEC_RS8: "RS8", na.NFEC_RS16: "RS16", na.NFEC_MDP: "MDP"}[kind],
+        "k": k, "m": m, "vec": vec, "blocks": nb, "erasures": er,
+        "init_s": round(init_s, 3),
+        "encode_ms": round(enc_ms, 3),
+        "encode_GiBps": round(k * vec * nb / (enc_ms * 1e-3) / 2**30, 2),
+    }
+    if er:
+        dec_ms = timed(lambda: dec.decode_blocks(blocks, locs, counts, status=status, stream=stream), a.steps)
+        keep = blocks.clone()
+        na.zero_erasures(blocks, locs, counts, vec, stream=stream)
+        dec.decode_blocks(blocks, locs, counts, status=status, stream=stream)
+        torch.cuda.synchronize()
+        out.update({
+            "decode_ms": round(dec_ms, 3),
+            "decode_GiBps": round(k * vec * nb / (dec_ms * 1e-3) / 2**30, 2),
+            "combined_GiBps": round(k * vec * nb / ((enc_ms + dec_ms) * 1e-3) / 2**30, 2),
+            "verified": bool(torch.equal(blocks, keep)) and bool((status == er).all()),
+        })
+    print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -34,8 +34,12 @@ class Cfg:
     lazy: emit the plane updates grouped by low-table entry, so at most one low entry is
           live at a time (shorter live ranges; lets higher occupancy targets fit)"""
 
-    def __init__(self, rows=16, pf=3, wpe=None, lazy=False, suffix=""):
+    def __init__(self, rows=16, pf=3, wpe=None, lazy=False, suffix="", probe=None):
         self.rows, self.pf, self.wpe, self.lazy, self.suffix = rows, pf, wpe, lazy, suffix
+        # probe (A/B only, never the default): "noload" replaces the source loads with
+        # synthetic registers (VALU-only time), "nocompute" keeps loads/stores but drops the
+        # GF arithmetic (memory-only time)
+        self.probe = probe
 
 
 DEFAULT = Cfg(rows=16, pf=3, lazy=True)
@@ -45,6 +49,8 @@ VARIANTS_64_32 = {
     2: Cfg(rows=12, pf=3, wpe=3, lazy=True, suffix="_v2"),
     3: Cfg(rows=8, pf=3, wpe=4, lazy=True, suffix="_v3"),
     4: Cfg(rows=16, pf=4, lazy=True, suffix="_v4"),
+    8: Cfg(rows=16, pf=3, lazy=True, suffix="_probe_noload", probe="noload"),
+    9: Cfg(rows=16, pf=3, lazy=True, suffix="_probe_nocompute", probe="nocompute"),
 }
 
 
@@ -139,9 +145,12 @@ def acc_update(acc, R):
     return None
 
 
-def col_loads(q, col, masked=False):
+def col_loads(q, col, masked=False, probe=None):
     """Refill prefetch slot q with source column col (buffer loads: VGPR item offset + SGPR
     slot offset).  masked (decode): erased columns read as zeros (bs::dec_off)."""
+    if probe == "noload":
+        return "; ".join(f"n{q}_{i} = make_uint2(o{i} * 0x9E3779B1u ^ {col}u, (o{i} + {col}u) * 0x85EBCA6Bu)"
+                         for i in range(4)) + ";"
     if masked:
         return "; ".join(f"n{q}_{i} = bs::bld8(it.rs, bs::dec_off<{col}>(o{i}, it.em0[{i}], it.em1[{i}]), {col}u * sstride)"
                          for i in range(4)) + ";"
@@ -153,7 +162,7 @@ def prologue_loads(L, k, cfg, masked=False):
     for r in range(cfg.pf):
         L.append(f"    uint2 n{r}_0, n{r}_1, n{r}_2, n{r}_3;")
     for r in range(min(cfg.pf, k)):
-        L.append(f"    " + col_loads(r, r, masked))
+        L.append(f"    " + col_loads(r, r, masked, cfg.probe))
 
 
 def column_body(L, G, k, r0, rows, j, masked, cfg):
@@ -165,8 +174,12 @@ def column_body(L, G, k, r0, rows, j, masked, cfg):
     L.append(f"    w0 = n{q}_0.x; w1 = n{q}_0.y; w2 = n{q}_1.x; w3 = n{q}_1.y; w4 = n{q}_2.x; w5 = n{q}_2.y; "
              f"w6 = n{q}_3.x; w7 = n{q}_3.y;")
     if j + pf < k:
-        L.append("    " + col_loads(q, j + pf, masked))
+        L.append("    " + col_loads(q, j + pf, masked, cfg.probe))
     L.append("    __builtin_amdgcn_sched_barrier(0);")
+    if cfg.probe == "nocompute":
+        for i in range(8):
+            L.append(f"    a0_{i} ^= w{i};")
+        return
     L.append("    bs::transpose8(w0, w1, w2, w3, w4, w5, w6, w7);")
     mats = [bitmatrix_rows(G[r0 + r][j]) for r in range(rows)]
     outs = [(f"a{r}_{i}", mats[r][i]) for r in range(rows) for i in range(8)]
