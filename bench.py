@@ -24,6 +24,7 @@ sys.path.insert(0, ROOT)
 
 METRIC = "FEC encode+erasure-decode GiB/s (device-resident), RS8 k=64/m=32 seg=1400B"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md); measured copy ~6300
+VALU_PEAK = 7.86e13    # 256 CU x 4 SIMD x 32 lanes x 2.4 GHz, 32-bit bitwise ops (ubench: 76% reachable)
 
 
 def parse():
@@ -174,12 +175,20 @@ def main():
     achieved = enc_bytes / (enc_ms * 1e-3) / 1e9
 
     traffic = None
+    valu = None
     pmc_path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if os.path.exists(pmc_path):
         try:
             pmc = json.load(open(pmc_path))
             if pmc.get("blocks") == nb and pmc.get("k") == k and pmc.get("m") == m and pmc.get("vec") == vec:
                 traffic = pmc.get("encode_hbm_bytes_per_launch")
+                if pmc.get("valu_insts_per_launch"):
+                    # the kernel is VALU-bound as much as HBM-bound: its
+                    # wave64 VALU instructions (PMC SQ_INSTS_VALU) over the measured launch time
+                    lane_ops = pmc["valu_insts_per_launch"] * 64 / (enc_ms * 1e-3)
+                    valu = {"achieved": float("%.4g" % lane_ops), "peak": VALU_PEAK, "unit": "lane-ops/s",
+                            "frac": round(lane_ops / VALU_PEAK, 4),
+                            "insts_per_launch": pmc["valu_insts_per_launch"]}
         except Exception:
             traffic = None
 
@@ -235,6 +244,8 @@ def main():
             if (k, m) in ((64, 32), (64, 16), (64, 8)) and not os.environ.get("NFEC_FORCE_GENERIC")
             else "gf8_matmul_kernel (RS8 encode)",
             "algorithmic_bytes_per_launch": enc_bytes,
+            "read_only_frac": round(k * vec * nb / (enc_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+            "valu": valu,
         },
         "kernels_ms": {"encode": round(enc_ms, 4), "decode": round(dec_ms, 4)},
         "cpu_baseline": cpu,

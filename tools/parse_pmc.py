@@ -13,8 +13,11 @@ from collections import defaultdict
 
 
 def main(root):
-    per = defaultdict(lambda: defaultdict(list))
+    # counter rows can come per XCD/SE instance: sum the rows of one dispatch, then average
+    # over dispatches (per-launch totals)
+    per = defaultdict(lambda: defaultdict(lambda: defaultdict(float)))
     for f in glob.glob(os.path.join(root, "p*", "**", "*counter_collection.csv"), recursive=True):
+        tag = os.path.relpath(f, root).split(os.sep)[0]  # pass directory: dispatch ids restart per pass
         for r in csv.DictReader(open(f)):
             name = r.get("Kernel_Name", "")
             cname = r.get("Counter_Name", "")
@@ -22,11 +25,11 @@ def main(root):
                 val = float(r.get("Counter_Value", "nan"))
             except ValueError:
                 continue
-            per[name][cname].append(val)
+            per[name][cname][(tag, r.get("Dispatch_Id", ""))] += val
     out = {}
     for name, ctrs in per.items():
         short = name.replace("(anonymous namespace)::", "").replace("void ", "").split("(")[0]
-        d = {c: sum(v) / len(v) for c, v in ctrs.items()}
+        d = {c: sum(v.values()) / len(v) for c, v in ctrs.items()}
         d["dispatches"] = max(len(v) for v in ctrs.values())
         if "FETCH_SIZE" in d:
             d["hbm_read_bytes_corrected"] = 2 * d["FETCH_SIZE"] * 1024
@@ -45,6 +48,7 @@ def main(root):
             "encode_hbm_bytes_per_launch": round(e["hbm_read_bytes_corrected"] + e["hbm_write_bytes"]),
             "read_bytes_corrected": round(e["hbm_read_bytes_corrected"]),
             "write_bytes": round(e["hbm_write_bytes"]),
+            "valu_insts_per_launch": round(e["SQ_INSTS_VALU"]) if "SQ_INSTS_VALU" in e else None,
             "method": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE in separate passes; read = 2 x FETCH_SIZE KiB "
                       "(gfx950 correction, MI355X_MICROARCH.md HBM), write = WRITE_SIZE KiB",
         }
