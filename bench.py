@@ -85,6 +85,7 @@ def main():
         if dist is not None:
             dist.barrier()
 
+    orig = blocks[:, :k].clone() if a.verify else None
     for _ in range(a.warmup):
         step()
     torch.cuda.synchronize(dev)
@@ -160,12 +161,14 @@ def main():
         keep = blocks.clone()
         from norm_amd import zero_erasures
 
-        # erase, repair with the parity the timed encodes produced: a wrong encode or a
-        # wrong decode both break the round trip
+        # every timed step re-encoded the batch and overwrote the erased source symbols with
+        # their repair: the source must still equal the pristine copy (a wrong encode or a
+        # wrong decode both break that), and one more erase + repair must reproduce it
+        ok = bool(torch.equal(blocks[:, :k], orig))
         zero_erasures(blocks, locs, counts, vec, stream=stream)
         dec.decode_blocks(blocks, locs, counts, status=status, stream=stream)
         torch.cuda.synchronize(dev)
-        ok = bool(torch.equal(blocks, keep)) and bool((status == a.erasures).all())
+        ok = ok and bool(torch.equal(blocks, keep)) and bool((status == a.erasures).all())
 
     total_blocks = nb * world
     src_bytes = k * vec * total_blocks

@@ -286,6 +286,15 @@ static uint32_t bs_flags()
     return f;
 }
 
+static bool use_asm()
+{
+    static const bool v = [] {
+        const char* e = std::getenv("NFEC_ASM");
+        return !(e && *e == '0');
+    }();
+    return v;
+}
+
 // ---- encode on a device batch ----
 int encode_device(nfec_codec* c, const nfec_block_batch* b, hipStream_t s)
 {
@@ -303,6 +312,11 @@ int encode_device(nfec_codec* c, const nfec_block_batch* b, hipStream_t s)
         e.accumulate = acc;
         e.xcd_remap = bs_flags() & 1u;
         e.nt_store = (bs_flags() >> 1) & 1u;
+        // hand-allocated assembly kernels first (NFEC_ASM=0 disables them for A/B runs)
+        if (use_asm()) {
+            const int rc = launch_rs8_asm_encode(c->k, c->m, e, s);
+            if (rc != NFEC_ENOTSUP) return rc == NFEC_OK ? NFEC_OK : fail(rc, "assembly encode launch failed");
+        }
         const int rc = launch_rs8_bitsliced_encode(c->k, c->m, e, s);
         if (rc != NFEC_ENOTSUP) return rc == NFEC_OK ? NFEC_OK : fail(rc, "bit-sliced encode launch failed");
     }

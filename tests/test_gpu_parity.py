@@ -58,6 +58,8 @@ ENC_CASES = [
     (NFEC_RS8, 64, 32, 1400, 1408, 5),
     (NFEC_RS8, 64, 16, 1400, 1400, 9),
     (NFEC_RS8, 64, 8, 1400, 1400, 7),
+    (NFEC_RS8, 64, 32, 1397, 1400, 6),   # segment tail (vec % 8 != 0)
+    (NFEC_RS8, 64, 32, 1400, 1400, 700),  # many workgroups
     (NFEC_RS8, 64, 32, 1401, 1408, 5),
     (NFEC_RS8, 1, 1, 17, 24, 3),
     (NFEC_RS8, 16, 4, 64, 64, 11),
@@ -97,13 +99,13 @@ def test_encode_shortened_blocks(orc, kind):
     assert np.array_equal(dev.cpu().numpy(), ref)
 
 
-@pytest.mark.parametrize("kind", [NFEC_RS8, NFEC_RS16])
-def test_encode_accumulates_like_reference(orc, kind):
+@pytest.mark.parametrize("kind,k,m,vec,nb", [(NFEC_RS8, 32, 8, 96, 4), (NFEC_RS16, 32, 8, 96, 4),
+                                              (NFEC_RS8, 64, 32, 1400, 9), (NFEC_RS8, 64, 16, 1397, 5)])
+def test_encode_accumulates_like_reference(orc, kind, k, m, vec, nb):
     """Encode XORs into the parity buffers (reference contract: caller zeroes them)."""
-    k, m, vec, nb = 32, 8, 96, 4
     enc, _ = _codecs(kind, k, m, vec)
     host = orc.make_blocks(k, m, vec, nb)
-    junk = np.random.default_rng(1).integers(0, 256, (nb, m, vec), dtype=np.uint8)
+    junk = np.random.default_rng(1).integers(0, 256, (nb, m, host.shape[2]), dtype=np.uint8)
     ref = orc.encode_blocks(kind, k, m, vec, host.copy())
     host[:, k:, :] = junk
     expect = ref.copy()
