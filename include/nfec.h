@@ -19,6 +19,8 @@
  *   nfec_decode           NormDecoder::Decode  (RS8 normEncoderRS8.cpp:652-757, RS16 :650-755,
  *                         MDP normEncoderMDP.cpp:333-430) for many blocks at once, as called
  *                         from NormObject::HandleObjectMessage src/common/normObject.cpp:1548-1644
+ *   nfec_encode_host_vectors / nfec_decode_host_vectors
+ *                         the same two sites on NORM's scattered segment lists (block->SegmentList())
  *   nfec_encode_segment   NormEncoder::Encode(segmentId, dataVector, parityVectorList)
  *                         (include/normEncoder.h:44), host pointers, exact per-call semantics
  *   nfec_decode_vectors   NormDecoder::Decode(vectorList, numData, erasureCount, erasureLocs)
@@ -137,6 +139,25 @@ int nfec_encode_host(nfec_codec* codec, const nfec_block_batch* host_batch);
 int nfec_decode_host(nfec_codec* codec, const nfec_block_batch* host_batch,
                      const uint16_t* erasure_locs, uint32_t erasure_stride,
                      const uint16_t* erasure_counts, int32_t* status);
+
+/* ---- host segment lists: many blocks, each a list of scattered segment pointers ----
+ * The batch form of NormObject::CalculateBlockParity (src/common/normObject.cpp:2203-2229)
+ * and of the receiver's NormSenderNode::Decode site (normObject.cpp:1548-1644), where a
+ * block is block->SegmentList(): pointers into NORM's segment pool (normSegment.cpp:14-86).
+ * vectors[b*(k+m) + s] is block b's slot s: slots [0, numData_b) source, [numData_b,
+ * numData_b + m) parity; each holds >= vector_size bytes.  num_data: host [nblocks] or NULL
+ * (= k).  Encode writes the parity vectors (XOR into them with NFEC_ACCUMULATE).  Decode
+ * writes only the erased source vectors listed in erasure_locs[b*erasure_stride ..] (sorted,
+ * erasure_counts[b] entries); parity pointers may be NULL (absent, never dereferenced;
+ * MDP reads them as zero).  status (host [nblocks], may be NULL) as nfec_decode.  RS16 never
+ * writes an odd last byte.  Synchronous; segments are gathered into pinned staging by host
+ * threads, with H2D / compute / D2H overlapped. */
+int nfec_encode_host_vectors(nfec_codec* codec, void* const* vectors, uint32_t nblocks,
+                             const uint16_t* num_data, uint32_t flags);
+int nfec_decode_host_vectors(nfec_codec* codec, void* const* vectors, uint32_t nblocks,
+                             const uint16_t* num_data, const uint16_t* erasure_locs,
+                             uint32_t erasure_stride, const uint16_t* erasure_counts,
+                             int32_t* status, uint32_t flags);
 
 /* ---- per-call NORM semantics with scattered host vectors (drop-in classes) ---- */
 /* NormEncoder::Encode: parity_vectors[i] ^= G[k+i][segment_id] * data over vector_size

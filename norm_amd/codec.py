@@ -184,6 +184,16 @@ class _Encoder(_Codec):
         N.check(N.lib().nfec_encode_host(self._h, ctypes.byref(b)), "nfec_encode_host")
 
 
+    def encode_vectors_host(self, vectors, num_data=None, accumulate=False):
+        """Batch form of CalculateBlockParity on NORM-style segment lists: vectors is a list of
+        blocks, each a list of k+m (or numData_b+m) writable host buffers (numpy uint8 arrays or
+        anything with a buffer) -- slots [0, numData_b) source, then m parity."""
+        self._need()
+        arr, keep, nd = _vector_table(vectors, self.ndata + self.npar, num_data, self.ndata)
+        N.check(N.lib().nfec_encode_host_vectors(self._h, arr, len(vectors), nd,
+                                                 N.NFEC_ACCUMULATE if accumulate else 0), "nfec_encode_host_vectors")
+
+
 class _Decoder(_Codec):
     def Decode(self, vectorList, numData, erasureCount, erasureLocs):
         self._need()
@@ -230,6 +240,44 @@ class _Decoder(_Codec):
         N.check(N.lib().nfec_decode_host(self._h, ctypes.byref(b), erasure_locs.ctypes.data, erasure_locs.shape[1],
                                          erasure_counts.ctypes.data, status.ctypes.data), "nfec_decode_host")
         return status
+
+
+    def decode_vectors_host(self, vectors, erasure_locs, erasure_counts, num_data=None, accumulate=False):
+        """Receiver repair of many blocks given as NORM-style segment lists (None allowed for
+        missing parity).  erasure_locs: uint16 [nblocks, stride]; erasure_counts: uint16
+        [nblocks].  Returns int32 status [nblocks]."""
+        import numpy as np
+
+        self._need()
+        arr, keep, nd = _vector_table(vectors, self.ndata + self.npar, num_data, self.ndata)
+        locs = np.ascontiguousarray(erasure_locs, dtype=np.uint16)
+        counts = np.ascontiguousarray(erasure_counts, dtype=np.uint16)
+        status = np.zeros(len(vectors), np.int32)
+        N.check(N.lib().nfec_decode_host_vectors(self._h, arr, len(vectors), nd, locs.ctypes.data, locs.shape[1],
+                                                 counts.ctypes.data, status.ctypes.data,
+                                                 N.NFEC_ACCUMULATE if accumulate else 0), "nfec_decode_host_vectors")
+        return status
+
+
+def _vector_table(vectors, n, num_data, k):
+    """(void*[nblocks * n] pointer table, keep-alive list, num_data pointer or None)"""
+    import numpy as np
+
+    arr = (ctypes.c_void_p * (len(vectors) * n))()
+    keep = []
+    for b, blk in enumerate(vectors):
+        for s, v in enumerate(blk):
+            if v is None:
+                continue
+            a, kk = _addr_rw(v)
+            arr[b * n + s] = a
+            keep.append(kk)
+    nd = None
+    if num_data is not None:
+        nd_arr = np.ascontiguousarray(num_data, dtype=np.uint16)
+        keep.append(nd_arr)
+        nd = nd_arr.ctypes.data
+    return arr, keep, nd
 
 
 class NormEncoderRS8(_Encoder):

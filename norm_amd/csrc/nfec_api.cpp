@@ -1105,6 +1105,214 @@ static int run_host_batch(nfec_codec* c, const nfec_block_batch* hb, const uint1
     return NFEC_OK;
 }
 
+// ---- host segment lists (NORM's scattered segment pool) ----
+// NormObject::CalculateBlockParity (src/common/normObject.cpp:2203-2229) and the receiver's
+// NormSenderNode::Decode path (normObject.cpp:1548-1644) hold a block as a list of segment
+// pointers from the segment pool (normSegment.cpp:14-86), not as one strided buffer.  These
+// batches gather the listed segments into pinned staging (host threads), run the device
+// kernels over a 3-slot H2D || compute || D2H pipeline, and scatter back only the bytes the
+// reference writes: parity slots for encode, the erased source slots for decode (RS16: the
+// even part of vector_size; an odd last byte is never written, normEncoderRS16.cpp:479).
+namespace {
+
+extern "C++" template <typename F>
+void parallel_blocks(uint32_t nb, uint64_t bytes, F fn)
+{
+    const unsigned nt = (unsigned)std::min<uint64_t>(std::min<uint64_t>(host_copy_threads(), nb),
+                                                      std::max<uint64_t>(1, bytes >> 22));
+    if (nt <= 1) {
+        fn(0u, nb);
+        return;
+    }
+    std::vector<std::thread> th;
+    const uint32_t per = (nb + nt - 1) / nt;
+    for (unsigned t = 1; t < nt; ++t) {
+        const uint32_t b0 = std::min<uint32_t>(nb, t * per), b1 = std::min<uint32_t>(nb, b0 + per);
+        if (b0 < b1) th.emplace_back(fn, b0, b1);
+    }
+    fn(0u, std::min(per, nb));
+    for (auto& t : th) t.join();
+}
+
+}  // namespace
+
+static int run_host_vectors(nfec_codec* c, void* const* vecs, uint32_t nblocks, const uint16_t* num_data,
+                            const uint16_t* locs, uint32_t lstride, const uint16_t* counts, int32_t* status,
+                            uint32_t flags, bool decode)
+{
+    if (!c || (nblocks && !vecs)) return fail(NFEC_EINVAL, "null codec or vector list");
+    if (decode && (!locs || !counts || lstride == 0)) return fail(NFEC_EINVAL, "bad erasure arrays");
+    if (nblocks == 0) return NFEC_OK;
+    const uint32_t n = c->k + c->m;
+    const uint64_t ss = round_up(c->vec, 8u);
+    const uint64_t dbs = (uint64_t)n * ss;
+    const bool acc = (flags & NFEC_ACCUMULATE) != 0;
+    const size_t out_bytes = c->sym == 2 ? (c->vec & ~1u) : c->vec;
+    // validate the lists (the reference dereferences every source vector and, for encode,
+    // every parity vector; decode never touches missing parity, normEncoderRS8.cpp:689-711)
+    for (uint32_t b = 0; b < nblocks; ++b) {
+        const uint32_t nd = num_data ? num_data[b] : c->k;
+        if (nd == 0 || nd > c->k) return fail(NFEC_EINVAL, "num_data out of range");
+        const uint32_t need = decode ? nd : nd + c->m;
+        for (uint32_t s = 0; s < need; ++s)
+            if (!vecs[(uint64_t)b * n + s]) return fail(NFEC_EINVAL, "null source/parity vector");
+    }
+    DeviceGuard g(c->device);
+    const uint32_t chunk = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(nblocks, (64ull << 20) / dbs));
+    constexpr uint32_t nslot = 3;
+    struct Slot {
+        uint8_t* dev = nullptr;
+        uint8_t* pin = nullptr;
+        uint16_t* dmeta = nullptr;
+        int32_t* dstat = nullptr;
+        int32_t* hstat = nullptr;
+        hipStream_t st = nullptr;
+        hipEvent_t done = nullptr;
+        uint32_t b0 = 0, nb = 0;
+        bool busy = false;
+    } slots[nslot];
+    const size_t meta = (size_t)chunk * (1 + lstride + 1);
+    auto cleanup = [&]() {
+        for (auto& s : slots) {
+            if (s.st) (void)hipStreamSynchronize(s.st);
+            if (s.dev) (void)hipFree(s.dev);
+            if (s.pin) (void)hipHostFree(s.pin);
+            if (s.hstat) (void)hipHostFree(s.hstat);
+            if (s.dmeta) (void)hipFree(s.dmeta);
+            if (s.dstat) (void)hipFree(s.dstat);
+            if (s.done) (void)hipEventDestroy(s.done);
+            if (s.st) (void)hipStreamDestroy(s.st);
+        }
+    };
+    const uint32_t used = std::min<uint32_t>(nslot, (nblocks + chunk - 1) / chunk);
+    for (uint32_t i = 0; i < used; ++i) {
+        Slot& s = slots[i];
+        if (hipMalloc(reinterpret_cast<void**>(&s.dev), (size_t)chunk * dbs) != hipSuccess ||
+            hipHostMalloc(reinterpret_cast<void**>(&s.pin), (size_t)chunk * dbs, hipHostMallocDefault) != hipSuccess ||
+            hipHostMalloc(reinterpret_cast<void**>(&s.hstat), (size_t)chunk * 4 + 16, hipHostMallocDefault) != hipSuccess ||
+            hipMalloc(reinterpret_cast<void**>(&s.dmeta), meta * 2 + 16) != hipSuccess ||
+            hipMalloc(reinterpret_cast<void**>(&s.dstat), (size_t)chunk * 4 + 16) != hipSuccess ||
+            hipStreamCreateWithFlags(&s.st, hipStreamNonBlocking) != hipSuccess ||
+            hipEventCreateWithFlags(&s.done, hipEventDisableTiming) != hipSuccess) {
+            cleanup();
+            return fail(NFEC_ENOMEM, "vector batch staging allocation failed");
+        }
+    }
+    const uint64_t blk_bytes = (uint64_t)n * c->vec;
+    auto gather = [&](Slot& s) {
+        parallel_blocks(s.nb, (uint64_t)s.nb * blk_bytes, [&](uint32_t i0, uint32_t i1) {
+            for (uint32_t i = i0; i < i1; ++i) {
+                const uint32_t b = s.b0 + i;
+                const uint32_t nd = num_data ? num_data[b] : c->k;
+                // encode without accumulate reads the source only; everything else reads the
+                // whole listed block (absent parity is zero, as MDP's decoder treats it)
+                const uint32_t up = (!decode && !acc) ? nd : nd + c->m;
+                uint8_t* dst = s.pin + (uint64_t)i * dbs;
+                for (uint32_t sl = 0; sl < up; ++sl) {
+                    const void* p = vecs[(uint64_t)b * n + sl];
+                    if (p) std::memcpy(dst + sl * ss, p, c->vec);
+                    else std::memset(dst + sl * ss, 0, c->vec);
+                }
+            }
+        });
+    };
+    auto scatter = [&](Slot& s) {
+        parallel_blocks(s.nb, (uint64_t)s.nb * (uint64_t)c->m * c->vec, [&](uint32_t i0, uint32_t i1) {
+            for (uint32_t i = i0; i < i1; ++i) {
+                const uint32_t b = s.b0 + i;
+                const uint32_t nd = num_data ? num_data[b] : c->k;
+                const uint8_t* src = s.pin + (uint64_t)i * dbs;
+                if (!decode) {
+                    for (uint32_t p = 0; p < c->m; ++p)
+                        std::memcpy(vecs[(uint64_t)b * n + nd + p], src + (nd + p) * ss, out_bytes);
+                } else if (s.hstat[i] > 0) {
+                    const uint16_t* l = locs + (uint64_t)b * lstride;
+                    for (uint32_t e = 0; e < counts[b] && e < lstride; ++e) {
+                        if (l[e] >= nd) break;  // only source erasures are filled (normEncoderRS8.cpp:732)
+                        std::memcpy(vecs[(uint64_t)b * n + l[e]], src + l[e] * ss, out_bytes);
+                    }
+                }
+            }
+        });
+    };
+    int rc = NFEC_OK;
+    auto finish = [&](Slot& s) -> int {
+        if (!s.busy) return NFEC_OK;
+        s.busy = false;
+        NFEC_HIP(hipEventSynchronize(s.done));
+        scatter(s);
+        if (decode && status) std::memcpy(status + s.b0, s.hstat, (size_t)s.nb * 4);
+        return NFEC_OK;
+    };
+    uint32_t idx = 0;
+    for (uint32_t b0 = 0; b0 < nblocks; b0 += chunk, ++idx) {
+        Slot& s = slots[idx % used];
+        if ((rc = finish(s))) { cleanup(); return rc; }
+        s.b0 = b0;
+        s.nb = std::min(chunk, nblocks - b0);
+        gather(s);
+        hipError_t ae = hipMemcpyAsync(s.dev, s.pin, (size_t)s.nb * dbs, hipMemcpyHostToDevice, s.st);
+        uint16_t* dnd = nullptr;
+        if (num_data && ae == hipSuccess) {
+            dnd = s.dmeta;
+            ae = hipMemcpyAsync(dnd, num_data + b0, (size_t)s.nb * 2, hipMemcpyHostToDevice, s.st);
+        }
+        if (ae != hipSuccess) { cleanup(); return hip_fail(ae, "vector batch upload"); }
+        nfec_block_batch db;
+        std::memset(&db, 0, sizeof(db));
+        db.blocks = s.dev;
+        db.block_stride = dbs;
+        db.seg_stride = (uint32_t)ss;
+        db.nblocks = s.nb;
+        db.num_data = dnd;
+        db.flags = flags;
+        if (decode) {
+            uint16_t* dl = s.dmeta + chunk;
+            uint16_t* dc = dl + (size_t)chunk * lstride;
+            ae = hipMemcpyAsync(dl, locs + (uint64_t)b0 * lstride, (size_t)s.nb * lstride * 2, hipMemcpyHostToDevice, s.st);
+            if (ae == hipSuccess) ae = hipMemcpyAsync(dc, counts + b0, (size_t)s.nb * 2, hipMemcpyHostToDevice, s.st);
+            if (ae != hipSuccess) { cleanup(); return hip_fail(ae, "vector batch upload"); }
+            rc = decode_device(c, &db, dl, lstride, dc, s.dstat, s.st);
+            if (!rc) {
+                ae = hipMemcpyAsync(s.hstat, s.dstat, (size_t)s.nb * 4, hipMemcpyDeviceToHost, s.st);
+                if (ae != hipSuccess) { cleanup(); return hip_fail(ae, "vector batch status"); }
+            }
+        } else {
+            rc = encode_device(c, &db, s.st);
+        }
+        if (rc) { cleanup(); return rc; }
+        // unshortened encode: only the parity region of each block comes back
+        if (!decode && !num_data)
+            ae = hipMemcpy2DAsync(s.pin + (uint64_t)c->k * ss, dbs, s.dev + (uint64_t)c->k * ss, dbs, (uint64_t)c->m * ss,
+                                  s.nb, hipMemcpyDeviceToHost, s.st);
+        else
+            ae = hipMemcpyAsync(s.pin, s.dev, (size_t)s.nb * dbs, hipMemcpyDeviceToHost, s.st);
+        if (ae == hipSuccess) ae = hipEventRecord(s.done, s.st);
+        if (ae != hipSuccess) { cleanup(); return hip_fail(ae, "vector batch download"); }
+        s.busy = true;
+    }
+    for (uint32_t i = 0; i < used; ++i)
+        if ((rc = finish(slots[(idx + i) % used]))) { cleanup(); return rc; }
+    hipError_t e = hipGetLastError();
+    cleanup();
+    if (e != hipSuccess) return hip_fail(e, "vector batch");
+    return NFEC_OK;
+}
+
+int nfec_encode_host_vectors(nfec_codec* codec, void* const* vectors, uint32_t nblocks, const uint16_t* num_data,
+                             uint32_t flags)
+{
+    return run_host_vectors(codec, vectors, nblocks, num_data, nullptr, 0, nullptr, nullptr, flags, false);
+}
+
+int nfec_decode_host_vectors(nfec_codec* codec, void* const* vectors, uint32_t nblocks, const uint16_t* num_data,
+                             const uint16_t* erasure_locs, uint32_t erasure_stride, const uint16_t* erasure_counts,
+                             int32_t* status, uint32_t flags)
+{
+    return run_host_vectors(codec, vectors, nblocks, num_data, erasure_locs, erasure_stride, erasure_counts, status,
+                            flags, true);
+}
+
 int nfec_encode_host(nfec_codec* codec, const nfec_block_batch* host_batch)
 {
     return run_host_batch(codec, host_batch, nullptr, 0, nullptr, nullptr, false);
