@@ -27,6 +27,15 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md); measured copy 
 VALU_PEAK = 7.86e13    # 256 CU x 4 SIMD x 32 lanes x 2.4 GHz, 32-bit bitwise ops (ubench: 76% reachable)
 
 
+def encode_kernel_name(k, m, vec):
+    """the kernel nfec_encode dispatches for this shape (nfec_api.cpp encode_device)"""
+    if (k, m) not in ((64, 32), (64, 16), (64, 8)) or os.environ.get("NFEC_FORCE_GENERIC", "0") not in ("", "0"):
+        return "gf8_matmul_kernel (RS8 encode, generic)"
+    if os.environ.get("NFEC_ASM", "1") != "0" and vec % 8 == 0:
+        return f"nfec::rs8_asm_enc_k{k}_m{m} (RS8 encode, hand-allocated assembly body)"
+    return f"nfec::rs8_enc_k{k}_m{m} (RS8 encode, compiler-allocated)"
+
+
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
@@ -243,9 +252,7 @@ def main():
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4),
             "traffic": traffic,
-            "kernel": f"nfec::{'rs8_enc' if os.environ.get('NFEC_BS_VARIANT', '0') == '0' else 'rs8_lenc'}_k{k}_m{m} (RS8 encode)"
-            if (k, m) in ((64, 32), (64, 16), (64, 8)) and not os.environ.get("NFEC_FORCE_GENERIC")
-            else "gf8_matmul_kernel (RS8 encode)",
+            "kernel": encode_kernel_name(k, m, vec),
             "algorithmic_bytes_per_launch": enc_bytes,
             "read_only_frac": round(k * vec * nb / (enc_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
             "valu": valu,

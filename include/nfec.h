@@ -127,7 +127,10 @@ int nfec_encode(nfec_codec* codec, const nfec_block_batch* batch, void* stream);
  * first, then missing parity, as NormObject builds them); erasure_counts: device
  * [nblocks]; status: device [nblocks] or NULL -- per block the reference Decode return
  * value (erasureCount on success, 0 when the block cannot be repaired).
- * Erased source slots are repaired; parity slots are never written. */
+ * Erased source slots are repaired; parity slots are never written.
+ * A codec owns one decode workspace (like the reference decoder's scratch matrices,
+ * normEncoderRS8.cpp:559-606): decode calls on one codec must be ordered (same stream, or
+ * synchronised by the caller); encode calls only read the codec and may run concurrently. */
 int nfec_decode(nfec_codec* codec, const nfec_block_batch* batch, const uint16_t* erasure_locs,
                 uint32_t erasure_stride, const uint16_t* erasure_counts, int32_t* status,
                 void* stream);

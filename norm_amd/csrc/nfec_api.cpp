@@ -970,6 +970,23 @@ void copy2d(uint8_t* dst, uint64_t dpitch, const uint8_t* src, uint64_t spitch, 
 
 }  // namespace
 
+// The codec's decode workspace (plan, z rows, inverses) is shared by all of its decode calls,
+// so the host pipelines run every chunk's decode on one compute stream: slot stream upload ->
+// event -> compute-stream decode -> event -> slot stream download.  (Encode reads only the
+// codec's constants and runs on the slot streams.)
+static int decode_serialized(nfec_codec* c, const nfec_block_batch* db, const uint16_t* dl, uint32_t lstride,
+                             const uint16_t* dc, int32_t* dstat, hipStream_t slot_st, hipStream_t cst,
+                             hipEvent_t ev_up, hipEvent_t ev_done)
+{
+    NFEC_HIP(hipEventRecord(ev_up, slot_st));
+    NFEC_HIP(hipStreamWaitEvent(cst, ev_up, 0));
+    const int rc = decode_device(c, db, dl, lstride, dc, dstat, cst);
+    if (rc) return rc;
+    NFEC_HIP(hipEventRecord(ev_done, cst));
+    NFEC_HIP(hipStreamWaitEvent(slot_st, ev_done, 0));
+    return NFEC_OK;
+}
+
 static int run_host_batch(nfec_codec* c, const nfec_block_batch* hb, const uint16_t* locs, uint32_t lstride,
                           const uint16_t* counts, int32_t* status, bool decode)
 {
@@ -1008,9 +1025,11 @@ static int run_host_batch(nfec_codec* c, const nfec_block_batch* hb, const uint1
         int32_t* hstat = nullptr;   // pinned status readback
         hipStream_t st = nullptr;
         hipEvent_t done = nullptr;
+        hipEvent_t ev_up = nullptr, ev_cd = nullptr;
         uint32_t b0 = 0, nb = 0;
         bool busy = false;
     } slots[nslot];
+    hipStream_t cst = nullptr;
     const size_t meta = (size_t)chunk * (1 + lstride + 1);
     auto cleanup = [&]() {
         for (auto& s : slots) {
@@ -1021,10 +1040,18 @@ static int run_host_batch(nfec_codec* c, const nfec_block_batch* hb, const uint1
             if (s.dmeta) (void)hipFree(s.dmeta);
             if (s.dstat) (void)hipFree(s.dstat);
             if (s.done) (void)hipEventDestroy(s.done);
+            if (s.ev_up) (void)hipEventDestroy(s.ev_up);
+            if (s.ev_cd) (void)hipEventDestroy(s.ev_cd);
             if (s.st) (void)hipStreamDestroy(s.st);
+        }
+        if (cst) {
+            (void)hipStreamSynchronize(cst);
+            (void)hipStreamDestroy(cst);
         }
     };
     const uint32_t used = std::min<uint32_t>(nslot, (hb->nblocks + chunk - 1) / chunk);
+    if (decode && hipStreamCreateWithFlags(&cst, hipStreamNonBlocking) != hipSuccess)
+        return fail(NFEC_ENOMEM, "host batch stream creation failed");
     for (uint32_t i = 0; i < used; ++i) {
         Slot& s = slots[i];
         if (hipMalloc(reinterpret_cast<void**>(&s.dev), (size_t)chunk * dbs) != hipSuccess ||
@@ -1034,7 +1061,9 @@ static int run_host_batch(nfec_codec* c, const nfec_block_batch* hb, const uint1
             hipMalloc(reinterpret_cast<void**>(&s.dmeta), meta * 2 + 16) != hipSuccess ||
             hipMalloc(reinterpret_cast<void**>(&s.dstat), (size_t)chunk * 4 + 16) != hipSuccess ||
             hipStreamCreateWithFlags(&s.st, hipStreamNonBlocking) != hipSuccess ||
-            hipEventCreateWithFlags(&s.done, hipEventDisableTiming) != hipSuccess) {
+            hipEventCreateWithFlags(&s.done, hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&s.ev_up, hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&s.ev_cd, hipEventDisableTiming) != hipSuccess) {
             cleanup();
             return fail(NFEC_ENOMEM, "host batch staging allocation failed");
         }
@@ -1079,7 +1108,7 @@ static int run_host_batch(nfec_codec* c, const nfec_block_batch* hb, const uint1
             ae = hipMemcpyAsync(dl, locs + (uint64_t)b0 * lstride, (size_t)s.nb * lstride * 2, hipMemcpyHostToDevice, s.st);
             if (ae == hipSuccess) ae = hipMemcpyAsync(dc, counts + b0, (size_t)s.nb * 2, hipMemcpyHostToDevice, s.st);
             if (ae != hipSuccess) { cleanup(); return hip_fail(ae, "host batch upload"); }
-            rc = decode_device(c, &db, dl, lstride, dc, s.dstat, s.st);
+            rc = decode_serialized(c, &db, dl, lstride, dc, s.dstat, s.st, cst, s.ev_up, s.ev_cd);
         } else {
             rc = encode_device(c, &db, s.st);
         }
@@ -1168,9 +1197,11 @@ static int run_host_vectors(nfec_codec* c, void* const* vecs, uint32_t nblocks, 
         int32_t* hstat = nullptr;
         hipStream_t st = nullptr;
         hipEvent_t done = nullptr;
+        hipEvent_t ev_up = nullptr, ev_cd = nullptr;
         uint32_t b0 = 0, nb = 0;
         bool busy = false;
     } slots[nslot];
+    hipStream_t cst = nullptr;
     const size_t meta = (size_t)chunk * (1 + lstride + 1);
     auto cleanup = [&]() {
         for (auto& s : slots) {
@@ -1181,10 +1212,18 @@ static int run_host_vectors(nfec_codec* c, void* const* vecs, uint32_t nblocks, 
             if (s.dmeta) (void)hipFree(s.dmeta);
             if (s.dstat) (void)hipFree(s.dstat);
             if (s.done) (void)hipEventDestroy(s.done);
+            if (s.ev_up) (void)hipEventDestroy(s.ev_up);
+            if (s.ev_cd) (void)hipEventDestroy(s.ev_cd);
             if (s.st) (void)hipStreamDestroy(s.st);
+        }
+        if (cst) {
+            (void)hipStreamSynchronize(cst);
+            (void)hipStreamDestroy(cst);
         }
     };
     const uint32_t used = std::min<uint32_t>(nslot, (nblocks + chunk - 1) / chunk);
+    if (decode && hipStreamCreateWithFlags(&cst, hipStreamNonBlocking) != hipSuccess)
+        return fail(NFEC_ENOMEM, "vector batch stream creation failed");
     for (uint32_t i = 0; i < used; ++i) {
         Slot& s = slots[i];
         if (hipMalloc(reinterpret_cast<void**>(&s.dev), (size_t)chunk * dbs) != hipSuccess ||
@@ -1193,7 +1232,9 @@ static int run_host_vectors(nfec_codec* c, void* const* vecs, uint32_t nblocks, 
             hipMalloc(reinterpret_cast<void**>(&s.dmeta), meta * 2 + 16) != hipSuccess ||
             hipMalloc(reinterpret_cast<void**>(&s.dstat), (size_t)chunk * 4 + 16) != hipSuccess ||
             hipStreamCreateWithFlags(&s.st, hipStreamNonBlocking) != hipSuccess ||
-            hipEventCreateWithFlags(&s.done, hipEventDisableTiming) != hipSuccess) {
+            hipEventCreateWithFlags(&s.done, hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&s.ev_up, hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&s.ev_cd, hipEventDisableTiming) != hipSuccess) {
             cleanup();
             return fail(NFEC_ENOMEM, "vector batch staging allocation failed");
         }
@@ -1272,7 +1313,7 @@ static int run_host_vectors(nfec_codec* c, void* const* vecs, uint32_t nblocks, 
             ae = hipMemcpyAsync(dl, locs + (uint64_t)b0 * lstride, (size_t)s.nb * lstride * 2, hipMemcpyHostToDevice, s.st);
             if (ae == hipSuccess) ae = hipMemcpyAsync(dc, counts + b0, (size_t)s.nb * 2, hipMemcpyHostToDevice, s.st);
             if (ae != hipSuccess) { cleanup(); return hip_fail(ae, "vector batch upload"); }
-            rc = decode_device(c, &db, dl, lstride, dc, s.dstat, s.st);
+            rc = decode_serialized(c, &db, dl, lstride, dc, s.dstat, s.st, cst, s.ev_up, s.ev_cd);
             if (!rc) {
                 ae = hipMemcpyAsync(s.hstat, s.dstat, (size_t)s.nb * 4, hipMemcpyDeviceToHost, s.st);
                 if (ae != hipSuccess) { cleanup(); return hip_fail(ae, "vector batch status"); }

@@ -39,7 +39,10 @@ def main(root):
     json.dump(out, sys.stdout, indent=1, sort_keys=True)
     print()
     # traffic summary for bench.py (encode kernel, bench workload)
-    enc = [v for k_, v in out.items() if ("rs8_lenc_k64_m32" in k_ or "rs8_enc_k64_m32" in k_) and "FETCH_SIZE" in v]
+    # the encode kernel of the bench workload (assembly kernel by default, else the compiler-built one)
+    names = sorted((k_ for k_, v in out.items() if "enc" in k_ and "k64_m32" in k_ and "FETCH_SIZE" in v),
+                   key=lambda n: "asm" not in n)
+    enc = [out[n] for n in names]
     if enc and len(sys.argv) > 2:
         e = enc[0]
         traffic = {
