@@ -83,6 +83,45 @@ uint32_t round_up(uint32_t v, uint32_t a) { return (v + a - 1) / a * a; }
 
 }  // namespace
 
+constexpr uint32_t kHostSlots = 3;
+struct HostSlot {
+    uint8_t* dev = nullptr;
+    uint8_t* pin = nullptr;     // pinned staging (pageable callers, segment lists)
+    uint16_t* dmeta = nullptr;  // num_data, erasure locs, counts
+    int32_t* dstat = nullptr;
+    int32_t* hstat = nullptr;   // pinned status readback
+    hipStream_t st = nullptr;
+    hipEvent_t done = nullptr, ev_up = nullptr, ev_cd = nullptr;
+    size_t dev_bytes = 0, pin_bytes = 0, meta_bytes = 0, dstat_bytes = 0, hstat_bytes = 0;
+};
+
+// host-batch pipeline resources cached per codec (run_host_batch / run_host_vectors)
+struct HostStage {
+    HostSlot slot[kHostSlots];
+    hipStream_t cst = nullptr;  // decode compute stream
+    void release()
+    {
+        for (auto& s : slot) {
+            if (s.st) (void)hipStreamSynchronize(s.st);
+            if (s.dev) (void)hipFree(s.dev);
+            if (s.pin) (void)hipHostFree(s.pin);
+            if (s.dmeta) (void)hipFree(s.dmeta);
+            if (s.dstat) (void)hipFree(s.dstat);
+            if (s.hstat) (void)hipHostFree(s.hstat);
+            if (s.done) (void)hipEventDestroy(s.done);
+            if (s.ev_up) (void)hipEventDestroy(s.ev_up);
+            if (s.ev_cd) (void)hipEventDestroy(s.ev_cd);
+            if (s.st) (void)hipStreamDestroy(s.st);
+            s = HostSlot();
+        }
+        if (cst) {
+            (void)hipStreamSynchronize(cst);
+            (void)hipStreamDestroy(cst);
+            cst = nullptr;
+        }
+    }
+};
+
 struct nfec_codec {
     int kind = 0;
     int device = 0;
@@ -108,10 +147,12 @@ struct nfec_codec {
     // per-call staging
     DevBuf<uint8_t> s_block;
     DevBuf<uint16_t> s_locs;
+    HostStage stage;
 
     ~nfec_codec()
     {
         DeviceGuard g(device);
+        stage.release();
         for (auto* b : {&d_coef, &d_gen, &d_exp, &w_coef1, &w_coef2, &w_z, &w_work, &s_block, &d_mdp_step})
             b->release();
         d_vtab.release();
@@ -970,20 +1011,92 @@ void copy2d(uint8_t* dst, uint64_t dpitch, const uint8_t* src, uint64_t spitch, 
 
 }  // namespace
 
+// ---- cached host staging ----
+// The pipelines' device slots, pinned staging, streams and events live in the codec and grow
+// on demand: allocating (and freeing, which synchronises the whole device) per call would
+// stall every other codec's work on the GPU -- two codecs driven from two host threads (the
+// mixed RS8/RS16 stream of BASELINE C5) would serialise.  A codec is used by one host thread
+// at a time, like the reference's codec instances (normApi.cpp:55,126).
+static int grow_dev(void** p, size_t& cap, size_t need)
+{
+    if (cap >= need) return NFEC_OK;
+    if (*p) (void)hipFree(*p);
+    *p = nullptr;
+    cap = 0;
+    if (hipMalloc(p, need) != hipSuccess) return fail(NFEC_ENOMEM, "staging allocation failed");
+    cap = need;
+    return NFEC_OK;
+}
+
+static int grow_pin(void** p, size_t& cap, size_t need)
+{
+    if (cap >= need) return NFEC_OK;
+    if (*p) (void)hipHostFree(*p);
+    *p = nullptr;
+    cap = 0;
+    if (hipHostMalloc(p, need, hipHostMallocDefault) != hipSuccess) return fail(NFEC_ENOMEM, "pinned staging allocation failed");
+    cap = need;
+    return NFEC_OK;
+}
+
+static int stage_slot(nfec_codec* c, uint32_t i, size_t dev_bytes, size_t pin_bytes, size_t meta_bytes,
+                      size_t stat_bytes, HostSlot*& out)
+{
+    HostSlot& s = c->stage.slot[i];
+    int rc;
+    if ((rc = grow_dev(reinterpret_cast<void**>(&s.dev), s.dev_bytes, dev_bytes)) ||
+        (pin_bytes && (rc = grow_pin(reinterpret_cast<void**>(&s.pin), s.pin_bytes, pin_bytes))) ||
+        (rc = grow_dev(reinterpret_cast<void**>(&s.dmeta), s.meta_bytes, meta_bytes)) ||
+        (rc = grow_dev(reinterpret_cast<void**>(&s.dstat), s.dstat_bytes, stat_bytes)) ||
+        (rc = grow_pin(reinterpret_cast<void**>(&s.hstat), s.hstat_bytes, stat_bytes)))
+        return rc;
+    if (!s.st) {
+        if (hipStreamCreateWithFlags(&s.st, hipStreamNonBlocking) != hipSuccess ||
+            hipEventCreateWithFlags(&s.done, hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&s.ev_up, hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&s.ev_cd, hipEventDisableTiming) != hipSuccess)
+            return fail(NFEC_ENOMEM, "staging stream creation failed");
+    }
+    if (!c->stage.cst && hipStreamCreateWithFlags(&c->stage.cst, hipStreamNonBlocking) != hipSuccess)
+        return fail(NFEC_ENOMEM, "staging stream creation failed");
+    out = &s;
+    return NFEC_OK;
+}
+
+// Blocks per pipeline chunk: about 256 MiB, but never fewer than the blocks it takes to fill
+// the GPU when the kernels run one wave per block (RS16, MDP, the generic RS8 kernels: 16 waves
+// per CU, 4096 blocks), and at most 4 GiB per slot.
+static uint32_t host_chunk(const nfec_codec* c, uint64_t dbs, uint32_t nblocks)
+{
+    if (const char* e = std::getenv("NFEC_HOST_CHUNK_BLOCKS"))  // tests: force multi-chunk pipelines
+        if (std::atol(e) > 0) return (uint32_t)std::min<uint64_t>((uint64_t)std::atol(e), nblocks);
+    const bool per_block = !(c->kind == NFEC_RS8 && has_bitsliced(c->k, c->m));
+    uint64_t ch = std::max<uint64_t>(1, (256ull << 20) / std::max<uint64_t>(dbs, 1));
+    if (per_block) ch = std::max<uint64_t>(ch, 4096);
+    ch = std::min<uint64_t>(ch, std::max<uint64_t>(1, (4ull << 30) / std::max<uint64_t>(dbs, 1)));
+    return (uint32_t)std::min<uint64_t>(ch, nblocks);
+}
+
+static void stage_drain(nfec_codec* c)
+{
+    for (auto& s : c->stage.slot)
+        if (s.st) (void)hipStreamSynchronize(s.st);
+    if (c->stage.cst) (void)hipStreamSynchronize(c->stage.cst);
+}
+
 // The codec's decode workspace (plan, z rows, inverses) is shared by all of its decode calls,
 // so the host pipelines run every chunk's decode on one compute stream: slot stream upload ->
 // event -> compute-stream decode -> event -> slot stream download.  (Encode reads only the
 // codec's constants and runs on the slot streams.)
 static int decode_serialized(nfec_codec* c, const nfec_block_batch* db, const uint16_t* dl, uint32_t lstride,
-                             const uint16_t* dc, int32_t* dstat, hipStream_t slot_st, hipStream_t cst,
-                             hipEvent_t ev_up, hipEvent_t ev_done)
+                             const uint16_t* dc, HostSlot& s)
 {
-    NFEC_HIP(hipEventRecord(ev_up, slot_st));
-    NFEC_HIP(hipStreamWaitEvent(cst, ev_up, 0));
-    const int rc = decode_device(c, db, dl, lstride, dc, dstat, cst);
+    NFEC_HIP(hipEventRecord(s.ev_up, s.st));
+    NFEC_HIP(hipStreamWaitEvent(c->stage.cst, s.ev_up, 0));
+    const int rc = decode_device(c, db, dl, lstride, dc, s.dstat, c->stage.cst);
     if (rc) return rc;
-    NFEC_HIP(hipEventRecord(ev_done, cst));
-    NFEC_HIP(hipStreamWaitEvent(slot_st, ev_done, 0));
+    NFEC_HIP(hipEventRecord(s.ev_cd, c->stage.cst));
+    NFEC_HIP(hipStreamWaitEvent(s.st, s.ev_cd, 0));
     return NFEC_OK;
 }
 
@@ -1014,123 +1127,88 @@ static int run_host_batch(nfec_codec* c, const nfec_block_batch* hb, const uint1
     const bool pinned = host_is_pinned(hb->blocks);
     uint8_t* const hbase = static_cast<uint8_t*>(hb->blocks);
 
-    const uint32_t chunk = (uint32_t)std::max<uint64_t>(
-        1, std::min<uint64_t>(hb->nblocks, (64ull << 20) / std::max<uint64_t>(dbs, 1)));
-    constexpr uint32_t nslot = 3;
-    struct Slot {
-        uint8_t* dev = nullptr;
-        uint8_t* pin = nullptr;     // staging (pageable caller buffers only), pitch dbs
-        uint16_t* dmeta = nullptr;  // num_data, locs, counts
-        int32_t* dstat = nullptr;
-        int32_t* hstat = nullptr;   // pinned status readback
-        hipStream_t st = nullptr;
-        hipEvent_t done = nullptr;
-        hipEvent_t ev_up = nullptr, ev_cd = nullptr;
+    const uint32_t chunk = host_chunk(c, dbs, hb->nblocks);
+    const uint32_t used = std::min<uint32_t>(kHostSlots, (hb->nblocks + chunk - 1) / chunk);
+    const size_t meta = (size_t)chunk * (1 + lstride + 1);
+    HostSlot* sl[kHostSlots] = {};
+    for (uint32_t i = 0; i < used; ++i)
+        if ((rc = stage_slot(c, i, (size_t)chunk * dbs, pinned ? 0 : (size_t)chunk * dbs, meta * 2 + 16,
+                             (size_t)chunk * 4 + 16, sl[i])))
+            return rc;
+    struct Job {
         uint32_t b0 = 0, nb = 0;
         bool busy = false;
-    } slots[nslot];
-    hipStream_t cst = nullptr;
-    const size_t meta = (size_t)chunk * (1 + lstride + 1);
-    auto cleanup = [&]() {
-        for (auto& s : slots) {
-            if (s.st) (void)hipStreamSynchronize(s.st);
-            if (s.dev) (void)hipFree(s.dev);
-            if (s.pin) (void)hipHostFree(s.pin);
-            if (s.hstat) (void)hipHostFree(s.hstat);
-            if (s.dmeta) (void)hipFree(s.dmeta);
-            if (s.dstat) (void)hipFree(s.dstat);
-            if (s.done) (void)hipEventDestroy(s.done);
-            if (s.ev_up) (void)hipEventDestroy(s.ev_up);
-            if (s.ev_cd) (void)hipEventDestroy(s.ev_cd);
-            if (s.st) (void)hipStreamDestroy(s.st);
-        }
-        if (cst) {
-            (void)hipStreamSynchronize(cst);
-            (void)hipStreamDestroy(cst);
-        }
-    };
-    const uint32_t used = std::min<uint32_t>(nslot, (hb->nblocks + chunk - 1) / chunk);
-    if (decode && hipStreamCreateWithFlags(&cst, hipStreamNonBlocking) != hipSuccess)
-        return fail(NFEC_ENOMEM, "host batch stream creation failed");
-    for (uint32_t i = 0; i < used; ++i) {
-        Slot& s = slots[i];
-        if (hipMalloc(reinterpret_cast<void**>(&s.dev), (size_t)chunk * dbs) != hipSuccess ||
-            (!pinned && hipHostMalloc(reinterpret_cast<void**>(&s.pin), (size_t)chunk * dbs, hipHostMallocDefault) !=
-                            hipSuccess) ||
-            hipHostMalloc(reinterpret_cast<void**>(&s.hstat), (size_t)chunk * 4 + 16, hipHostMallocDefault) != hipSuccess ||
-            hipMalloc(reinterpret_cast<void**>(&s.dmeta), meta * 2 + 16) != hipSuccess ||
-            hipMalloc(reinterpret_cast<void**>(&s.dstat), (size_t)chunk * 4 + 16) != hipSuccess ||
-            hipStreamCreateWithFlags(&s.st, hipStreamNonBlocking) != hipSuccess ||
-            hipEventCreateWithFlags(&s.done, hipEventDisableTiming) != hipSuccess ||
-            hipEventCreateWithFlags(&s.ev_up, hipEventDisableTiming) != hipSuccess ||
-            hipEventCreateWithFlags(&s.ev_cd, hipEventDisableTiming) != hipSuccess) {
-            cleanup();
-            return fail(NFEC_ENOMEM, "host batch staging allocation failed");
-        }
-    }
-    auto finish = [&](Slot& s) -> int {
-        if (!s.busy) return NFEC_OK;
-        s.busy = false;
+    } jobs[kHostSlots];
+    auto finish = [&](uint32_t i) -> int {
+        Job& j = jobs[i];
+        HostSlot& s = *sl[i];
+        if (!j.busy) return NFEC_OK;
+        j.busy = false;
         NFEC_HIP(hipEventSynchronize(s.done));
         if (!pinned)
-            for (const auto& pc : dn) copy2d(hbase + (uint64_t)s.b0 * hbs + pc.first, hbs, s.pin + pc.first, dbs, pc.second, s.nb);
-        if (decode && status) std::memcpy(status + s.b0, s.hstat, (size_t)s.nb * 4);
+            for (const auto& pc : dn) copy2d(hbase + (uint64_t)j.b0 * hbs + pc.first, hbs, s.pin + pc.first, dbs, pc.second, j.nb);
+        if (decode && status) std::memcpy(status + j.b0, s.hstat, (size_t)j.nb * 4);
         return NFEC_OK;
+    };
+    auto bail = [&](int code) {
+        stage_drain(c);
+        return code;
     };
     uint32_t idx = 0;
     for (uint32_t b0 = 0; b0 < hb->nblocks; b0 += chunk, ++idx) {
-        Slot& s = slots[idx % used];
-        if ((rc = finish(s))) { cleanup(); return rc; }
-        s.b0 = b0;
-        s.nb = std::min(chunk, hb->nblocks - b0);
+        const uint32_t i = idx % used;
+        if ((rc = finish(i))) return bail(rc);
+        HostSlot& s = *sl[i];
+        Job& j = jobs[i];
+        j.b0 = b0;
+        j.nb = std::min(chunk, hb->nblocks - b0);
         uint8_t* hsrc = hbase + (uint64_t)b0 * hbs;
         hipError_t ae;
         if (pinned) {
-            ae = hipMemcpy2DAsync(s.dev + up_off, dbs, hsrc + up_off, hbs, up_len, s.nb, hipMemcpyHostToDevice, s.st);
+            ae = hipMemcpy2DAsync(s.dev + up_off, dbs, hsrc + up_off, hbs, up_len, j.nb, hipMemcpyHostToDevice, s.st);
         } else {
-            copy2d(s.pin + up_off, dbs, hsrc + up_off, hbs, up_len, s.nb);
-            ae = hipMemcpyAsync(s.dev, s.pin, (size_t)(s.nb - 1) * dbs + up_off + up_len, hipMemcpyHostToDevice, s.st);
+            copy2d(s.pin + up_off, dbs, hsrc + up_off, hbs, up_len, j.nb);
+            ae = hipMemcpyAsync(s.dev, s.pin, (size_t)(j.nb - 1) * dbs + up_off + up_len, hipMemcpyHostToDevice, s.st);
         }
         uint16_t* dnd = nullptr;
         if (hb->num_data) {
             dnd = s.dmeta;
-            if (ae == hipSuccess) ae = hipMemcpyAsync(dnd, hb->num_data + b0, (size_t)s.nb * 2, hipMemcpyHostToDevice, s.st);
+            if (ae == hipSuccess) ae = hipMemcpyAsync(dnd, hb->num_data + b0, (size_t)j.nb * 2, hipMemcpyHostToDevice, s.st);
         }
         nfec_block_batch db = *hb;
         db.blocks = s.dev;
         db.block_stride = dbs;
-        db.nblocks = s.nb;
+        db.nblocks = j.nb;
         db.num_data = dnd;
-        if (ae != hipSuccess) { cleanup(); return hip_fail(ae, "host batch upload"); }
+        if (ae != hipSuccess) return bail(hip_fail(ae, "host batch upload"));
         if (decode) {
             uint16_t* dl = s.dmeta + chunk;
             uint16_t* dc = dl + (size_t)chunk * lstride;
-            ae = hipMemcpyAsync(dl, locs + (uint64_t)b0 * lstride, (size_t)s.nb * lstride * 2, hipMemcpyHostToDevice, s.st);
-            if (ae == hipSuccess) ae = hipMemcpyAsync(dc, counts + b0, (size_t)s.nb * 2, hipMemcpyHostToDevice, s.st);
-            if (ae != hipSuccess) { cleanup(); return hip_fail(ae, "host batch upload"); }
-            rc = decode_serialized(c, &db, dl, lstride, dc, s.dstat, s.st, cst, s.ev_up, s.ev_cd);
+            ae = hipMemcpyAsync(dl, locs + (uint64_t)b0 * lstride, (size_t)j.nb * lstride * 2, hipMemcpyHostToDevice, s.st);
+            if (ae == hipSuccess) ae = hipMemcpyAsync(dc, counts + b0, (size_t)j.nb * 2, hipMemcpyHostToDevice, s.st);
+            if (ae != hipSuccess) return bail(hip_fail(ae, "host batch upload"));
+            rc = decode_serialized(c, &db, dl, lstride, dc, s);
         } else {
             rc = encode_device(c, &db, s.st);
         }
-        if (rc) { cleanup(); return rc; }
+        if (rc) return bail(rc);
         if (pinned)
-            for (size_t i = 0; i < dn.size() && ae == hipSuccess; ++i)
-                ae = hipMemcpy2DAsync(hsrc + dn[i].first, hbs, s.dev + dn[i].first, dbs, dn[i].second, s.nb,
+            for (size_t q = 0; q < dn.size() && ae == hipSuccess; ++q)
+                ae = hipMemcpy2DAsync(hsrc + dn[q].first, hbs, s.dev + dn[q].first, dbs, dn[q].second, j.nb,
                                       hipMemcpyDeviceToHost, s.st);
         else
-            ae = hipMemcpyAsync(s.pin + dn_off, s.dev + dn_off, (size_t)(s.nb - 1) * dbs + dn_len, hipMemcpyDeviceToHost,
+            ae = hipMemcpyAsync(s.pin + dn_off, s.dev + dn_off, (size_t)(j.nb - 1) * dbs + dn_len, hipMemcpyDeviceToHost,
                                 s.st);
         if (ae == hipSuccess && decode && status)
-            ae = hipMemcpyAsync(s.hstat, s.dstat, (size_t)s.nb * 4, hipMemcpyDeviceToHost, s.st);
+            ae = hipMemcpyAsync(s.hstat, s.dstat, (size_t)j.nb * 4, hipMemcpyDeviceToHost, s.st);
         if (ae == hipSuccess) ae = hipEventRecord(s.done, s.st);
-        if (ae != hipSuccess) { cleanup(); return hip_fail(ae, "host batch copy"); }
-        s.busy = true;
+        if (ae != hipSuccess) return bail(hip_fail(ae, "host batch copy"));
+        j.busy = true;
     }
-    for (uint32_t i = 0; i < used; ++i)
-        if ((rc = finish(slots[(idx + i) % used]))) { cleanup(); return rc; }
+    for (uint32_t q = 0; q < used; ++q)
+        if ((rc = finish((idx + q) % used))) return bail(rc);
     hipError_t e = hipGetLastError();
-    cleanup();
-    if (e != hipSuccess) return hip_fail(e, "host batch");
+    if (e != hipSuccess) return bail(hip_fail(e, "host batch"));
     return NFEC_OK;
 }
 
@@ -1187,80 +1265,41 @@ static int run_host_vectors(nfec_codec* c, void* const* vecs, uint32_t nblocks, 
             if (!vecs[(uint64_t)b * n + s]) return fail(NFEC_EINVAL, "null source/parity vector");
     }
     DeviceGuard g(c->device);
-    const uint32_t chunk = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(nblocks, (64ull << 20) / dbs));
-    constexpr uint32_t nslot = 3;
-    struct Slot {
-        uint8_t* dev = nullptr;
-        uint8_t* pin = nullptr;
-        uint16_t* dmeta = nullptr;
-        int32_t* dstat = nullptr;
-        int32_t* hstat = nullptr;
-        hipStream_t st = nullptr;
-        hipEvent_t done = nullptr;
-        hipEvent_t ev_up = nullptr, ev_cd = nullptr;
+    const uint32_t chunk = host_chunk(c, dbs, nblocks);
+    const uint32_t used = std::min<uint32_t>(kHostSlots, (nblocks + chunk - 1) / chunk);
+    const size_t meta = (size_t)chunk * (1 + lstride + 1);
+    HostSlot* sl[kHostSlots] = {};
+    int rc;
+    for (uint32_t i = 0; i < used; ++i)
+        if ((rc = stage_slot(c, i, (size_t)chunk * dbs, (size_t)chunk * dbs, meta * 2 + 16, (size_t)chunk * 4 + 16,
+                             sl[i])))
+            return rc;
+    struct Job {
         uint32_t b0 = 0, nb = 0;
         bool busy = false;
-    } slots[nslot];
-    hipStream_t cst = nullptr;
-    const size_t meta = (size_t)chunk * (1 + lstride + 1);
-    auto cleanup = [&]() {
-        for (auto& s : slots) {
-            if (s.st) (void)hipStreamSynchronize(s.st);
-            if (s.dev) (void)hipFree(s.dev);
-            if (s.pin) (void)hipHostFree(s.pin);
-            if (s.hstat) (void)hipHostFree(s.hstat);
-            if (s.dmeta) (void)hipFree(s.dmeta);
-            if (s.dstat) (void)hipFree(s.dstat);
-            if (s.done) (void)hipEventDestroy(s.done);
-            if (s.ev_up) (void)hipEventDestroy(s.ev_up);
-            if (s.ev_cd) (void)hipEventDestroy(s.ev_cd);
-            if (s.st) (void)hipStreamDestroy(s.st);
-        }
-        if (cst) {
-            (void)hipStreamSynchronize(cst);
-            (void)hipStreamDestroy(cst);
-        }
-    };
-    const uint32_t used = std::min<uint32_t>(nslot, (nblocks + chunk - 1) / chunk);
-    if (decode && hipStreamCreateWithFlags(&cst, hipStreamNonBlocking) != hipSuccess)
-        return fail(NFEC_ENOMEM, "vector batch stream creation failed");
-    for (uint32_t i = 0; i < used; ++i) {
-        Slot& s = slots[i];
-        if (hipMalloc(reinterpret_cast<void**>(&s.dev), (size_t)chunk * dbs) != hipSuccess ||
-            hipHostMalloc(reinterpret_cast<void**>(&s.pin), (size_t)chunk * dbs, hipHostMallocDefault) != hipSuccess ||
-            hipHostMalloc(reinterpret_cast<void**>(&s.hstat), (size_t)chunk * 4 + 16, hipHostMallocDefault) != hipSuccess ||
-            hipMalloc(reinterpret_cast<void**>(&s.dmeta), meta * 2 + 16) != hipSuccess ||
-            hipMalloc(reinterpret_cast<void**>(&s.dstat), (size_t)chunk * 4 + 16) != hipSuccess ||
-            hipStreamCreateWithFlags(&s.st, hipStreamNonBlocking) != hipSuccess ||
-            hipEventCreateWithFlags(&s.done, hipEventDisableTiming) != hipSuccess ||
-            hipEventCreateWithFlags(&s.ev_up, hipEventDisableTiming) != hipSuccess ||
-            hipEventCreateWithFlags(&s.ev_cd, hipEventDisableTiming) != hipSuccess) {
-            cleanup();
-            return fail(NFEC_ENOMEM, "vector batch staging allocation failed");
-        }
-    }
+    } jobs[kHostSlots];
     const uint64_t blk_bytes = (uint64_t)n * c->vec;
-    auto gather = [&](Slot& s) {
-        parallel_blocks(s.nb, (uint64_t)s.nb * blk_bytes, [&](uint32_t i0, uint32_t i1) {
+    auto gather = [&](HostSlot& s, const Job& j) {
+        parallel_blocks(j.nb, (uint64_t)j.nb * blk_bytes, [&](uint32_t i0, uint32_t i1) {
             for (uint32_t i = i0; i < i1; ++i) {
-                const uint32_t b = s.b0 + i;
+                const uint32_t b = j.b0 + i;
                 const uint32_t nd = num_data ? num_data[b] : c->k;
                 // encode without accumulate reads the source only; everything else reads the
                 // whole listed block (absent parity is zero, as MDP's decoder treats it)
                 const uint32_t up = (!decode && !acc) ? nd : nd + c->m;
                 uint8_t* dst = s.pin + (uint64_t)i * dbs;
-                for (uint32_t sl = 0; sl < up; ++sl) {
-                    const void* p = vecs[(uint64_t)b * n + sl];
-                    if (p) std::memcpy(dst + sl * ss, p, c->vec);
-                    else std::memset(dst + sl * ss, 0, c->vec);
+                for (uint32_t q = 0; q < up; ++q) {
+                    const void* p = vecs[(uint64_t)b * n + q];
+                    if (p) std::memcpy(dst + q * ss, p, c->vec);
+                    else std::memset(dst + q * ss, 0, c->vec);
                 }
             }
         });
     };
-    auto scatter = [&](Slot& s) {
-        parallel_blocks(s.nb, (uint64_t)s.nb * (uint64_t)c->m * c->vec, [&](uint32_t i0, uint32_t i1) {
+    auto scatter = [&](HostSlot& s, const Job& j) {
+        parallel_blocks(j.nb, (uint64_t)j.nb * (uint64_t)c->m * c->vec, [&](uint32_t i0, uint32_t i1) {
             for (uint32_t i = i0; i < i1; ++i) {
-                const uint32_t b = s.b0 + i;
+                const uint32_t b = j.b0 + i;
                 const uint32_t nd = num_data ? num_data[b] : c->k;
                 const uint8_t* src = s.pin + (uint64_t)i * dbs;
                 if (!decode) {
@@ -1276,67 +1315,72 @@ static int run_host_vectors(nfec_codec* c, void* const* vecs, uint32_t nblocks, 
             }
         });
     };
-    int rc = NFEC_OK;
-    auto finish = [&](Slot& s) -> int {
-        if (!s.busy) return NFEC_OK;
-        s.busy = false;
-        NFEC_HIP(hipEventSynchronize(s.done));
-        scatter(s);
-        if (decode && status) std::memcpy(status + s.b0, s.hstat, (size_t)s.nb * 4);
+    auto finish = [&](uint32_t i) -> int {
+        Job& j = jobs[i];
+        if (!j.busy) return NFEC_OK;
+        j.busy = false;
+        NFEC_HIP(hipEventSynchronize(sl[i]->done));
+        scatter(*sl[i], j);
+        if (decode && status) std::memcpy(status + j.b0, sl[i]->hstat, (size_t)j.nb * 4);
         return NFEC_OK;
+    };
+    auto bail = [&](int code) {
+        stage_drain(c);
+        return code;
     };
     uint32_t idx = 0;
     for (uint32_t b0 = 0; b0 < nblocks; b0 += chunk, ++idx) {
-        Slot& s = slots[idx % used];
-        if ((rc = finish(s))) { cleanup(); return rc; }
-        s.b0 = b0;
-        s.nb = std::min(chunk, nblocks - b0);
-        gather(s);
-        hipError_t ae = hipMemcpyAsync(s.dev, s.pin, (size_t)s.nb * dbs, hipMemcpyHostToDevice, s.st);
+        const uint32_t i = idx % used;
+        if ((rc = finish(i))) return bail(rc);
+        HostSlot& s = *sl[i];
+        Job& j = jobs[i];
+        j.b0 = b0;
+        j.nb = std::min(chunk, nblocks - b0);
+        gather(s, j);
+        hipError_t ae = hipMemcpyAsync(s.dev, s.pin, (size_t)j.nb * dbs, hipMemcpyHostToDevice, s.st);
         uint16_t* dnd = nullptr;
         if (num_data && ae == hipSuccess) {
             dnd = s.dmeta;
-            ae = hipMemcpyAsync(dnd, num_data + b0, (size_t)s.nb * 2, hipMemcpyHostToDevice, s.st);
+            ae = hipMemcpyAsync(dnd, num_data + b0, (size_t)j.nb * 2, hipMemcpyHostToDevice, s.st);
         }
-        if (ae != hipSuccess) { cleanup(); return hip_fail(ae, "vector batch upload"); }
+        if (ae != hipSuccess) return bail(hip_fail(ae, "vector batch upload"));
         nfec_block_batch db;
         std::memset(&db, 0, sizeof(db));
         db.blocks = s.dev;
         db.block_stride = dbs;
         db.seg_stride = (uint32_t)ss;
-        db.nblocks = s.nb;
+        db.nblocks = j.nb;
         db.num_data = dnd;
         db.flags = flags;
         if (decode) {
             uint16_t* dl = s.dmeta + chunk;
             uint16_t* dc = dl + (size_t)chunk * lstride;
-            ae = hipMemcpyAsync(dl, locs + (uint64_t)b0 * lstride, (size_t)s.nb * lstride * 2, hipMemcpyHostToDevice, s.st);
-            if (ae == hipSuccess) ae = hipMemcpyAsync(dc, counts + b0, (size_t)s.nb * 2, hipMemcpyHostToDevice, s.st);
-            if (ae != hipSuccess) { cleanup(); return hip_fail(ae, "vector batch upload"); }
-            rc = decode_serialized(c, &db, dl, lstride, dc, s.dstat, s.st, cst, s.ev_up, s.ev_cd);
+            ae = hipMemcpyAsync(dl, locs + (uint64_t)b0 * lstride, (size_t)j.nb * lstride * 2, hipMemcpyHostToDevice, s.st);
+            if (ae == hipSuccess) ae = hipMemcpyAsync(dc, counts + b0, (size_t)j.nb * 2, hipMemcpyHostToDevice, s.st);
+            if (ae != hipSuccess) return bail(hip_fail(ae, "vector batch upload"));
+            rc = decode_serialized(c, &db, dl, lstride, dc, s);
             if (!rc) {
-                ae = hipMemcpyAsync(s.hstat, s.dstat, (size_t)s.nb * 4, hipMemcpyDeviceToHost, s.st);
-                if (ae != hipSuccess) { cleanup(); return hip_fail(ae, "vector batch status"); }
+                ae = hipMemcpyAsync(s.hstat, s.dstat, (size_t)j.nb * 4, hipMemcpyDeviceToHost, s.st);
+                if (ae != hipSuccess) return bail(hip_fail(ae, "vector batch status"));
             }
         } else {
             rc = encode_device(c, &db, s.st);
         }
-        if (rc) { cleanup(); return rc; }
+        if (rc) return bail(rc);
         // unshortened encode: only the parity region of each block comes back
         if (!decode && !num_data)
             ae = hipMemcpy2DAsync(s.pin + (uint64_t)c->k * ss, dbs, s.dev + (uint64_t)c->k * ss, dbs, (uint64_t)c->m * ss,
-                                  s.nb, hipMemcpyDeviceToHost, s.st);
+                                  j.nb, hipMemcpyDeviceToHost, s.st);
         else
-            ae = hipMemcpyAsync(s.pin, s.dev, (size_t)s.nb * dbs, hipMemcpyDeviceToHost, s.st);
+            ae = hipMemcpyAsync(s.pin, s.dev, (size_t)j.nb * dbs, hipMemcpyDeviceToHost, s.st);
         if (ae == hipSuccess) ae = hipEventRecord(s.done, s.st);
-        if (ae != hipSuccess) { cleanup(); return hip_fail(ae, "vector batch download"); }
-        s.busy = true;
+        if (ae != hipSuccess) return bail(hip_fail(ae, "vector batch download"));
+        j.busy = true;
     }
-    for (uint32_t i = 0; i < used; ++i)
-        if ((rc = finish(slots[(idx + i) % used]))) { cleanup(); return rc; }
+    for (uint32_t q = 0; q < used; ++q)
+        if ((rc = finish((idx + q) % used))) return bail(rc);
     hipError_t e = hipGetLastError();
-    cleanup();
-    if (e != hipSuccess) return hip_fail(e, "vector batch");
+    if (e != hipSuccess) return bail(hip_fail(e, "vector batch"));
     return NFEC_OK;
 }
 

@@ -264,9 +264,10 @@ def test_host_batch_paths_match_device(orc):
     (NFEC_RS16, 30, 10, 998, 1000, 33),
     (NFEC_MDP, 24, 8, 600, 608, 50),
 ])
-def test_host_batch_pipeline(orc, kind, k, m, vec, stride, nb, pinned):
+def test_host_batch_pipeline(orc, kind, k, m, vec, stride, nb, pinned, monkeypatch):
     """nfec_encode_host/nfec_decode_host over multi-chunk batches, pinned and pageable caller
     buffers: parity and repaired source match the oracle and slot padding is never written."""
+    monkeypatch.setenv("NFEC_HOST_CHUNK_BLOCKS", str(max(1, nb // 4)))  # several pipeline chunks
     enc, dec = _codecs(kind, k, m, vec)
     base = orc.make_blocks(k, m, vec, nb, seg_stride=stride)
     base[:, :, vec:] = 0xA5

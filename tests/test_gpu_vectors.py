@@ -45,6 +45,11 @@ ENC = [  # kind, k, m, vec, nblocks, shortened
 ]
 
 
+@pytest.fixture(autouse=True)
+def _small_chunks(monkeypatch):
+    monkeypatch.setenv("NFEC_HOST_CHUNK_BLOCKS", "300")  # several pipeline chunks per batch
+
+
 @pytest.mark.parametrize("kind,k,m,vec,nb,short", ENC)
 def test_encode_vectors_matches_oracle(orc, kind, k, m, vec, nb, short):
     rng = np.random.default_rng(5)
