@@ -261,7 +261,7 @@ __global__ __launch_bounds__(kThreads) void gf8_solve_kernel(Gf8SolveArgs a)
     const uint32_t blk = uni(blockIdx.x * kWavesPerGroup + w);
     if (blk >= a.nblocks) return;
     const int32_t rows = (int32_t)uni((uint32_t)a.rows[blk]);
-    if (rows <= 0) return;
+    if (rows <= 0 || rows <= a.min_rows) return;
     const uint32_t cols = min(uni((uint32_t)a.cols[blk]), (uint32_t)kMaxCols);
     const uint32_t cols2 = (cols + 1) & ~1u;
 

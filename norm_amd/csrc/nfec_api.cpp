@@ -592,6 +592,23 @@ int decode_device(nfec_codec* c, const nfec_block_batch* b, const uint16_t* locs
             a2.nblocks = nb;
             a2.vec_bytes = c->vec;
             a2.accumulate = acc;
+            // bit-sliced snippet-table solve for blocks with <= 16 erasures (NFEC_SOLVE_BS=0: off),
+            // the v_perm kernel for the rest
+            static const bool use_bs = [] {
+                const char* e = std::getenv("NFEC_SOLVE_BS");
+                return !(e && e[0] == '0');
+            }();
+            if (use_bs) {
+                rc = launch_gf8_solve_bs(a2, s);
+                if (rc != NFEC_OK && rc != NFEC_ENOTSUP) return fail(rc, "bit-sliced solve launch failed");
+                if (rc == NFEC_OK) {
+                    if (std::min(c->m, c->k) > 16) {
+                        a2.min_rows = 16;
+                        if ((rc = launch_gf8_solve(a2, std::min(c->m, c->k), c->m, s))) return rc;
+                    }
+                    continue;
+                }
+            }
             if ((rc = launch_gf8_solve(a2, std::min(c->m, c->k), c->m, s))) return rc;
             continue;
         }

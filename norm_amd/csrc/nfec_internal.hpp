@@ -117,8 +117,11 @@ struct Gf8SolveArgs {
     uint32_t nblocks = 0;
     uint32_t vec_bytes = 0;
     uint32_t accumulate = 0;
+    int32_t min_rows = 0;                // skip blocks with rows <= min_rows (done by another kernel)
 };
 int launch_gf8_solve(const Gf8SolveArgs& a, uint32_t max_rows, uint32_t max_cols, hipStream_t s);
+// gen_solve_asm.hip: bit-sliced solve for blocks with rows <= 16 (NFEC_ENOTSUP: other shapes)
+int launch_gf8_solve_bs(const Gf8SolveArgs& a, hipStream_t s);
 
 // GF(2^16) variant (log/exp); coef holds generator elements (uint16) at the same indexing.
 struct Gf16MatmulArgs {
