@@ -137,8 +137,12 @@ def solve_asm():
           f"s_addc_u32 s{S_TAB + 1}, s{S_TAB + 1}, 0"]
 
     def zload(t):
+        # rows past e are issued (the vmcnt accounting stays static) but as out-of-range loads
+        # (num_records 0): no memory traffic
         w = ring_slot(t)
-        out = [f"s_mul_i32 s{S_ZOFF}, %[zs], {t}"]
+        out = [f"s_mul_i32 s{S_ZOFF}, %[zs], {t}",
+               f"s_cmp_lt_u32 {t}, %[e]",
+               f"s_cselect_b32 s{S_ZRS + 2}, -1, 0"]
         for q in range(4):
             out.append(f"buffer_load_dwordx2 v[{w[2 * q]}:{w[2 * q + 1]}], {offs[q]}, s[{S_ZRS}:{S_ZRS + 3}], s{S_ZOFF} offen")
         return out
