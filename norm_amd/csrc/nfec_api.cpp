@@ -533,6 +533,32 @@ int decode_device(nfec_codec* c, const nfec_block_batch* b, const uint16_t* locs
             p2.coef_stride = c->cs;
             p2.coef2 = c->w_coef2.p;
             if ((rc = launch_rs_plan2(p2, s))) return rc;
+            // fused per-block repair for the blocks it qualifies for (NFEC_FUSED=0: off); the
+            // unfused stage 1 and solve below skip the blocks it marked
+            static const bool use_fused = [] {
+                const char* e = std::getenv("NFEC_FUSED");
+                return !(e && e[0] == '0');
+            }();
+            if (use_fused) {
+                FdecArgs f;
+                f.base = blocks;
+                f.block_stride = b->block_stride;
+                f.seg_stride = b->seg_stride;
+                f.nblocks = nb;
+                f.vec = c->vec;
+                f.ips = c->vec / 8;
+                f.rows = c->w_rows.p;
+                f.psel = c->w_psel.p;
+                f.emask = c->w_emask.p;
+                f.coef = c->w_coef2.p;
+                f.coef_block_stride = (uint64_t)c->cs * c->cs;
+                f.coef_col_stride = c->cs;
+                f.out_slots = c->w_oslots.p;
+                f.slots_stride = c->k;
+                f.accumulate = acc;
+                rc = launch_rs8_fused_decode(c->k, c->m, f, s);
+                if (rc != NFEC_OK && rc != NFEC_ENOTSUP) return fail(rc, "fused decode launch failed");
+            }
             bs::DecArgs d;
             d.base = blocks;
             d.block_stride = b->block_stride;

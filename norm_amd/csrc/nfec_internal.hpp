@@ -206,6 +206,28 @@ struct RsPlan2Args {
 };
 int launch_rs_plan2(const RsPlan2Args& a, hipStream_t s);
 
+// Fused RS8 repair (gen_fdec_asm.hip): re-encode + e x e solve in registers, one wave per block,
+// for blocks with e <= 16 repaired from parity rows 0..e-1.  Marks the blocks it repaired
+// (rows = 0, psel = 0) so the unfused kernels that follow skip them.
+struct FdecArgs {
+    uint8_t* base = nullptr;
+    uint64_t block_stride = 0;
+    uint32_t seg_stride = 0;
+    uint32_t nblocks = 0;
+    uint32_t vec = 0;
+    uint32_t ips = 0;                    // vec / 8
+    int32_t* rows = nullptr;             // plan outputs (consumed and cleared)
+    uint32_t* psel = nullptr;
+    const uint32_t* emask = nullptr;
+    const uint8_t* coef = nullptr;       // [b][t][s], column stride 32
+    uint64_t coef_block_stride = 0;
+    uint32_t coef_col_stride = 0;
+    const uint16_t* out_slots = nullptr; // [b][slots_stride]: erased source slots
+    uint32_t slots_stride = 0;
+    uint32_t accumulate = 0;
+};
+int launch_rs8_fused_decode(uint32_t k, uint32_t m, const FdecArgs& a, hipStream_t s);
+
 // MDP decode planning: per block one-stage coefficient matrix over the surviving slots.
 struct MdpPlanArgs {
     uint32_t k = 0, m = 0, nblocks = 0;

@@ -325,3 +325,45 @@ def test_full_size_roundtrip_c2_c3(orc):
     torch.cuda.synchronize()
     assert bool((st == 16).all())
     assert torch.equal(blocks, keep)
+
+
+@pytest.mark.parametrize("m", [32, 16])
+@pytest.mark.parametrize("accumulate", [False, True])
+def test_fused_decode_mixed_batch(orc, m, accumulate):
+    """The fused per-block repair (gen_fdec_asm.hip) takes blocks with e <= 16 repaired from
+    parity rows 0..e-1; the unfused kernels take the rest of the same batch.  Mix both kinds:
+    1..16 source erasures, every third block also losing parity rows among the first ones,
+    and (accumulate) junk in the erased buffers XORed into the repair."""
+    k, vec, nb = 64, 1400, 48
+    enc, dec = _codecs(NFEC_RS8, k, m, vec)
+    clean = orc.encode_blocks(NFEC_RS8, k, m, vec, orc.make_blocks(k, m, vec, nb))
+    rng = np.random.default_rng(21)
+    locs = np.zeros((nb, m), np.uint16)
+    counts = np.zeros(nb, np.uint16)
+    for b in range(nb):
+        es = 1 + b % 16
+        src = np.sort(rng.choice(k, es, replace=False))
+        par = k + np.sort(rng.choice(4, 2, replace=False)) if b % 3 == 0 and es + 2 <= m else np.array([], int)
+        e = np.concatenate([src, par]).astype(np.uint16)
+        locs[b, :len(e)] = e
+        counts[b] = len(e)
+    rx = clean.copy()
+    for b in range(nb):
+        for s in locs[b, :counts[b]]:
+            rx[b, s] = rng.integers(0, 256, vec, dtype=np.uint8) if (accumulate and s < k) else 0
+    ref = rx.copy()
+    st_ref = orc.decode_blocks(NFEC_RS8, k, m, vec, ref, locs, counts)
+    if accumulate:  # reference contract: repair XORs into the erased buffers
+        expect = rx.copy()
+        for b in range(nb):
+            for s in locs[b, :counts[b]]:
+                if s < k:
+                    expect[b, s] ^= clean[b, s]
+    else:
+        expect = ref
+    dev = torch.from_numpy(rx).cuda()
+    st = dec.decode_blocks(dev, torch.from_numpy(locs.astype(np.int16)).cuda(),
+                           torch.from_numpy(counts.astype(np.int16)).cuda(), accumulate=accumulate)
+    torch.cuda.synchronize()
+    assert np.array_equal(st.cpu().numpy(), st_ref)
+    assert np.array_equal(dev.cpu().numpy(), expect)

@@ -1,0 +1,346 @@
+#!/usr/bin/env python3
+"""Generate norm_amd/csrc/gen_fdec_asm.hip: fused RS8 erasure repair, one wavefront per block.
+
+The closed-form RS8 decode (same bytes as the reference's k x k inverse,
+src/common/normEncoderRS8.cpp:652-757) has two linear stages:
+    z_t = parity(P_t) ^ sum_{c present} G[P_t][c] * d_c         (constant generator rows)
+    d_E = A^-1 z                                                (per-block e x e matrix)
+The unfused path writes z to HBM between the two (gen_rs8_bitsliced.hip stage 1, then
+gen_solve_asm.hip).  Here one wave owns one block, so the block's erasure pattern and its
+coefficients are wave-uniform and both stages run back to back in registers:
+
+  * stage 1 = the bit-sliced re-encode of gen_rs8_asm.py (bank-separated VGPR layout, 11-column
+    load ring) over the 64 source columns plus the e used parity rows as 16 extra "columns"
+    (identity coefficient on their own row).  Erased columns are neither read (their loads go
+    through a descriptor with 0 records) nor computed (uniform branch).
+  * stage 2 = the snippet-table solve of gen_solve_asm.py: for each row t, z_t's planes are
+    copied into a fixed window and expanded into M4RM tables; for each output s the wave jumps
+    into the 128-byte snippet of c[s][t], whose accumulator operands are relative to M0.
+    Outputs are produced in two halves of 8 (64 accumulators in the freed load ring).
+  * z never leaves the register file: the block's HBM traffic is the 48 + 16 segments read and
+    the e repaired segments written.
+
+A block qualifies when e <= 16 and the used parity rows are exactly rows 0..e-1 (no parity
+erasures among them: NORM's usual case); the kernel marks the blocks it repaired (rows = 0,
+psel = 0) so the unfused kernels that run after it on the same stream skip them.
+
+Usage: gen_fdec_asm.py OUT.hip [k,m ...]
+"""
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from gen_rs8_asm import (MASKS, MULTI, NSLOT, S_MASK, TEMP, acc_reg, bank, combo_reg, ring_temps,  # noqa: E402
+                         slot_regs, split, table_code, transpose)
+from gen_rs8_bitsliced import bitmatrix_rows, generator  # noqa: E402
+
+DEFAULT_SHAPES = [(64, 32), (64, 16)]
+IN_REGS = [0, 1, 4, 5, 8, 9, 12, 13]      # compiler-placed inputs: load / store offsets
+S_RET, S_EM = 56, 58                       # return address; erased-column mask (64 bit)
+S_COEF2 = 60
+S_LRS, S_SRS = 64, 68
+S_COL, S_T = 78, 79
+S_COEF1 = 80
+S_SLOT = 84
+S_TAB = 92                                 # s92:93 snippet table, s94:95 jump target
+GPR_MODE = 0x9000                          # M0[15:12]: index SRC0 and DST
+SNIP_ALIGN = 7
+D_P0 = 19                                  # solve accumulators d[sl][i]: pairs 19..50 (ring)
+WIN_P0 = 51                                # solve window: pairs 51..54
+NCOLS_PAR = 16                             # parity rows handled as extra columns
+
+
+def d_reg(sl, i):
+    return 4 * (D_P0 + 4 * sl + i // 2) + (i & 1)
+
+
+def win_regs():
+    w = []
+    for q in range(4):
+        w += [4 * (WIN_P0 + q), 4 * (WIN_P0 + q) + 1]
+    return w
+
+
+def solve_pool():
+    """transpose temporaries for the outputs (d in banks 0/1; banks 2/3 still hold z)"""
+    free = list(TEMP[0]) + list(TEMP[1]) + [combo_reg(g, a) for a in MULTI for g in (0, 1)]
+
+    def make():
+        avail = list(free)
+
+        def pick(avoid):
+            for i, r in enumerate(avail):
+                if bank(r) != avoid:
+                    return avail.pop(i)
+            return avail.pop(0)
+        return pick
+    return make
+
+
+def all_tables(w):
+    code, regs = [], [{}, {}]
+    for g in (0, 1):
+        single = [w[2 * t + g] for t in range(4)]
+        built = {1 << t: single[t] for t in range(4)}
+        for a in sorted(MULTI, key=lambda a: bin(a).count("1")):
+            top = a.bit_length() - 1
+            dst = combo_reg(g, a)
+            code.append(f"v_xor_b32 v{dst}, v{built[a & ~(1 << top)]}, v{single[top]}")
+            built[a] = dst
+        regs[g] = built
+    return code, regs
+
+
+def snippets(regs):
+    A, B = regs
+    out = []
+    for c in range(256):
+        out.append(f".p2align {SNIP_ALIGN}")
+        if c == 0:
+            out.append("Lsnip0_%=:")
+        rows = bitmatrix_rows(c) if c else [0] * 8
+        for i in range(8):
+            a, b = split(rows[i])
+            d = d_reg(0, i)
+            if a and b:
+                out.append(f"v_bitop3_b32 v{d}, v{d}, v{A[a]}, v{B[b]} bitop3:0x96")
+            elif a:
+                out.append(f"v_xor_b32 v{d}, v{d}, v{A[a]}")
+            elif b:
+                out.append(f"v_xor_b32 v{d}, v{d}, v{B[b]}")
+        out.append(f"s_setpc_b64 s[{S_RET}:{S_RET + 1}]")
+    return out
+
+
+def fdec_asm(k, m):
+    G = generator(k, m)
+    L = []
+    offs = ["%[o0]", "%[o1]", "%[o2]", "%[o3]"]
+    soffs = ["%[s0]", "%[s1]", "%[s2]", "%[s3]"]
+    ncol = k + NCOLS_PAR
+    L += [f"s_mov_b64 s[{S_LRS}:{S_LRS + 1}], %[base]", f"s_mov_b32 s{S_LRS + 2}, -1",
+          f"s_mov_b32 s{S_LRS + 3}, 0x00020000",
+          f"s_mov_b64 s[{S_SRS}:{S_SRS + 1}], %[base]", f"s_mov_b32 s{S_SRS + 2}, 0x80000000",
+          f"s_mov_b32 s{S_SRS + 3}, 0x00020000",
+          f"s_mov_b64 s[{S_EM}:{S_EM + 1}], %[em]"]
+    for i, mk in enumerate(MASKS):
+        L.append(f"s_mov_b32 s{S_MASK + i}, 0x{mk:08x}")
+    L += [f"s_load_dwordx8 s[{S_SLOT}:{S_SLOT + 7}], %[sp], 0x0",
+          f"s_load_dwordx4 s[{S_COEF1}:{S_COEF1 + 3}], %[cp], 0x0",
+          f"s_getpc_b64 s[{S_TAB}:{S_TAB + 1}]",
+          "Lpc_%=:",
+          f"s_add_u32 s{S_TAB}, s{S_TAB}, Lsnip0_%=-Lpc_%=",
+          f"s_addc_u32 s{S_TAB + 1}, s{S_TAB + 1}, 0"]
+
+    def loads(c):
+        """column c: source slot c (c < k) or parity row c - k (slot c); unused ones read nothing"""
+        w = slot_regs(c % NSLOT)
+        if c < k:
+            out = [f"s_bitcmp1_b64 s[{S_EM}:{S_EM + 1}], {c}", f"s_cselect_b32 s{S_LRS + 2}, 0, -1"]
+        else:
+            out = [f"s_cmp_lt_u32 {c - k}, %[e]", f"s_cselect_b32 s{S_LRS + 2}, -1, 0"]
+        out.append(f"s_mul_i32 s{S_COL}, %[ss], {c}")
+        for q in range(4):
+            out.append(f"buffer_load_dwordx2 v[{w[2 * q]}:{w[2 * q + 1]}], {offs[q]}, s[{S_LRS}:{S_LRS + 3}], s{S_COL} offen")
+        return out
+
+    for r in range(16):
+        for i in range(8):
+            L.append(f"v_mov_b32 v{acc_reg(r, i)}, 0")
+    issued = -1
+    for c in range(min(NSLOT, ncol)):
+        L += loads(c)
+        issued = c
+    # ---- stage 1: z_t for rows 0..15 (rows >= e are computed but unused) ----
+    for c in range(ncol):
+        w = slot_regs(c % NSLOT)
+        L.append(f"s_waitcnt vmcnt({4 * (issued - c)})")
+        if c < k:
+            L += [f"s_bitcmp1_b64 s[{S_EM}:{S_EM + 1}], {c}", f"s_cbranch_scc1 Lskip{c}_%="]
+            L += transpose(w, ring_temps())
+            ups, need = [], [set(), set()]
+            for r in range(16):
+                mat = bitmatrix_rows(G[r][c])
+                for i in range(8):
+                    a, b = split(mat[i])
+                    ups.append((acc_reg(r, i), a, b))
+                    if a:
+                        need[0].add(a)
+                    if b:
+                        need[1].add(b)
+            L += table_code(w, need)
+            A, B = need
+            for acc, a, b in ups:
+                if a and b:
+                    L.append(f"v_bitop3_b32 v{acc}, v{acc}, v{A[a]}, v{B[b]} bitop3:0x96")
+                elif a:
+                    L.append(f"v_xor_b32 v{acc}, v{A[a]}, v{acc}")
+                elif b:
+                    L.append(f"v_xor_b32 v{acc}, v{B[b]}, v{acc}")
+        else:
+            t = c - k
+            L += [f"s_cmp_le_u32 %[e], {t}", f"s_cbranch_scc1 Lskip{c}_%="]
+            L += transpose(w, ring_temps())
+            for i in range(8):
+                L.append(f"v_xor_b32 v{acc_reg(t, i)}, v{w[i]}, v{acc_reg(t, i)}")
+        L.append(f"Lskip{c}_%=:")
+        if c + NSLOT < ncol:
+            L += loads(c + NSLOT)
+            issued = c + NSLOT
+    # ---- stage 2: d_s = sum_t c[s][t] z_t, outputs in two halves of 8 ----
+    win = win_regs()
+    cbuf = [S_COEF1, S_COEF2]
+    tmp = [4 * (WIN_P0 + p) + h for p in range(4) for h in (0, 1)]
+    regs = None
+    for h in range(2):
+        if h == 1:
+            L += ["s_cmp_le_u32 %[e], 8", "s_cbranch_scc1 Ldone_%="]
+        for sl in range(8):
+            for i in range(8):
+                L.append(f"v_mov_b32 v{d_reg(sl, i)}, 0")
+        for t in range(16):
+            L += [f"s_cmp_le_u32 %[e], {t}", f"s_cbranch_scc1 Lrows{h}_%="]
+            cur = cbuf[t % 2]
+            L.append("s_waitcnt lgkmcnt(0)")
+            # next coefficient row (after row 15: row 0 again, for the second half)
+            nt = (t + 1) % 16
+            L.append(f"s_load_dwordx4 s[{cbuf[nt % 2]}:{cbuf[nt % 2] + 3}], %[cp], 0x{32 * nt:x}")
+            for i in range(8):
+                L.append(f"v_mov_b32 v{win[i]}, v{acc_reg(t, i)}")
+            tcode, regs = all_tables(win)
+            L += tcode
+            L += [f"s_mov_b32 s{S_T}, 0", f"s_set_gpr_idx_on s{S_T}, gpr_idx(SRC0,DST)"]
+            for sl in range(8):
+                s = 8 * h + sl
+                L += [f"s_cmp_le_u32 %[e], {s}", f"s_cbranch_scc1 Lsend{h}_{t}_%="]
+                L += [f"s_bfe_u32 s{S_T}, s{cur + s // 4}, 0x{(8 << 16) | (8 * (s % 4)):x}",
+                      f"s_lshl_b32 s{S_T}, s{S_T}, {SNIP_ALIGN}",
+                      f"s_add_u32 s{S_TAB + 2}, s{S_TAB}, s{S_T}",
+                      f"s_addc_u32 s{S_TAB + 3}, s{S_TAB + 1}, 0",
+                      f"s_mov_b32 m0, 0x{GPR_MODE | (16 * sl):x}",
+                      f"s_swappc_b64 s[{S_RET}:{S_RET + 1}], s[{S_TAB + 2}:{S_TAB + 3}]"]
+            L += [f"Lsend{h}_{t}_%=:", "s_set_gpr_idx_off"]
+        L.append(f"Lrows{h}_%=:")
+        # the coefficient row that leaving early left in flight must land before the next half
+        L.append("s_waitcnt lgkmcnt(0)")
+        if h == 0:
+            # the next half starts at row 0, which must sit in buffer 0
+            L.append(f"s_load_dwordx4 s[{S_COEF1}:{S_COEF1 + 3}], %[cp], 0x0")
+        for sl in range(8):
+            s = 8 * h + sl
+            L += [f"s_cmp_le_u32 %[e], {s}", "s_cbranch_scc1 Ldone_%=" if h == 1 else f"s_cbranch_scc1 Lhalf{h}_%="]
+            w = [d_reg(sl, i) for i in range(8)]
+            L += transpose(w, solve_pool())
+            L += [f"s_bfe_u32 s{S_T}, s{S_SLOT + s // 2}, 0x{(16 << 16) | (16 * (s % 2)):x}",
+                  f"s_mul_i32 s{S_T}, s{S_T}, %[ss]",
+                  "s_cmp_eq_u32 %[acc], 0", f"s_cbranch_scc1 Lna{s}_%="]
+            for q in range(4):
+                L.append(f"buffer_load_dwordx2 v[{tmp[2 * q]}:{tmp[2 * q + 1]}], {soffs[q]}, s[{S_SRS}:{S_SRS + 3}], s{S_T} offen")
+            L.append("s_waitcnt vmcnt(0)")
+            for q in range(4):
+                L.append(f"v_xor_b32 v{w[2 * q]}, v{tmp[2 * q]}, v{w[2 * q]}")
+                L.append(f"v_xor_b32 v{w[2 * q + 1]}, v{tmp[2 * q + 1]}, v{w[2 * q + 1]}")
+            L.append(f"Lna{s}_%=:")
+            for q in range(4):
+                L.append(f"buffer_store_dwordx2 v[{w[2 * q]}:{w[2 * q + 1]}], {soffs[q]}, s[{S_SRS}:{S_SRS + 3}], s{S_T} offen")
+        if h == 0:
+            L.append(f"Lhalf{h}_%=:")
+    L.append("Ldone_%=:")
+    L.append("s_waitcnt lgkmcnt(0)")
+    L.append("s_branch Lend_%=")
+    L += snippets(regs)
+    L.append("Lend_%=:")
+    return L
+
+
+def clobbers():
+    v = [f'"v{i}"' for i in range(256) if i not in IN_REGS]
+    s = [f'"s{i}"' for i in range(S_RET, 96)]
+    return ", ".join(v + s + ['"m0"', '"scc"', '"memory"'])
+
+
+def gen_kernel(k, m):
+    K = f"rs8_fdec_k{k}_m{m}"
+    body = "\\n\"\n        \"".join(fdec_asm(k, m))
+    return f"""__global__ __launch_bounds__(256, 2) void {K}(FdecArgs a)
+{{
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t blk = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
+    if (blk >= a.nblocks) return;
+    const int32_t rows = (int32_t)__builtin_amdgcn_readfirstlane((uint32_t)a.rows[blk]);
+    const uint32_t ps0 = __builtin_amdgcn_readfirstlane(a.psel[2 * (uint64_t)blk]);
+    const uint32_t ps1 = __builtin_amdgcn_readfirstlane(a.psel[2 * (uint64_t)blk + 1]);
+    // qualifies: 1..16 source erasures repaired from parity rows 0..e-1
+    if (rows <= 0 || rows > 16 || ps1 != 0 || ps0 != ((1u << rows) - 1u)) return;
+    const uint32_t e = (uint32_t)rows;
+    // (readfirstlane yields int: widen through uint32_t, or bit 31 would sign-extend into the
+    // high word)
+    const uint64_t em = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane(a.emask[2 * (uint64_t)blk]) |
+                        ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane(a.emask[2 * (uint64_t)blk + 1]) << 32);
+    // hand the block off: the unfused stage 1 and solve that follow on the stream skip it
+    if (lane == 0) {{
+        a.rows[blk] = 0;
+        a.psel[2 * (uint64_t)blk] = 0;
+    }}
+    uint32_t o[4], so[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {{
+        const uint32_t item = (uint32_t)q * 64u + lane;
+        const bool ok = item < a.ips;
+        o[q] = ok ? item * 8u : 0u;
+        so[q] = ok ? item * 8u : 0x80000000u;  // past the store descriptor's records: dropped
+    }}
+    const uint8_t* base = a.base + (uint64_t)blk * a.block_stride;
+    const uint8_t* cp = a.coef + (uint64_t)blk * a.coef_block_stride;
+    const uint16_t* sp = a.out_slots + (uint64_t)blk * a.slots_stride;
+    asm volatile(
+        "{body}\\n"
+        :
+        : [base] "s"(base), [em] "s"(em), [cp] "s"(cp), [sp] "s"(sp), [e] "s"(e), [ss] "s"(a.seg_stride),
+          [acc] "s"(a.accumulate),
+          [o0] "v"(o[0]), [o1] "v"(o[1]), [o2] "v"(o[2]), [o3] "v"(o[3]),
+          [s0] "v"(so[0]), [s1] "v"(so[1]), [s2] "v"(so[2]), [s3] "v"(so[3])
+        : {clobbers()});
+}}
+"""
+
+
+def main():
+    path = sys.argv[1]
+    shapes = DEFAULT_SHAPES
+    if len(sys.argv) > 2:
+        shapes = [tuple(int(v) for v in s.split(",")) for s in sys.argv[2:]]
+    parts = [
+        "// GENERATED by tools/codegen/gen_fdec_asm.py -- do not edit by hand.",
+        "// Fused RS8 erasure repair (re-encode + e x e solve in registers, one wave per block) for",
+        "// (k, m) in: " + ", ".join(f"({k},{m})" for k, m in shapes),
+        '#include "nfec_internal.hpp"',
+        "",
+        "namespace nfec {",
+        "namespace {",
+    ]
+    for k, m in shapes:
+        parts.append(gen_kernel(k, m))
+    parts.append("}  // namespace")
+    parts.append("")
+    parts.append("// NFEC_ENOTSUP when (k, m) has no fused kernel or the batch shape needs the unfused path")
+    parts.append("int launch_rs8_fused_decode(uint32_t k, uint32_t m, const FdecArgs& a, hipStream_t s)")
+    parts.append("{")
+    parts.append("    if (a.nblocks == 0) return NFEC_OK;")
+    parts.append("    if ((a.vec & 7u) || a.vec > 2048 || a.coef_col_stride != 32 || (a.coef_block_stride & 15) ||")
+    parts.append("        (a.slots_stride & 1) || (uint64_t)a.seg_stride * (k + 16) + a.vec >= (1ull << 31))")
+    parts.append("        return NFEC_ENOTSUP;")
+    for k, m in shapes:
+        parts.append(f"    if (k == {k} && m == {m}) {{")
+        parts.append(f"        hipLaunchKernelGGL(rs8_fdec_k{k}_m{m}, dim3((a.nblocks + 3) / 4), dim3(256), 0, s, a);")
+        parts.append("        return hipGetLastError() == hipSuccess ? NFEC_OK : NFEC_EDEVICE;")
+        parts.append("    }")
+    parts.append("    return NFEC_ENOTSUP;")
+    parts.append("}")
+    parts.append("")
+    parts.append("}  // namespace nfec")
+    open(path, "w").write("\n".join(parts) + "\n")
+
+
+if __name__ == "__main__":
+    main()
