@@ -317,12 +317,13 @@ bool has_bitsliced(uint32_t k, uint32_t m)
 }
 
 // tuning knobs of the bit-sliced kernels (A/B runs): bit 0 XCD-contiguous workgroup
-// mapping, bit 1 nontemporal parity stores
+// mapping (default on: neighbouring item groups share the 128-byte lines at their boundaries,
+// so one XCD's L2 fetches them once; encode 2.38 -> 2.35 ms), bit 1 nontemporal parity stores
 static uint32_t bs_flags()
 {
     static const uint32_t f = [] {
         const char* e = std::getenv("NFEC_BS_FLAGS");
-        return e ? (uint32_t)std::strtoul(e, nullptr, 0) : 0u;
+        return e ? (uint32_t)std::strtoul(e, nullptr, 0) : 1u;
     }();
     return f;
 }
