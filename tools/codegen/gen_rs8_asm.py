@@ -35,7 +35,11 @@ ROWS = 16            # parity rows per role (one wavefront)
 # A/B probes for (64, 32), NFEC_ASM_VARIANT=<id>: VALU only (no source loads) / memory only
 # (measured and dropped: nt loads 2.42 ms / nt stores 2.42 / one role loading for both 1.91 in the
 # memory-only probe -- none beat the default policy)
-PROBES = {8: ("noload", "_probe_noload"), 9: ("nocompute", "_probe_nocompute")}
+PROBES = {8: ("noload", "_probe_noload"), 9: ("nocompute", "_probe_nocompute"),
+          10: ("nocompute,nostore", "_probe_readonly"), 11: ("nocompute,noload", "_probe_writeonly")}
+# (measured and dropped: "halftr", transposing only every other column -- the upper bound of
+# sharing the transposes of the two role waves through LDS -- 2.27 -> 2.12 ms before any LDS or
+# barrier cost)
 
 # ---- register map ----
 IN_REGS = [0, 1, 4, 5, 8, 9, 12, 13]         # left to the compiler for the asm inputs
@@ -196,7 +200,8 @@ def role_asm(G, k, m, r0, rows, probe=None):
                 L += loads(j + NSLOT)
                 issued = j + NSLOT
             continue
-        L += transpose(w, mk_ring)
+        if not ("halftr" in flags and j % 2 == 1):  # probe: upper bound of sharing transposes
+            L += transpose(w, mk_ring)
         mats = [bitmatrix_rows(G[r0 + r][j]) for r in range(rows)]
         ups = []
         need = [set(), set()]
@@ -244,7 +249,8 @@ def role_asm(G, k, m, r0, rows, probe=None):
             L.append(f"v_xor_b32 v{w[2 * q + 1]}, v{tmp[2 * q + 1]}, v{w[2 * q + 1]}")
         L.append(f"Lnoacc_{r}_%=:")
         for q in range(4):
-            L.append(f"buffer_store_dwordx2 v[{w[2 * q]}:{w[2 * q + 1]}], {soffs[q]}, s[{S_SRS}:{S_SRS + 3}], s{S_ROW} offen{spol}")
+            if "nostore" not in flags:
+                L.append(f"buffer_store_dwordx2 v[{w[2 * q]}:{w[2 * q + 1]}], {soffs[q]}, s[{S_SRS}:{S_SRS + 3}], s{S_ROW} offen{spol}")
     return L
 
 
