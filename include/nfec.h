@@ -186,6 +186,52 @@ int nfec_util_zero_slots(const nfec_block_batch* batch, const uint16_t* erasure_
                          uint32_t erasure_stride, const uint16_t* erasure_counts,
                          uint32_t vector_size, void* stream);
 
+/* ---- NORM wire format on the FEC path (host only; no device work) ----
+ * The FEC Object Transmission Information header extension (type 64) a sender attaches to
+ * NORM_INFO/NORM_DATA and a receiver reads to build its decoder, the FEC payload ID in every
+ * NORM_DATA, and the codec choice each side makes from them.  Big-endian on the wire. */
+typedef struct nfec_fti {
+    uint8_t fec_id;         /* 2, 5 or 129 */
+    uint8_t fec_m;          /* field bits: 8 or 16 for fec_id 2; 8 for 5 and 129 (read side) */
+    uint8_t fec_group_size; /* fec_id 2 'G' (symbols per packet); read as 1 for 5, 129 */
+    uint8_t reserved;
+    uint16_t instance_id;   /* fec_id 129 */
+    uint16_t segment_size;
+    uint16_t num_data;      /* FEC max block length (u8 on the wire for fec_id 5) */
+    uint16_t num_parity;
+    uint64_t object_size;   /* NormObjectSize, 48 bits */
+} nfec_fti;
+
+/* NormFtiExtension2/5/129::SetObjectSize...SetFecNumParity (normMessage.h:785-1029):
+ * writes the whole extension (16 bytes; 12 for fec_id 5) into ext and returns its length,
+ * NFEC_EINVAL for an unknown fec_id, cap too small or object_size >= 2^48, NFEC_ERANGE when
+ * num_data/num_parity do not fit fec_id 5's u8 fields. */
+int nfec_fti_write(const nfec_fti* fti, void* ext, size_t cap);
+/* The matching getters: parses ext (len bytes) for fec_id; returns bytes consumed or
+ * NFEC_EINVAL (unknown fec_id, short buffer, type != 64 or length field too small). */
+int nfec_fti_read(uint8_t fec_id, const void* ext, size_t len, nfec_fti* out);
+/* NormPayloadId (normMessage.h:396-567): 4 bytes for fec_id 2 and 5, 8 for 129, 0 unknown. */
+int nfec_payload_id_length(uint8_t fec_id);
+/* fec 2/m 8 and fec 5: u32 block<<8 | symbol; fec 2/m 16: u16 block, u16 symbol; fec 129:
+ * u32 block, u16 block length, u16 symbol.  Return the length, or NFEC_EINVAL.
+ * block_len is only carried by fec 129 (read returns 0 for it otherwise; may be NULL). */
+int nfec_payload_id_write(uint8_t fec_id, uint8_t fec_m, uint32_t block_id, uint16_t symbol_id,
+                          uint16_t block_len, void* out);
+int nfec_payload_id_read(uint8_t fec_id, uint8_t fec_m, const void* in, uint32_t* block_id,
+                         uint16_t* symbol_id, uint16_t* block_len);
+/* Sender choice (NormSession::StartSender, normSession.cpp:764-883): numData + numParity <=
+ * 255 -> RS8 with fec_id_pref (0 = 5) and m 8, or MDP/129 when assume_mdp; else RS16, fec 2, m 16. */
+int nfec_sender_codec(uint16_t num_data, uint16_t num_parity, uint8_t fec_id_pref, int assume_mdp,
+                      int* kind, uint8_t* fec_id, uint8_t* fec_m);
+/* Receiver choice (NormSenderNode::AllocateBuffers, normNode.cpp:290-356): fec 2 m 8 -> RS8,
+ * m 16 -> RS16; fec 5 -> RS8; fec 129 -> MDP when assume_mdp, RS8 for instance 0; anything
+ * else NFEC_ENOTSUP. */
+int nfec_receiver_codec(uint8_t fec_id, uint8_t fec_m, uint16_t instance_id, int assume_mdp,
+                        int* kind);
+/* The codec vector size for a segment size: segment_size + the 8-byte stream payload header
+ * NORM codes along with the data (NormDataMsg::GetStreamPayloadHeaderLength). */
+uint32_t nfec_vector_size(uint16_t segment_size);
+
 #ifdef __cplusplus
 }
 #endif

@@ -46,7 +46,23 @@ class CodecInfo(ctypes.Structure):
     ]
 
 
+class Fti(ctypes.Structure):
+    _fields_ = [
+        ("fec_id", ctypes.c_uint8),
+        ("fec_m", ctypes.c_uint8),
+        ("fec_group_size", ctypes.c_uint8),
+        ("reserved", ctypes.c_uint8),
+        ("instance_id", ctypes.c_uint16),
+        ("segment_size", ctypes.c_uint16),
+        ("num_data", ctypes.c_uint16),
+        ("num_parity", ctypes.c_uint16),
+        ("object_size", ctypes.c_uint64),
+    ]
+
+
 _P = ctypes.c_void_p
+_U8 = ctypes.c_uint8
+_U16 = ctypes.c_uint16
 _U32 = ctypes.c_uint32
 _U64 = ctypes.c_uint64
 _I = ctypes.c_int
@@ -70,6 +86,14 @@ _SIGS = {
     "nfec_util_fill": (_I, [ctypes.POINTER(BlockBatch), _U32, _U32, _U64, _U64, _P]),
     "nfec_util_erasures": (_I, [_P, _U32, _P, _U32, _U32, _U32, _U64, _U64, _P]),
     "nfec_util_zero_slots": (_I, [ctypes.POINTER(BlockBatch), _P, _U32, _P, _U32, _P]),
+    "nfec_fti_write": (_I, [ctypes.POINTER(Fti), _P, ctypes.c_size_t]),
+    "nfec_fti_read": (_I, [_U8, _P, ctypes.c_size_t, ctypes.POINTER(Fti)]),
+    "nfec_payload_id_length": (_I, [_U8]),
+    "nfec_payload_id_write": (_I, [_U8, _U8, _U32, _U16, _U16, _P]),
+    "nfec_payload_id_read": (_I, [_U8, _U8, _P, ctypes.POINTER(_U32), ctypes.POINTER(_U16), ctypes.POINTER(_U16)]),
+    "nfec_sender_codec": (_I, [_U16, _U16, _U8, _I, ctypes.POINTER(_I), ctypes.POINTER(_U8), ctypes.POINTER(_U8)]),
+    "nfec_receiver_codec": (_I, [_U8, _U8, _U16, _I, ctypes.POINTER(_I)]),
+    "nfec_vector_size": (_U32, [_U16]),
 }
 
 _lib = None
