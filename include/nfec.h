@@ -232,6 +232,54 @@ int nfec_receiver_codec(uint8_t fec_id, uint8_t fec_m, uint16_t instance_id, int
  * NORM codes along with the data (NormDataMsg::GetStreamPayloadHeaderLength). */
 uint32_t nfec_vector_size(uint16_t segment_size);
 
+/* ---- npc: the offline file precoder (src/common/normPrecode.cpp) on the GPU path ----
+ * .npc files are byte-identical to the reference tool's for the same input and parameters
+ * (meta segment, CRC-32 per segment, interleaving, the encoder's segment-id rotation). */
+typedef struct nfec_npc_params {
+    uint32_t segment_size;   /* "segment": 12..8192 bytes, the last 4 hold the segment's CRC-32 */
+    uint32_t num_data;       /* "block": used when parity_fraction < 0 */
+    uint32_t num_parity;     /* "parity" */
+    double parity_fraction;  /* "auto" percent / 100; >= 0 sizes the block from the file size.
+                                The reference's default is 100.0 (auto mode, 100x parity). */
+    uint64_t b_max;          /* "bmax": auto-mode block cap */
+    uint64_t i_max;          /* "imax": interleaver max dimension, 0 = none */
+} nfec_npc_params;
+
+typedef struct nfec_npc_layout {
+    uint64_t num_segments;    /* segments in the .npc file */
+    uint64_t input_segments;  /* meta + data segments */
+    uint64_t num_blocks;
+    uint32_t num_data, num_parity;
+    uint32_t last_block_data;     /* numData of the last FEC block */
+    uint32_t segment_size;
+    uint32_t last_segment_bytes;  /* encode: file bytes in the last data segment (0 on decode) */
+    int32_t kind;                 /* NFEC_RS8, or NFEC_RS16 when numData + numParity > 256 */
+    uint64_t il_width, il_height, il_size, i_max;
+} nfec_npc_layout;
+
+/* NormPrecodeApp's constructor defaults (normPrecode.cpp:111-115). */
+void nfec_npc_default_params(nfec_npc_params* params);
+/* Block sizing (OnStartup :383-434) and file layout (Encode :611-637 / Decode :886-909,
+ * InitInterleaver :450-462) for an input of file_size bytes.  Host only. */
+int nfec_npc_layout_for(const nfec_npc_params* params, uint64_t file_size, int encode,
+                        nfec_npc_layout* out);
+/* File slot of FEC-order segments [first, first+count) (ComputeInterleaverOffset :465-556
+ * divided by segment_size).  Host only.  NFEC_ENOTSUP where the reference's remap fails. */
+int nfec_npc_positions(const nfec_npc_layout* layout, uint64_t first, uint64_t count, uint64_t* pos);
+/* NormPrecodeApp::Encode: in_path -> out_path (.npc) on HIP device `device`. */
+int nfec_npc_encode_file(int device, const char* in_path, const char* out_path,
+                         const nfec_npc_params* params);
+/* NormPrecodeApp::Decode: out_path NULL writes to the file name stored in the meta segment
+ * (current directory), as the reference does; that name goes to name_out when given.
+ * NFEC_ERANGE when a block has more bad segments than parity (the reference's fatal case). */
+int nfec_npc_decode_file(int device, const char* in_path, const char* out_path,
+                         const nfec_npc_params* params, uint64_t* out_bytes, char* name_out,
+                         size_t name_cap);
+/* CRC-32 (npc's ComputeCRC32, :1303-1313) of the first len bytes of slots [0, slots) of every
+ * block of a device batch -> crc[b*slots + s] (device), asynchronously on stream. */
+int nfec_crc32_slots(const nfec_block_batch* batch, uint32_t slots, uint32_t len, uint32_t* crc,
+                     void* stream);
+
 #ifdef __cplusplus
 }
 #endif

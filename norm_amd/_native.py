@@ -60,6 +60,35 @@ class Fti(ctypes.Structure):
     ]
 
 
+class NpcParams(ctypes.Structure):
+    _fields_ = [
+        ("segment_size", ctypes.c_uint32),
+        ("num_data", ctypes.c_uint32),
+        ("num_parity", ctypes.c_uint32),
+        ("parity_fraction", ctypes.c_double),
+        ("b_max", ctypes.c_uint64),
+        ("i_max", ctypes.c_uint64),
+    ]
+
+
+class NpcLayout(ctypes.Structure):
+    _fields_ = [
+        ("num_segments", ctypes.c_uint64),
+        ("input_segments", ctypes.c_uint64),
+        ("num_blocks", ctypes.c_uint64),
+        ("num_data", ctypes.c_uint32),
+        ("num_parity", ctypes.c_uint32),
+        ("last_block_data", ctypes.c_uint32),
+        ("segment_size", ctypes.c_uint32),
+        ("last_segment_bytes", ctypes.c_uint32),
+        ("kind", ctypes.c_int32),
+        ("il_width", ctypes.c_uint64),
+        ("il_height", ctypes.c_uint64),
+        ("il_size", ctypes.c_uint64),
+        ("i_max", ctypes.c_uint64),
+    ]
+
+
 _P = ctypes.c_void_p
 _U8 = ctypes.c_uint8
 _U16 = ctypes.c_uint16
@@ -94,6 +123,13 @@ _SIGS = {
     "nfec_sender_codec": (_I, [_U16, _U16, _U8, _I, ctypes.POINTER(_I), ctypes.POINTER(_U8), ctypes.POINTER(_U8)]),
     "nfec_receiver_codec": (_I, [_U8, _U8, _U16, _I, ctypes.POINTER(_I)]),
     "nfec_vector_size": (_U32, [_U16]),
+    "nfec_npc_default_params": (None, [ctypes.POINTER(NpcParams)]),
+    "nfec_npc_layout_for": (_I, [ctypes.POINTER(NpcParams), _U64, _I, ctypes.POINTER(NpcLayout)]),
+    "nfec_npc_positions": (_I, [ctypes.POINTER(NpcLayout), _U64, _U64, _P]),
+    "nfec_npc_encode_file": (_I, [_I, ctypes.c_char_p, ctypes.c_char_p, ctypes.POINTER(NpcParams)]),
+    "nfec_npc_decode_file": (_I, [_I, ctypes.c_char_p, ctypes.c_char_p, ctypes.POINTER(NpcParams),
+                                  ctypes.POINTER(_U64), ctypes.c_char_p, ctypes.c_size_t]),
+    "nfec_crc32_slots": (_I, [ctypes.POINTER(BlockBatch), _U32, _U32, _P, _P]),
 }
 
 _lib = None

@@ -77,6 +77,12 @@ __global__ __launch_bounds__(kWave) void rs_plan_kernel(RsPlanArgs a)
 
     // ---- validate and split erasures (sorted: source first, then parity) ----
     bool ok = nd >= 1 && nd <= k && ec <= a.erasure_stride && ec <= m;
+    if (ok) {
+        // the LDS lists hold 256 erasures; decode_device rejects codecs that could need more
+        uint32_t src = 0;
+        for (uint32_t i = 0; i < ec; ++i) src += locs[i] < nd;
+        ok = src <= 256;
+    }
     uint32_t es = 0;
     if (ok) {
         for (uint32_t i = 0; i < ec; ++i) {

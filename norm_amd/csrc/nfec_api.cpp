@@ -434,6 +434,8 @@ int decode_device(nfec_codec* c, const nfec_block_batch* b, const uint16_t* locs
     if (!locs || !counts) return fail(NFEC_EINVAL, "null erasure arrays");
     const bool acc = b->flags & NFEC_ACCUMULATE;
     if (c->kind == NFEC_MDP && acc) return fail(NFEC_ENOTSUP, "MDP decode requires zero-filled erased segments");
+    if (c->kind != NFEC_MDP && std::min(c->k, c->m) > 256)
+        return fail(NFEC_ENOTSUP, "RS decode supports at most 256 source erasures per block (min(k, m) <= 256)");
     std::lock_guard<std::mutex> lk(c->mu);
     const uint32_t n = c->k + c->m;
     const uint32_t zstride = round_up(c->vec, 8);

@@ -257,4 +257,33 @@ int launch_zero_slots(uint8_t* base, uint64_t block_stride, uint32_t seg_stride,
                       const uint16_t* locs, uint32_t stride, const uint16_t* counts, uint32_t vec,
                       hipStream_t s);
 
+// npc segment checksums (kernels_crc.hip): CRC-32 of the first len bytes of every slot
+// (crc[b*slots + s], optional) and, optionally, whether it differs from the big-endian CRC
+// stored right after them (bad[b*slots + s]).
+struct CrcArgs {
+    const uint8_t* base = nullptr;
+    uint64_t block_stride = 0;
+    uint32_t seg_stride = 0;
+    uint32_t nblocks = 0;
+    uint32_t slots = 0;
+    uint32_t len = 0;
+    uint32_t* crc = nullptr;
+    uint8_t* bad = nullptr;
+};
+int launch_crc32_slots(const CrcArgs& a, hipStream_t s);
+
+// Per block: ascending list of bad slots among [0, num_data + m) -> locs[b*stride ..] (at most
+// stride entries), counts[b] = the full count (saturated at 65535).
+struct ErasureListArgs {
+    const uint8_t* bad = nullptr;        // [b][slots]
+    uint32_t slots = 0;
+    const uint16_t* num_data = nullptr;  // per block, or null = k
+    uint32_t k = 0, m = 0;
+    uint32_t nblocks = 0;
+    uint16_t* locs = nullptr;
+    uint32_t stride = 0;
+    uint16_t* counts = nullptr;
+};
+int launch_erasure_list(const ErasureListArgs& a, hipStream_t s);
+
 }  // namespace nfec
