@@ -198,7 +198,7 @@ struct MappedFile {
         if (fstat(fd, &st)) return fail(NFEC_EINVAL, "npc: stat failed");
         size = (uint64_t)st.st_size;
         if (size) {
-            void* m = mmap(nullptr, size, PROT_READ, MAP_PRIVATE, fd, 0);
+            void* m = mmap(nullptr, size, PROT_READ, MAP_PRIVATE | MAP_POPULATE, fd, 0);
             if (m == MAP_FAILED) return fail(NFEC_ENOMEM, "npc: mmap of input failed");
             p = static_cast<uint8_t*>(m);
         }
@@ -211,7 +211,8 @@ struct MappedFile {
         if (ftruncate(fd, (off_t)bytes)) return fail(NFEC_ENOMEM, "npc: cannot size output file");
         size = bytes;
         if (size) {
-            void* m = mmap(nullptr, size, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+            // populated up front: one kernel pass instead of a page fault per 4 KiB from the copy threads
+            void* m = mmap(nullptr, size, PROT_READ | PROT_WRITE, MAP_SHARED | MAP_POPULATE, fd, 0);
             if (m == MAP_FAILED) return fail(NFEC_ENOMEM, "npc: mmap of output failed");
             p = static_cast<uint8_t*>(m);
         }
@@ -286,7 +287,7 @@ uint32_t chunk_blocks(uint64_t block_bytes, uint64_t nblocks)
 {
     static const uint64_t budget = [] {
         const char* e = std::getenv("NFEC_NPC_CHUNK_MB");
-        const long mb = e ? std::atol(e) : 1024L;
+        const long mb = e ? std::atol(e) : 256L;
         return (uint64_t)std::max(1L, mb) << 20;
     }();
     const uint64_t cb = std::max<uint64_t>(1, budget / std::max<uint64_t>(block_bytes, 1));
@@ -310,8 +311,10 @@ struct Phases {
     void report(const char* what) const
     {
         if (on)
-            std::fprintf(stderr, "npc %s: setup %.3f s, host in %.3f s, gpu enqueue %.3f s, host out %.3f s\n", what,
-                         t[0], t[1], t[2], t[3]);
+            std::fprintf(stderr,
+                         "npc %s: map input %.3f s, positions %.3f s, staging+output %.3f s, host in %.3f s, "
+                         "gpu enqueue %.3f s, host out %.3f s\n",
+                         what, t[4], t[5], t[0], t[1], t[2], t[3]);
     }
 };
 
@@ -410,6 +413,7 @@ int nfec_npc_encode_file(int device, const char* in_path, const char* out_path, 
     MappedFile in;
     int rc = in.open_read(in_path);
     if (rc) return rc;
+    ph.mark(4);
     nfec_npc_layout l;
     if ((rc = nfec_npc_layout_for(p, in.size, 1, &l))) return rc;
     const uint32_t k = l.num_data, m = l.num_parity, n = k + m;
@@ -419,6 +423,7 @@ int nfec_npc_encode_file(int device, const char* in_path, const char* out_path, 
     // the whole interleaver map first: a bad geometry fails before any output is written
     std::vector<uint64_t> pos(l.num_segments);
     if ((rc = nfec_npc_positions(&l, 0, l.num_segments, pos.data()))) return rc;
+    ph.mark(5);
 
     // meta segment (normPrecode.cpp:650-678)
     std::vector<uint8_t> meta(ds, 0);
@@ -539,6 +544,7 @@ int nfec_npc_decode_file(int device, const char* in_path, const char* out_path, 
     MappedFile in;
     int rc = in.open_read(in_path);
     if (rc) return rc;
+    ph.mark(4);
     nfec_npc_layout l;
     if ((rc = nfec_npc_layout_for(p, in.size, 0, &l))) return rc;
     const uint32_t k = l.num_data, m = l.num_parity, n = k + m;
@@ -546,6 +552,7 @@ int nfec_npc_decode_file(int device, const char* in_path, const char* out_path, 
     const uint64_t bstride = (uint64_t)n * stride;
     std::vector<uint64_t> pos(l.num_segments);
     if ((rc = nfec_npc_positions(&l, 0, l.num_segments, pos.data()))) return rc;
+    ph.mark(5);
 
     int prev_dev = -1;
     (void)hipGetDevice(&prev_dev);
@@ -556,9 +563,8 @@ int nfec_npc_decode_file(int device, const char* in_path, const char* out_path, 
         return rc;
     }
 
-    int ofd = -1;
+    MappedFile outm;
     uint64_t out_size = 0, written = 0;
-    std::vector<uint8_t> obuf;
 
     auto gather = [&](int slot, uint64_t b0, uint32_t nb) {
         uint8_t* H = S.hblk[slot];
@@ -630,8 +636,15 @@ int nfec_npc_decode_file(int device, const char* in_path, const char* out_path, 
                 name_out[c] = 0;
             }
             const std::string target = out_path ? std::string(out_path) : nm;
-            ofd = ::open(target.c_str(), O_WRONLY | O_CREAT | O_TRUNC, 0644);
-            if (ofd < 0) return fail(NFEC_EINVAL, "npc: error opening output file " + target);
+            // every data segment but the meta one, the last cut to the file size (:1156-1161)
+            uint64_t total = 0;
+            if (l.input_segments >= 2) {
+                uint64_t last = out_size % ds;
+                if (last == 0) last = ds;
+                total = (l.input_segments - 2) * ds + last;
+            }
+            int r = outm.open_write(target.c_str(), total);
+            if (r) return r;
         }
         // offsets of each block's output in this chunk
         std::vector<uint64_t> off(nb + 1, 0);
@@ -650,12 +663,11 @@ int nfec_npc_decode_file(int device, const char* in_path, const char* out_path, 
             }
             off[bi + 1] = off[bi] + bytes;
         }
-        obuf.resize(off[nb]);
         Threads::run(nb, [&](uint64_t lo, uint64_t hi) {
             for (uint64_t bi = lo; bi < hi; ++bi) {
                 const uint64_t b = b0 + bi;
                 const uint32_t nd = S.hnd[slot][bi];
-                uint8_t* dst = obuf.data() + off[bi];
+                uint8_t* dst = outm.p + written + off[bi];
                 for (uint32_t i = 0; i < nd; ++i) {
                     if (b == 0 && i == 0) continue;
                     uint32_t len = ds;
@@ -668,13 +680,7 @@ int nfec_npc_decode_file(int device, const char* in_path, const char* out_path, 
                 }
             }
         });
-        size_t done = 0;
-        while (done < obuf.size()) {
-            const ssize_t w = ::write(ofd, obuf.data() + done, obuf.size() - done);
-            if (w <= 0) return fail(NFEC_EINVAL, "npc: unexpected error writing to output file");
-            done += (size_t)w;
-        }
-        written += obuf.size();
+        written += off[nb];
         return NFEC_OK;
     };
 
@@ -697,7 +703,6 @@ int nfec_npc_decode_file(int device, const char* in_path, const char* out_path, 
     if (!rc && pnb) rc = emit(slot ^ 1, pb0, pnb);
     ph.mark(3);
     ph.report("decode");
-    if (ofd >= 0) close(ofd);
     if (prev_dev >= 0) (void)hipSetDevice(prev_dev);
     if (!rc && out_bytes) *out_bytes = written;
     return rc;
