@@ -77,12 +77,6 @@ __global__ __launch_bounds__(kWave) void rs_plan_kernel(RsPlanArgs a)
 
     // ---- validate and split erasures (sorted: source first, then parity) ----
     bool ok = nd >= 1 && nd <= k && ec <= a.erasure_stride && ec <= m;
-    if (ok) {
-        // the LDS lists hold 256 erasures; decode_device rejects codecs that could need more
-        uint32_t src = 0;
-        for (uint32_t i = 0; i < ec; ++i) src += locs[i] < nd;
-        ok = src <= 256;
-    }
     uint32_t es = 0;
     if (ok) {
         for (uint32_t i = 0; i < ec; ++i) {
@@ -92,19 +86,28 @@ __global__ __launch_bounds__(kWave) void rs_plan_kernel(RsPlanArgs a)
         }
     }
     if (!ok) status = 0;
+    // erased / substitute-parity lists and pivot factors: LDS up to 256 erasures, else the
+    // block's global scratch after its e x 2e matrix
+    const uint32_t cs = a.coef_stride;
+    uint8_t* wb = a.work ? reinterpret_cast<uint8_t*>(a.work) + (uint64_t)b * a.work_block_bytes : nullptr;
+    const bool big = es > 256;
+    if (ok && big && (!wb || es > cs)) { ok = false; status = 0; }  // workspace not sized for it
+    uint16_t* listE = big ? reinterpret_cast<uint16_t*>(wb + (uint64_t)cs * 2 * cs * sizeof(E)) : lds_E;
+    uint16_t* listP = big ? listE + cs : lds_P;
+    E* fac = big ? reinterpret_cast<E*>(listP + cs) : lds_fac;
     if (ok && es > 0) {
         // surviving parities in ascending slot order (reference scan :660-718)
         if (lane == 0) {
             uint32_t next = es, np = 0;
             for (uint32_t s = nd; s < nd + m && np < es; ++s) {
                 if (next < ec && locs[next] == s) { ++next; continue; }
-                lds_P[np++] = (uint16_t)s;
+                listP[np++] = (uint16_t)s;
             }
-            for (uint32_t i = 0; i < es; ++i) lds_E[i] = locs[i];
-            if (np < es) lds_P[0] = 0xffff;  // not enough parity
+            for (uint32_t i = 0; i < es; ++i) listE[i] = locs[i];
+            if (np < es) listP[0] = 0xffff;  // not enough parity
         }
         __syncthreads();
-        if (lds_P[0] == 0xffff) { ok = false; status = 0; }
+        if (listP[0] == 0xffff) { ok = false; status = 0; }
     }
     const uint32_t e = ok ? es : 0;
     if (lane == 0) {
@@ -116,20 +119,19 @@ __global__ __launch_bounds__(kWave) void rs_plan_kernel(RsPlanArgs a)
 
     // ---- stage-1 gather matrix and slots ----
     const E* gp = reinterpret_cast<const E*>(a.gen_parity);
-    const uint32_t cs = a.coef_stride;
     E* coef1 = reinterpret_cast<E*>(a.coef1) + (uint64_t)b * k * cs;
     uint16_t* islots = a.in_slots1 + (uint64_t)b * k;
     for (uint32_t c = lane; c < nd; c += kWave) {
         // is c erased? (E sorted)
         int32_t s_idx = -1;
         for (uint32_t i = 0; i < e; ++i)
-            if (lds_E[i] == c) s_idx = (int32_t)i;
-        islots[c] = s_idx >= 0 ? lds_P[s_idx] : (uint16_t)c;
+            if (listE[i] == c) s_idx = (int32_t)i;
+        islots[c] = s_idx >= 0 ? listP[s_idx] : (uint16_t)c;
         for (uint32_t t = 0; t < cs; ++t) {
             E v = 0;
             if (t < e) {
                 if (s_idx >= 0) v = (E)((uint32_t)s_idx == t);
-                else v = gp[(uint64_t)(lds_P[t] - nd) * k + c];
+                else v = gp[(uint64_t)(listP[t] - nd) * k + c];
             }
             coef1[(uint64_t)c * cs + t] = v;
         }
@@ -137,11 +139,11 @@ __global__ __launch_bounds__(kWave) void rs_plan_kernel(RsPlanArgs a)
 
     // ---- stage 2: invert A[t][s] = G[P_t][E_s] via Gauss-Jordan on [A | I] ----
     const uint32_t w2 = 2 * e;
-    E* work = e <= kPlanLdsMaxE ? lds_work : reinterpret_cast<E*>(a.work) + (uint64_t)b * m * 2 * m;
+    E* work = e <= kPlanLdsMaxE ? lds_work : reinterpret_cast<E*>(wb);
     for (uint32_t idx = lane; idx < e * w2; idx += kWave) {
         const uint32_t t = idx / w2, col = idx % w2;
         E v;
-        if (col < e) v = gp[(uint64_t)(lds_P[t] - nd) * k + lds_E[col]];
+        if (col < e) v = gp[(uint64_t)(listP[t] - nd) * k + listE[col]];
         else v = (E)(col - e == t);
         work[idx] = v;
     }
@@ -172,12 +174,12 @@ __global__ __launch_bounds__(kWave) void rs_plan_kernel(RsPlanArgs a)
         for (uint32_t col = lane; col < w2; col += kWave) work[j * w2 + col] = (E)f.mul(pinv, work[j * w2 + col]);
         __syncthreads();
         // snapshot column j (the elimination factors) before any row is updated
-        for (uint32_t r = lane; r < e; r += kWave) lds_fac[r] = work[r * w2 + j];
+        for (uint32_t r = lane; r < e; r += kWave) fac[r] = work[r * w2 + j];
         __syncthreads();
         for (uint32_t idx = lane; idx < e * w2; idx += kWave) {
             const uint32_t r = idx / w2, col = idx % w2;
             if (r == j) continue;
-            const uint32_t factor = lds_fac[r];
+            const uint32_t factor = fac[r];
             if (factor) work[idx] ^= (E)f.mul(factor, work[j * w2 + col]);
         }
         __syncthreads();
@@ -198,7 +200,7 @@ __global__ __launch_bounds__(kWave) void rs_plan_kernel(RsPlanArgs a)
         coef2[idx] = v;
     }
     uint16_t* oslots = a.out_slots2 + (uint64_t)b * k;
-    for (uint32_t s = lane; s < e; s += kWave) oslots[s] = lds_E[s];
+    for (uint32_t s = lane; s < e; s += kWave) oslots[s] = listE[s];
 }
 
 

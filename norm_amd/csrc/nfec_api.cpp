@@ -76,7 +76,7 @@ static uint32_t sub_batch(uint64_t ws_bytes_per_block)
     }();
     if (env > 0) return (uint32_t)std::max(256L, std::min(env, 1L << 20));
     const uint64_t cap = (4ull << 30) / std::max<uint64_t>(ws_bytes_per_block, 1);
-    return (uint32_t)std::max<uint64_t>(256, std::min<uint64_t>(65536, cap));
+    return (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(65536, cap));
 }
 
 uint32_t round_up(uint32_t v, uint32_t a) { return (v + a - 1) / a * a; }
@@ -434,15 +434,17 @@ int decode_device(nfec_codec* c, const nfec_block_batch* b, const uint16_t* locs
     if (!locs || !counts) return fail(NFEC_EINVAL, "null erasure arrays");
     const bool acc = b->flags & NFEC_ACCUMULATE;
     if (c->kind == NFEC_MDP && acc) return fail(NFEC_ENOTSUP, "MDP decode requires zero-filled erased segments");
-    if (c->kind != NFEC_MDP && std::min(c->k, c->m) > 256)
-        return fail(NFEC_ENOTSUP, "RS decode supports at most 256 source erasures per block (min(k, m) <= 256)");
     std::lock_guard<std::mutex> lk(c->mu);
     const uint32_t n = c->k + c->m;
     const uint32_t zstride = round_up(c->vec, 8);
+    // RS decode rows: at most min(k, m) source erasures are solved per block, so the plan's
+    // matrices and the z rows are sized by that, not by m (m >> k codes, e.g. npc's auto mode)
+    const uint32_t dcs = c->kind == NFEC_MDP ? c->cs : round_up(std::max(1u, std::min(c->k, c->m)), kRowPad);
+    const bool big_plan = c->kind != NFEC_MDP && std::min(c->k, c->m) > 64;
     const uint64_t ws_per_block = c->kind == NFEC_MDP
                                       ? (uint64_t)n * c->cs
-                                      : (uint64_t)c->cs * zstride + ((uint64_t)c->k + c->cs) * c->cs * c->sym +
-                                            (c->m > 64 ? (uint64_t)c->m * 2 * c->m * c->sym : 0);
+                                      : (uint64_t)dcs * zstride + ((uint64_t)c->k + dcs) * dcs * c->sym +
+                                            (big_plan ? rs_plan_work_bytes(dcs, c->sym) : 0);
     const uint32_t sb = std::min(b->nblocks, sub_batch(ws_per_block + 4ull * n + 64));
     int rc;
     if ((rc = c->w_rows.reserve(sb))) return rc;
@@ -451,12 +453,12 @@ int decode_device(nfec_codec* c, const nfec_block_batch* b, const uint16_t* locs
     if ((rc = c->w_islots.reserve((size_t)sb * n))) return rc;
     if ((rc = c->w_oslots.reserve((size_t)sb * n))) return rc;
     if (c->kind == NFEC_MDP) {
-        if ((rc = c->w_coef1.reserve((size_t)sb * n * c->cs))) return rc;
+        if ((rc = c->w_coef1.reserve((size_t)sb * n * dcs))) return rc;
     } else {
-        if ((rc = c->w_coef1.reserve((size_t)sb * c->k * c->cs * c->sym))) return rc;
-        if ((rc = c->w_coef2.reserve((size_t)sb * c->cs * c->cs * c->sym))) return rc;
-        if ((rc = c->w_z.reserve((size_t)sb * c->cs * zstride))) return rc;
-        if (c->m > 64 && (rc = c->w_work.reserve((size_t)sb * c->m * 2 * c->m * c->sym))) return rc;
+        if ((rc = c->w_coef1.reserve((size_t)sb * c->k * dcs * c->sym))) return rc;
+        if ((rc = c->w_coef2.reserve((size_t)sb * dcs * dcs * c->sym))) return rc;
+        if ((rc = c->w_z.reserve((size_t)sb * dcs * zstride))) return rc;
+        if (big_plan && (rc = c->w_work.reserve((size_t)sb * rs_plan_work_bytes(dcs, c->sym)))) return rc;
     }
     const bool fast = c->kind == NFEC_RS8 && !b->num_data && c->m <= 32 && c->k <= 64 && !force_generic() &&
                       has_bitsliced(c->k, c->m) && bs::offsets_fit(b->block_stride, b->seg_stride);
@@ -488,7 +490,7 @@ int decode_device(nfec_codec* c, const nfec_block_batch* b, const uint16_t* locs
             p.cols = c->w_cols.p;
             p.in_slots = c->w_islots.p;
             p.out_slots = c->w_oslots.p;
-            p.coef_stride = c->cs;
+            p.coef_stride = dcs;
             p.coef = c->w_coef1.p;
             if ((rc = launch_mdp_plan(p, s))) return rc;
             Gf8MatmulArgs a;
@@ -505,8 +507,8 @@ int decode_device(nfec_codec* c, const nfec_block_batch* b, const uint16_t* locs
             a.row_count = c->w_rows.p;
             a.slots_stride = n;
             a.coef = c->w_coef1.p;
-            a.coef_block_stride = (uint64_t)n * c->cs;
-            a.coef_col_stride = c->cs;
+            a.coef_block_stride = (uint64_t)n * dcs;
+            a.coef_col_stride = dcs;
             a.vtab = c->d_vtab.p;
             a.nblocks = nb;
             a.vec_bytes = c->vec;
@@ -533,7 +535,7 @@ int decode_device(nfec_codec* c, const nfec_block_batch* b, const uint16_t* locs
             p2.emask = c->w_emask.p;
             p2.psel = c->w_psel.p;
             p2.pmap = c->w_pmap.p;
-            p2.coef_stride = c->cs;
+            p2.coef_stride = dcs;
             p2.coef2 = c->w_coef2.p;
             if ((rc = launch_rs_plan2(p2, s))) return rc;
             // fused per-block repair for the blocks it qualifies for (NFEC_FUSED=0: off); the
@@ -554,8 +556,8 @@ int decode_device(nfec_codec* c, const nfec_block_batch* b, const uint16_t* locs
                 f.psel = c->w_psel.p;
                 f.emask = c->w_emask.p;
                 f.coef = c->w_coef2.p;
-                f.coef_block_stride = (uint64_t)c->cs * c->cs;
-                f.coef_col_stride = c->cs;
+                f.coef_block_stride = (uint64_t)dcs * dcs;
+                f.coef_col_stride = dcs;
                 f.out_slots = c->w_oslots.p;
                 f.slots_stride = c->k;
                 f.accumulate = acc;
@@ -572,7 +574,7 @@ int decode_device(nfec_codec* c, const nfec_block_batch* b, const uint16_t* locs
             d.psel = c->w_psel.p;
             d.pmap = c->w_pmap.p;
             d.z = c->w_z.p;
-            d.z_block_stride = (uint64_t)c->cs * zstride;
+            d.z_block_stride = (uint64_t)dcs * zstride;
             d.z_stride = zstride;
             d.xcd_remap = bs_flags() & 1u;
             if ((rc = launch_rs8_bitsliced_reencode(c->k, c->m, d, s))) return fail(rc, "bit-sliced re-encode launch failed");
@@ -583,7 +585,7 @@ int decode_device(nfec_codec* c, const nfec_block_batch* b, const uint16_t* locs
             if (!use_solve) {
                 Gf8MatmulArgs g2;
                 g2.in_base = c->w_z.p;
-                g2.in_block_stride = (uint64_t)c->cs * zstride;
+                g2.in_block_stride = (uint64_t)dcs * zstride;
                 g2.in_seg_stride = zstride;
                 g2.in_count = c->w_cols.p;
                 g2.out_base = blocks;
@@ -594,8 +596,8 @@ int decode_device(nfec_codec* c, const nfec_block_batch* b, const uint16_t* locs
                 g2.row_count = c->w_rows.p;
                 g2.slots_stride = c->k;
                 g2.coef = c->w_coef2.p;
-                g2.coef_block_stride = (uint64_t)c->cs * c->cs;
-                g2.coef_col_stride = c->cs;
+                g2.coef_block_stride = (uint64_t)dcs * dcs;
+                g2.coef_col_stride = dcs;
                 g2.vtab = c->d_vtab.p;
                 g2.nblocks = nb;
                 g2.vec_bytes = c->vec;
@@ -605,7 +607,7 @@ int decode_device(nfec_codec* c, const nfec_block_batch* b, const uint16_t* locs
             }
             Gf8SolveArgs a2;
             a2.z = c->w_z.p;
-            a2.z_block_stride = (uint64_t)c->cs * zstride;
+            a2.z_block_stride = (uint64_t)dcs * zstride;
             a2.z_stride = zstride;
             a2.cols = c->w_cols.p;
             a2.rows = c->w_rows.p;
@@ -615,8 +617,8 @@ int decode_device(nfec_codec* c, const nfec_block_batch* b, const uint16_t* locs
             a2.out_block_stride = b->block_stride;
             a2.out_seg_stride = b->seg_stride;
             a2.coef = c->w_coef2.p;
-            a2.coef_block_stride = (uint64_t)c->cs * c->cs;
-            a2.coef_col_stride = c->cs;
+            a2.coef_block_stride = (uint64_t)dcs * dcs;
+            a2.coef_col_stride = dcs;
             a2.vtab = c->d_vtab.p;
             a2.nblocks = nb;
             a2.vec_bytes = c->vec;
@@ -658,10 +660,11 @@ int decode_device(nfec_codec* c, const nfec_block_batch* b, const uint16_t* locs
         p.in_slots1 = c->w_islots.p;
         p.out_slots2 = c->w_oslots.p;
         p.cols2 = c->w_cols.p;
-        p.coef_stride = c->cs;
+        p.coef_stride = dcs;
         p.coef1 = c->w_coef1.p;
         p.coef2 = c->w_coef2.p;
-        p.work = c->w_work.p;
+        p.work = big_plan ? c->w_work.p : nullptr;
+        p.work_block_bytes = rs_plan_work_bytes(dcs, c->sym);
         if ((rc = launch_rs_plan(p, s))) return rc;
         // stage 1: z_t = parity(P_t) ^ sum_{present c} G[P_t][c] d_c  -> scratch rows
         // stage 2: d_E = A^-1 z                                          -> erased slots
@@ -674,21 +677,21 @@ int decode_device(nfec_codec* c, const nfec_block_batch* b, const uint16_t* locs
             a.in_count = nd;
             a.cols_const = c->k;
             a.out_base = c->w_z.p;
-            a.out_block_stride = (uint64_t)c->cs * zstride;
+            a.out_block_stride = (uint64_t)dcs * zstride;
             a.out_seg_stride = zstride;
             a.out_slot_mode = OUT_SLOT_ROW;
             a.row_count = c->w_rows.p;
             a.slots_stride = c->k;
             a.coef = c->w_coef1.p;
-            a.coef_block_stride = (uint64_t)c->k * c->cs;
-            a.coef_col_stride = c->cs;
+            a.coef_block_stride = (uint64_t)c->k * dcs;
+            a.coef_col_stride = dcs;
             a.vtab = c->d_vtab.p;
             a.nblocks = nb;
             a.vec_bytes = c->vec;
             if ((rc = launch_gf8_matmul(a, false, s))) return rc;
             Gf8MatmulArgs a2;
             a2.in_base = c->w_z.p;
-            a2.in_block_stride = (uint64_t)c->cs * zstride;
+            a2.in_block_stride = (uint64_t)dcs * zstride;
             a2.in_seg_stride = zstride;
             a2.in_count = c->w_cols.p;
             a2.out_base = blocks;
@@ -699,8 +702,8 @@ int decode_device(nfec_codec* c, const nfec_block_batch* b, const uint16_t* locs
             a2.row_count = c->w_rows.p;
             a2.slots_stride = c->k;
             a2.coef = c->w_coef2.p;
-            a2.coef_block_stride = (uint64_t)c->cs * c->cs;
-            a2.coef_col_stride = c->cs;
+            a2.coef_block_stride = (uint64_t)dcs * dcs;
+            a2.coef_col_stride = dcs;
             a2.vtab = c->d_vtab.p;
             a2.nblocks = nb;
             a2.vec_bytes = c->vec;
@@ -716,14 +719,14 @@ int decode_device(nfec_codec* c, const nfec_block_batch* b, const uint16_t* locs
             a.in_count = nd;
             a.cols_const = c->k;
             a.out_base = c->w_z.p;
-            a.out_block_stride = (uint64_t)c->cs * zstride;
+            a.out_block_stride = (uint64_t)dcs * zstride;
             a.out_seg_stride = zstride;
             a.out_slot_mode = OUT_SLOT_ROW;
             a.row_count = c->w_rows.p;
             a.slots_stride = c->k;
             a.coef = reinterpret_cast<const uint16_t*>(c->w_coef1.p);
-            a.coef_block_stride = (uint64_t)c->k * c->cs;
-            a.coef_col_stride = c->cs;
+            a.coef_block_stride = (uint64_t)c->k * dcs;
+            a.coef_col_stride = dcs;
             a.exp_tab = reinterpret_cast<const uint16_t*>(c->d_exp.p);
             a.log_tab = c->d_log.p;
             a.nblocks = nb;
@@ -731,7 +734,7 @@ int decode_device(nfec_codec* c, const nfec_block_batch* b, const uint16_t* locs
             if ((rc = launch_gf16_matmul(a, s))) return rc;
             Gf16MatmulArgs a2 = a;
             a2.in_base = c->w_z.p;
-            a2.in_block_stride = (uint64_t)c->cs * zstride;
+            a2.in_block_stride = (uint64_t)dcs * zstride;
             a2.in_seg_stride = zstride;
             a2.in_slots = nullptr;
             a2.in_count = c->w_cols.p;
@@ -741,7 +744,7 @@ int decode_device(nfec_codec* c, const nfec_block_batch* b, const uint16_t* locs
             a2.out_slots = c->w_oslots.p;
             a2.out_slot_mode = OUT_SLOT_LIST;
             a2.coef = reinterpret_cast<const uint16_t*>(c->w_coef2.p);
-            a2.coef_block_stride = (uint64_t)c->cs * c->cs;
+            a2.coef_block_stride = (uint64_t)dcs * dcs;
             a2.accumulate = acc;
             if ((rc = launch_gf16_matmul(a2, s))) return rc;
         }

@@ -173,8 +173,15 @@ struct RsPlanArgs {
     uint32_t coef_stride = 0;                // padded row count of coef1/coef2 (multiple of 16)
     void* coef1 = nullptr;                   // [b][k][cs] gathered generator / unit columns
     void* coef2 = nullptr;                   // [b][cs][cs] inverse (column-major: [t][s])
-    void* work = nullptr;                    // [b][m][2m] scratch
+    void* work = nullptr;                    // [b] work_block_bytes: e x 2e matrix, then the E/P
+                                             // lists and pivot factors (used when e > 64 / > 256)
+    uint64_t work_block_bytes = 0;
 };
+// per-block scratch of launch_rs_plan for decode row stride cs (elements of sym bytes)
+inline uint64_t rs_plan_work_bytes(uint32_t cs, uint32_t sym)
+{
+    return ((uint64_t)cs * 2 * cs * sym + (uint64_t)cs * (4 + sym) + 7) & ~7ull;
+}
 int launch_rs_plan(const RsPlanArgs& a, hipStream_t s);
 
 // RS decode planning, closed form (RS8, m <= 64): the systematic generator is the Lagrange

@@ -135,6 +135,9 @@ DEC_CASES = [
     (NFEC_RS16, 40, 10, 65, 3, 7, 3),
     (NFEC_RS16, 400, 100, 64, 2, 2, 0),
     (NFEC_RS16, 400, 100, 64, 1, 90, 10),
+    (NFEC_RS16, 300, 400, 64, 2, 280, 10),   # > 256 source erasures: plan lists in global scratch
+    (NFEC_RS16, 100, 300, 66, 2, 90, 5),     # m > k: decode rows sized by min(k, m)
+    (NFEC_RS8, 16, 200, 64, 3, 16, 20),
     (NFEC_MDP, 64, 32, 1400, 4, 16, 0),
     (NFEC_MDP, 64, 32, 200, 4, 20, 12),
     (NFEC_MDP, 16, 4, 33, 6, 2, 2),

@@ -159,6 +159,7 @@ def _corrupt(buf, ss, lay, per_block, rng, p):
     ("m_mult_k", 200_000, dict(block=16, parity=16), 16),  # (b*m) % k == 0: every block exact
     ("rotated", 100_000, dict(block=20, parity=6), 3),    # the reference's rotation: mis-repairs
     ("rs16", 150_000, dict(segment=516, block=300, parity=20), 20),  # one (shortened) block
+    ("default_auto", 20_000, dict(), 15),  # the reference's defaults: RS16 k=21, m=2100
 ])
 def test_decode_file_matches_reference_loop(tmp_path, name, size, kw, damage):
     src, data = _write(tmp_path, f"{name}.dat", size, seed=3)
