@@ -151,6 +151,26 @@ struct Gf16MatmulArgs {
 };
 int launch_gf16_matmul(const Gf16MatmulArgs& a, hipStream_t s);
 
+// RS16 encode, bit-sliced with per-lane four-Russians tables in LDS (kernels_gf16bs.hip).
+// In and out share the batch layout; parity row r goes to slot numData_b + r.
+struct Gf16BsEncArgs {
+    const uint8_t* base = nullptr;
+    uint8_t* out_base = nullptr;
+    uint64_t block_stride = 0;
+    uint32_t seg_stride = 0;
+    uint32_t nblocks = 0;
+    const uint16_t* num_data = nullptr;  // per block or null (k)
+    uint32_t k = 0, m = 0;
+    uint32_t vec_bytes = 0;              // even
+    uint32_t chunks = 0;                 // 64-byte chunks per segment
+    const uint16_t* sel = nullptr;       // [k][m_pad][64] table offsets (gf16_bs_selectors)
+    uint32_t m_pad = 0;                  // gf16_bs_rows_padded(m)
+    uint32_t accumulate = 0;
+};
+inline uint32_t gf16_bs_rows_padded(uint32_t m) { return (m + 7u) & ~7u; }
+int launch_gf16_bs_encode(const Gf16BsEncArgs& a, hipStream_t s);  // NFEC_ENOTSUP: layout not 8-byte aligned
+void gf16_bs_selectors(const std::vector<uint32_t>& parity_rows, uint32_t k, uint32_t m, uint16_t* sel);
+
 // RS decode planning (per block): pick parities, invert the e x e system, emit the
 // stage-1 (gather) and stage-2 (inverse) matrices and slot lists.
 struct RsPlanArgs {

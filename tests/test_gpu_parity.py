@@ -70,6 +70,7 @@ ENC_CASES = [
     (NFEC_RS16, 40, 10, 65, 72, 3),
     (NFEC_RS16, 400, 100, 64, 64, 2),
     (NFEC_RS16, 100, 20, 1400, 1400, 3),
+    (NFEC_RS16, 700, 200, 64, 64, 2),     # offsets table > 16 MB: the exp-table encode kernel
     (NFEC_MDP, 64, 32, 1400, 1400, 4),
     (NFEC_MDP, 16, 4, 33, 40, 5),
 ]
