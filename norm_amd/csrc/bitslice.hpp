@@ -273,6 +273,8 @@ __device__ __forceinline__ void bst8(const Items& it, uint32_t voff, uint32_t so
 int launch_rs8_bitsliced_encode(uint32_t k, uint32_t m, const bs::EncArgs& a, hipStream_t s);
 // gen_rs8_asm.hip: hand-allocated assembly bodies; NFEC_ENOTSUP for tails / shortened batches
 int launch_rs8_asm_encode(uint32_t k, uint32_t m, const bs::EncArgs& a, hipStream_t s);
+// gen_rs8_asm.hip: MDP encode of full blocks with the same assembly bodies (NFEC_ENOTSUP otherwise)
+int launch_mdp_asm_encode(uint32_t k, uint32_t m, const bs::EncArgs& a, hipStream_t s);
 int launch_rs8_bitsliced_reencode(uint32_t k, uint32_t m, const bs::DecArgs& a, hipStream_t s);
 int bitsliced_encode_generator(uint32_t k, uint32_t m, uint8_t* out);
 

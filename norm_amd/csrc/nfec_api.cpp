@@ -441,6 +441,23 @@ int encode_device(nfec_codec* c, const nfec_block_batch* b, hipStream_t s)
     // MDP: the in-order LFSR is a linear map of the block; the caller's parity buffers are
     // zeroed at block start by contract, so accumulate has no reference meaning.
     if (acc) return fail(NFEC_ENOTSUP, "MDP encode does not accumulate (LFSR restarts from zeroed parity)");
+    if (!b->num_data && use_asm() && !force_generic()) {
+        // full blocks: the LFSR's block map is a constant matrix, folded into the bit-sliced
+        // assembly bodies of the RS8 encode
+        bs::EncArgs e;
+        e.base = static_cast<const uint8_t*>(b->blocks);
+        e.out = static_cast<uint8_t*>(b->blocks);
+        e.block_stride = b->block_stride;
+        e.seg_stride = b->seg_stride;
+        e.nblocks = b->nblocks;
+        e.vec = c->vec;
+        e.num_data = nullptr;
+        e.accumulate = 0;
+        e.xcd_remap = bs_flags() & 1u;
+        e.nt_store = (bs_flags() >> 1) & 1u;
+        const int rc = launch_mdp_asm_encode(c->k, c->m, e, s);
+        if (rc != NFEC_ENOTSUP) return rc == NFEC_OK ? NFEC_OK : fail(rc, "MDP assembly encode launch failed");
+    }
     Gf8MatmulArgs a;
     a.in_base = static_cast<const uint8_t*>(b->blocks);
     a.in_block_stride = b->block_stride;

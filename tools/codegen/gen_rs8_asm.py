@@ -28,9 +28,10 @@ import os
 import sys
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
-from gen_rs8_bitsliced import bitmatrix_rows, generator  # noqa: E402
+from gen_rs8_bitsliced import EXP, bitmatrix_rows, generator, mul  # noqa: E402
 
 DEFAULT_SHAPES = [(64, 32), (64, 16), (64, 8)]
+MDP_SHAPES = [(64, 32), (64, 16)]
 ROWS = 16            # parity rows per role (one wavefront)
 # A/B probes for (64, 32), NFEC_ASM_VARIANT=<id>: VALU only (no source loads) / memory only
 # (measured and dropped: nt loads 2.42 ms / nt stores 2.42 / one role loading for both 1.91 in the
@@ -260,13 +261,39 @@ def clobbers():
     return ", ".join(v + s + ['"scc"', '"memory"'])
 
 
-def gen_kernel(k, m, probe=None, suffix=""):
-    G = generator(k, m)
+def mdp_matrix(k, m):
+    """m x k block map of the MDP LFSR encoder for a full block of k source symbols: the same
+    linear map as norm_amd/csrc/gf_host.cpp mdp_encode_matrix (reference
+    normEncoderMDP.cpp:102-170 generator polynomial, :178-211 in-order Encode steps)."""
+    g = [1] + [0] * m
+    for n in range(1, m + 1):
+        a = EXP[n]
+        for i in range(n, 0, -1):
+            g[i] = g[i - 1] ^ mul(g[i], a)
+        g[0] = mul(g[0], a)
+    st = [0] * m
+
+    def step(d):
+        fb = d ^ st[0]
+        st[:] = [st[i + 1] ^ mul(g[m - 1 - i], fb) for i in range(m - 1)] + [mul(g[0], fb)]
+
+    out = [[0] * k for _ in range(m)]
+    step(1)
+    for j in range(k - 1, -1, -1):
+        for i in range(m):
+            out[i][j] = st[i]
+        if j:
+            step(0)
+    return out
+
+
+def gen_kernel(k, m, probe=None, suffix="", G=None, prefix="rs8_asm_enc"):
+    G = G if G is not None else generator(k, m)
     roles = [(r0, min(ROWS, m - r0)) for r0 in range(0, m, ROWS)]
     nroles = len(roles)
     groups = max(1, 4 // nroles)
     threads = 64 * nroles * groups
-    K = f"rs8_asm_enc{suffix}_k{k}_m{m}"
+    K = f"{prefix}{suffix}_k{k}_m{m}"
     out = []
     for ri, (r0, rows) in enumerate(roles):
         body = role_asm(G, k, m, r0, rows, probe)
@@ -332,6 +359,9 @@ def main():
         if (k, m) == (64, 32):
             for v, (probe, suffix) in PROBES.items():
                 parts.append(gen_kernel(k, m, probe, suffix))
+    # MDP full blocks: the LFSR encoder is a fixed linear map too, so the same bodies apply
+    for k, m in MDP_SHAPES:
+        parts.append(gen_kernel(k, m, G=mdp_matrix(k, m), prefix="mdp_asm_enc"))
     parts.append("}  // namespace")
     parts.append("")
     parts.append("static int asm_variant()")
@@ -348,6 +378,14 @@ def main():
             for v, (probe, suffix) in PROBES.items():
                 parts.append(f"    if (k == {k} && m == {m} && asm_variant() == {v}) return launch_rs8_asm_enc{suffix}_k{k}_m{m}(a, s);")
         parts.append(f"    if (k == {k} && m == {m}) return launch_rs8_asm_enc_k{k}_m{m}(a, s);")
+    parts.append("    return NFEC_ENOTSUP;")
+    parts.append("}")
+    parts.append("")
+    parts.append("// MDP encode of full blocks (num_data == NULL); NFEC_ENOTSUP otherwise")
+    parts.append("int launch_mdp_asm_encode(uint32_t k, uint32_t m, const bs::EncArgs& a, hipStream_t s)")
+    parts.append("{")
+    for k, m in MDP_SHAPES:
+        parts.append(f"    if (k == {k} && m == {m}) return launch_mdp_asm_enc_k{k}_m{m}(a, s);")
     parts.append("    return NFEC_ENOTSUP;")
     parts.append("}")
     parts.append("")
