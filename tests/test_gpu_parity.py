@@ -331,7 +331,7 @@ def test_full_size_roundtrip_c2_c3(orc):
     assert torch.equal(blocks, keep)
 
 
-@pytest.mark.parametrize("m", [32, 16])
+@pytest.mark.parametrize("m", [32, 16, 8])
 @pytest.mark.parametrize("accumulate", [False, True])
 def test_fused_decode_mixed_batch(orc, m, accumulate):
     """The fused per-block repair (gen_fdec_asm.hip) takes blocks with e <= 16 repaired from
@@ -345,7 +345,7 @@ def test_fused_decode_mixed_batch(orc, m, accumulate):
     locs = np.zeros((nb, m), np.uint16)
     counts = np.zeros(nb, np.uint16)
     for b in range(nb):
-        es = 1 + b % 16
+        es = 1 + b % min(16, m)
         src = np.sort(rng.choice(k, es, replace=False))
         par = k + np.sort(rng.choice(4, 2, replace=False)) if b % 3 == 0 and es + 2 <= m else np.array([], int)
         e = np.concatenate([src, par]).astype(np.uint16)

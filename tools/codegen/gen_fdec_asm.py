@@ -34,7 +34,7 @@ from gen_rs8_asm import (MASKS, MULTI, NSLOT, S_MASK, TEMP, acc_reg, bank, combo
                          slot_regs, split, table_code, transpose)
 from gen_rs8_bitsliced import bitmatrix_rows, generator  # noqa: E402
 
-DEFAULT_SHAPES = [(64, 32), (64, 16)]
+DEFAULT_SHAPES = [(64, 32), (64, 16), (64, 8)]
 IN_REGS = [0, 1, 4, 5, 8, 9, 12, 13]      # compiler-placed inputs: load / store offsets
 S_RET, S_EM = 56, 58                       # return address; erased-column mask (64 bit)
 S_COEF2 = 60
@@ -114,10 +114,11 @@ def snippets(regs):
 
 def fdec_asm(k, m):
     G = generator(k, m)
+    nr = min(NCOLS_PAR, m)  # z rows that can be in use (e <= m)
     L = []
     offs = ["%[o0]", "%[o1]", "%[o2]", "%[o3]"]
     soffs = ["%[s0]", "%[s1]", "%[s2]", "%[s3]"]
-    ncol = k + NCOLS_PAR
+    ncol = k + nr
     L += [f"s_mov_b64 s[{S_LRS}:{S_LRS + 1}], %[base]", f"s_mov_b32 s{S_LRS + 2}, -1",
           f"s_mov_b32 s{S_LRS + 3}, 0x00020000",
           f"s_mov_b64 s[{S_SRS}:{S_SRS + 1}], %[base]", f"s_mov_b32 s{S_SRS + 2}, 0x80000000",
@@ -159,7 +160,7 @@ def fdec_asm(k, m):
             L += [f"s_bitcmp1_b64 s[{S_EM}:{S_EM + 1}], {c}", f"s_cbranch_scc1 Lskip{c}_%="]
             L += transpose(w, ring_temps())
             ups, need = [], [set(), set()]
-            for r in range(16):
+            for r in range(nr):
                 mat = bitmatrix_rows(G[r][c])
                 for i in range(8):
                     a, b = split(mat[i])
