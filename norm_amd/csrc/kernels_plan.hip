@@ -212,7 +212,7 @@ __global__ __launch_bounds__(kWave) void mdp_plan_kernel(MdpPlanArgs a)
     __shared__ uint8_t ex[512];
     __shared__ uint16_t lg[256];
     __shared__ uint8_t lam[512];
-    __shared__ uint8_t lamb[256][256 / 4];  // per erased row: prefix sums Lambda_u(beta_r) (u < m)
+    extern __shared__ uint8_t lamb[];       // [erased row r][u < m]: prefix sums Lambda_u(beta_r)
     __shared__ uint16_t surv[256];
     __shared__ uint16_t eras[256];
     __shared__ uint8_t dinv_s[256], beta_s[256];
@@ -229,7 +229,7 @@ __global__ __launch_bounds__(kWave) void mdp_plan_kernel(MdpPlanArgs a)
     const uint32_t ec = uni(a.erasure_counts[b]);
     const uint16_t* locs = a.erasure_locs + (uint64_t)b * a.erasure_stride;
     const uint32_t nvecs = nd + m;
-    bool ok = nd >= 1 && nd <= a.k && ec <= m && ec <= a.erasure_stride && m <= 64;
+    bool ok = nd >= 1 && nd <= a.k && ec <= m && ec <= a.erasure_stride;
     uint32_t es = 0;
     if (ok)
         for (uint32_t i = 0; i < ec; ++i) {
@@ -292,7 +292,7 @@ __global__ __launch_bounds__(kWave) void mdp_plan_kernel(MdpPlanArgs a)
         for (uint32_t u = 0; u < m; ++u) {
             acc ^= mul(lam[u], bp);
             bp = mul(bp, beta);
-            lamb[r][u] = (uint8_t)acc;
+            lamb[r * m + u] = (uint8_t)acc;
         }
     }
     __syncthreads();
@@ -308,8 +308,8 @@ __global__ __launch_bounds__(kWave) void mdp_plan_kernel(MdpPlanArgs a)
             uint32_t val = 0;
             if (r < es) {
                 const uint32_t w = mul(gamma, beta_s[r]);
-                uint32_t h = lamb[r][0];
-                for (uint32_t u = 1; u < m; ++u) h = mul(h, w) ^ lamb[r][u];
+                uint32_t h = lamb[r * m];
+                for (uint32_t u = 1; u < m; ++u) h = mul(h, w) ^ lamb[r * m + u];
                 val = mul(dinv_s[r], mul(gamma, h));
             }
             coef[(uint64_t)j * cs + r] = (uint8_t)val;
@@ -334,7 +334,9 @@ int launch_rs_plan(const RsPlanArgs& a, hipStream_t s)
 int launch_mdp_plan(const MdpPlanArgs& a, hipStream_t s)
 {
     if (a.nblocks == 0) return NFEC_OK;
-    hipLaunchKernelGGL(mdp_plan_kernel, dim3(a.nblocks), dim3(kWave), 0, s, a);
+    // erased source rows are at most min(k, m); k + m <= 255 keeps this under 16 KiB
+    const size_t lds = (size_t)std::min(a.k, a.m) * a.m;
+    hipLaunchKernelGGL(mdp_plan_kernel, dim3(a.nblocks), dim3(kWave), lds, s, a);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return hip_fail(e, "mdp_plan launch");
     return NFEC_OK;

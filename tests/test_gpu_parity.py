@@ -142,6 +142,8 @@ DEC_CASES = [
     (NFEC_MDP, 64, 32, 1400, 4, 16, 0),
     (NFEC_MDP, 64, 32, 200, 4, 20, 12),
     (NFEC_MDP, 16, 4, 33, 6, 2, 2),
+    (NFEC_MDP, 100, 100, 64, 3, 90, 10),    # m > 64: the locator prefix sums in dynamic LDS
+    (NFEC_MDP, 50, 150, 40, 3, 50, 60),
 ]
 
 

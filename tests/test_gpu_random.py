@@ -25,7 +25,7 @@ def _draw(seed):
         vec = int(rng.integers(2, 600))
     else:
         k = int(rng.integers(1, 200))
-        m = int(rng.integers(1, min(255 - k, 64) + 1))
+        m = int(rng.integers(1, (255 - k if rng.integers(0, 3) == 0 else min(255 - k, 64)) + 1))
         vec = int(rng.choice([int(rng.integers(1, 3000)), 1400, 1408, 8 * int(rng.integers(1, 200))]))
     stride = (vec + 7) // 8 * 8 + 8 * int(rng.integers(0, 3))
     nb = int(rng.integers(1, 40))
