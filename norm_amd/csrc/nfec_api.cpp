@@ -1189,12 +1189,47 @@ static void stage_drain(nfec_codec* c)
 // so the host pipelines run every chunk's decode on one compute stream: slot stream upload ->
 // event -> compute-stream decode -> event -> slot stream download.  (Encode reads only the
 // codec's constants and runs on the slot streams.)
+// Blocks whose numData (known on the host) equals k go to the unshortened fast kernels in
+// sub-batches of their own; only the others carry their numData.  NORM batches are mostly full
+// blocks with one short block ending each object, and one short block would otherwise send the
+// whole batch down the generic (numData-aware) kernels.  Full runs shorter than kMinFullRun stay
+// with their neighbours: a launch per handful of blocks costs more than it saves.
+extern "C++" template <typename F>
+static int split_full_runs(const uint16_t* hnd, uint32_t n, uint32_t k, F launch)
+{
+    constexpr uint32_t kMinFullRun = 32;
+    if (!hnd) return launch(0u, n, false);
+    uint32_t i = 0;
+    while (i < n) {
+        uint32_t rs = n, re = n;
+        for (uint32_t j = i; j < n;) {
+            if (hnd[j] != k) {
+                ++j;
+                continue;
+            }
+            uint32_t e = j;
+            while (e < n && hnd[e] == k) ++e;
+            if (e - j >= kMinFullRun) {
+                rs = j;
+                re = e;
+                break;
+            }
+            j = e;
+        }
+        int rc;
+        if (rs > i && (rc = launch(i, rs - i, true))) return rc;
+        if (rs < n && (rc = launch(rs, re - rs, false))) return rc;
+        i = re;
+    }
+    return NFEC_OK;
+}
+
 static int decode_serialized(nfec_codec* c, const nfec_block_batch* db, const uint16_t* dl, uint32_t lstride,
-                             const uint16_t* dc, HostSlot& s)
+                             const uint16_t* dc, HostSlot& s, uint32_t status_off = 0)
 {
     NFEC_HIP(hipEventRecord(s.ev_up, s.st));
     NFEC_HIP(hipStreamWaitEvent(c->stage.cst, s.ev_up, 0));
-    const int rc = decode_device(c, db, dl, lstride, dc, s.dstat, c->stage.cst);
+    const int rc = decode_device(c, db, dl, lstride, dc, s.dstat + status_off, c->stage.cst);
     if (rc) return rc;
     NFEC_HIP(hipEventRecord(s.ev_cd, c->stage.cst));
     NFEC_HIP(hipStreamWaitEvent(s.st, s.ev_cd, 0));
@@ -1288,9 +1323,23 @@ static int run_host_batch(nfec_codec* c, const nfec_block_batch* hb, const uint1
             ae = hipMemcpyAsync(dl, locs + (uint64_t)b0 * lstride, (size_t)j.nb * lstride * 2, hipMemcpyHostToDevice, s.st);
             if (ae == hipSuccess) ae = hipMemcpyAsync(dc, counts + b0, (size_t)j.nb * 2, hipMemcpyHostToDevice, s.st);
             if (ae != hipSuccess) return bail(hip_fail(ae, "host batch upload"));
-            rc = decode_serialized(c, &db, dl, lstride, dc, s);
+            rc = split_full_runs(hb->num_data ? hb->num_data + b0 : nullptr, j.nb, c->k,
+                                 [&](uint32_t o, uint32_t n, bool nd) {
+                                     nfec_block_batch sb = db;
+                                     sb.blocks = s.dev + o * dbs;
+                                     sb.nblocks = n;
+                                     sb.num_data = nd ? dnd + o : nullptr;
+                                     return decode_serialized(c, &sb, dl + (uint64_t)o * lstride, lstride, dc + o, s, o);
+                                 });
         } else {
-            rc = encode_device(c, &db, s.st);
+            rc = split_full_runs(hb->num_data ? hb->num_data + b0 : nullptr, j.nb, c->k,
+                                 [&](uint32_t o, uint32_t n, bool nd) {
+                                     nfec_block_batch sb = db;
+                                     sb.blocks = s.dev + o * dbs;
+                                     sb.nblocks = n;
+                                     sb.num_data = nd ? dnd + o : nullptr;
+                                     return encode_device(c, &sb, s.st);
+                                 });
         }
         if (rc) return bail(rc);
         if (pinned)
@@ -1459,13 +1508,25 @@ static int run_host_vectors(nfec_codec* c, void* const* vecs, uint32_t nblocks, 
             ae = hipMemcpyAsync(dl, locs + (uint64_t)b0 * lstride, (size_t)j.nb * lstride * 2, hipMemcpyHostToDevice, s.st);
             if (ae == hipSuccess) ae = hipMemcpyAsync(dc, counts + b0, (size_t)j.nb * 2, hipMemcpyHostToDevice, s.st);
             if (ae != hipSuccess) return bail(hip_fail(ae, "vector batch upload"));
-            rc = decode_serialized(c, &db, dl, lstride, dc, s);
+            rc = split_full_runs(num_data ? num_data + b0 : nullptr, j.nb, c->k, [&](uint32_t o, uint32_t n, bool nd) {
+                nfec_block_batch sb = db;
+                sb.blocks = s.dev + o * dbs;
+                sb.nblocks = n;
+                sb.num_data = nd ? dnd + o : nullptr;
+                return decode_serialized(c, &sb, dl + (uint64_t)o * lstride, lstride, dc + o, s, o);
+            });
             if (!rc) {
                 ae = hipMemcpyAsync(s.hstat, s.dstat, (size_t)j.nb * 4, hipMemcpyDeviceToHost, s.st);
                 if (ae != hipSuccess) return bail(hip_fail(ae, "vector batch status"));
             }
         } else {
-            rc = encode_device(c, &db, s.st);
+            rc = split_full_runs(num_data ? num_data + b0 : nullptr, j.nb, c->k, [&](uint32_t o, uint32_t n, bool nd) {
+                nfec_block_batch sb = db;
+                sb.blocks = s.dev + o * dbs;
+                sb.nblocks = n;
+                sb.num_data = nd ? dnd + o : nullptr;
+                return encode_device(c, &sb, s.st);
+            });
         }
         if (rc) return bail(rc);
         // unshortened encode: only the parity region of each block comes back

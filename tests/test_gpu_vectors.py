@@ -127,3 +127,49 @@ def test_vector_lists_reject_null_source():
         enc.encode_vectors_host(segs)
     with pytest.raises(N.NfecError):
         dec.decode_vectors_host(segs, np.zeros((1, 4), np.uint16), np.zeros(1, np.uint16))
+
+
+def test_mixed_full_and_short_blocks(orc):
+    """NORM batches are mostly full blocks with a short block ending each object.  Full runs
+    go to the fast (unshortened) kernels as sub-batches, the rest with their numData; every
+    byte and status must match the reference calls, for strided host batches and segment
+    lists, encode and decode."""
+    k, m, vec, nb = 64, 32, 1400, 200
+    rng = np.random.default_rng(31)
+    nd = np.full(nb, k, np.uint16)
+    nd[39::40] = [7, 63, 1, 40, 20]
+    nd[100:103] = 5          # a cluster of short blocks
+    nd[150:170:3] = 60       # full runs shorter than the split threshold
+    host = orc.make_blocks(k, m, vec, nb, num_data=nd)
+    ref = orc.encode_blocks(N.NFEC_RS8, k, m, vec, host.copy(), nd)
+    enc, dec = _codecs(N.NFEC_RS8, k, m, vec)
+    hb = host.copy()
+    enc.encode_blocks_host(hb, num_data=nd)
+    assert np.array_equal(hb, ref)
+    segs = _scatter(host, vec, nd, m, rng)
+    enc.encode_vectors_host(segs, num_data=nd)
+    for b in range(nb):
+        for s in range(int(nd[b]) + m):
+            assert np.array_equal(segs[b][s][:vec], ref[b, s, :vec]), (b, s)
+
+    locs = np.zeros((nb, m), np.uint16)
+    counts = np.zeros(nb, np.uint16)
+    rx = ref.copy()
+    for b in range(nb):
+        es = min(16, int(nd[b]))
+        e = np.sort(rng.choice(int(nd[b]), es, replace=False)).astype(np.uint16)
+        locs[b, :es] = e
+        counts[b] = es
+        for s in e:
+            rx[b, s] = 0
+    want = rx.copy()
+    st_ref = orc.decode_blocks(N.NFEC_RS8, k, m, vec, want, locs, counts, nd)
+    hb = rx.copy()
+    st = dec.decode_blocks_host(hb, locs, counts, num_data=nd)
+    assert np.array_equal(st, st_ref) and np.array_equal(hb, want)
+    segs = _scatter(rx, vec, nd, m, rng)
+    st = dec.decode_vectors_host(segs, locs, counts, num_data=nd)
+    assert np.array_equal(st, st_ref)
+    for b in range(nb):
+        for s in range(int(nd[b])):
+            assert np.array_equal(segs[b][s][:vec], want[b, s, :vec]), (b, s)
