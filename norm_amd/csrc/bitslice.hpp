@@ -145,6 +145,8 @@ struct DecArgs {
     uint64_t z_block_stride = 0;
     uint32_t z_stride = 0;
     uint32_t xcd_remap = 0;
+    const uint32_t* gate = nullptr;   // non-null: skip the launch unless *gate == gate_gen
+    uint32_t gate_gen = 0;            // (RsPlan2Args::gate)
 };
 
 // Workgroup -> work index.  The dispatcher deals workgroups round-robin over the 8 XCDs

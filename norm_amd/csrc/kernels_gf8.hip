@@ -258,6 +258,7 @@ __global__ __launch_bounds__(kThreads) void gf8_solve_kernel(Gf8SolveArgs a)
     __shared__ uint32_t lds_t1[kWavesPerGroup][kMaxCols * RC + LA];
     const uint32_t lane = threadIdx.x & (kWave - 1);
     const uint32_t w = threadIdx.x >> 6;
+    if (a.gate && *a.gate != a.gate_gen) return;  // every block repaired by the fused kernel
     const uint32_t blk = uni(blockIdx.x * kWavesPerGroup + w);
     if (blk >= a.nblocks) return;
     const int32_t rows = (int32_t)uni((uint32_t)a.rows[blk]);

@@ -419,6 +419,9 @@ __global__ __launch_bounds__(64) void rs_plan2_kernel(RsPlan2Args a)
         emask[1] = (uint32_t)(em >> 32);
         psel[0] = (uint32_t)pused;
         psel[1] = (uint32_t)(pused >> 32);
+        // a block the fused repair kernel will not take (it takes 1..16 source erasures
+        // repaired from parity rows 0..e-1) opens this call's gate for the unfused kernels
+        if (a.gate && e > 0 && (e > 16 || pused != ((1ull << e) - 1ull))) a.gate[0] = a.gate_gen;
     }
     if (e == 0) return;
     if (used) {

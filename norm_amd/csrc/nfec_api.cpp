@@ -144,7 +144,8 @@ struct nfec_codec {
     DevBuf<int32_t> w_status, w_rows;
     DevBuf<uint16_t> w_islots, w_oslots, w_cols;
     DevBuf<uint8_t> w_coef1, w_coef2, w_z, w_work, w_pmap;
-    DevBuf<uint32_t> w_emask, w_psel;
+    DevBuf<uint32_t> w_emask, w_psel, w_gate;
+    uint32_t gate_gen = 0;         // per-pass generation written into w_gate (RsPlan2Args)
     // per-call staging
     DevBuf<uint8_t> s_block;
     DevBuf<uint16_t> s_locs;
@@ -164,6 +165,7 @@ struct nfec_codec {
         w_pmap.release();
         w_emask.release();
         w_psel.release();
+        w_gate.release();
         w_status.release();
         w_rows.release();
         w_islots.release();
@@ -518,6 +520,7 @@ int decode_device(nfec_codec* c, const nfec_block_batch* b, const uint16_t* locs
         if ((rc = c->w_emask.reserve((size_t)sb * 2))) return rc;
         if ((rc = c->w_psel.reserve((size_t)sb * 2))) return rc;
         if ((rc = c->w_pmap.reserve((size_t)sb * c->m))) return rc;
+        if ((rc = c->w_gate.reserve(1))) return rc;
     }
     for (uint32_t b0 = 0; b0 < b->nblocks; b0 += sb) {
         const uint32_t nb = std::min(sb, b->nblocks - b0);
@@ -589,13 +592,21 @@ int decode_device(nfec_codec* c, const nfec_block_batch* b, const uint16_t* locs
             p2.pmap = c->w_pmap.p;
             p2.coef_stride = dcs;
             p2.coef2 = c->w_coef2.p;
-            if ((rc = launch_rs_plan2(p2, s))) return rc;
             // fused per-block repair for the blocks it qualifies for (NFEC_FUSED=0: off); the
             // unfused stage 1 and solve below skip the blocks it marked
             static const bool use_fused = [] {
                 const char* e = std::getenv("NFEC_FUSED");
                 return !(e && e[0] == '0');
             }();
+            // gate: the plan writes this pass's generation into w_gate when some block needs the
+            // unfused kernels; when the fused kernel ran they skip their whole launch otherwise
+            const uint32_t gen = ++c->gate_gen;
+            if (use_fused) {
+                p2.gate = c->w_gate.p;
+                p2.gate_gen = gen;
+            }
+            if ((rc = launch_rs_plan2(p2, s))) return rc;
+            const uint32_t* gate = nullptr;
             if (use_fused) {
                 FdecArgs f;
                 f.base = blocks;
@@ -615,6 +626,7 @@ int decode_device(nfec_codec* c, const nfec_block_batch* b, const uint16_t* locs
                 f.accumulate = acc;
                 rc = launch_rs8_fused_decode(c->k, c->m, f, s);
                 if (rc != NFEC_OK && rc != NFEC_ENOTSUP) return fail(rc, "fused decode launch failed");
+                if (rc == NFEC_OK) gate = c->w_gate.p;
             }
             bs::DecArgs d;
             d.base = blocks;
@@ -629,6 +641,8 @@ int decode_device(nfec_codec* c, const nfec_block_batch* b, const uint16_t* locs
             d.z_block_stride = (uint64_t)dcs * zstride;
             d.z_stride = zstride;
             d.xcd_remap = bs_flags() & 1u;
+            d.gate = gate;
+            d.gate_gen = gen;
             if ((rc = launch_rs8_bitsliced_reencode(c->k, c->m, d, s))) return fail(rc, "bit-sliced re-encode launch failed");
             static const bool use_solve = [] {
                 const char* e = std::getenv("NFEC_SOLVE");
@@ -675,6 +689,8 @@ int decode_device(nfec_codec* c, const nfec_block_batch* b, const uint16_t* locs
             a2.nblocks = nb;
             a2.vec_bytes = c->vec;
             a2.accumulate = acc;
+            a2.gate = gate;
+            a2.gate_gen = gen;
             // bit-sliced snippet-table solve for blocks with <= 16 erasures (NFEC_SOLVE_BS=0: off),
             // the v_perm kernel for the rest
             static const bool use_bs = [] {

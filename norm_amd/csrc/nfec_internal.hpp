@@ -118,6 +118,8 @@ struct Gf8SolveArgs {
     uint32_t vec_bytes = 0;
     uint32_t accumulate = 0;
     int32_t min_rows = 0;                // skip blocks with rows <= min_rows (done by another kernel)
+    const uint32_t* gate = nullptr;      // non-null: skip the launch unless *gate == gate_gen
+    uint32_t gate_gen = 0;
 };
 int launch_gf8_solve(const Gf8SolveArgs& a, uint32_t max_rows, uint32_t max_cols, hipStream_t s);
 // gen_solve_asm.hip: bit-sliced solve for blocks with rows <= 16 (NFEC_ENOTSUP: other shapes)
@@ -230,6 +232,11 @@ struct RsPlan2Args {
     uint8_t* pmap = nullptr;            // [b][m]: index t of parity row p in P
     uint32_t coef_stride = 0;
     uint8_t* coef2 = nullptr;           // [b][cs][cs]: Ainv column-major ([t][s])
+    // gate word: set to gate_gen when some block needs the unfused stage 1 + solve (one the
+    // fused kernel does not take); those kernels skip their whole launch unless *gate == gate_gen.
+    // The generation changes per call, so the word never needs clearing.
+    uint32_t* gate = nullptr;
+    uint32_t gate_gen = 0;
 };
 int launch_rs_plan2(const RsPlan2Args& a, hipStream_t s);
 

@@ -277,6 +277,8 @@ def gen_dec_kernel(k, m, cfg):
     groups = 4
     K = f"rs8_dec{cfg.suffix}_k{k}_m{m}"
     body = [f"__global__ {kernel_attrs(cfg)} void {K}(bs::DecArgs a)", "{"]
+    # every block already repaired by the fused kernel: nothing to re-encode
+    body.append("    if (a.gate && *a.gate != a.gate_gen) return;")
     body.append("    const uint32_t lane = threadIdx.x & 63;")
     body.append("    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);")
     body.append(f"    const uint64_t group = (uint64_t)bs::wg_index(a.xcd_remap) * {groups} + wave;")

@@ -227,6 +227,7 @@ namespace {{
 
 __global__ __launch_bounds__(256, 2) void gf8_solve_bs_kernel(Gf8SolveArgs a, uint32_t ips)
 {{
+    if (a.gate && *a.gate != a.gate_gen) return;  // every block repaired by the fused kernel
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t blk = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
     if (blk >= a.nblocks) return;
