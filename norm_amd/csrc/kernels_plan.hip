@@ -438,16 +438,19 @@ __global__ __launch_bounds__(64) void rs_plan2_kernel(RsPlan2Args a)
     // per-s: lA[s] = lWp(x_s) + lPP(s) - lQp(s);  per-t: lB[t] = lQ(t) - lW(t) - lD(t)
     if (lane < e) {
         const uint32_t x = xs[lane];
-        int32_t acc = (int32_t)a.lwp[sE[lane]];
-        for (uint32_t t = 0; t < e; ++t) acc += lg[x ^ yt[t]];
-        for (uint32_t s2 = 0; s2 < e; ++s2)
-            if (s2 != lane) acc -= lg[x ^ xs[s2]];
-        lA[lane] = acc;
+        // unrolled so the (uniform-address) point reads and the table reads they feed are
+        // issued in batches instead of one dependent LDS round trip per term; the s2 == lane
+        // and t2 == lane terms are lg[0] (x ^ x), subtracted back out instead of branched on
         const uint32_t y = yt[lane];
-        int32_t bcc = -(int32_t)a.lw[sP[lane]];
-        for (uint32_t s2 = 0; s2 < e; ++s2) bcc += lg[y ^ xs[s2]];
-        for (uint32_t t2 = 0; t2 < e; ++t2)
-            if (t2 != lane) bcc -= lg[y ^ yt[t2]];
+        int32_t acc = (int32_t)a.lwp[sE[lane]], bcc = -(int32_t)a.lw[sP[lane]];
+#pragma unroll 8
+        for (uint32_t t = 0; t < e; ++t) {
+            acc += (int32_t)lg[x ^ yt[t]] - (int32_t)lg[x ^ xs[t]];
+            bcc += (int32_t)lg[y ^ xs[t]] - (int32_t)lg[y ^ yt[t]];
+        }
+        acc += (int32_t)lg[0];
+        bcc += (int32_t)lg[0];
+        lA[lane] = acc;
         lB[lane] = bcc;
     }
     __syncthreads();
