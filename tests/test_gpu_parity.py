@@ -373,3 +373,43 @@ def test_fused_decode_mixed_batch(orc, m, accumulate):
     torch.cuda.synchronize()
     assert np.array_equal(st.cpu().numpy(), st_ref)
     assert np.array_equal(dev.cpu().numpy(), expect)
+
+
+@pytest.mark.parametrize("m", [32, 8])
+def test_unfused_gate_across_calls(orc, m):
+    """The unfused stage 1 + solve run only when the plan opened this call's gate word (some
+    block the fused kernel does not take).  One decoder, three calls in a row: a batch with
+    unfused blocks, an all-fused batch (the word still holds the first call's generation),
+    then a batch whose only unfused block is the last one."""
+    k, vec, nb = 64, 1400, 40
+    enc, dec = _codecs(NFEC_RS8, k, m, vec)
+    clean = orc.encode_blocks(NFEC_RS8, k, m, vec, orc.make_blocks(k, m, vec, nb))
+    rng = np.random.default_rng(5)
+
+    def run(unfused):
+        locs = np.zeros((nb, m), np.uint16)
+        counts = np.zeros(nb, np.uint16)
+        for b in range(nb):
+            es = 1 + b % min(8, m - 1)
+            src = np.sort(rng.choice(k, es, replace=False))
+            # losing parity row 0 sends the block to the unfused kernels
+            par = np.array([k], int) if b in unfused else np.array([], int)
+            e = np.concatenate([src, par]).astype(np.uint16)
+            locs[b, :len(e)] = e
+            counts[b] = len(e)
+        rx = clean.copy()
+        for b in range(nb):
+            rx[b, locs[b, :counts[b]]] = 0
+        ref = rx.copy()
+        st_ref = orc.decode_blocks(NFEC_RS8, k, m, vec, ref, locs, counts)
+        dev = torch.from_numpy(rx).cuda()
+        st = dec.decode_blocks(dev, torch.from_numpy(locs.astype(np.int16)).cuda(),
+                               torch.from_numpy(counts.astype(np.int16)).cuda())
+        torch.cuda.synchronize()
+        assert np.array_equal(st.cpu().numpy(), st_ref)
+        assert np.array_equal(dev.cpu().numpy(), ref)
+        assert np.array_equal(dev.cpu().numpy()[:, :k], clean[:, :k])
+
+    run({0, 7, 19})
+    run(set())
+    run({nb - 1})
