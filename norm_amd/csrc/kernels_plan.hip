@@ -357,39 +357,34 @@ __global__ __launch_bounds__(64) void rs_plan2_kernel(RsPlan2Args a)
     __shared__ uint8_t xs[64], yt[64];             // points of E and P
     __shared__ uint16_t sP[64], sE[64];
     __shared__ int32_t lA[64], lB[64];             // per-s and per-t log factors
+    __shared__ uint8_t ers[256];                   // erased-slot flags (k + m <= 255)
     const uint32_t lane = threadIdx.x;
     const uint32_t b = blockIdx.x;
-    for (uint32_t i = lane; i < 510; i += 64) ex[i] = a.exp_tab[i];
-    for (uint32_t i = lane; i < 256; i += 64) lg[i] = a.log_tab[i];
-    __syncthreads();
-
     const uint32_t k = a.k, m = a.m;
+    // the erasure list is fetched first so its two dependent loads overlap the table staging
     const uint32_t ec = uni(a.erasure_counts[b]);
     const uint16_t* locs = a.erasure_locs + (uint64_t)b * a.erasure_stride;
-    bool ok = ec <= m && ec <= a.erasure_stride;
+    bool ok = ec <= m && ec <= a.erasure_stride;   // then ec <= 64: one entry per lane
+    const uint32_t myl = (ok && lane < ec) ? (uint32_t)locs[lane] : 0u;
+    for (uint32_t i = lane; i < 510; i += 64) ex[i] = a.exp_tab[i];
+    for (uint32_t i = lane; i < 256; i += 64) lg[i] = a.log_tab[i];
+    for (uint32_t i = lane; i < 256; i += 64) ers[i] = 0;
     uint32_t es = 0;
-    // lane-parallel validation: sorted, in range; count source erasures
+    // lane-parallel validation: sorted, in range; count source erasures (sorted list => the
+    // source entries are a prefix); a valid list marks its slots in ers
     if (ok) {
-        bool bad = false;
-        uint32_t nsrc = 0;
-        for (uint32_t i = lane; i < ec; i += 64) {
-            const uint32_t l = locs[i];
-            if (l >= k + m || (i > 0 && l <= locs[i - 1])) bad = true;
-            if (l < k) ++nsrc;
-        }
-        bad = __any(bad);
-        // es = number of entries < k (sorted list => prefix)
-        for (int off = 32; off > 0; off >>= 1) nsrc += __shfl_xor(nsrc, off);
-        ok = !bad;
-        es = nsrc;
+        const uint32_t prev = __shfl_up(myl, 1);
+        const bool bad = lane < ec && (myl >= k + m || (lane > 0 && myl <= prev));
+        es = (uint32_t)__popcll(__ballot(lane < ec && myl < k));
+        ok = !__any(bad);
     }
-    // surviving parity rows: lane p tests slot k+p against the parity erasures
+    __syncthreads();
+    if (ok && lane < ec) ers[myl] = 1;
+    __syncthreads();
+    // surviving parity rows: lane p tests slot k+p
     uint64_t surv = 0;
     if (ok) {
-        bool alive = lane < m;
-        for (uint32_t i = es; i < ec; ++i)
-            if (locs[i] == k + lane) alive = false;
-        surv = __ballot(alive);
+        surv = __ballot(lane < m && !ers[k + lane]);
         if ((uint32_t)__popcll(surv) < es) ok = false;
     }
     const uint32_t e = ok ? es : 0;
@@ -406,14 +401,8 @@ __global__ __launch_bounds__(64) void rs_plan2_kernel(RsPlan2Args a)
     const bool used = e > 0 && lane < m && ((surv >> lane) & 1ull) && rank < e;
     const uint64_t pused = __ballot(used);
     if (lane < m) a.pmap[(uint64_t)b * m + lane] = used ? (uint8_t)rank : (uint8_t)0xff;
-    uint64_t em = 0;
-    {
-        // erased-source bitmap (k <= 64 for the specialised kernels; others ignore it)
-        bool er = false;
-        for (uint32_t i = 0; i < e; ++i)
-            if (locs[i] == lane) er = true;
-        em = __ballot(er && lane < k);
-    }
+    // erased-source bitmap (k <= 64 for the specialised kernels; others ignore it)
+    const uint64_t em = e > 0 ? __ballot(lane < k && ers[lane]) : 0ull;
     if (lane == 0) {
         emask[0] = (uint32_t)em;
         emask[1] = (uint32_t)(em >> 32);
@@ -430,7 +419,7 @@ __global__ __launch_bounds__(64) void rs_plan2_kernel(RsPlan2Args a)
         yt[rank] = ex[(row - 1) % 255u];
     }
     if (lane < e) {
-        const uint32_t s = locs[lane];
+        const uint32_t s = myl;
         sE[lane] = (uint16_t)s;
         xs[lane] = s == 0 ? 0 : ex[(s - 1) % 255u];
     }
