@@ -212,10 +212,11 @@ __global__ __launch_bounds__(kWave) void mdp_plan_kernel(MdpPlanArgs a)
     __shared__ uint8_t ex[512];
     __shared__ uint16_t lg[256];
     __shared__ uint8_t lam[512];
-    extern __shared__ uint8_t lamb[];       // [erased row r][u < m]: prefix sums Lambda_u(beta_r)
+    extern __shared__ uint16_t llamb[];     // [erased row r][u < m]: log of prefix sums Lambda_u(beta_r)
+                                            // (0xffff: the sum is 0)
     __shared__ uint16_t surv[256];
     __shared__ uint16_t eras[256];
-    __shared__ uint8_t dinv_s[256], beta_s[256];
+    __shared__ uint8_t dinv_s[256], lbeta_s[256];
 
     const uint32_t lane = threadIdx.x;
     const uint32_t b = blockIdx.x;
@@ -287,12 +288,12 @@ __global__ __launch_bounds__(kWave) void mdp_plan_kernel(MdpPlanArgs a)
         uint32_t denom = 0;
         for (uint32_t j = 1; j < deg; j += 2) denom ^= mul(lam[j], ex[(lb * (j - 1)) % 255u]);
         dinv_s[r] = (uint8_t)(denom ? ex[255u - lg[denom]] : 1u);  // GINV[0] = 1 (galois.cpp:39)
-        beta_s[r] = (uint8_t)beta;
+        lbeta_s[r] = (uint8_t)lb;
         uint32_t acc = 0, bp = 1;
         for (uint32_t u = 0; u < m; ++u) {
             acc ^= mul(lam[u], bp);
             bp = mul(bp, beta);
-            lamb[r * m + u] = (uint8_t)acc;
+            llamb[r * m + u] = acc ? lg[acc] : (uint16_t)0xffff;
         }
     }
     __syncthreads();
@@ -303,13 +304,24 @@ __global__ __launch_bounds__(kWave) void mdp_plan_kernel(MdpPlanArgs a)
     for (uint32_t j = lane; j < ns; j += kWave) {
         const uint32_t v = surv[j];
         isl[j] = (uint16_t)v;
-        const uint32_t gamma = ex[nvecs - 1 - v];
+        const uint32_t lgamma = (nvecs - 1 - v) % 255u;
+        const uint32_t gamma = ex[lgamma];
         for (uint32_t r = 0; r < cs; ++r) {
             uint32_t val = 0;
             if (r < es) {
-                const uint32_t w = mul(gamma, beta_s[r]);
-                uint32_t h = lamb[r * m];
-                for (uint32_t u = 1; u < m; ++u) h = mul(h, w) ^ lamb[r * m + u];
+                // h = sum_u Lambda_u * w^(m-1-u), w = gamma * beta_r, as independent table
+                // terms in the log domain (a Horner chain would make every step wait on the
+                // previous product's table reads)
+                const uint32_t lw = (lgamma + lbeta_s[r]) % 255u;
+                uint32_t pw = ((m - 1) * lw) % 255u;
+                uint32_t h = 0;
+                const uint16_t* row = llamb + r * m;
+#pragma unroll 4
+                for (uint32_t u = 0; u < m; ++u) {
+                    const uint32_t ll = row[u];
+                    if (ll != 0xffffu) h ^= ex[ll + pw];
+                    pw = pw >= lw ? pw - lw : pw + 255u - lw;
+                }
                 val = mul(dinv_s[r], mul(gamma, h));
             }
             coef[(uint64_t)j * cs + r] = (uint8_t)val;
@@ -334,8 +346,8 @@ int launch_rs_plan(const RsPlanArgs& a, hipStream_t s)
 int launch_mdp_plan(const MdpPlanArgs& a, hipStream_t s)
 {
     if (a.nblocks == 0) return NFEC_OK;
-    // erased source rows are at most min(k, m); k + m <= 255 keeps this under 16 KiB
-    const size_t lds = (size_t)std::min(a.k, a.m) * a.m;
+    // erased source rows are at most min(k, m); k + m <= 255 keeps this under 32 KiB
+    const size_t lds = (size_t)std::min(a.k, a.m) * a.m * sizeof(uint16_t);
     hipLaunchKernelGGL(mdp_plan_kernel, dim3(a.nblocks), dim3(kWave), lds, s, a);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return hip_fail(e, "mdp_plan launch");
