@@ -212,32 +212,46 @@ __global__ __launch_bounds__(kWave) void mdp_plan_kernel(MdpPlanArgs a)
     __shared__ uint8_t ex[512];
     __shared__ uint16_t lg[256];
     __shared__ uint8_t lam[512];
-    extern __shared__ uint16_t llamb[];     // [erased row r][u < m]: log of prefix sums Lambda_u(beta_r)
-                                            // (0xffff: the sum is 0)
-    __shared__ uint16_t surv[256];
-    __shared__ uint16_t eras[256];
+    extern __shared__ uint8_t llamb[];      // [erased row r][u < m]: log of prefix sums Lambda_u(beta_r)
+                                            // (0xff: the sum is 0; logs are < 255)
+    // byte-wide: slots, logs and flags are all < 255 (k + m <= 255), and the smaller LDS
+    // footprint keeps more of these latency-bound waves resident
+    __shared__ uint8_t surv[256];
+    __shared__ uint8_t eras[256];
     __shared__ uint8_t dinv_s[256], lbeta_s[256];
+    __shared__ uint8_t ers[256];            // erased-slot flags (nvecs <= 255)
+    __shared__ uint8_t loc_s[256];          // the block's erasure list (ec <= m < 255)
+    __shared__ uint8_t llam[512];           // log lambda_j (0xff: lambda_j = 0)
 
     const uint32_t lane = threadIdx.x;
     const uint32_t b = blockIdx.x;
-    for (uint32_t i = lane; i < 510; i += kWave) ex[i] = a.exp_tab[i];
-    for (uint32_t i = lane; i < 256; i += kWave) lg[i] = a.log_tab[i];
-    __syncthreads();
-    auto mul = [&](uint32_t x, uint32_t y) -> uint32_t { return (x && y) ? ex[lg[x] + lg[y]] : 0u; };
-
     const uint32_t m = a.m;
+    // the erasure list is fetched first so its dependent loads overlap the table staging
     const uint32_t nd = a.num_data ? uni(a.num_data[b]) : a.k;
     const uint32_t ec = uni(a.erasure_counts[b]);
     const uint16_t* locs = a.erasure_locs + (uint64_t)b * a.erasure_stride;
     const uint32_t nvecs = nd + m;
     bool ok = nd >= 1 && nd <= a.k && ec <= m && ec <= a.erasure_stride;
+    for (uint32_t i = lane; i < 510; i += kWave) ex[i] = a.exp_tab[i];
+    for (uint32_t i = lane; i < 256; i += kWave) lg[i] = a.log_tab[i];
+    for (uint32_t i = lane; i < 256; i += kWave) ers[i] = 0;
+    auto mul = [&](uint32_t x, uint32_t y) -> uint32_t { return (x && y) ? ex[lg[x] + lg[y]] : 0u; };
+    // lane-parallel validation (sorted, in range) and source-erasure count (a prefix)
     uint32_t es = 0;
-    if (ok)
-        for (uint32_t i = 0; i < ec; ++i) {
+    if (ok) {
+        bool bad = false;
+        uint32_t nsrc = 0;
+        for (uint32_t i = lane; i < ec; i += kWave) {
             const uint32_t l = locs[i];
-            if (l >= nvecs || (i > 0 && l <= locs[i - 1])) ok = false;
-            if (l < nd) ++es;
+            if (l >= nvecs || (i > 0 && l <= locs[i - 1])) bad = true;
+            if (l < nd) ++nsrc;
+            loc_s[i] = (uint8_t)l;
         }
+        for (int off = 32; off > 0; off >>= 1) nsrc += __shfl_xor(nsrc, off);
+        ok = !__any(bad);
+        es = uni(nsrc);
+    }
+    __syncthreads();
     if (!ok) {
         if (lane == 0) {
             if (a.status) a.status[b] = 0;
@@ -259,7 +273,7 @@ __global__ __launch_bounds__(kWave) void mdp_plan_kernel(MdpPlanArgs a)
     for (uint32_t j = lane; j < deg; j += kWave) lam[j] = (j == 0);
     __syncthreads();
     for (uint32_t i = 0; i < ec; ++i) {
-        const uint32_t X = ex[nvecs - 1 - locs[i]];
+        const uint32_t X = ex[nvecs - 1 - loc_s[i]];
         uint8_t nv[8];
         uint32_t n = 0;
         for (uint32_t j = lane; j < deg; j += kWave) nv[n++] = (uint8_t)(j ? (lam[j] ^ mul(X, lam[j - 1])) : lam[0]);
@@ -268,32 +282,45 @@ __global__ __launch_bounds__(kWave) void mdp_plan_kernel(MdpPlanArgs a)
         for (uint32_t j = lane; j < deg; j += kWave) lam[j] = nv[n++];
         __syncthreads();
     }
-    // surviving slots, erased source rows
-    if (lane == 0) {
-        uint32_t nxt = 0, ns = 0;
-        for (uint32_t v = 0; v < nvecs; ++v) {
-            if (nxt < ec && locs[nxt] == v) { ++nxt; continue; }
-            surv[ns++] = (uint16_t)v;
-        }
-        for (uint32_t i = 0; i < es; ++i) eras[i] = locs[i];
-        a.cols[b] = (uint16_t)ns;
+    for (uint32_t j = lane; j < deg; j += kWave) llam[j] = lam[j] ? (uint8_t)lg[lam[j]] : (uint8_t)0xff;
+    // surviving slots (ballot compaction over erased-slot flags), erased source rows
+    for (uint32_t i = lane; i < ec; i += kWave) {
+        const uint32_t l = loc_s[i];
+        ers[l] = 1;
+        if (i < es) eras[i] = (uint8_t)l;
     }
     __syncthreads();
     const uint32_t ns = nvecs - ec;
-    // per erased row r: beta, Forney denominator, Lambda prefix sums
+    for (uint32_t v0 = 0, base = 0; v0 < nvecs; v0 += kWave) {
+        const uint32_t v = v0 + lane;
+        const bool alive = v < nvecs && !ers[v];
+        const uint64_t bal = __ballot(alive);
+        if (alive) surv[base + (uint32_t)__popcll(bal & ((1ull << lane) - 1ull))] = (uint8_t)v;
+        base += (uint32_t)__popcll(bal);
+    }
+    if (lane == 0) a.cols[b] = (uint16_t)ns;
+    __syncthreads();
+    // per erased row r: beta, Forney denominator, Lambda prefix sums.  Products with powers of
+    // beta are log-domain table terms (exponents stepped in registers), independent of each
+    // other instead of a chain through the running power.
     for (uint32_t r = lane; r < es; r += kWave) {
         const uint32_t kk = nvecs - 1 - eras[r];
         const uint32_t lb = (255u - kk) % 255u;  // log beta
-        const uint32_t beta = ex[lb];
-        uint32_t denom = 0;
-        for (uint32_t j = 1; j < deg; j += 2) denom ^= mul(lam[j], ex[(lb * (j - 1)) % 255u]);
+        const uint32_t l2 = (2u * lb) % 255u;
+        uint32_t denom = 0, pj = 0;  // pj = lb * (j - 1) mod 255
+        for (uint32_t j = 1; j < deg; j += 2) {
+            const uint32_t ll = llam[j];
+            if (ll != 0xffu) denom ^= ex[ll + pj];
+            pj = pj + l2 >= 255u ? pj + l2 - 255u : pj + l2;
+        }
         dinv_s[r] = (uint8_t)(denom ? ex[255u - lg[denom]] : 1u);  // GINV[0] = 1 (galois.cpp:39)
         lbeta_s[r] = (uint8_t)lb;
-        uint32_t acc = 0, bp = 1;
+        uint32_t acc = 0, pu = 0;  // pu = lb * u mod 255
         for (uint32_t u = 0; u < m; ++u) {
-            acc ^= mul(lam[u], bp);
-            bp = mul(bp, beta);
-            llamb[r * m + u] = acc ? lg[acc] : (uint16_t)0xffff;
+            const uint32_t ll = llam[u];
+            if (ll != 0xffu) acc ^= ex[ll + pu];
+            pu = pu + lb >= 255u ? pu + lb - 255u : pu + lb;
+            llamb[r * m + u] = acc ? (uint8_t)lg[acc] : (uint8_t)0xff;
         }
     }
     __syncthreads();
@@ -315,11 +342,11 @@ __global__ __launch_bounds__(kWave) void mdp_plan_kernel(MdpPlanArgs a)
                 const uint32_t lw = (lgamma + lbeta_s[r]) % 255u;
                 uint32_t pw = ((m - 1) * lw) % 255u;
                 uint32_t h = 0;
-                const uint16_t* row = llamb + r * m;
+                const uint8_t* row = llamb + r * m;
 #pragma unroll 4
                 for (uint32_t u = 0; u < m; ++u) {
                     const uint32_t ll = row[u];
-                    if (ll != 0xffffu) h ^= ex[ll + pw];
+                    if (ll != 0xffu) h ^= ex[ll + pw];
                     pw = pw >= lw ? pw - lw : pw + 255u - lw;
                 }
                 val = mul(dinv_s[r], mul(gamma, h));
@@ -346,8 +373,8 @@ int launch_rs_plan(const RsPlanArgs& a, hipStream_t s)
 int launch_mdp_plan(const MdpPlanArgs& a, hipStream_t s)
 {
     if (a.nblocks == 0) return NFEC_OK;
-    // erased source rows are at most min(k, m); k + m <= 255 keeps this under 32 KiB
-    const size_t lds = (size_t)std::min(a.k, a.m) * a.m * sizeof(uint16_t);
+    // erased source rows are at most min(k, m); k + m <= 255 keeps this under 16 KiB
+    const size_t lds = (size_t)std::min(a.k, a.m) * a.m;
     hipLaunchKernelGGL(mdp_plan_kernel, dim3(a.nblocks), dim3(kWave), lds, s, a);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return hip_fail(e, "mdp_plan launch");
