@@ -329,30 +329,28 @@ __global__ __launch_bounds__(kWave) void mdp_plan_kernel(MdpPlanArgs a)
     uint8_t* coef = a.coef + (uint64_t)b * (a.k + a.m) * cs;
     uint16_t* isl = a.in_slots + (uint64_t)b * (a.k + a.m);
     for (uint32_t j = lane; j < ns; j += kWave) {
-        const uint32_t v = surv[j];
-        isl[j] = (uint16_t)v;
-        const uint32_t lgamma = (nvecs - 1 - v) % 255u;
-        const uint32_t gamma = ex[lgamma];
-        for (uint32_t r = 0; r < cs; ++r) {
-            uint32_t val = 0;
-            if (r < es) {
-                // h = sum_u Lambda_u * w^(m-1-u), w = gamma * beta_r, as independent table
-                // terms in the log domain (a Horner chain would make every step wait on the
-                // previous product's table reads)
-                const uint32_t lw = (lgamma + lbeta_s[r]) % 255u;
-                uint32_t pw = ((m - 1) * lw) % 255u;
-                uint32_t h = 0;
-                const uint8_t* row = llamb + r * m;
+        isl[j] = surv[j];
+        for (uint32_t r = es; r < cs; ++r) coef[(uint64_t)j * cs + r] = 0;  // padding rows
+    }
+    // one (r, slot) pair per lane, r-major: every lane is busy (ns is rarely a multiple of
+    // 64) and a wave's lanes share r, so the Lambda row reads are broadcasts
+    for (uint32_t idx = lane; idx < es * ns; idx += kWave) {
+        const uint32_t r = idx / ns, j = idx - r * ns;
+        const uint32_t lgamma = (nvecs - 1 - surv[j]) % 255u;
+        // h = sum_u Lambda_u * w^(m-1-u), w = gamma * beta_r, as independent table terms in
+        // the log domain (a Horner chain would make every step wait on the previous
+        // product's table reads)
+        const uint32_t lw = (lgamma + lbeta_s[r]) % 255u;
+        uint32_t pw = ((m - 1) * lw) % 255u;
+        uint32_t h = 0;
+        const uint8_t* row = llamb + r * m;
 #pragma unroll 4
-                for (uint32_t u = 0; u < m; ++u) {
-                    const uint32_t ll = row[u];
-                    if (ll != 0xffu) h ^= ex[ll + pw];
-                    pw = pw >= lw ? pw - lw : pw + 255u - lw;
-                }
-                val = mul(dinv_s[r], mul(gamma, h));
-            }
-            coef[(uint64_t)j * cs + r] = (uint8_t)val;
+        for (uint32_t u = 0; u < m; ++u) {
+            const uint32_t ll = row[u];
+            if (ll != 0xffu) h ^= ex[ll + pw];
+            pw = pw >= lw ? pw - lw : pw + 255u - lw;
         }
+        coef[(uint64_t)j * cs + r] = (uint8_t)mul(dinv_s[r], mul(ex[lgamma], h));
     }
     uint16_t* osl = a.out_slots + (uint64_t)b * (a.k + a.m);
     for (uint32_t r = lane; r < es; r += kWave) osl[r] = eras[r];
