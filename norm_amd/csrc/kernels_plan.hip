@@ -26,6 +26,7 @@ namespace {
 
 constexpr int kWave = 64;
 constexpr uint32_t kPlanLdsMaxE = 64;
+constexpr uint32_t kPlanLrowMaxE = 256;  // log-domain elimination up to this e
 
 __device__ __forceinline__ uint32_t uni(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
 
@@ -52,6 +53,7 @@ __global__ __launch_bounds__(kWave) void rs_plan_kernel(RsPlanArgs a)
     __shared__ E lds_fac[256];
     __shared__ uint8_t lds_exp8[512];
     __shared__ uint16_t lds_log8[256];
+    __shared__ uint16_t lds_lrow[2 * kPlanLrowMaxE];  // log of the normalised pivot row (q: zero)
 
     const uint32_t lane = threadIdx.x;
     const uint32_t b = blockIdx.x;
@@ -170,19 +172,44 @@ __global__ __launch_bounds__(kWave) void rs_plan_kernel(RsPlanArgs a)
             }
             __syncthreads();
         }
-        const uint32_t pinv = f.inv(work[j * w2 + j]);
-        for (uint32_t col = lane; col < w2; col += kWave) work[j * w2 + col] = (E)f.mul(pinv, work[j * w2 + col]);
-        __syncthreads();
-        // snapshot column j (the elimination factors) before any row is updated
-        for (uint32_t r = lane; r < e; r += kWave) fac[r] = work[r * w2 + j];
-        __syncthreads();
-        for (uint32_t idx = lane; idx < e * w2; idx += kWave) {
-            const uint32_t r = idx / w2, col = idx % w2;
-            if (r == j) continue;
-            const uint32_t factor = fac[r];
-            if (factor) work[idx] ^= (E)f.mul(factor, work[j * w2 + col]);
+        if (e <= kPlanLrowMaxE) {
+            // log domain: the normalised pivot row and the factors are turned into logs once
+            // per pivot, so each eliminated entry costs one exp-table read instead of two log
+            // reads and an exp read (for GF(2^16) these are L2 gathers)
+            const uint32_t q = f.q;
+            const uint32_t lpinv = (q - (uint32_t)f.log[work[j * w2 + j]]) % q;
+            for (uint32_t col = lane; col < w2; col += kWave) {
+                const uint32_t v = work[j * w2 + col];
+                const uint32_t lv = v ? ((uint32_t)f.log[v] + lpinv) % q : q;
+                lds_lrow[col] = (uint16_t)lv;
+                work[j * w2 + col] = v ? f.exp[lv] : (E)0;
+            }
+            // factors: column j of the other rows (not touched by the normalisation)
+            for (uint32_t r = lane; r < e; r += kWave)
+                if (r != j) fac[r] = (E)f.log[work[r * w2 + j]];  // log 0 = q: no update
+            __syncthreads();
+            for (uint32_t idx = lane; idx < e * w2; idx += kWave) {
+                const uint32_t r = idx / w2, col = idx % w2;
+                if (r == j) continue;
+                const uint32_t lf = fac[r], lc = lds_lrow[col];
+                if (lf != q && lc != q) work[idx] ^= f.exp[lf + lc];
+            }
+            __syncthreads();
+        } else {
+            const uint32_t pinv = f.inv(work[j * w2 + j]);
+            for (uint32_t col = lane; col < w2; col += kWave) work[j * w2 + col] = (E)f.mul(pinv, work[j * w2 + col]);
+            __syncthreads();
+            // snapshot column j (the elimination factors) before any row is updated
+            for (uint32_t r = lane; r < e; r += kWave) fac[r] = work[r * w2 + j];
+            __syncthreads();
+            for (uint32_t idx = lane; idx < e * w2; idx += kWave) {
+                const uint32_t r = idx / w2, col = idx % w2;
+                if (r == j) continue;
+                const uint32_t factor = fac[r];
+                if (factor) work[idx] ^= (E)f.mul(factor, work[j * w2 + col]);
+            }
+            __syncthreads();
         }
-        __syncthreads();
     }
     if (singular) {
         if (lane == 0) {
