@@ -124,10 +124,17 @@ __global__ __launch_bounds__(kWave) void rs_plan_kernel(RsPlanArgs a)
     E* coef1 = reinterpret_cast<E*>(a.coef1) + (uint64_t)b * k * cs;
     uint16_t* islots = a.in_slots1 + (uint64_t)b * k;
     for (uint32_t c = lane; c < nd; c += kWave) {
-        // is c erased? (E sorted)
+        // is c erased? (E sorted: binary search)
         int32_t s_idx = -1;
-        for (uint32_t i = 0; i < e; ++i)
-            if (listE[i] == c) s_idx = (int32_t)i;
+        {
+            uint32_t lo = 0, hi = e;  // first index with listE[i] >= c
+            while (lo < hi) {
+                const uint32_t mid = (lo + hi) >> 1;
+                if (listE[mid] < c) lo = mid + 1;
+                else hi = mid;
+            }
+            if (lo < e && listE[lo] == c) s_idx = (int32_t)lo;
+        }
         islots[c] = s_idx >= 0 ? listP[s_idx] : (uint16_t)c;
         for (uint32_t t = 0; t < cs; ++t) {
             E v = 0;
