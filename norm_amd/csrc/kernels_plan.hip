@@ -421,25 +421,48 @@ int launch_mdp_plan(const MdpPlanArgs& a, hipStream_t s)
 namespace nfec {
 namespace {
 
-__global__ __launch_bounds__(64) void rs_plan2_kernel(RsPlan2Args a)
+// Intra-wave LDS hand-off: every block is one wave's, so after the shared tables are staged
+// no workgroup barrier is needed; this orders the wave's LDS writes before its later reads
+// (and keeps the compiler from moving them across).
+__device__ __forceinline__ void wave_lds_sync()
+{
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+constexpr uint32_t kPlan2Waves = 4;  // blocks per workgroup, one wave each: they share the tables
+
+__global__ __launch_bounds__(64 * kPlan2Waves) void rs_plan2_kernel(RsPlan2Args a)
 {
     __shared__ uint8_t ex[512];
     __shared__ uint16_t lg[256];
-    __shared__ uint8_t xs[64], yt[64];             // points of E and P
-    __shared__ uint16_t sP[64], sE[64];
-    __shared__ int32_t lA[64], lB[64];             // per-s and per-t log factors
-    __shared__ uint8_t ers[256];                   // erased-slot flags (k + m <= 255)
-    const uint32_t lane = threadIdx.x;
-    const uint32_t b = blockIdx.x;
+    __shared__ uint8_t xs_w[kPlan2Waves][64], yt_w[kPlan2Waves][64];   // points of E and P
+    __shared__ uint16_t sP_w[kPlan2Waves][64], sE_w[kPlan2Waves][64];
+    __shared__ int32_t lA_w[kPlan2Waves][64], lB_w[kPlan2Waves][64];   // per-s / per-t log factors
+    __shared__ uint8_t ers_w[kPlan2Waves][256];    // erased-slot flags (k + m <= 255)
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t w = uni(threadIdx.x >> 6);
+    uint8_t* xs = xs_w[w];
+    uint8_t* yt = yt_w[w];
+    uint16_t* sP = sP_w[w];
+    uint16_t* sE = sE_w[w];
+    int32_t* lA = lA_w[w];
+    int32_t* lB = lB_w[w];
+    uint8_t* ers = ers_w[w];
+    const uint32_t b = blockIdx.x * kPlan2Waves + w;
+    const bool live = b < a.nblocks;
     const uint32_t k = a.k, m = a.m;
     // the erasure list is fetched first so its two dependent loads overlap the table staging
-    const uint32_t ec = uni(a.erasure_counts[b]);
+    const uint32_t ec = live ? uni(a.erasure_counts[b]) : 0u;
     const uint16_t* locs = a.erasure_locs + (uint64_t)b * a.erasure_stride;
     bool ok = ec <= m && ec <= a.erasure_stride;   // then ec <= 64: one entry per lane
-    const uint32_t myl = (ok && lane < ec) ? (uint32_t)locs[lane] : 0u;
-    for (uint32_t i = lane; i < 510; i += 64) ex[i] = a.exp_tab[i];
-    for (uint32_t i = lane; i < 256; i += 64) lg[i] = a.log_tab[i];
+    const uint32_t myl = (live && ok && lane < ec) ? (uint32_t)locs[lane] : 0u;
+    for (uint32_t i = threadIdx.x; i < 510; i += 64 * kPlan2Waves) ex[i] = a.exp_tab[i];
+    for (uint32_t i = threadIdx.x; i < 256; i += 64 * kPlan2Waves) lg[i] = a.log_tab[i];
     for (uint32_t i = lane; i < 256; i += 64) ers[i] = 0;
+    __syncthreads();  // the only workgroup barrier: tables staged
+    if (!live) return;
     uint32_t es = 0;
     // lane-parallel validation: sorted, in range; count source erasures (sorted list => the
     // source entries are a prefix); a valid list marks its slots in ers
@@ -449,9 +472,9 @@ __global__ __launch_bounds__(64) void rs_plan2_kernel(RsPlan2Args a)
         es = (uint32_t)__popcll(__ballot(lane < ec && myl < k));
         ok = !__any(bad);
     }
-    __syncthreads();
+    wave_lds_sync();
     if (ok && lane < ec) ers[myl] = 1;
-    __syncthreads();
+    wave_lds_sync();
     // surviving parity rows: lane p tests slot k+p
     uint64_t surv = 0;
     if (ok) {
@@ -494,7 +517,7 @@ __global__ __launch_bounds__(64) void rs_plan2_kernel(RsPlan2Args a)
         sE[lane] = (uint16_t)s;
         xs[lane] = s == 0 ? 0 : ex[(s - 1) % 255u];
     }
-    __syncthreads();
+    wave_lds_sync();
     // per-s: lA[s] = lWp(x_s) + lPP(s) - lQp(s);  per-t: lB[t] = lQ(t) - lW(t) - lD(t)
     if (lane < e) {
         const uint32_t x = xs[lane];
@@ -513,7 +536,7 @@ __global__ __launch_bounds__(64) void rs_plan2_kernel(RsPlan2Args a)
         lA[lane] = acc;
         lB[lane] = bcc;
     }
-    __syncthreads();
+    wave_lds_sync();
     uint8_t* coef = a.coef2 + (uint64_t)b * cs * cs;
     for (uint32_t idx = lane; idx < e * e; idx += 64) {
         const uint32_t t = idx / e, s = idx % e;
@@ -531,7 +554,8 @@ int launch_rs_plan2(const RsPlan2Args& a, hipStream_t s)
 {
     if (a.nblocks == 0) return NFEC_OK;
     if (a.m > 64 || a.k + a.m > 255) return NFEC_ENOTSUP;
-    hipLaunchKernelGGL(rs_plan2_kernel, dim3(a.nblocks), dim3(64), 0, s, a);
+    hipLaunchKernelGGL(rs_plan2_kernel, dim3((a.nblocks + kPlan2Waves - 1) / kPlan2Waves), dim3(64 * kPlan2Waves),
+                       0, s, a);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return hip_fail(e, "rs_plan2 launch");
     return NFEC_OK;
