@@ -36,6 +36,22 @@ def encode_kernel_name(k, m, vec):
     return f"nfec::rs8_enc_k{k}_m{m} (RS8 encode, compiler-allocated)"
 
 
+def host_cores():
+    """(cores this process can actually use, cores visible in its affinity mask).  A GPU box
+    shows the whole machine's CPUs in the affinity mask while a cgroup quota (cpu.max) grants
+    the job a share of them; threads beyond the share only time-slice."""
+    visible = len(os.sched_getaffinity(0))
+    usable = visible
+    for path in ("/sys/fs/cgroup/cpu.max",):
+        try:
+            quota, period = open(path).read().split()[:2]
+            if quota != "max":
+                usable = min(usable, max(1, int(int(quota) // int(period))))
+        except (OSError, ValueError):
+            pass
+    return usable, visible
+
+
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
@@ -47,7 +63,9 @@ def parse():
     p.add_argument("--vec", type=int, default=1400)
     p.add_argument("--erasures", type=int, default=16)
     p.add_argument("--cpu-blocks", type=int, default=4096)
-    p.add_argument("--cpu-threads", type=int, default=16)
+    p.add_argument("--cpu-threads", type=int, default=0,
+                   help="CPU-baseline threads (0 = every core this process may run on: the affinity mask, "
+                        "capped by a cgroup CPU quota when one is set)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--verify", action="store_true", help="check the round trip after timing")
     p.add_argument("--host-steps", type=int, default=0,
@@ -215,7 +233,8 @@ def main():
     if world == 1 and not a.no_cpu_baseline:
         from oracle import pyoracle as orc
 
-        threads = max(1, min(a.cpu_threads, len(os.sched_getaffinity(0))))
+        usable, visible = host_cores()
+        threads = a.cpu_threads if a.cpu_threads > 0 else usable
         te, td, bad = orc.bench_rs8(k, m, vec, a.cpu_blocks, a.erasures, threads)
         te1, td1, bad1 = orc.bench_rs8(k, m, vec, 256, a.erasures, 1)
         cpu = {
@@ -224,8 +243,10 @@ def main():
             "cores": threads,
             "kind": "port",
             "sample": (f"oracle C restatement (per-segment Encode + Gauss-Jordan Decode, -O2) on {a.cpu_blocks} "
-                       f"blocks RS8({k},{m}) x {vec} B, {a.erasures} source erasures/block, {threads} threads; "
-                       f"encode {te:.2f}s decode {td:.2f}s, bad blocks {bad}"),
+                       f"blocks RS8({k},{m}) x {vec} B, {a.erasures} source erasures/block, one codec per thread on "
+                       f"{threads} threads ({visible} CPUs in the affinity mask, {usable} usable under the cgroup "
+                       f"quota); encode {te:.2f}s decode {td:.2f}s wall, bad blocks {bad}"),
+            "host_cpus_visible": visible,
             "single_thread_value": round(k * vec * 256 / (te1 + td1) / 2**30, 4),
         }
 

@@ -137,7 +137,9 @@ int nfec_decode(nfec_codec* codec, const nfec_block_batch* batch, const uint16_t
 
 /* ---- host-resident batched path: same layouts, host pointers (pageable or pinned).
  * Staged through pinned buffers with H2D / compute / D2H overlapped on streams.
- * Synchronous: returns when all outputs are back in host memory. */
+ * Synchronous: returns when all outputs are back in host memory.  A codec owns one staging
+ * pipeline: host-batch calls (these and the *_host_vectors calls) on one codec from several
+ * host threads are serialised; calls on different codecs run concurrently. */
 int nfec_encode_host(nfec_codec* codec, const nfec_block_batch* host_batch);
 int nfec_decode_host(nfec_codec* codec, const nfec_block_batch* host_batch,
                      const uint16_t* erasure_locs, uint32_t erasure_stride,
@@ -219,8 +221,9 @@ int nfec_payload_id_write(uint8_t fec_id, uint8_t fec_m, uint32_t block_id, uint
                           uint16_t block_len, void* out);
 int nfec_payload_id_read(uint8_t fec_id, uint8_t fec_m, const void* in, uint32_t* block_id,
                          uint16_t* symbol_id, uint16_t* block_len);
-/* Sender choice (NormSession::StartSender, normSession.cpp:764-883): numData + numParity <=
- * 255 -> RS8 with fec_id_pref (0 = 5) and m 8, or MDP/129 when assume_mdp; else RS16, fec 2, m 16. */
+/* Sender choice (NormSession::StartSender, normSession.cpp:764-898): numParity == 0 -> no
+ * codec (*kind = 0), fec_id_pref (0 = 5), m 8; numData + numParity <= 255 -> RS8 with
+ * fec_id_pref (0 = 5) and m 8, or MDP/129 when assume_mdp; else RS16, fec 2, m 16. */
 int nfec_sender_codec(uint16_t num_data, uint16_t num_parity, uint8_t fec_id_pref, int assume_mdp,
                       int* kind, uint8_t* fec_id, uint8_t* fec_m);
 /* Receiver choice (NormSenderNode::AllocateBuffers, normNode.cpp:290-356): fec 2 m 8 -> RS8,

@@ -8,6 +8,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <map>
 #include <memory>
 #include <thread>
 #include <vector>
@@ -146,9 +147,13 @@ struct nfec_codec {
     DevBuf<uint8_t> w_coef1, w_coef2, w_z, w_work, w_pmap;
     DevBuf<uint32_t> w_emask, w_psel, w_gate;
     uint32_t gate_gen = 0;         // per-pass generation written into w_gate (RsPlan2Args)
-    // per-call staging
+    // per-call staging (nfec_encode_segment / nfec_decode_vectors, guarded by mu)
     DevBuf<uint8_t> s_block;
     DevBuf<uint16_t> s_locs;
+    DevBuf<int32_t> s_status;
+    // host-batch pipelines (slots, pinned staging, streams): one host-batch call at a time per
+    // codec.  Separate from mu, which the decode kernels' workspace takes inside such a call.
+    std::mutex stage_mu;
     HostStage stage;
 
     ~nfec_codec()
@@ -172,6 +177,7 @@ struct nfec_codec {
         w_oslots.release();
         w_cols.release();
         s_locs.release();
+        s_status.release();
     }
 };
 
@@ -324,11 +330,22 @@ bool force_generic()
     return v;
 }
 
-// whether the generated bit-sliced kernels cover this RS8 shape
+// whether the generated bit-sliced kernels cover this RS8 shape (cached per shape; codecs on
+// other host threads ask concurrently, so the answer is computed into a per-call buffer under
+// a lock, never into shared scratch -- the reference's unlocked fec_initialized race,
+// normEncoderRS8.cpp:379-388, is not reintroduced)
 bool has_bitsliced(uint32_t k, uint32_t m)
 {
-    static std::vector<uint8_t> scratch(256 * 256);
-    return bitsliced_encode_generator(k, m, scratch.data()) == NFEC_OK;
+    static std::mutex mu;
+    static std::map<uint32_t, bool> known;
+    const uint32_t key = (k << 16) | m;
+    std::lock_guard<std::mutex> lk(mu);
+    auto it = known.find(key);
+    if (it != known.end()) return it->second;
+    std::vector<uint8_t> scratch(256 * 256);
+    const bool v = bitsliced_encode_generator(k, m, scratch.data()) == NFEC_OK;
+    known.emplace(key, v);
+    return v;
 }
 
 // tuning knobs of the bit-sliced kernels (A/B runs): bit 0 XCD-contiguous workgroup
@@ -482,13 +499,16 @@ int encode_device(nfec_codec* c, const nfec_block_batch* b, hipStream_t s)
 }
 
 // ---- decode on a device batch ----
+// caller_locked: the caller already holds c->mu (nfec_decode_vectors keeps it for the whole
+// per-call decode, staging included)
 int decode_device(nfec_codec* c, const nfec_block_batch* b, const uint16_t* locs, uint32_t lstride,
-                  const uint16_t* counts, int32_t* status, hipStream_t s)
+                  const uint16_t* counts, int32_t* status, hipStream_t s, bool caller_locked = false)
 {
     if (!locs || !counts) return fail(NFEC_EINVAL, "null erasure arrays");
     const bool acc = b->flags & NFEC_ACCUMULATE;
     if (c->kind == NFEC_MDP && acc) return fail(NFEC_ENOTSUP, "MDP decode requires zero-filled erased segments");
-    std::lock_guard<std::mutex> lk(c->mu);
+    std::unique_lock<std::mutex> lk(c->mu, std::defer_lock);
+    if (!caller_locked) lk.lock();
     const uint32_t n = c->k + c->m;
     const uint32_t zstride = round_up(c->vec, 8);
     // RS decode rows: at most min(k, m) source erasures are solved per block, so the plan's
@@ -1017,17 +1037,15 @@ int nfec_decode_vectors(nfec_codec* c, void* const* vectors, uint32_t num_data, 
     DeviceGuard g(c->device);
     const uint32_t stride = round_up(c->vec, 8);
     const uint32_t nslots = num_data + c->m;
-    uint8_t* d = nullptr;
-    uint16_t* dl = nullptr;
-    {
-        std::lock_guard<std::mutex> lk(c->mu);
-        int rc = c->s_block.reserve((size_t)(c->k + c->m) * stride + 64);
-        if (rc) return rc;
-        rc = c->s_locs.reserve(c->m + 8);
-        if (rc) return rc;
-        d = c->s_block.p;
-        dl = c->s_locs.p;
-    }
+    // the whole call runs under mu: the staging block, list and status word are the codec's,
+    // and nfec_encode_segment may grow s_block concurrently otherwise
+    std::lock_guard<std::mutex> lk(c->mu);
+    int rc0 = c->s_block.reserve((size_t)(c->k + c->m) * stride + 64);
+    if (!rc0) rc0 = c->s_locs.reserve(c->m + 8);
+    if (!rc0) rc0 = c->s_status.reserve(1);
+    if (rc0) return rc0;
+    uint8_t* d = c->s_block.p;
+    uint16_t* dl = c->s_locs.p;
     NFEC_HIP(hipMemset(d, 0, (size_t)nslots * stride));
     for (uint32_t s = 0; s < nslots; ++s)
         if (vectors[s]) NFEC_HIP(hipMemcpy(d + (size_t)s * stride, vectors[s], c->vec, hipMemcpyHostToDevice));
@@ -1036,8 +1054,7 @@ int nfec_decode_vectors(nfec_codec* c, void* const* vectors, uint32_t num_data, 
     hl[c->m] = (uint16_t)erasure_count;
     hl[c->m + 1] = (uint16_t)num_data;
     NFEC_HIP(hipMemcpy(dl, hl.data(), hl.size() * 2, hipMemcpyHostToDevice));
-    int32_t* dstatus = nullptr;
-    NFEC_HIP(hipMalloc(reinterpret_cast<void**>(&dstatus), sizeof(int32_t)));
+    int32_t* dstatus = c->s_status.p;
     nfec_block_batch b{};
     b.blocks = d;
     b.block_stride = (uint64_t)(c->k + c->m) * stride;
@@ -1045,13 +1062,12 @@ int nfec_decode_vectors(nfec_codec* c, void* const* vectors, uint32_t num_data, 
     b.nblocks = 1;
     b.num_data = dl + c->m + 1;
     b.flags = c->kind == NFEC_MDP ? 0 : NFEC_ACCUMULATE;
-    int rc = decode_device(c, &b, dl, c->m, dl + c->m, dstatus, nullptr);
+    int rc = decode_device(c, &b, dl, c->m, dl + c->m, dstatus, nullptr, true);
     int32_t st = 0;
     if (rc == NFEC_OK) {
         hipError_t e = hipMemcpy(&st, dstatus, sizeof(st), hipMemcpyDeviceToHost);
         if (e != hipSuccess) rc = hip_fail(e, "decode status copy");
     }
-    (void)hipFree(dstatus);
     if (rc) return rc;
     if (st > 0) {
         for (uint32_t i = 0; i < erasure_count; ++i) {
@@ -1132,8 +1148,9 @@ void copy2d(uint8_t* dst, uint64_t dpitch, const uint8_t* src, uint64_t spitch, 
 // The pipelines' device slots, pinned staging, streams and events live in the codec and grow
 // on demand: allocating (and freeing, which synchronises the whole device) per call would
 // stall every other codec's work on the GPU -- two codecs driven from two host threads (the
-// mixed RS8/RS16 stream of BASELINE C5) would serialise.  A codec is used by one host thread
-// at a time, like the reference's codec instances (normApi.cpp:55,126).
+// mixed RS8/RS16 stream of BASELINE C5) would serialise.  Host-batch calls on one codec are
+// serialised by the codec's stage_mu (the reference's codec instances are single-threaded,
+// normApi.cpp:55,126; here concurrent callers of one codec wait rather than race).
 static int grow_dev(void** p, size_t& cap, size_t need)
 {
     if (cap >= need) return NFEC_OK;
@@ -1258,6 +1275,7 @@ static int run_host_batch(nfec_codec* c, const nfec_block_batch* hb, const uint1
     int rc = check_batch(c, hb);
     if (rc || hb->nblocks == 0) return rc;
     DeviceGuard g(c->device);
+    std::lock_guard<std::mutex> stage_lock(c->stage_mu);
     const uint64_t hbs = hb->block_stride;
     const uint64_t ss = hb->seg_stride;
     const uint64_t dbs = (uint64_t)(c->k + c->m) * ss;       // compact device pitch
@@ -1431,6 +1449,7 @@ static int run_host_vectors(nfec_codec* c, void* const* vecs, uint32_t nblocks, 
             if (!vecs[(uint64_t)b * n + s]) return fail(NFEC_EINVAL, "null source/parity vector");
     }
     DeviceGuard g(c->device);
+    std::lock_guard<std::mutex> stage_lock(c->stage_mu);
     const uint32_t chunk = host_chunk(c, dbs, nblocks);
     const uint32_t used = std::min<uint32_t>(kHostSlots, (nblocks + chunk - 1) / chunk);
     const size_t meta = (size_t)chunk * (1 + lstride + 1);

@@ -192,7 +192,13 @@ int nfec_sender_codec(uint16_t num_data, uint16_t num_parity, uint8_t fec_id_pre
 {
     if (!kind || !fec_id || !fec_m) return NFEC_EINVAL;
     const uint32_t block = (uint32_t)num_data + num_parity;
-    if (block <= 255) {
+    if (num_parity == 0) {
+        // no parity: no encoder is created, the RS8 fec_id is advertised whatever the block
+        // size or ASSUME_MDP_FEC (normSession.cpp:890-898)
+        *kind = 0;
+        *fec_id = fec_id_pref ? fec_id_pref : 5;
+        *fec_m = 8;
+    } else if (block <= 255) {
         if (assume_mdp) {
             *kind = NFEC_MDP;
             *fec_id = 129;

@@ -96,6 +96,8 @@ def make_encoder(num_data: int, num_parity: int, segment_size: int, fec_id: int 
                  object_size: int = 0):
     """Sender side: -> (Init()ed encoder, the FecObjectInfo to advertise)."""
     kind, fid, fm = sender_codec(num_data, num_parity, fec_id, assume_mdp)
+    if kind == 0:  # numParity 0: the reference sends without an encoder (normSession.cpp:890-898)
+        raise N.NfecError(N.NFEC_EINVAL, "numParity 0: NORM creates no encoder")
     enc = _classes()[kind][0]()
     if not enc.Init(num_data, num_parity, vector_size(segment_size)):
         raise N.NfecError(N.NFEC_ERANGE, "encoder Init")

@@ -35,7 +35,9 @@ def payload_id(fec_id, fec_m, block, symbol, block_len=0):
 
 def sender_codec(num_data, num_parity, fec_id=0, assume_mdp=False):
     """NormSession::StartSender codec choice, normSession.cpp:834-873 -> (kind, fec_id, m)
-    with kind 1 RS8, 2 RS16, 3 MDP."""
+    with kind 1 RS8, 2 RS16, 3 MDP, 0 no codec (numParity 0, normSession.cpp:890-898)."""
+    if num_parity == 0:
+        return (0, fec_id or 5, 8)
     if num_data + num_parity <= 255:
         return (3, 129, 8) if assume_mdp else (1, fec_id or 5, 8)
     return (2, 2, 16)

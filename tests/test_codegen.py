@@ -1,0 +1,29 @@
+"""The generated kernel sources under norm_amd/csrc/gen_*.hip are committed (the GPU box builds
+nothing), so they must be exactly what tools/codegen/*.py produce: a hand edit or a stale
+generator would otherwise ship unnoticed.  Each generator is rerun into a temp dir and the
+output byte-compared with the committed file."""
+import filecmp
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+GENERATORS = ["rs8_asm", "rs8_bitsliced", "fdec_asm", "solve_asm"]
+
+
+@pytest.mark.parametrize("name", GENERATORS)
+def test_generated_kernel_is_reproducible(name, tmp_path):
+    out = tmp_path / f"gen_{name}.hip"
+    subprocess.run([sys.executable, os.path.join(ROOT, "tools", "codegen", f"gen_{name}.py"), str(out)],
+                   check=True, cwd=ROOT)
+    committed = os.path.join(ROOT, "norm_amd", "csrc", f"gen_{name}.hip")
+    assert filecmp.cmp(str(out), committed, shallow=False), \
+        f"norm_amd/csrc/gen_{name}.hip differs from tools/codegen/gen_{name}.py's output: regenerate it"
+
+
+def test_every_generated_source_has_a_generator():
+    gen = sorted(f[4:-4] for f in os.listdir(os.path.join(ROOT, "norm_amd", "csrc"))
+                 if f.startswith("gen_") and f.endswith(".hip"))
+    assert gen == sorted(GENERATORS)

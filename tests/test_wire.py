@@ -81,9 +81,21 @@ def test_payload_id_known_bytes():
 
 
 @pytest.mark.parametrize("nd,npar,fid,mdp", [(64, 32, 0, False), (200, 55, 2, False), (200, 56, 0, False),
-                                             (1000, 200, 5, False), (64, 32, 0, True), (255, 1, 0, True)])
+                                             (1000, 200, 5, False), (64, 32, 0, True), (255, 1, 0, True),
+                                             (64, 0, 0, False), (300, 0, 0, False), (64, 0, 0, True),
+                                             (300, 0, 2, True)])
 def test_sender_codec_choice(nd, npar, fid, mdp):
     assert W.sender_codec(nd, npar, fid, mdp) == R.sender_codec(nd, npar, fid, mdp)
+
+
+def test_sender_without_parity_advertises_rs8_fec_id():
+    # normSession.cpp:890-898: no parity -> no encoder, fec_id = fecId or 5, m = 8, whatever
+    # the block size or ASSUME_MDP_FEC
+    assert W.sender_codec(300, 0) == (0, 5, 8)
+    assert W.sender_codec(64, 0, 0, True) == (0, 5, 8)
+    assert W.sender_codec(64, 0, 2) == (0, 2, 8)
+    with pytest.raises(N.NfecError):
+        W.make_encoder(64, 0, 1392)
 
 
 @pytest.mark.parametrize("fid", [0, 1, 2, 5, 129, 200])
