@@ -10,7 +10,9 @@ own 65,536 blocks (weak scaling: FEC blocks are independent, no data-path collec
 process group only provides the barrier and the max-over-ranks timing).
 
 value = k * vec * blocks_total / step_time  (source bytes through encode+decode, GiB/s),
-the same formula as the CPU baseline.  roofline = the encode kernel's
+the same formula as the CPU baseline; SURVEY.md 8d's "combined" figure,
+2*k*vec*B / (t_enc + t_dec), counts each source byte twice and is exactly 2x this value.
+--strong splits a fixed total of --blocks over the ranks instead (norm_amd/dist.py shard).  roofline = the encode kernel's
 algorithmic HBM bytes ((k+m)*vec per block) / its measured launch time vs 8 TB/s.
 """
 import argparse
@@ -57,7 +59,10 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=3)
-    p.add_argument("--blocks", type=int, default=65536, help="FEC blocks per GPU")
+    p.add_argument("--blocks", type=int, default=65536,
+                   help="FEC blocks per GPU (weak scaling), or in total with --strong")
+    p.add_argument("--strong", action="store_true",
+                   help="strong scaling: --blocks is the fixed total, split over the ranks by block_range")
     p.add_argument("--k", type=int, default=64)
     p.add_argument("--m", type=int, default=32)
     p.add_argument("--vec", type=int, default=1400)
@@ -92,13 +97,15 @@ def main():
     dev = torch.device("cuda", local if world > 1 else 0)
 
     from norm_amd import NormDecoderRS8, NormEncoderRS8, fill_blocks, make_erasures
+    from norm_amd.dist import shard
 
-    k, m, vec, nb = a.k, a.m, a.vec, a.blocks
+    k, m, vec = a.k, a.m, a.vec
     seed = 0x4E4F524D
     enc, dec = NormEncoderRS8(device=dev.index), NormDecoderRS8(device=dev.index)
     assert enc.Init(k, m, vec) and dec.Init(k, m, vec)
+    first, nb = shard(a.blocks, world, rank, a.strong)
+    assert nb > 0, "every rank needs at least one block"
     blocks = torch.zeros((nb, k + m, vec), dtype=torch.uint8, device=dev)
-    first = rank * nb
     fill_blocks(blocks, k, vec, seed, first_block=first)
     locs, counts = make_erasures(nb, k, a.erasures, seed, m, first_block=first)
     status = torch.empty(nb, dtype=torch.int32, device=dev)
@@ -174,7 +181,7 @@ def main():
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             he = float(t.item())
         host = {
-            "value": round(k * vec * nb * world / (he / a.host_steps) / 2**30, 2),
+            "value": round(k * vec * (a.blocks if a.strong else nb * world) / (he / a.host_steps) / 2**30, 2),
             "unit": "GiB/s",
             "steps": a.host_steps,
             "ms_per_step": round(he / a.host_steps * 1e3, 2),
@@ -199,7 +206,7 @@ def main():
         torch.cuda.synchronize(dev)
         ok = bool(torch.equal(blocks, keep)) and bool((status == a.erasures).all())
 
-    total_blocks = nb * world
+    total_blocks = a.blocks if a.strong else nb * world
     src_bytes = k * vec * total_blocks
     ms_per_step = elapsed / a.steps * 1e3
     value = src_bytes / (elapsed / a.steps) / 2**30
@@ -259,13 +266,15 @@ def main():
         "warmup": a.warmup,
         "ms_per_step": round(ms_per_step, 4),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if a.strong else "weak",
         "vs_baseline": None,
         "dtype": "u8",
         "data": "synthetic (splitmix64 source segments generated in HBM; reference RS8 generator)",
         "config": {
-            "workload": f"RS8 k={k} m={m} seg={vec}B: encode + {a.erasures}-source-erasure decode of {nb} blocks per GPU in HBM",
-            "k": k, "m": m, "vec": vec, "blocks_per_gpu": nb, "erasures": a.erasures,
+            "workload": (f"RS8 k={k} m={m} seg={vec}B: encode + {a.erasures}-source-erasure decode of "
+                         + (f"{a.blocks} blocks in total over {world} GPU(s)" if a.strong else f"{nb} blocks per GPU")
+                         + " in HBM"),
+            "k": k, "m": m, "vec": vec, "blocks_per_gpu": nb, "blocks_total": total_blocks, "erasures": a.erasures,
             "parallelism": f"block-striped x{world} (no collective)",
         },
         "roofline": {

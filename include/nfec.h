@@ -164,6 +164,28 @@ int nfec_decode_host_vectors(nfec_codec* codec, void* const* vectors, uint32_t n
                              uint32_t erasure_stride, const uint16_t* erasure_counts,
                              int32_t* status, uint32_t flags);
 
+/* ---- asynchronous segment-list batches: receiver-side cross-block batching ----
+ * The receiver's decode site (NormObject::HandleObjectMessage -> NormSenderNode::Decode,
+ * normObject.cpp:1548-1644, normNode.h:484-487) runs one block per call on NORM's protocol
+ * thread.  These queue a batch of blocks on the codec and return at once; the protocol thread
+ * keeps receiving and later collects the completion.  Arguments as the synchronous calls; the
+ * pointer table, num_data, erasure lists and counts are copied at submission, the segment
+ * buffers and the status array must stay valid until the request completes.  A codec runs its
+ * requests in submission order on a worker thread of its own; different codecs (one decoder
+ * per remote sender, normNode.h:649) run concurrently.  Destroying a codec completes its
+ * queued requests first (their handles must still be waited on or were already). */
+typedef struct nfec_request nfec_request;
+int nfec_encode_host_vectors_async(nfec_codec* codec, void* const* vectors, uint32_t nblocks,
+                                   const uint16_t* num_data, uint32_t flags, nfec_request** request);
+int nfec_decode_host_vectors_async(nfec_codec* codec, void* const* vectors, uint32_t nblocks,
+                                   const uint16_t* num_data, const uint16_t* erasure_locs,
+                                   uint32_t erasure_stride, const uint16_t* erasure_counts,
+                                   int32_t* status, uint32_t flags, nfec_request** request);
+/* 1 when the request has completed, 0 while pending (non-blocking poll). */
+int nfec_request_test(nfec_request* request);
+/* Blocks until completion, frees the request and returns the call's status code. */
+int nfec_request_wait(nfec_request* request);
+
 /* ---- per-call NORM semantics with scattered host vectors (drop-in classes) ---- */
 /* NormEncoder::Encode: parity_vectors[i] ^= G[k+i][segment_id] * data over vector_size
  * bytes (RS16: vector_size/2 symbols).  MDP: one in-order LFSR step. Synchronous. */

@@ -110,6 +110,10 @@ _SIGS = {
     "nfec_decode_host": (_I, [_P, ctypes.POINTER(BlockBatch), _P, _U32, _P, _P]),
     "nfec_encode_host_vectors": (_I, [_P, _P, _U32, _P, _U32]),
     "nfec_decode_host_vectors": (_I, [_P, _P, _U32, _P, _P, _U32, _P, _P, _U32]),
+    "nfec_encode_host_vectors_async": (_I, [_P, _P, _U32, _P, _U32, _P]),
+    "nfec_decode_host_vectors_async": (_I, [_P, _P, _U32, _P, _P, _U32, _P, _P, _U32, _P]),
+    "nfec_request_test": (_I, [_P]),
+    "nfec_request_wait": (_I, [_P]),
     "nfec_encode_segment": (_I, [_P, _U32, _P, _P]),
     "nfec_decode_vectors": (_I, [_P, _P, _U32, _U32, _P]),
     "nfec_util_fill": (_I, [ctypes.POINTER(BlockBatch), _U32, _U32, _U64, _U64, _P]),

@@ -194,6 +194,17 @@ class _Encoder(_Codec):
                                                  N.NFEC_ACCUMULATE if accumulate else 0), "nfec_encode_host_vectors")
 
 
+    def encode_vectors_host_async(self, vectors, num_data=None, accumulate=False):
+        """encode_vectors_host queued on the codec's worker thread; returns a Request."""
+        self._need()
+        arr, keep, nd = _vector_table(vectors, self.ndata + self.npar, num_data, self.ndata)
+        h = ctypes.c_void_p()
+        N.check(N.lib().nfec_encode_host_vectors_async(self._h, arr, len(vectors), nd,
+                                                       N.NFEC_ACCUMULATE if accumulate else 0, ctypes.byref(h)),
+                "nfec_encode_host_vectors_async")
+        return Request(h, (arr, keep, vectors, self), None)
+
+
 class _Decoder(_Codec):
     def Decode(self, vectorList, numData, erasureCount, erasureLocs):
         self._need()
@@ -242,6 +253,23 @@ class _Decoder(_Codec):
         return status
 
 
+    def decode_vectors_host_async(self, vectors, erasure_locs, erasure_counts, num_data=None, accumulate=False):
+        """decode_vectors_host queued on the codec's worker thread: returns a Request at once
+        (the receiver keeps going; Request.wait() gives the status array)."""
+        import numpy as np
+
+        self._need()
+        arr, keep, nd = _vector_table(vectors, self.ndata + self.npar, num_data, self.ndata)
+        locs = np.ascontiguousarray(erasure_locs, dtype=np.uint16)
+        counts = np.ascontiguousarray(erasure_counts, dtype=np.uint16)
+        status = np.zeros(len(vectors), np.int32)
+        h = ctypes.c_void_p()
+        N.check(N.lib().nfec_decode_host_vectors_async(self._h, arr, len(vectors), nd, locs.ctypes.data, locs.shape[1],
+                                                       counts.ctypes.data, status.ctypes.data,
+                                                       N.NFEC_ACCUMULATE if accumulate else 0, ctypes.byref(h)),
+                "nfec_decode_host_vectors_async")
+        return Request(h, (arr, keep, locs, counts, vectors, self), status)
+
     def decode_vectors_host(self, vectors, erasure_locs, erasure_counts, num_data=None, accumulate=False):
         """Receiver repair of many blocks given as NORM-style segment lists (None allowed for
         missing parity).  erasure_locs: uint16 [nblocks, stride]; erasure_counts: uint16
@@ -257,6 +285,33 @@ class _Decoder(_Codec):
                                                  counts.ctypes.data, status.ctypes.data,
                                                  N.NFEC_ACCUMULATE if accumulate else 0), "nfec_decode_host_vectors")
         return status
+
+
+class Request:
+    """An asynchronous segment-list batch (nfec_*_host_vectors_async).  Keeps the caller's
+    buffers alive until completion; test() polls, wait() blocks and returns the status array
+    (decode) or None (encode), raising NfecError if the call failed."""
+
+    def __init__(self, handle, keep, status):
+        self._h, self._keep, self._status = handle, keep, status
+
+    def test(self):
+        if not self._h:
+            return True
+        return N.check(N.lib().nfec_request_test(self._h), "nfec_request_test") == 1
+
+    def wait(self):
+        if self._h:
+            h, self._h = self._h, None
+            N.check(N.lib().nfec_request_wait(h), "nfec_request_wait")
+            self._keep = None
+        return self._status
+
+    def __del__(self):
+        try:
+            self.wait()
+        except Exception:
+            pass
 
 
 def _vector_table(vectors, n, num_data, k):

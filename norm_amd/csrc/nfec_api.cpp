@@ -5,7 +5,10 @@
 // (built once on the host, uploaded to HBM) and the per-value kernel tables.  Batched calls
 // only enqueue kernels on the caller's stream; no host<->device traffic on the hot path.
 #include <algorithm>
+#include <condition_variable>
 #include <cstdio>
+#include <deque>
+#include <functional>
 #include <cstdlib>
 #include <cstring>
 #include <map>
@@ -123,6 +126,67 @@ struct HostStage {
     }
 };
 
+// An asynchronous host-batch call (nfec_*_host_vectors_async): the arguments are copied at
+// submission, a codec-owned worker thread runs the call, the caller polls or waits.
+struct nfec_request {
+    std::mutex mu;
+    std::condition_variable cv;
+    bool done = false;
+    int rc = NFEC_OK;
+    std::string err;  // the worker thread's error message, handed to the waiting thread
+    std::function<int()> run;
+};
+
+// One worker thread per codec that has seen an async call: requests on a codec complete in
+// submission order (they share the codec's staging pipeline anyway); codecs run concurrently,
+// so a receiver with one decoder per remote sender (normNode.h:649) overlaps its senders.
+struct AsyncQueue {
+    std::mutex mu;
+    std::condition_variable cv;
+    std::deque<nfec_request*> q;
+    std::thread th;
+    bool stop = false;
+    int device = 0;
+
+    void loop()
+    {
+        (void)hipSetDevice(device);
+        for (;;) {
+            nfec_request* r = nullptr;
+            {
+                std::unique_lock<std::mutex> lk(mu);
+                cv.wait(lk, [&] { return stop || !q.empty(); });
+                if (q.empty()) return;  // stop requested and drained
+                r = q.front();
+                q.pop_front();
+            }
+            const int rc = r->run();
+            std::lock_guard<std::mutex> lk(r->mu);
+            if (rc < 0) r->err = last_error_cstr();
+            r->rc = rc;
+            r->done = true;
+            r->cv.notify_all();
+        }
+    }
+    void submit(nfec_request* r)
+    {
+        std::lock_guard<std::mutex> lk(mu);
+        if (!th.joinable()) th = std::thread([this] { loop(); });
+        q.push_back(r);
+        cv.notify_one();
+    }
+    // finishes every queued request, then stops the thread
+    void shutdown()
+    {
+        {
+            std::lock_guard<std::mutex> lk(mu);
+            stop = true;
+            cv.notify_all();
+        }
+        if (th.joinable()) th.join();
+    }
+};
+
 struct nfec_codec {
     int kind = 0;
     int device = 0;
@@ -155,9 +219,11 @@ struct nfec_codec {
     // codec.  Separate from mu, which the decode kernels' workspace takes inside such a call.
     std::mutex stage_mu;
     HostStage stage;
+    AsyncQueue async;
 
     ~nfec_codec()
     {
+        async.shutdown();  // outstanding async requests complete before the codec goes away
         DeviceGuard g(device);
         stage.release();
         for (auto* b : {&d_coef, &d_gen, &d_exp, &w_coef1, &w_coef2, &w_z, &w_work, &s_block, &d_mdp_step})
@@ -1605,6 +1671,84 @@ int nfec_decode_host(nfec_codec* codec, const nfec_block_batch* host_batch, cons
 {
     if (!erasure_locs || !erasure_counts || erasure_stride == 0) return fail(NFEC_EINVAL, "bad erasure arrays");
     return run_host_batch(codec, host_batch, erasure_locs, erasure_stride, erasure_counts, status, true);
+}
+
+// ---- asynchronous segment-list batches (receiver cross-block batching) ----
+// The receiver's decode site (NormObject::HandleObjectMessage -> NormSenderNode::Decode,
+// normObject.cpp:1548-1644, normNode.h:484-487) repairs one block per call on the protocol
+// thread.  These calls queue many blocks (from one remote sender's decoder) and return at
+// once; the protocol thread keeps receiving and collects completions with nfec_request_test /
+// nfec_request_wait.  The pointer table, numData, erasure lists and counts are copied at
+// submission; the segment buffers and status array must stay valid until completion.
+namespace {
+
+int submit_vectors(nfec_codec* c, void* const* vecs, uint32_t nblocks, const uint16_t* num_data, const uint16_t* locs,
+                   uint32_t lstride, const uint16_t* counts, int32_t* status, uint32_t flags, bool decode,
+                   nfec_request** out)
+{
+    if (!out) return fail(NFEC_EINVAL, "null request pointer");
+    *out = nullptr;
+    if (!c || (nblocks && !vecs)) return fail(NFEC_EINVAL, "null codec or vector list");
+    if (decode && (!locs || !counts || lstride == 0)) return fail(NFEC_EINVAL, "bad erasure arrays");
+    const uint64_t n = (uint64_t)c->k + c->m;
+    auto tab = std::make_shared<std::vector<void*>>(vecs, vecs + n * nblocks);
+    auto nd = std::make_shared<std::vector<uint16_t>>();
+    if (num_data) nd->assign(num_data, num_data + nblocks);
+    auto el = std::make_shared<std::vector<uint16_t>>();
+    auto ec = std::make_shared<std::vector<uint16_t>>();
+    if (decode) {
+        el->assign(locs, locs + (uint64_t)lstride * nblocks);
+        ec->assign(counts, counts + nblocks);
+    }
+    std::unique_ptr<nfec_request> r(new nfec_request);
+    r->run = [=]() {
+        return run_host_vectors(c, tab->data(), nblocks, num_data ? nd->data() : nullptr,
+                                decode ? el->data() : nullptr, lstride, decode ? ec->data() : nullptr, status,
+                                flags, decode);
+    };
+    c->async.device = c->device;
+    c->async.submit(r.get());
+    *out = r.release();
+    return NFEC_OK;
+}
+
+}  // namespace
+
+int nfec_encode_host_vectors_async(nfec_codec* codec, void* const* vectors, uint32_t nblocks, const uint16_t* num_data,
+                                   uint32_t flags, nfec_request** request)
+{
+    return submit_vectors(codec, vectors, nblocks, num_data, nullptr, 0, nullptr, nullptr, flags, false, request);
+}
+
+int nfec_decode_host_vectors_async(nfec_codec* codec, void* const* vectors, uint32_t nblocks,
+                                   const uint16_t* num_data, const uint16_t* erasure_locs, uint32_t erasure_stride,
+                                   const uint16_t* erasure_counts, int32_t* status, uint32_t flags,
+                                   nfec_request** request)
+{
+    return submit_vectors(codec, vectors, nblocks, num_data, erasure_locs, erasure_stride, erasure_counts, status,
+                          flags, true, request);
+}
+
+int nfec_request_test(nfec_request* r)
+{
+    if (!r) return fail(NFEC_EINVAL, "null request");
+    std::lock_guard<std::mutex> lk(r->mu);
+    return r->done ? 1 : 0;
+}
+
+int nfec_request_wait(nfec_request* r)
+{
+    if (!r) return fail(NFEC_EINVAL, "null request");
+    int rc;
+    std::string err;
+    {
+        std::unique_lock<std::mutex> lk(r->mu);
+        r->cv.wait(lk, [&] { return r->done; });
+        rc = r->rc;
+        err.swap(r->err);
+    }
+    delete r;
+    return rc < 0 ? fail(rc, err) : rc;
 }
 
 // ---- synthetic workload utilities ----

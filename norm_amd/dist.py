@@ -17,6 +17,20 @@ def block_range(total, world, rank):
     return lo, hi
 
 
+def shard(blocks, world, rank, strong=False):
+    """(first_block, nblocks) of `rank` for a benchmark run.
+
+    weak (default): every rank owns `blocks` blocks of its own, [rank*blocks, (rank+1)*blocks):
+    the per-GPU work stays fixed as the world grows.
+    strong: `blocks` is the fixed total, split into contiguous ranges by block_range."""
+    if strong:
+        lo, hi = block_range(blocks, world, rank)
+        return lo, hi - lo
+    if world <= 0 or not (0 <= rank < world):
+        raise ValueError("bad world/rank")
+    return rank * blocks, blocks
+
+
 def env_ranks():
     """(world, rank, local_rank) from the torchrun environment (defaults: single process)."""
     return (int(os.environ.get("WORLD_SIZE", "1")), int(os.environ.get("RANK", "0")),

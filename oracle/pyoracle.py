@@ -125,6 +125,22 @@ def encode_blocks(kind, k, m, vec, blocks, num_data=None):
     return blocks
 
 
+def encode_block_with_generator(kind, enc_full, k, m, vec, src):
+    """Reference call pattern for one block (zeroed parity, one Encode() per source segment,
+    normEncoderRS8.cpp:473-483 / normEncoderRS16.cpp:472-482) with a given full (k+m) x k
+    generator -- for codes whose generator the oracle would take too long to rebuild per call
+    (C4: RS16 k=4096, ~30 s).  src: uint8 [k, >= vec].  Returns parity uint8 [m, vec]."""
+    enc_full = np.ascontiguousarray(enc_full, np.uint16 if kind == RS16 else np.uint8)
+    assert enc_full.shape == (k + m, k)
+    par = np.zeros((m, vec), np.uint8)
+    ptrs = (ctypes.c_void_p * m)(*[par[i].ctypes.data for i in range(m)])
+    fn = lib().orc_rs16_encode if kind == RS16 else lib().orc_rs8_encode
+    src = np.ascontiguousarray(src)
+    for j in range(k):
+        fn(enc_full.ctypes.data, k, m, vec, j, src[j].ctypes.data, ptrs)
+    return par
+
+
 def decode_blocks(kind, k, m, vec, blocks, locs, counts, num_data=None):
     """Reference Decode() per block (MDP: missing parity passed as NULL).  Returns status."""
     nd = None if num_data is None else np.ascontiguousarray(num_data, np.uint16)

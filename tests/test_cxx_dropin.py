@@ -1,0 +1,90 @@
+"""The C++ drop-in surface (include/norm_fec/nfecCodecs.h) exercised the way NORM uses it.
+
+tests/native/nfec_fectest is the reference's fecTest (src/common/fecTest.cpp:23-135) restated
+against the GPU classes: Init, per-segment Encode and whole-block Decode called through
+NormEncoder* / NormDecoder* base pointers, Destroy + re-Init, delete through the base class.
+It is built with plain g++ against libnfec.so (no HIP headers), as a NORM tree would link it.
+Its encoded block, Decode() return value and repaired block are compared byte for byte with
+the oracle's reference call pattern on the same input.
+"""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+EXE = os.path.join(ROOT, "tests", "native", "_build", "nfec_fectest")
+
+
+def test_fectest_links_against_libnfec_only():
+    """Every symbol resolves at load (LD_BIND_NOW) and the usage path runs without a GPU."""
+    assert os.path.exists(EXE), "build() builds tests/native"
+    r = subprocess.run([EXE], env=dict(os.environ, LD_BIND_NOW="1"), capture_output=True, text=True, timeout=60)
+    assert r.returncode == 2 and "usage" in r.stderr
+    ldd = subprocess.run(["ldd", EXE], capture_output=True, text=True).stdout
+    assert "libnfec.so" in ldd and "not found" not in ldd
+
+
+KINDS = {"rs8": 1, "rs16": 2, "mdp": 3}
+CASES = [
+    # kind, k, m, vec, numData, erasures (sorted), null parity, input ("-": fecTest's printable data)
+    ("rs16", 400, 100, 64, 400, [17, 433], False, "-"),          # fecTest.cpp:13-16 shape, 2 of n erased
+    ("rs16", 400, 100, 1400, 400, list(range(0, 400, 8)), True, "rand"),  # 50 source erasures, vec 1400
+    ("rs16", 40, 10, 65, 40, [3, 39, 41], True, "rand"),        # odd vector: last byte never written
+    ("rs8", 64, 32, 1400, 64, list(range(3, 64, 4)), True, "rand"),        # the headline shape, 16 lost
+    ("rs8", 64, 32, 1400, 64, [0, 5, 63, 64, 70, 95], True, "rand"),      # source + parity lost
+    ("rs8", 64, 16, 1408, 40, [1, 2, 39, 40, 55], True, "rand"),          # shortened block, vec = 1400 + 8
+    ("rs8", 16, 4, 64, 16, [0, 1, 2, 3, 4], False, "rand"),               # more erasures than parity -> 0
+    ("mdp", 64, 32, 1400, 64, list(range(5, 64, 6)) + [70], True, "rand"),
+    ("mdp", 16, 4, 33, 12, [2, 7, 13], True, "rand"),
+]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind,k,m,vec,nd,locs,nullpar,src", CASES)
+def test_fectest_matches_oracle(orc, tmp_path, kind, k, m, vec, nd, locs, nullpar, src):
+    n = nd + m
+    if src == "-":
+        data = np.zeros((nd, vec), np.uint8)
+        for i in range(nd):
+            data[i, : vec - 1] = ord("a") + i % 26
+        inp = "-"
+    else:
+        data = np.random.default_rng(nd * 131 + m).integers(0, 256, (nd, vec), dtype=np.uint8)
+        inp = str(tmp_path / "in.bin")
+        data.tofile(inp)
+    out = tmp_path / "out.bin"
+    r = subprocess.run([EXE, kind, str(k), str(m), str(vec), str(nd), inp, str(out), str(int(nullpar))]
+                       + [str(x) for x in locs], capture_output=True, text=True, timeout=120)
+    dump = np.fromfile(out, np.uint8)
+    assert dump.size == 2 * n * vec + 4, r.stderr
+    tx = dump[: n * vec].reshape(n, vec)
+    status = int(dump[n * vec: n * vec + 4].view(np.int32)[0])
+    rx = dump[n * vec + 4:].reshape(n, vec)
+
+    # oracle: the same block through the reference call pattern
+    blocks = np.zeros((1, k + m, vec), np.uint8)
+    blocks[0, :nd] = data
+    nda = np.array([nd], np.uint16)
+    kid = KINDS[kind]
+    ref = orc.encode_blocks(kid, k, m, vec, blocks.copy(), nda)
+    assert np.array_equal(tx, ref[0, :n]), "parity differs from the oracle's Encode"
+    want = ref.copy()
+    for s in locs:
+        want[0, s] = 0
+    el = np.zeros((1, m + len(locs)), np.uint16)
+    el[0, : len(locs)] = locs
+    st_ref = orc.decode_blocks(kid, k, m, vec, want, el, np.array([len(locs)], np.uint16), nda)
+    assert status == int(st_ref[0])
+    # source slots: repaired (or left as received); parity slots are never written by Decode
+    assert np.array_equal(rx[:nd], want[0, :nd])
+    got_par = rx[nd:]
+    exp_par = ref[0, nd:n].copy()
+    for s in locs:
+        if s >= nd:
+            exp_par[s - nd] = 0
+    assert np.array_equal(got_par, exp_par)
+    if status:
+        assert r.returncode == 0, r.stderr
+        assert np.array_equal(rx[:nd], data)

@@ -183,6 +183,30 @@ def test_decode_shortened_blocks(orc, kind):
 
 
 @pytest.mark.parametrize("kind", [NFEC_RS8, NFEC_RS16])
+def test_decode_shortened_many_erasures_generic_plan(orc, kind):
+    """RS8 and RS16 through the generic plan with 65..255 erasures per block and per-block
+    numData: the log-domain elimination with its lists in the block's global scratch
+    (min(k, m) > 64), shortened-block column offsets included."""
+    k, m, vec, nb = 128, 127, 72, 4
+    nd = np.array([128, 100, 90, 127], np.uint16)
+    enc, dec = _codecs(kind, k, m, vec)
+    host = orc.encode_blocks(kind, k, m, vec, orc.make_blocks(k, m, vec, nb, num_data=nd), nd)
+    locs, counts = _erasures(orc, kind, k, m, nb, 90, 20, num_data=nd, seed_off=77)
+    assert counts.min() >= 65 and counts.max() <= m
+    _erase(host, locs, counts)
+    ref = host.copy()
+    st_ref = orc.decode_blocks(kind, k, m, vec, ref, locs, counts, nd)
+    assert (st_ref == counts).all()
+    dev = torch.from_numpy(host).cuda()
+    st = dec.decode_blocks(dev, torch.from_numpy(locs.astype(np.int16)).cuda(),
+                           torch.from_numpy(counts.astype(np.int16)).cuda(),
+                           num_data=torch.from_numpy(nd.astype(np.int16)).cuda())
+    torch.cuda.synchronize()
+    assert np.array_equal(st.cpu().numpy(), st_ref)
+    assert np.array_equal(dev.cpu().numpy(), ref)
+
+
+@pytest.mark.parametrize("kind", [NFEC_RS8, NFEC_RS16])
 def test_decode_accumulates_into_nonzero_erased_buffers(orc, kind):
     """Reference Decode XORs the repair into the erased buffer; with a non-zeroed buffer
     the output is junk ^ data, and the accumulate flag reproduces it byte for byte."""

@@ -173,3 +173,73 @@ def test_mixed_full_and_short_blocks(orc):
     for b in range(nb):
         for s in range(int(nd[b])):
             assert np.array_equal(segs[b][s][:vec], want[b, s, :vec]), (b, s)
+
+
+def test_async_receiver_two_senders_interleaved(orc):
+    """Receiver-side cross-block batching: blocks from two remote senders (one
+    decoder each, normNode.h:649; RS8(64,32) and RS16(100,20)) are submitted asynchronously in
+    interleaved batches, the caller keeps going, and every completion is checked against the
+    oracle.  Submission order is kept per codec; the two codecs run concurrently."""
+    senders = [(N.NFEC_RS8, 64, 32, 1400, 16, 2), (N.NFEC_RS16, 100, 20, 1400, 12, 3)]
+    rng = np.random.default_rng(21)
+    state = []
+    for i, (kind, k, m, vec, es, ep) in enumerate(senders):
+        nb = 96
+        clean = orc.encode_blocks(kind, k, m, vec, orc.make_blocks(k, m, vec, nb, first_block=500 * i))
+        locs = np.zeros((nb, m), np.uint16)
+        counts = np.full(nb, es + ep, np.uint16)
+        rx = clean.copy()
+        for b in range(nb):
+            e = np.sort(np.concatenate([rng.choice(k, es, replace=False), k + rng.choice(m, ep, replace=False)]))
+            locs[b, :es + ep] = e
+            rx[b, e] = 0
+        ref = rx.copy()
+        st_ref = orc.decode_blocks(kind, k, m, vec, ref, locs, counts)
+        segs = _scatter(rx, vec, np.full(nb, k), m, rng)
+        for b in range(nb):
+            for s in locs[b, :counts[b]]:
+                if s >= k:
+                    segs[b][s] = None
+        _, dec = _codecs(kind, k, m, vec)
+        state.append(dict(k=k, vec=vec, segs=segs, locs=locs, counts=counts, ref=ref, st_ref=st_ref, dec=dec))
+    # interleave: sender 0 blocks [0,32), sender 1 [0,32), sender 0 [32,96), sender 1 [32,96)
+    reqs = []
+    for lo, hi in ((0, 32), (32, 96)):
+        for i, s in enumerate(state):
+            reqs.append((i, lo, hi, s["dec"].decode_vectors_host_async(
+                s["segs"][lo:hi], s["locs"][lo:hi], s["counts"][lo:hi])))
+    polled = [r.test() for _, _, _, r in reqs]  # non-blocking; any mix of done/pending is valid
+    assert all(isinstance(p, bool) for p in polled)
+    for i, lo, hi, r in reqs:
+        st = r.wait()
+        s = state[i]
+        assert np.array_equal(st, s["st_ref"][lo:hi])
+        for b in range(lo, hi):
+            for q in range(s["k"]):
+                assert np.array_equal(s["segs"][b][q][:s["vec"]], s["ref"][b, q, :s["vec"]]), (i, b, q)
+
+
+def test_async_encode_then_decode_same_codec_pair(orc):
+    """Async encode of segment lists, then async decode of a damaged copy: per-codec order and
+    completion through nfec_request_wait."""
+    k, m, vec, nb = 64, 16, 1400, 40
+    rng = np.random.default_rng(3)
+    host = orc.make_blocks(k, m, vec, nb)
+    ref = orc.encode_blocks(N.NFEC_RS8, k, m, vec, host.copy())
+    segs = _scatter(host, vec, np.full(nb, k), m, rng)
+    enc, dec = _codecs(N.NFEC_RS8, k, m, vec)
+    assert enc.encode_vectors_host_async(segs).wait() is None
+    for b in range(nb):
+        for s in range(k + m):
+            assert np.array_equal(segs[b][s][:vec], ref[b, s, :vec])
+    locs = np.zeros((nb, m), np.uint16)
+    counts = np.full(nb, 16, np.uint16)
+    for b in range(nb):
+        locs[b] = np.sort(rng.choice(k, 16, replace=False))
+        for s in locs[b]:
+            segs[b][s][:vec] = 0
+    st = dec.decode_vectors_host_async(segs, locs, counts).wait()
+    assert (st == 16).all()
+    for b in range(nb):
+        for s in range(k):
+            assert np.array_equal(segs[b][s][:vec], ref[b, s, :vec])

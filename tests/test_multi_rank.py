@@ -11,7 +11,7 @@ import numpy as np
 import pytest
 import torch.multiprocessing as mp
 
-from norm_amd.dist import block_range
+from norm_amd.dist import block_range, shard
 
 
 def test_block_range_partition():
@@ -25,6 +25,16 @@ def test_block_range_partition():
             assert max(sizes) - min(sizes) <= 1
 
 
+def test_shard_weak_and_strong():
+    # weak: every rank its own fixed share; strong: one fixed total split contiguously
+    assert [shard(100, 4, r) for r in range(4)] == [(0, 100), (100, 100), (200, 100), (300, 100)]
+    got = [shard(65536, 8, r, strong=True) for r in range(8)]
+    assert sum(n for _, n in got) == 65536 and got[0][0] == 0
+    assert all(a + n == b for (a, n), (b, _) in zip(got, got[1:]))
+    with pytest.raises(ValueError):
+        shard(10, 2, 2)
+
+
 def _free_port():
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
@@ -33,18 +43,21 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, strong=True):
     import hashlib
 
     import torch.distributed as dist
 
-    from norm_amd.dist import max_over_ranks
+    from norm_amd.dist import env_ranks, max_over_ranks
     from oracle import pyoracle as orc
 
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(world), RANK=str(rank))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     k, m, vec, total = 16, 4, 48, 10
-    lo, hi = block_range(total, world, rank)
+    # the partition bench.py --strong uses (total fixed) or its default weak one (total/world each)
+    w, r, _ = env_ranks()
+    lo, nb = shard(total if strong else total // world, w, r, strong)
+    hi = lo + nb
     blocks = orc.make_blocks(k, m, vec, hi - lo, first_block=lo)
     orc.encode_blocks(orc.RS8, k, m, vec, blocks)
     digest = hashlib.sha256(blocks[:, k:].tobytes()).hexdigest()
@@ -56,14 +69,15 @@ def _worker(rank, world, port, q):
     q.put((rank, gathered, mx))
 
 
-def test_two_rank_gloo_striping(orc):
+@pytest.mark.parametrize("strong", [True, False])
+def test_two_rank_gloo_striping(orc, strong):
     import hashlib
 
     world = 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, strong)) for r in range(world)]
     for p in procs:
         p.start()
     results = [q.get(timeout=120) for _ in range(world)]
