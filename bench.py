@@ -34,6 +34,8 @@ def encode_kernel_name(k, m, vec):
     if (k, m) not in ((64, 32), (64, 16), (64, 8)) or os.environ.get("NFEC_FORCE_GENERIC", "0") not in ("", "0"):
         return "gf8_matmul_kernel (RS8 encode, generic)"
     if os.environ.get("NFEC_ASM", "1") != "0" and vec % 8 == 0:
+        if os.environ.get("NFEC_Q4", "1") != "0":
+            return f"nfec::rs8_q4_enc_k{k}_m{m} (RS8 encode, 4 role waves sharing each column's transpose through LDS)"
         return f"nfec::rs8_asm_enc_k{k}_m{m} (RS8 encode, hand-allocated assembly body)"
     return f"nfec::rs8_enc_k{k}_m{m} (RS8 encode, compiler-allocated)"
 

@@ -163,6 +163,12 @@ __device__ __forceinline__ uint32_t wg_index(uint32_t remap)
     return x < r ? x * (q + 1) + i : r * (q + 1) + (x - r) * q + i;
 }
 
+// LDS byte address (what ds_read/ds_write take) of a __shared__ object
+__device__ __forceinline__ uint32_t lds_addr(const void* p)
+{
+    return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
+}
+
 struct DecItems {
     const uint8_t* wbase;   // uniform: slot 0 of the wave's first block
     __amdgpu_buffer_rsrc_t rs;   // num_records = 2^31: offsets with bit 31 set read as zero
@@ -277,6 +283,9 @@ int launch_rs8_bitsliced_encode(uint32_t k, uint32_t m, const bs::EncArgs& a, hi
 int launch_rs8_asm_encode(uint32_t k, uint32_t m, const bs::EncArgs& a, hipStream_t s);
 // gen_rs8_asm.hip: MDP encode of full blocks with the same assembly bodies (NFEC_ENOTSUP otherwise)
 int launch_mdp_asm_encode(uint32_t k, uint32_t m, const bs::EncArgs& a, hipStream_t s);
+// gen_rs8_q4.hip: 4 role waves per workgroup sharing each column's transpose through LDS
+int launch_rs8_q4_encode(uint32_t k, uint32_t m, const bs::EncArgs& a, hipStream_t s);
+int launch_mdp_q4_encode(uint32_t k, uint32_t m, const bs::EncArgs& a, hipStream_t s);
 int launch_rs8_bitsliced_reencode(uint32_t k, uint32_t m, const bs::DecArgs& a, hipStream_t s);
 int bitsliced_encode_generator(uint32_t k, uint32_t m, uint8_t* out);
 

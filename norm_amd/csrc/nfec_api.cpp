@@ -426,6 +426,17 @@ static uint32_t bs_flags()
     return f;
 }
 
+// NFEC_Q4=0 disables the 4-role-wave encode kernels (gen_rs8_q4.hip; A/B runs), falling
+// back to the 2-role assembly kernels
+static bool use_q4()
+{
+    static const bool v = [] {
+        const char* e = std::getenv("NFEC_Q4");
+        return !(e && *e == '0');
+    }();
+    return v;
+}
+
 static bool use_asm()
 {
     static const bool v = [] {
@@ -452,7 +463,12 @@ int encode_device(nfec_codec* c, const nfec_block_batch* b, hipStream_t s)
         e.accumulate = acc;
         e.xcd_remap = bs_flags() & 1u;
         e.nt_store = (bs_flags() >> 1) & 1u;
-        // hand-allocated assembly kernels first (NFEC_ASM=0 disables them for A/B runs)
+        // hand-allocated assembly kernels first (NFEC_ASM=0 disables them for A/B runs): the
+        // 4-role-wave kernels sharing each column's transpose, then the 2-role kernels
+        if (use_asm() && use_q4()) {
+            const int rc = launch_rs8_q4_encode(c->k, c->m, e, s);
+            if (rc != NFEC_ENOTSUP) return rc == NFEC_OK ? NFEC_OK : fail(rc, "q4 encode launch failed");
+        }
         if (use_asm()) {
             const int rc = launch_rs8_asm_encode(c->k, c->m, e, s);
             if (rc != NFEC_ENOTSUP) return rc == NFEC_OK ? NFEC_OK : fail(rc, "assembly encode launch failed");
@@ -540,6 +556,10 @@ int encode_device(nfec_codec* c, const nfec_block_batch* b, hipStream_t s)
         e.accumulate = 0;
         e.xcd_remap = bs_flags() & 1u;
         e.nt_store = (bs_flags() >> 1) & 1u;
+        if (use_q4()) {
+            const int rc = launch_mdp_q4_encode(c->k, c->m, e, s);
+            if (rc != NFEC_ENOTSUP) return rc == NFEC_OK ? NFEC_OK : fail(rc, "MDP q4 encode launch failed");
+        }
         const int rc = launch_mdp_asm_encode(c->k, c->m, e, s);
         if (rc != NFEC_ENOTSUP) return rc == NFEC_OK ? NFEC_OK : fail(rc, "MDP assembly encode launch failed");
     }

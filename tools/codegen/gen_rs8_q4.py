@@ -1,0 +1,355 @@
+#!/usr/bin/env python3
+"""Generate norm_amd/csrc/gen_rs8_q4.hip: bit-sliced RS8 (and full-block MDP) encode kernels in
+which FOUR role waves share every source column's bit transpose through LDS.
+
+Same arithmetic as gen_rs8_asm.py (8x8 bit transpose per source column, method of four
+Russians over the constant generator of NormEncoderRS8, src/common/normEncoderRS8.cpp:400-462,
+one v_bitop3 per parity bit-plane and column), different work split:
+
+  * a workgroup is 4 waves over the same 256 items (8 bytes each, 32 bytes per lane); wave w
+    owns parity rows [w*m/4, (w+1)*m/4): m/4 x 8 plane accumulators (64 VGPRs at m = 32);
+  * source columns are dealt round-robin: in step s wave w loads column 4s+w (a 2-slot VGPR
+    ring, buffer loads), transposes it (48 VALU) and writes its 8 planes to an LDS slot
+    (4 x ds_write_b64); after one s_barrier every wave reads the other three columns' planes
+    back (ds_read_b64, double-buffered) and applies all four columns to its rows;
+  * the transpose is done once per column instead of once per role, and the register file
+    fits in 128 VGPRs, so 4 waves per SIMD are resident (the 2-role kernel holds 256 VGPRs:
+    2 waves per SIMD, and its VALU and memory phases overlap badly).
+
+VGPR banks (index mod 4; a VOP3 whose operands share a bank stalls): accumulators in banks 2/3
+of quads 0..31, everything a bitop3 reads besides the accumulator in banks 0/1 -- M4RM group A
+(even planes and their combinations) in bank 0, group B (odd planes) in bank 1.  A
+buffer_load_dwordx2 / ds_read_b64 into the aligned pair (4P, 4P+1) lands dword/plane pair
+(2q, 2q+1) in banks (0, 1); the in-place transpose leaves plane b in dword b's register.
+
+Usage: gen_rs8_q4.py OUT.hip
+"""
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from gen_rs8_asm import MASKS, mdp_matrix, split, transpose  # noqa: E402
+from gen_rs8_bitsliced import bitmatrix_rows, generator  # noqa: E402
+
+SHAPES = [(64, 32), (64, 16), (64, 8)]
+MDP_SHAPES = [(64, 32), (64, 16)]
+NW = 4                       # role waves per workgroup (share each column's transpose)
+MULTI = [a for a in range(1, 16) if bin(a).count("1") >= 2]   # 11 combination indices
+
+# ---- register map (v0..v127) ----
+IN_REGS = [0, 1, 4, 5, 8]    # left to the compiler: 4 item offsets + the lane's LDS address
+COMBO_Q0 = 3                 # combos: quads 3..13, A at 4q (bank 0), B at 4q+1 (bank 1)
+RING_Q0 = 14                 # 2 ring slots x 4 quads: quads 14..21
+P_Q0 = 22                    # 2 LDS plane buffers x 4 quads: quads 22..29
+NQUAD = 32
+S_LRS, S_SRS = 64, 68        # load / store buffer descriptors
+S_MASK = 72                  # s72..s77 transpose masks (gen_rs8_asm.transpose reads them here)
+S_COL, S_ROW = 78, 79
+SLOT_BYTES = NW * 4 * 512    # one LDS slot: 4 columns x 4 plane pairs x 64 lanes x 8 bytes
+# A/B probes of the (64, 32) kernel, NFEC_Q4_VARIANT=<id> (never the default): VALU + LDS only
+# (no source loads), memory only (loads and stores, no arithmetic, no LDS), no LDS exchange
+# (every wave reuses its own column's planes: the cost of the exchange and its barrier)
+PROBES = {8: "noload", 9: "nocompute", 10: "nolds"}
+
+
+def acc_reg(r, i):
+    return 4 * (4 * r + i // 2) + 2 + (i & 1)
+
+
+def combo_reg(group, a):
+    return 4 * (COMBO_Q0 + MULTI.index(a)) + group
+
+
+def quad_planes(q0):
+    """w[d], d = 0..7, of the 4 quads starting at q0 (pairs (4q, 4q+1))."""
+    w = []
+    for q in range(4):
+        w += [4 * (q0 + q), 4 * (q0 + q) + 1]
+    return w
+
+
+def ring_slot(s):
+    return quad_planes(RING_Q0 + 4 * s)
+
+
+def pbuf(b):
+    return quad_planes(P_Q0 + 4 * b)
+
+
+def combo_temps():
+    """transpose temporaries (4 per bank per stage) from the combination registers, which are
+    dead while a column is transposed"""
+    def make():
+        avail = {0: [combo_reg(0, MULTI[i]) for i in range(4)], 1: [combo_reg(1, MULTI[i]) for i in range(4)]}
+
+        def pick(avoid):
+            return avail[1 if avoid == 0 else 0].pop(0)
+        return pick
+    return make
+
+
+def epi_temps():
+    """temporaries for an accumulator transpose (accs in banks 2/3): ring/P/combo registers"""
+    def make():
+        free = ring_slot(0) + ring_slot(1) + pbuf(0) + pbuf(1)
+
+        def pick(avoid):
+            for i, r in enumerate(free):
+                if r % 4 != avoid:
+                    return free.pop(i)
+            raise RuntimeError("no temp")
+        return pick
+    return make
+
+
+def combos(w, need):
+    """the multi-plane combinations needed for this column (group A = w[0,2,4,6] in bank 0,
+    group B = w[1,3,5,7] in bank 1); returns (code, {a: reg} for A, {b: reg} for B)"""
+    code = []
+    tabs = []
+    for g in (0, 1):
+        single = [w[2 * t + g] for t in range(4)]
+        built = {1 << t: single[t] for t in range(4)}
+        for a in sorted({a for a in need[g] if a in MULTI}, key=lambda a: bin(a).count("1")):
+            dst = combo_reg(g, a)
+            top = a.bit_length() - 1
+            rest = a & ~(1 << top)
+            if rest in built:
+                code.append(f"v_xor_b32 v{dst}, v{built[rest]}, v{single[top]}")
+            else:
+                bits = [t for t in range(4) if (a >> t) & 1]
+                code.append(f"v_bitop3_b32 v{dst}, v{single[bits[0]]}, v{single[bits[1]]}, v{single[bits[2]]} bitop3:0x96")
+                if len(bits) == 4:
+                    code.append(f"v_xor_b32 v{dst}, v{dst}, v{single[bits[3]]}")
+            built[a] = dst
+        tabs.append(built)
+    return code, tabs[0], tabs[1]
+
+
+def column_code(G, r0, rows, j, w, first):
+    """updates of rows [r0, r0+rows) by source column j whose planes are in w[0..7]"""
+    mats = [bitmatrix_rows(G[r0 + r][j]) for r in range(rows)]
+    ups, need = [], [set(), set()]
+    for r in range(rows):
+        for i in range(8):
+            a, b = split(mats[r][i])
+            ups.append((acc_reg(r, i), a, b))
+            if a:
+                need[0].add(a)
+            if b:
+                need[1].add(b)
+    code, A, B = combos(w, need)
+    for acc, a, b in ups:
+        if first:
+            if a and b:
+                code.append(f"v_xor_b32 v{acc}, v{A[a]}, v{B[b]}")
+            elif a or b:
+                code.append(f"v_mov_b32 v{acc}, v{A[a] if a else B[b]}")
+            else:
+                code.append(f"v_mov_b32 v{acc}, 0")
+        elif a and b:
+            code.append(f"v_bitop3_b32 v{acc}, v{acc}, v{A[a]}, v{B[b]} bitop3:0x96")
+        elif a:
+            code.append(f"v_xor_b32 v{acc}, v{A[a]}, v{acc}")
+        elif b:
+            code.append(f"v_xor_b32 v{acc}, v{B[b]}, v{acc}")
+    return code
+
+
+def lds_off(slot, c, i):
+    return ((slot * NW + c) * 4 + i) * 512
+
+
+def role_asm(G, k, m, w, probe=None):
+    noload, nocompute, nolds = probe == "noload", probe == "nocompute", probe == "nolds"
+    rows = m // NW
+    r0 = w * rows
+    steps = k // NW
+    L = []
+    L.append(f"s_mov_b64 s[{S_LRS}:{S_LRS + 1}], %[ib]")
+    L.append(f"s_mov_b32 s{S_LRS + 2}, 0x80000000")   # offsets with bit 31 set read as zero
+    L.append(f"s_mov_b32 s{S_LRS + 3}, 0x00020000")
+    L.append(f"s_mov_b64 s[{S_SRS}:{S_SRS + 1}], %[ob]")
+    L.append(f"s_mov_b32 s{S_SRS + 2}, 0x80000000")   # ... and stores there are dropped
+    L.append(f"s_mov_b32 s{S_SRS + 3}, 0x00020000")
+    for i, mk in enumerate(MASKS):
+        L.append(f"s_mov_b32 s{S_MASK + i}, 0x{mk:08x}")
+    offs = ["%[o0]", "%[o1]", "%[o2]", "%[o3]"]
+
+    def loads(step):
+        if noload:
+            return []
+        col = NW * step + w
+        rs = ring_slot(step % 2)
+        out = [f"s_mul_i32 s{S_COL}, %[ss], {col}"]
+        for q in range(4):
+            out.append(f"buffer_load_dwordx2 v[{rs[2 * q]}:{rs[2 * q + 1]}], {offs[q]}, s[{S_LRS}:{S_LRS + 3}], s{S_COL} offen")
+        return out
+
+    L += loads(0)
+    if steps > 1:
+        L += loads(1)
+    for s in range(steps):
+        slot = s % 2
+        own = ring_slot(slot)
+        pending_next = s + 1 < steps  # step s+1's loads are in flight behind ours
+        if not noload:
+            L.append(f"s_waitcnt vmcnt({4 if pending_next else 0})")
+        if nocompute:
+            for i in range(8):  # keep the loaded data live
+                L.append(f"v_xor_b32 v{acc_reg(0, i)}, v{own[i]}, v{acc_reg(0, i)}")
+            if s + 2 < steps:
+                L += loads(s + 2)
+            continue
+        L += transpose(own, combo_temps())
+        if nolds:
+            for c in range(NW):
+                L += column_code(G, r0, rows, NW * s + c, own, first=(s == 0 and c == 0))
+            if s + 2 < steps:
+                L += loads(s + 2)
+            continue
+        for i in range(4):
+            L.append(f"ds_write_b64 %[la], v[{own[2 * i]}:{own[2 * i + 1]}] offset:{lds_off(slot, w, i)}")
+        L += column_code(G, r0, rows, NW * s + w, own, first=(s == 0))
+        if s + 2 < steps:
+            L += loads(s + 2)
+        L.append("s_waitcnt lgkmcnt(0)")
+        L.append("s_barrier")
+        others = [(w + d) % NW for d in range(1, NW)]
+
+        def reads(c, buf):
+            p = pbuf(buf)
+            return [f"ds_read_b64 v[{p[2 * i]}:{p[2 * i + 1]}], %[la] offset:{lds_off(slot, c, i)}" for i in range(4)]
+
+        L += reads(others[0], 0)
+        L += reads(others[1], 1)
+        for t, c in enumerate(others):
+            buf = t % 2
+            more = t + 1 < len(others)  # the next column's reads are in flight
+            L.append(f"s_waitcnt lgkmcnt({4 if more else 0})")
+            L += column_code(G, r0, rows, NW * s + c, pbuf(buf), first=False)
+            if t + 2 < len(others):
+                L += reads(others[t + 2], buf)
+    # epilogue: planes back to bytes, optional accumulate, store
+    for r in range(rows):
+        acc = [acc_reg(r, i) for i in range(8)]
+        L += transpose(acc, epi_temps())
+        L.append(f"s_mul_i32 s{S_ROW}, %[ss], {k + r0 + r}")
+        tmp = ring_slot(0)
+        L.append("s_cmp_eq_u32 %[acc], 0")
+        L.append(f"s_cbranch_scc1 Lnoacc_{r}_%=")
+        for q in range(4):
+            L.append(f"buffer_load_dwordx2 v[{tmp[2 * q]}:{tmp[2 * q + 1]}], {offs[q]}, s[{S_SRS}:{S_SRS + 3}], s{S_ROW} offen")
+        L.append("s_waitcnt vmcnt(0)")
+        for q in range(4):
+            L.append(f"v_xor_b32 v{acc[2 * q]}, v{tmp[2 * q]}, v{acc[2 * q]}")
+            L.append(f"v_xor_b32 v{acc[2 * q + 1]}, v{tmp[2 * q + 1]}, v{acc[2 * q + 1]}")
+        L.append(f"Lnoacc_{r}_%=:")
+        for q in range(4):
+            L.append(f"buffer_store_dwordx2 v[{acc[2 * q]}:{acc[2 * q + 1]}], {offs[q]}, s[{S_SRS}:{S_SRS + 3}], s{S_ROW} offen")
+    return L
+
+
+def clobbers():
+    v = [f'"v{i}"' for i in range(4 * NQUAD) if i not in IN_REGS]
+    s = [f'"s{i}"' for i in range(S_LRS, S_ROW + 1)]
+    return ", ".join(v + s + ['"scc"', '"memory"'])
+
+
+def gen_kernel(k, m, G=None, prefix="rs8_q4_enc", probe=None, suffix=""):
+    assert k % NW == 0 and m % NW == 0
+    G = G if G is not None else generator(k, m)
+    K = f"{prefix}{suffix}_k{k}_m{m}"
+    out = []
+    for w in range(NW):
+        body = role_asm(G, k, m, w, probe)
+        s = "\\n\"\n        \"".join(body)
+        out.append(f"""__device__ __forceinline__ void {K}_role{w}(const bs::EncArgs& a, const bs::Items& it, const uint32_t o[4], uint32_t la)
+{{
+    asm volatile(
+        "{s}\\n"
+        :
+        : [ib] "s"(it.wbase), [ob] "s"(it.obase), [ss] "s"(a.seg_stride), [acc] "s"(a.accumulate),
+          [o0] "v"(o[0]), [o1] "v"(o[1]), [o2] "v"(o[2]), [o3] "v"(o[3]), [la] "v"(la)
+        : {clobbers()});
+}}""")
+    body = [f"__global__ __launch_bounds__({64 * NW}, {NW}) void {K}(bs::EncArgs a)", "{"]
+    body.append(f"    __shared__ uint32_t lds[{2 * SLOT_BYTES // 4}];")
+    body.append("    const uint32_t lane = threadIdx.x & 63;")
+    body.append("    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);")
+    body.append("    bs::Items it;")
+    body.append("    bs::make_items(a, bs::wg_index(a.xcd_remap) * 256u, lane, it);")
+    body.append("    // out-of-range items: loads read zero, stores are dropped (bit 31 past num_records)")
+    body.append("    uint32_t o[4];")
+    body.append("#pragma unroll")
+    body.append("    for (int i = 0; i < 4; ++i) o[i] = it.nbytes[i] == 8 ? it.off[i] : 0x80000000u;")
+    body.append("    const uint32_t la = bs::lds_addr(lds) + lane * 8u;")
+    for w in range(NW):
+        kw = "if" if w == 0 else "else if"
+        body.append(f"    {kw} (wave == {w}) {K}_role{w}(a, it, o, la);")
+    body.append("}")
+    out.append("\n".join(body))
+    out.append(f"""
+static int launch_{K}(const bs::EncArgs& a, hipStream_t s)
+{{
+    const uint64_t items = (uint64_t)a.nblocks * ((a.vec + 7) / 8);
+    if (a.num_data || (a.vec & 7u) || a.nt_store || items >= (1ull << 31) ||
+        !bs::offsets_fit(a.block_stride, a.seg_stride))
+        return NFEC_ENOTSUP;
+    const uint64_t wgs = (items + 255) / 256;
+    hipLaunchKernelGGL({K}, dim3((uint32_t)wgs), dim3({64 * NW}), 0, s, a);
+    return hipGetLastError() == hipSuccess ? NFEC_OK : NFEC_EDEVICE;
+}}""")
+    return "\n\n".join(out)
+
+
+def main():
+    path = sys.argv[1]
+    parts = [
+        "// GENERATED by tools/codegen/gen_rs8_q4.py -- do not edit by hand.",
+        "// Bit-sliced RS8 / MDP encode: 4 role waves per workgroup share each column's transpose",
+        "// through LDS; (k, m) in: " + ", ".join(f"({k},{m})" for k, m in SHAPES),
+        "#include <cstdlib>",
+        '#include "bitslice.hpp"',
+        "",
+        "namespace nfec {",
+        "namespace {",
+    ]
+    for k, m in SHAPES:
+        parts.append(gen_kernel(k, m))
+        if (k, m) == (64, 32):
+            for v, probe in PROBES.items():
+                parts.append(gen_kernel(k, m, probe=probe, suffix=f"_probe_{probe}"))
+    for k, m in MDP_SHAPES:
+        parts.append(gen_kernel(k, m, G=mdp_matrix(k, m), prefix="mdp_q4_enc"))
+    parts.append("}  // namespace")
+    parts.append("")
+    parts.append("static int q4_variant()")
+    parts.append("{")
+    parts.append("    static const int v = [] { const char* e = std::getenv(\"NFEC_Q4_VARIANT\"); return e ? std::atoi(e) : 0; }();")
+    parts.append("    return v;")
+    parts.append("}")
+    parts.append("")
+    parts.append("// NFEC_ENOTSUP when no kernel covers (k, m) or the batch (tails, shortened blocks)")
+    parts.append("int launch_rs8_q4_encode(uint32_t k, uint32_t m, const bs::EncArgs& a, hipStream_t s)")
+    parts.append("{")
+    for v, probe in PROBES.items():
+        parts.append(f"    if (k == 64 && m == 32 && q4_variant() == {v}) return launch_rs8_q4_enc_probe_{probe}_k64_m32(a, s);")
+    for k, m in SHAPES:
+        parts.append(f"    if (k == {k} && m == {m}) return launch_rs8_q4_enc_k{k}_m{m}(a, s);")
+    parts.append("    return NFEC_ENOTSUP;")
+    parts.append("}")
+    parts.append("")
+    parts.append("int launch_mdp_q4_encode(uint32_t k, uint32_t m, const bs::EncArgs& a, hipStream_t s)")
+    parts.append("{")
+    for k, m in MDP_SHAPES:
+        parts.append(f"    if (k == {k} && m == {m}) return launch_mdp_q4_enc_k{k}_m{m}(a, s);")
+    parts.append("    return NFEC_ENOTSUP;")
+    parts.append("}")
+    parts.append("")
+    parts.append("}  // namespace nfec")
+    open(path, "w").write("\n".join(parts) + "\n")
+
+
+if __name__ == "__main__":
+    main()
