@@ -149,3 +149,36 @@ void vperm_table(uint32_t c, uint32_t out[8])
 }
 
 }  // namespace nfec
+
+namespace nfec {
+
+// LDS byte offsets for the shared-table RS16 encode (gen_gf16_t3.hip): coefficient (c, r) is
+// the 16 x 16 GF(2) matrix M of x -> G[r][c] * x (column q = G[r][c] * alpha^q); output plane
+// p XORs input planes q with bit q of row p of M.  Input planes split into groups 0..5,
+// 6..10 and 11..15 whose subset XORs sit in table rows [0, 64), [64, 96), [96, 128), 512 bytes
+// apart: out[(c * m_pad + r) * 48 + p * 3 + g] = (table row) * 512.  Rows r >= m (padding up
+// to gf16_t3_rows_padded) and the one extra column (the kernel prefetches one past the end)
+// point at the zero rows.
+void gf16_t3_offsets(const std::vector<uint32_t>& parity_rows, uint32_t k, uint32_t m, uint16_t* out)
+{
+    const Field& f = gf16();
+    const uint32_t mp = gf16_t3_rows_padded(m);
+    static const uint32_t first[3] = {0, 6, 11}, width[3] = {6, 5, 5}, row0[3] = {0, 64, 96};
+    for (uint32_t c = 0; c <= k; ++c)
+        for (uint32_t r = 0; r < mp; ++r) {
+            const uint32_t g = (c < k && r < m) ? parity_rows[(size_t)r * k + c] : 0u;
+            uint32_t col[16];
+            for (int q = 0; q < 16; ++q) col[q] = f.mul(g, 1u << q);
+            uint16_t* o = out + ((size_t)c * mp + r) * 48;
+            for (int p = 0; p < 16; ++p) {
+                uint32_t mask = 0;
+                for (int q = 0; q < 16; ++q) mask |= ((col[q] >> p) & 1u) << q;
+                for (int t = 0; t < 3; ++t) {
+                    const uint32_t e = (mask >> first[t]) & ((1u << width[t]) - 1u);
+                    o[p * 3 + t] = (uint16_t)((row0[t] + e) * 512u);
+                }
+            }
+        }
+}
+
+}  // namespace nfec

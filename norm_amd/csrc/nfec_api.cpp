@@ -203,6 +203,7 @@ struct nfec_codec {
     DevBuf<uint8_t> d_mdp_step;  // MDP single LFSR step matrix, column-major [m+1][cs]
     DevBuf<uint16_t> d_lwp, d_lw;  // RS8 closed-form plan constants: log W'(x_j), log W(y_p)
     DevBuf<uint16_t> d_sel16;      // RS16 bit-sliced encode table offsets [k][m][64] (may be absent)
+    DevBuf<uint16_t> d_t3off;      // RS16 shared-table encode LDS offsets [k+1][m_pad][48]
 
     // decode workspace (guarded by mu)
     std::mutex mu;
@@ -233,6 +234,7 @@ struct nfec_codec {
         d_lwp.release();
         d_lw.release();
         d_sel16.release();
+        d_t3off.release();
         w_pmap.release();
         w_emask.release();
         w_psel.release();
@@ -268,6 +270,16 @@ int check_batch(const nfec_codec* c, const nfec_block_batch* b)
     if (b->block_stride < (uint64_t)(c->k + c->m) * b->seg_stride && b->nblocks > 1)
         return fail(NFEC_EINVAL, "block_stride smaller than (k+m)*seg_stride");
     return NFEC_OK;
+}
+
+// NFEC_GF16_T3=0 disables the shared-table RS16 encode (A/B runs)
+bool use_gf16_t3()
+{
+    static const bool v = [] {
+        const char* e = std::getenv("NFEC_GF16_T3");
+        return !(e && *e == '0');
+    }();
+    return v;
 }
 
 // ---- codec construction ----
@@ -336,6 +348,15 @@ int build_codec(nfec_codec* c)
             gf16_bs_selectors(c->gen, c->k, c->m, sel.data());
             if ((rc = c->d_sel16.reserve(sel.size()))) return rc;
             NFEC_HIP(hipMemcpy(c->d_sel16.p, sel.data(), sel.size() * 2, hipMemcpyHostToDevice));
+        }
+        // RS16: LDS offsets of the shared-table encode (gen_gf16_t3.hip), 96 bytes per
+        // coefficient (C4, k = 4096, m = 256: 104 MB)
+        if (wide && use_gf16_t3()) {
+            const uint32_t mp = gf16_t3_rows_padded(c->m);
+            std::vector<uint16_t> off((size_t)(c->k + 1) * mp * 48);
+            gf16_t3_offsets(c->gen, c->k, c->m, off.data());
+            if ((rc = c->d_t3off.reserve(off.size()))) return rc;
+            NFEC_HIP(hipMemcpy(c->d_t3off.p, off.data(), off.size() * 2, hipMemcpyHostToDevice));
         }
         if (!wide) {
             // log W'(x_j) over the k source points and log W(y_p) at the parity points
@@ -501,6 +522,21 @@ int encode_device(nfec_codec* c, const nfec_block_batch* b, hipStream_t s)
             const char* e = std::getenv("NFEC_GF16_BS");
             return !(e && e[0] == '0');
         }();
+        if (c->d_t3off.p && !b->num_data) {
+            Gf16T3Args t;
+            t.base = static_cast<const uint8_t*>(b->blocks);
+            t.block_stride = b->block_stride;
+            t.seg_stride = b->seg_stride;
+            t.nblocks = b->nblocks;
+            t.k = c->k;
+            t.m = c->m;
+            t.m_pad = gf16_t3_rows_padded(c->m);
+            t.vec_bytes = c->vec & ~1u;
+            t.offs = c->d_t3off.p;
+            t.accumulate = acc;
+            const int rc = launch_gf16_t3_encode(t, s);
+            if (rc != NFEC_ENOTSUP) return rc;
+        }
         if (use_bs16 && c->d_sel16.p) {
             Gf16BsEncArgs e;
             e.base = static_cast<const uint8_t*>(b->blocks);

@@ -170,6 +170,24 @@ struct Gf16BsEncArgs {
     uint32_t accumulate = 0;
 };
 inline uint32_t gf16_bs_rows_padded(uint32_t m) { return (m + 7u) & ~7u; }
+
+// RS16 encode, bit-sliced with three shared four-Russians tables per column (gen_gf16_t3.hip):
+// one builder wave + 11 row waves of 4 parity rows per workgroup, 44 rows per pass.
+struct Gf16T3Args {
+    const uint8_t* base = nullptr;       // batch (parity written in place, slot k + r)
+    uint64_t block_stride = 0;
+    uint32_t seg_stride = 0;
+    uint32_t nblocks = 0;
+    const uint16_t* num_data = nullptr;  // must be null (unshortened batches only)
+    uint32_t k = 0, m = 0, m_pad = 0;    // m_pad = gf16_t3_rows_padded(m)
+    uint32_t vec_bytes = 0;              // multiple of 8
+    const uint16_t* offs = nullptr;      // [k + 1][m_pad][48] LDS offsets (gf16_t3_offsets)
+    uint32_t accumulate = 0;
+    uint32_t passes = 0;                 // set by the launcher
+};
+inline uint32_t gf16_t3_rows_padded(uint32_t m) { return (m + 43u) / 44u * 44u; }
+int launch_gf16_t3_encode(const Gf16T3Args& a, hipStream_t s);  // NFEC_ENOTSUP: shape not covered
+void gf16_t3_offsets(const std::vector<uint32_t>& parity_rows, uint32_t k, uint32_t m, uint16_t* out);
 int launch_gf16_bs_encode(const Gf16BsEncArgs& a, hipStream_t s);  // NFEC_ENOTSUP: layout not 8-byte aligned
 void gf16_bs_selectors(const std::vector<uint32_t>& parity_rows, uint32_t k, uint32_t m, uint16_t* sel);
 

@@ -1,0 +1,378 @@
+#!/usr/bin/env python3
+"""Generate norm_amd/csrc/gen_gf16_t3.hip: RS16 (GF(2^16)) encode, bit-sliced, with the
+four-Russians tables of each source column built ONCE per workgroup in LDS and shared by 11
+row waves.
+
+The reference multiplies symbol by symbol through log/exp tables (NormEncoderRS16::Encode,
+src/common/normEncoderRS16.cpp:472-482, addmul1 :261-298).  Over GF(2) multiplication by a
+constant c is a 16 x 16 bit matrix M_c, so with the data bit-sliced (plane q = bit q of 32
+symbols) output plane p of c*x is the XOR of the input planes q with bit q of row p of M_c.
+The 16 input planes are split into three groups of 6, 5 and 5 planes; per source column the
+XOR of every subset of each group is tabulated (64 + 32 + 32 rows), so each output plane is
+three table reads and two XORs.  The row of M_c for a plane only picks table rows: the
+generator's coefficients become a precomputed list of LDS offsets (gf16_t3_offsets, 96 bytes
+per coefficient) read by scalar loads.
+
+Workgroup = 12 waves on one item group (64 lanes x 64 symbols: lane L holds 16 pieces of
+8 bytes, piece i at flat position f0 + 512 i + 8 L, so every load is a 512-byte run):
+  * wave 0 (builder) loads source column c+2 (16 x buffer_load_dwordx2 per lane), transposes
+    column c+1 (two 16 x 16 bit transposes: the lane's 64 symbols are 2 x 32), and writes its
+    tables into the LDS buffer (c+1) % 2 (Gray-code order, one XOR per row and half);
+  * waves 1..11 (row waves) each own 4 parity rows (16 planes x 2 halves = 128 accumulator
+    VGPRs) and apply column c from buffer c % 2: per plane three v_add_u32_sdwa address
+    (16-bit offset from the SGPR list + lane base) + ds_read_b64, a bitop3 and a xor per half;
+  * one s_barrier per column; tables 2 x 64 KiB.
+A workgroup covers 44 rows; the grid runs ceil(m / 44) passes per item group.
+
+VGPR banks (index mod 4): the table reads land as pairs (banks 0,1 / 2,3), so half 0 of an
+accumulator sits in an odd bank and half 1 in an even one -- every bitop3 reads three banks.
+
+Usage: gen_gf16_t3.py OUT.hip
+"""
+import sys
+
+ROWS = 4                 # parity rows per row wave
+RWAVES = 11              # row waves per workgroup
+RP = ROWS * RWAVES       # rows per pass
+NWAVES = RWAVES + 1
+GROUPS = [(0, 6, 0), (6, 5, 64), (11, 5, 96)]   # (first plane, planes, first table row)
+TROWS = 128
+BUF = TROWS * 512        # one table buffer: 128 rows x 64 lanes x 8 bytes
+OFF_LDS = 2 * BUF        # piece offsets (epilogue): 64 lanes x 16 dwords
+MASKS = {8: 0x00FF00FF, 4: 0x0F0F0F0F, 2: 0x33333333, 1: 0x55555555}
+
+# ---- SGPRs used inside the asm bodies (clobbered) ----
+S_SB = [36, 60]          # row waves: offsets double buffer, 24 SGPRs each (4-aligned)
+S_DESC = 84              # buffer descriptor (4)
+S_PTR = 88               # row waves: offsets pointer (2)
+S_CNT = 90               # column counter
+S_T0, S_T1 = 91, 92      # scratch
+S_MASK = 36              # s36..s43 transpose masks (builder; row waves: epilogue, over S_SB[0])
+S_LAST = 92
+
+
+# ---- row-wave VGPRs ----
+def acc(r, p, h):
+    """half 0 in an odd bank, half 1 in the even one below it"""
+    return 2 * (16 * r + p) + (1 - h)
+
+
+T_BASE = 128             # 4 planes in flight x (quad tA|tB + pair tC): v128..v151
+A_BASE = 152             # 12 address registers v152..v163
+V_B0, V_B1 = 164, 165    # lane*8 + buffer base (0 / 64 KiB)
+V_LOFF = 166             # lane*64 + OFF_LDS: the lane's piece offsets
+
+
+def row_slot(pp):
+    """(tA, tB, tC) register pairs for plane slot pp (0..3): tA banks (0,1), tB (2,3)"""
+    quad = T_BASE + 4 * pp           # v128, 132, 136, 140: tA = (q, q+1), tB = (q+2, q+3)
+    tc = T_BASE + 16 + 2 * pp        # v144, 146, 148, 150
+    return (quad, quad + 1), (quad + 2, quad + 3), (tc, tc + 1)
+
+
+def transpose16(x, temps):
+    """16 x 16 bit transpose (low and high halves of x[0..15] at once), in place;
+    swapmove stages 8, 4, 2, 1 (kernels_gf16bs.hip transpose16)."""
+    out = []
+    ti = 0
+    for s in (8, 4, 2, 1):
+        mi = {8: 0, 4: 2, 2: 4, 1: 6}[s]
+        for d in range(16):
+            if d & s:
+                continue
+            lo, hi = x[d], x[d + s]
+            tu, tv = temps[ti % len(temps)], temps[(ti + 1) % len(temps)]
+            ti += 2
+            out.append(f"v_lshrrev_b32 v{tu}, {s}, v{lo}")
+            out.append(f"v_lshlrev_b32 v{tv}, {s}, v{hi}")
+            out.append(f"v_bitop3_b32 v{hi}, s{S_MASK + mi}, v{tu}, v{hi} bitop3:0xca")
+            out.append(f"v_bitop3_b32 v{lo}, s{S_MASK + mi + 1}, v{tv}, v{lo} bitop3:0xca")
+    return out
+
+
+def mask_init():
+    out = []
+    for s, mi in ((8, 0), (4, 2), (2, 4), (1, 6)):
+        out.append(f"s_mov_b32 s{S_MASK + mi}, 0x{MASKS[s]:08x}")
+        out.append(f"s_mov_b32 s{S_MASK + mi + 1}, 0x{(MASKS[s] << s) & 0xFFFFFFFF:08x}")
+    return out
+
+
+# ---- builder (wave 0) ----
+B_RING = [0, 32]         # two 32-register data slots: v0..v31, v32..v63
+B_TMP = [64, 65, 66, 67]
+B_CUR = [(68, 69), (70, 71)]   # Gray-code running values (ping-pong), half 0 / half 1
+B_ZERO = (72, 73)
+
+
+def builder_asm():
+    L = []
+    L += [f"s_mov_b64 s[{S_DESC}:{S_DESC + 1}], %[wb]", f"s_mov_b32 s{S_DESC + 2}, 0x80000000",
+          f"s_mov_b32 s{S_DESC + 3}, 0x00020000"]
+    L += mask_init()
+    offs = [f"%[o{i}]" for i in range(16)]
+
+    def loads(slot):
+        # column index in S_T0 (set by the caller): s_T1 = col * seg_stride
+        out = [f"s_mul_i32 s{S_T1}, s{S_T0}, %[ss]"]
+        base = B_RING[slot]
+        for i in range(16):
+            out.append(f"buffer_load_dwordx2 v[{base + 2 * i}:{base + 2 * i + 1}], {offs[i]}, s[{S_DESC}:{S_DESC + 3}], s{S_T1} offen")
+        return out
+
+    def build(slot, buf):
+        """transpose the slot, write its tables into LDS buffer buf"""
+        out = []
+        base = B_RING[slot]
+        halves = [[base + d for d in range(16)], [base + 16 + d for d in range(16)]]
+        for h in (0, 1):
+            out += transpose16(halves[h], B_TMP)
+        lb = "%[lb0]" if buf == 0 else "%[lb1]"
+        for first, n, row0 in GROUPS:
+            prev, k = 0, 0
+            for i in range(1, 1 << n):
+                g = i ^ (i >> 1)
+                q = (g ^ prev).bit_length() - 1
+                dst = B_CUR[k % 2]
+                srcp = B_CUR[(k + 1) % 2]
+                for h in (0, 1):
+                    plane = halves[h][first + q]
+                    if prev == 0:
+                        out.append(f"v_mov_b32 v{dst[h]}, v{plane}")
+                    else:
+                        out.append(f"v_xor_b32 v{dst[h]}, v{srcp[h]}, v{plane}")
+                out.append(f"ds_write_b64 {lb}, v[{dst[0]}:{dst[1]}] offset:{(row0 + g) * 512}")
+                prev, k = g, k + 1
+        return out
+
+    # zero rows of both buffers; piece offsets for the row waves' epilogue
+    L += [f"v_mov_b32 v{B_ZERO[0]}, 0", f"v_mov_b32 v{B_ZERO[1]}, 0"]
+    for lb in ("%[lb0]", "%[lb1]"):
+        for _, _, row0 in GROUPS:
+            L.append(f"ds_write_b64 {lb}, v[{B_ZERO[0]}:{B_ZERO[1]}] offset:{row0 * 512}")
+    # prologue: column 0 -> slot 0 (wait), column 1 -> slot 1 (in flight), build column 0
+    L += [f"s_mov_b32 s{S_T0}, 0"] + loads(0)
+    L += ["s_cmp_gt_u32 %[k], 1", "s_cbranch_scc0 Lb_one_%=", f"s_mov_b32 s{S_T0}, 1"] + loads(1)
+    L += ["s_waitcnt vmcnt(16)", "s_branch Lb_built0_%=", "Lb_one_%=:", "s_waitcnt vmcnt(0)", "Lb_built0_%=:"]
+    L += build(0, 0)
+    # column 2 into the slot column 0 just left
+    L += ["s_cmp_gt_u32 %[k], 2", "s_cbranch_scc0 Lb_no2_%=", f"s_mov_b32 s{S_T0}, 2"] + loads(0) + ["Lb_no2_%=:"]
+    L += ["s_waitcnt lgkmcnt(0)", "s_barrier"]
+    # loop: at column c build c+1 (slot (c+1)%2, buffer (c+1)%2), load c+3 into slot c%2...
+    # unrolled by two so slots and buffers are compile-time: iteration A has c even.
+    L += [f"s_mov_b32 s{S_CNT}, 0"]
+    for par in (0, 1):
+        L.append(f"Lb_it{par}_%=:")
+        nxt = 1 - par                    # slot / buffer of column c+1
+        # done when c == k-1 (nothing left to build); the last barrier still happens
+        L += [f"s_add_u32 s{S_T0}, s{S_CNT}, 1", "s_cmp_ge_u32 s%d, %%[k]" % S_T0, "s_cbranch_scc1 Lb_tail_%="]
+        # data of column c+1 must be in: if column c+2 was issued, 16 loads are younger
+        L += [f"s_add_u32 s{S_T1}, s{S_CNT}, 2", "s_cmp_lt_u32 s%d, %%[k]" % S_T1,
+              f"s_cbranch_scc0 Lb_w0_{par}_%=", "s_waitcnt vmcnt(16)", f"s_branch Lb_w1_{par}_%=",
+              f"Lb_w0_{par}_%=:", "s_waitcnt vmcnt(0)", f"Lb_w1_{par}_%=:"]
+        L += build(nxt, nxt)
+        # column c+3 into slot (c+1)%2 ... no: slot of column c+3 is (c+3)%2 = (c+1)%2, which
+        # holds column c+1 until its tables are written: issue after the build
+        L += [f"s_add_u32 s{S_T0}, s{S_CNT}, 3", "s_cmp_lt_u32 s%d, %%[k]" % S_T0, f"s_cbranch_scc0 Lb_nl_{par}_%="]
+        L += loads(nxt)
+        L.append(f"Lb_nl_{par}_%=:")
+        L += ["s_waitcnt lgkmcnt(0)", "s_barrier", f"s_add_u32 s{S_CNT}, s{S_CNT}, 1"]
+        if par == 0:
+            pass
+        else:
+            L.append("s_branch Lb_it0_%=")
+    L += ["Lb_tail_%=:", "s_waitcnt vmcnt(0)", "s_barrier"]
+    return L
+
+
+def builder_clobbers():
+    v = [f'"v{i}"' for i in range(74)]
+    s = [f'"s{i}"' for i in range(S_DESC, S_LAST + 1)]
+    return ", ".join(v + s + ['"scc"', '"memory"'])
+
+
+# ---- row waves ----
+def row_asm():
+    L = []
+    L += [f"s_mov_b64 s[{S_DESC}:{S_DESC + 1}], %[wb]", f"s_mov_b32 s{S_DESC + 2}, 0x80000000",
+          f"s_mov_b32 s{S_DESC + 3}, 0x00020000"]
+    for r in range(ROWS):
+        for p in range(16):
+            for h in (0, 1):
+                L.append(f"v_mov_b32 v{acc(r, p, h)}, 0")
+    L += [f"s_mov_b64 s[{S_PTR}:{S_PTR + 1}], %[op]"]
+    sb = S_SB
+
+    def sload(dst):
+        return [f"s_load_dwordx8 s[{dst + 8 * i}:{dst + 8 * i + 7}], s[{S_PTR}:{S_PTR + 1}], 0x{32 * i:x}" for i in range(3)]
+
+    def advance(row_in_wave):
+        """move the pointer to the next (column, row): +96 within a column, else to the next
+        column's first row of this wave"""
+        if row_in_wave < ROWS - 1:
+            return [f"s_add_u32 s{S_PTR}, s{S_PTR}, 96", f"s_addc_u32 s{S_PTR + 1}, s{S_PTR + 1}, 0"]
+        return [f"s_add_u32 s{S_PTR}, s{S_PTR}, %[cstep]", f"s_addc_u32 s{S_PTR + 1}, s{S_PTR + 1}, 0"]
+
+    # prologue: offsets of (column 0, row 0)
+    L += sload(sb[0]) + advance(0) + ["s_waitcnt lgkmcnt(0)", "s_barrier", f"s_mov_b32 s{S_CNT}, 0"]
+
+    def column(buf):
+        out = []
+        vb = V_B0 if buf == 0 else V_B1
+        for r in range(ROWS):
+            cur = sb[r % 2]
+            nxt = sb[(r + 1) % 2]
+            for bt in range(4):
+                for pp in range(4):
+                    p = 4 * bt + pp
+                    ta, tb, tc = row_slot(pp)
+                    for g, t in enumerate((ta, tb, tc)):
+                        idx = 3 * p + g
+                        a = A_BASE + 3 * pp + g
+                        out.append(f"v_add_u32_sdwa v{a}, s{cur + idx // 2}, v{vb} dst_sel:DWORD dst_unused:UNUSED_PAD "
+                                   f"src0_sel:WORD_{idx % 2} src1_sel:DWORD")
+                        out.append(f"ds_read_b64 v[{t[0]}:{t[1]}], v{a}")
+                if bt == 1:
+                    # next (column, row) offsets: lands during the remaining batches
+                    out += sload(nxt)
+                    out += advance((r + 1) % ROWS)
+                out.append("s_waitcnt lgkmcnt(0)")
+                for pp in range(4):
+                    p = 4 * bt + pp
+                    ta, tb, tc = row_slot(pp)
+                    for h in (0, 1):
+                        a_ = acc(r, p, h)
+                        out.append(f"v_bitop3_b32 v{a_}, v{a_}, v{ta[h]}, v{tb[h]} bitop3:0x96")
+                    for h in (0, 1):
+                        a_ = acc(r, p, h)
+                        out.append(f"v_xor_b32 v{a_}, v{tc[h]}, v{a_}")
+        return out
+
+    for par in (0, 1):
+        L.append(f"Lr_it{par}_%=:")
+        L += ["s_cmp_ge_u32 s%d, %%[k]" % S_CNT, "s_cbranch_scc1 Lr_done_%="]
+        L += column(par)
+        L += ["s_barrier", f"s_add_u32 s{S_CNT}, s{S_CNT}, 1"]
+        if par == 1:
+            L.append("s_branch Lr_it0_%=")
+    L.append("Lr_done_%=:")
+    # the prefetched offsets load past the last column may still be in flight
+    L.append("s_waitcnt lgkmcnt(0)")
+    L += mask_init()
+    # epilogue: piece offsets from LDS, inverse transposes, stores of valid rows
+    offv = list(range(T_BASE, T_BASE + 16))          # piece offsets v128..v143
+    for i in range(4):
+        L.append(f"ds_read_b128 v[{offv[4 * i]}:{offv[4 * i + 3]}], v{V_LOFF} offset:{16 * i}")
+    L.append("s_waitcnt lgkmcnt(0)")
+    tmp = list(range(144, 152)) + list(range(A_BASE, A_BASE + 12))
+    for r in range(ROWS):
+        L += [f"s_add_u32 s{S_T0}, %[row0], {r}", "s_cmp_ge_u32 s%d, %%[m]" % S_T0, f"s_cbranch_scc1 Lr_skip{r}_%="]
+        L += [f"s_add_u32 s{S_T0}, s{S_T0}, %[k]", f"s_mul_i32 s{S_T1}, s{S_T0}, %[ss]"]
+        for h in (0, 1):
+            x = [acc(r, p, h) for p in range(16)]
+            L += transpose16(x, tmp[:4])
+            for i in range(8):
+                piece = 8 * h + i
+                d0, d1 = tmp[4], tmp[5]
+                L += [f"v_mov_b32 v{d0}, v{x[2 * i]}", f"v_mov_b32 v{d1}, v{x[2 * i + 1]}"]
+                L += ["s_cmp_eq_u32 %[acc], 0", f"s_cbranch_scc1 Lr_na{r}_{piece}_%="]
+                L += [f"buffer_load_dwordx2 v[{tmp[6]}:{tmp[7]}], v{offv[piece]}, s[{S_DESC}:{S_DESC + 3}], s{S_T1} offen",
+                      "s_waitcnt vmcnt(0)", f"v_xor_b32 v{d0}, v{d0}, v{tmp[6]}", f"v_xor_b32 v{d1}, v{d1}, v{tmp[7]}"]
+                L.append(f"Lr_na{r}_{piece}_%=:")
+                L.append(f"buffer_store_dwordx2 v[{d0}:{d1}], v{offv[piece]}, s[{S_DESC}:{S_DESC + 3}], s{S_T1} offen")
+        L.append(f"Lr_skip{r}_%=:")
+    return L
+
+
+def row_clobbers():
+    v = [f'"v{i}"' for i in range(164)]
+    s = [f'"s{i}"' for i in range(S_SB[0], S_LAST + 1)]
+    return ", ".join(v + s + ['"scc"', '"memory"'])
+
+
+def main():
+    path = sys.argv[1]
+    bb = "\\n\"\n        \"".join(builder_asm())
+    rb = "\\n\"\n        \"".join(row_asm())
+    ins = ", ".join(f'[o{i}] "v"(off[{i}])' for i in range(16))
+    src = f"""// GENERATED by tools/codegen/gen_gf16_t3.py -- do not edit by hand.
+// RS16 encode: bit-sliced, three shared four-Russians tables per source column in LDS.
+#include "nfec_internal.hpp"
+#include "bitslice.hpp"
+
+namespace nfec {{
+namespace {{
+
+__global__ __launch_bounds__({64 * NWAVES}, 1) void gf16_t3_encode_kernel(Gf16T3Args a)
+{{
+    __shared__ uint32_t lds[{(OFF_LDS + 64 * 64) // 4}];
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t wg = bs::wg_index(1);
+    const uint32_t group = wg / a.passes, pass = wg - group * a.passes;
+    const uint64_t total = (uint64_t)a.nblocks * a.vec_bytes;   // flat bytes over blocks
+    const uint64_t f0 = (uint64_t)group * 8192u;
+    const uint32_t b0 = __builtin_amdgcn_readfirstlane((uint32_t)(min(f0, total - 1) / a.vec_bytes));
+    const uint8_t* wb = a.base + (uint64_t)b0 * a.block_stride;
+    const uint32_t lbase = bs::lds_addr(lds);
+    if (wave == 0) {{
+        uint32_t off[16];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {{
+            const uint64_t f = f0 + (uint64_t)i * 512u + lane * 8u;
+            const uint32_t b = (uint32_t)(f / a.vec_bytes);
+            const uint32_t p = (uint32_t)(f - (uint64_t)b * a.vec_bytes);
+            off[i] = f < total ? (uint32_t)((uint64_t)(b - b0) * a.block_stride) + p : 0x80000000u;
+        }}
+        uint4* po = reinterpret_cast<uint4*>(lds + {OFF_LDS // 4} + lane * 16);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) po[i] = make_uint4(off[4 * i], off[4 * i + 1], off[4 * i + 2], off[4 * i + 3]);
+        const uint32_t lb0 = lbase + lane * 8u, lb1 = lb0 + {BUF}u;
+        asm volatile(
+        "{bb}\\n"
+        :
+        : [wb] "s"(wb), [ss] "s"(a.seg_stride), [k] "s"(a.k), [lb0] "v"(lb0), [lb1] "v"(lb1), {ins}
+        : {builder_clobbers()});
+    }} else {{
+        const uint32_t row0 = pass * {RP}u + (wave - 1u) * {ROWS}u;
+        const uint8_t* op = reinterpret_cast<const uint8_t*>(a.offs) + (uint64_t)row0 * 96u;
+        const uint32_t cstep = (a.m_pad - {ROWS - 1}u) * 96u;   // last row of a column -> first row of the next
+        const uint32_t vb0 = lbase + lane * 8u, vb1 = vb0 + {BUF}u, vloff = lbase + {OFF_LDS}u + lane * 64u;
+        asm volatile(
+        "{rb}\\n"
+        :
+        : [wb] "s"(wb), [op] "s"(op), [ss] "s"(a.seg_stride), [k] "s"(a.k), [m] "s"(a.m), [row0] "s"(row0),
+          [cstep] "s"(cstep), [acc] "s"(a.accumulate), [vb0] "{{v{V_B0}}}"(vb0), [vb1] "{{v{V_B1}}}"(vb1),
+          [vloff] "{{v{V_LOFF}}}"(vloff)
+        : {row_clobbers()});
+    }}
+}}
+
+}}  // namespace
+
+int launch_gf16_t3_encode(const Gf16T3Args& a, hipStream_t s)
+{{
+    if (a.nblocks == 0) return NFEC_OK;
+    if ((a.vec_bytes & 7u) || a.vec_bytes == 0 || !a.offs || a.num_data ||
+        a.m_pad != (a.m + {RP - 1}u) / {RP}u * {RP}u)
+        return NFEC_ENOTSUP;
+    // every piece offset of a group (8 KiB of flat positions) plus slot offsets within 2^31
+    const uint64_t span = (8192u / a.vec_bytes + 2u) * a.block_stride + (uint64_t)(a.k + a.m) * a.seg_stride;
+    if (span >= (1ull << 31)) return NFEC_ENOTSUP;
+    const uint64_t total = (uint64_t)a.nblocks * a.vec_bytes;
+    Gf16T3Args b = a;
+    b.passes = (a.m + {RP - 1}u) / {RP}u;
+    const uint64_t groups = (total + 8191u) / 8192u;
+    if (groups * b.passes >= (1ull << 31)) return NFEC_ENOTSUP;
+    hipLaunchKernelGGL(gf16_t3_encode_kernel, dim3((uint32_t)(groups * b.passes)), dim3({64 * NWAVES}), 0, s, b);
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? NFEC_OK : hip_fail(e, "gf16 t3 encode launch");
+}}
+
+}}  // namespace nfec
+"""
+    open(path, "w").write(src)
+
+
+if __name__ == "__main__":
+    main()

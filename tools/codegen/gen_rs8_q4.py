@@ -37,19 +37,10 @@ NW = 4                       # role waves per workgroup (share each column's tra
 MULTI = [a for a in range(1, 16) if bin(a).count("1") >= 2]   # 11 combination indices
 
 # ---- register map (v0..v127) ----
-IN_REGS = [0, 1, 4, 5, 8]    # left to the compiler: 4 item offsets + the lane's LDS address
 COMBO_Q0 = 3                 # combos: quads 3..13, A at 4q (bank 0), B at 4q+1 (bank 1)
-RING_Q0 = 14                 # 2 ring slots x 4 quads: quads 14..21
+RING_Q0 = 14                 # ring slots 0, 1: quads 14..21
 P_Q0 = 22                    # 2 LDS plane buffers x 4 quads: quads 22..29
 NQUAD = 32
-S_LRS, S_SRS = 64, 68        # load / store buffer descriptors
-S_MASK = 72                  # s72..s77 transpose masks (gen_rs8_asm.transpose reads them here)
-S_COL, S_ROW = 78, 79
-SLOT_BYTES = NW * 4 * 512    # one LDS slot: 4 columns x 4 plane pairs x 64 lanes x 8 bytes
-# A/B probes of the (64, 32) kernel, NFEC_Q4_VARIANT=<id> (never the default): VALU + LDS only
-# (no source loads), memory only (loads and stores, no arithmetic, no LDS), no LDS exchange
-# (every wave reuses its own column's planes: the cost of the exchange and its barrier)
-PROBES = {8: "noload", 9: "nocompute", 10: "nolds"}
 
 
 def acc_reg(r, i):
@@ -60,6 +51,55 @@ def combo_reg(group, a):
     return 4 * (COMBO_Q0 + MULTI.index(a)) + group
 
 
+class Cfg:
+    """nslot: own-column loads in flight per wave (VGPR ring slots)
+    lazy:  build group-A combinations one at a time, updates grouped by A entry (2 VGPRs
+           instead of 11: room for a third ring slot)
+    share: what a column's owner hands the other waves through LDS -- "planes" (the 8
+           transposed planes; every wave builds the 22 combinations itself), "A" (planes and
+           the 11 group-A combinations), "AB" (all combinations: one slot, two barriers per
+           step)"""
+
+    def __init__(self, nslot=2, lazy=False, share="planes"):
+        self.nslot, self.lazy, self.share = nslot, lazy, share
+        assert share == "planes" or not lazy
+        if lazy:
+            # 4 item offsets + LDS address in freed A-combination registers (bank 0)
+            self.in_regs = [20, 24, 28, 32, 36]
+            self.areg = [12, 16]
+            self.temps = {0: [12, 16, 40, 44], 1: [13, 17, 21, 25]}
+            slot2 = [0, 1, 2, 30]
+        else:
+            self.in_regs = [0, 1, 4, 5, 8] + ([9] if share == "A" else [])
+            self.areg = None
+            self.temps = {0: [combo_reg(0, MULTI[i]) for i in range(4)], 1: [combo_reg(1, MULTI[i]) for i in range(4)]}
+            slot2 = None
+        self.slot_quads = [[RING_Q0 + q for q in range(4)], [RING_Q0 + 4 + q for q in range(4)]]
+        if nslot == 3:
+            assert lazy, "the third ring slot needs the lazy A combinations' registers"
+            self.slot_quads.append(slot2)
+        assert nslot in (2, 3)
+
+    def ring_slot(self, i):
+        w = []
+        for q in self.slot_quads[i]:
+            w += [4 * q, 4 * q + 1]
+        return w
+
+
+DEFAULT = Cfg(2, False)
+# variants of the (64, 32) kernel selectable with NFEC_Q4_VARIANT=<id> for A/B runs
+VARIANTS = {1: Cfg(3, True), 2: Cfg(2, True), 3: Cfg(2, share="A"), 4: Cfg(2, share="AB")}
+S_LRS, S_SRS = 64, 68        # load / store buffer descriptors
+S_MASK = 72                  # s72..s77 transpose masks (gen_rs8_asm.transpose reads them here)
+S_COL, S_ROW = 78, 79
+SLOT_BYTES = NW * 4 * 512    # one LDS slot: 4 columns x 4 plane pairs x 64 lanes x 8 bytes
+# A/B probes of the (64, 32) kernel, NFEC_Q4_VARIANT=<id> (never the default): VALU + LDS only
+# (no source loads), memory only (loads and stores, no arithmetic, no LDS), no LDS exchange
+# (every wave reuses its own column's planes: the cost of the exchange and its barrier)
+PROBES = {8: "noload", 9: "nocompute", 10: "nolds"}
+
+
 def quad_planes(q0):
     """w[d], d = 0..7, of the 4 quads starting at q0 (pairs (4q, 4q+1))."""
     w = []
@@ -68,19 +108,15 @@ def quad_planes(q0):
     return w
 
 
-def ring_slot(s):
-    return quad_planes(RING_Q0 + 4 * s)
-
-
 def pbuf(b):
     return quad_planes(P_Q0 + 4 * b)
 
 
-def combo_temps():
+def combo_temps(cfg):
     """transpose temporaries (4 per bank per stage) from the combination registers, which are
     dead while a column is transposed"""
     def make():
-        avail = {0: [combo_reg(0, MULTI[i]) for i in range(4)], 1: [combo_reg(1, MULTI[i]) for i in range(4)]}
+        avail = {0: list(cfg.temps[0]), 1: list(cfg.temps[1])}
 
         def pick(avoid):
             return avail[1 if avoid == 0 else 0].pop(0)
@@ -88,10 +124,10 @@ def combo_temps():
     return make
 
 
-def epi_temps():
-    """temporaries for an accumulator transpose (accs in banks 2/3): ring/P/combo registers"""
+def epi_temps(cfg):
+    """temporaries for an accumulator transpose (accs in banks 2/3): ring/P registers"""
     def make():
-        free = ring_slot(0) + ring_slot(1) + pbuf(0) + pbuf(1)
+        free = cfg.ring_slot(0) + cfg.ring_slot(1) + pbuf(0) + pbuf(1)
 
         def pick(avoid):
             for i, r in enumerate(free):
@@ -126,7 +162,57 @@ def combos(w, need):
     return code, tabs[0], tabs[1]
 
 
-def column_code(G, r0, rows, j, w, first):
+def update(acc, A, B, a, b, first):
+    if first:
+        if a and b:
+            return f"v_xor_b32 v{acc}, v{A[a]}, v{B[b]}"
+        if a or b:
+            return f"v_mov_b32 v{acc}, v{A[a] if a else B[b]}"
+        return f"v_mov_b32 v{acc}, 0"
+    if a and b:
+        return f"v_bitop3_b32 v{acc}, v{acc}, v{A[a]}, v{B[b]} bitop3:0x96"
+    if a:
+        return f"v_xor_b32 v{acc}, v{A[a]}, v{acc}"
+    if b:
+        return f"v_xor_b32 v{acc}, v{B[b]}, v{acc}"
+    return None
+
+
+def lazy_column(w, ups, need, areg, first):
+    """group-B combinations up front, group-A ones built one at a time into two alternating
+    registers, each followed by the updates that use it"""
+    code, _, B = combos(w, [set(), need[1]])
+    single = [w[2 * t] for t in range(4)]
+    order = sorted({a for _, a, _ in ups}, key=lambda a: (bin(a).count("1"), a))
+    if 15 in order:  # build 15 right after a 3-subset, from it
+        order.remove(15)
+        order.append(15)
+    A = {1 << t: single[t] for t in range(4)}
+    prev, k = None, 0
+    for a in order:
+        if a in MULTI:
+            dst = areg[k % 2]
+            k += 1
+            bits = [t for t in range(4) if (a >> t) & 1]
+            if prev is not None and prev[0] & a == prev[0] and bin(a & ~prev[0]).count("1") == 1:
+                code.append(f"v_xor_b32 v{dst}, v{prev[1]}, v{single[(a & ~prev[0]).bit_length() - 1]}")
+            elif len(bits) == 2:
+                code.append(f"v_xor_b32 v{dst}, v{single[bits[0]]}, v{single[bits[1]]}")
+            else:
+                code.append(f"v_bitop3_b32 v{dst}, v{single[bits[0]]}, v{single[bits[1]]}, v{single[bits[2]]} bitop3:0x96")
+                if len(bits) == 4:
+                    code.append(f"v_xor_b32 v{dst}, v{dst}, v{single[bits[3]]}")
+            A[a] = dst
+            prev = (a, dst)
+        for acc, ua, ub in ups:
+            if ua == a:
+                u = update(acc, A, B, ua, ub, first)
+                if u:
+                    code.append(u)
+    return code
+
+
+def column_code(G, r0, rows, j, w, first, cfg=None):
     """updates of rows [r0, r0+rows) by source column j whose planes are in w[0..7]"""
     mats = [bitmatrix_rows(G[r0 + r][j]) for r in range(rows)]
     ups, need = [], [set(), set()]
@@ -138,6 +224,8 @@ def column_code(G, r0, rows, j, w, first):
                 need[0].add(a)
             if b:
                 need[1].add(b)
+    if cfg is not None and cfg.lazy:
+        return lazy_column(w, ups, need, cfg.areg, first)
     code, A, B = combos(w, need)
     for acc, a, b in ups:
         if first:
@@ -160,8 +248,49 @@ def lds_off(slot, c, i):
     return ((slot * NW + c) * 4 + i) * 512
 
 
-def role_asm(G, k, m, w, probe=None):
+def updates(ups, A, B, first):
+    out = []
+    for acc, a, b in ups:
+        u = update(acc, A, B, a, b, first)
+        if u:
+            out.append(u)
+    return out
+
+
+def column_ups(G, r0, rows, j):
+    mats = [bitmatrix_rows(G[r0 + r][j]) for r in range(rows)]
+    ups, need = [], [set(), set()]
+    for r in range(rows):
+        for i in range(8):
+            a, b = split(mats[r][i])
+            ups.append((acc_reg(r, i), a, b))
+            if a:
+                need[0].add(a)
+            if b:
+                need[1].add(b)
+    return ups, need
+
+
+# ---- shared-combination layouts (Cfg.share "A" / "AB") ----
+A_COL = 4 * 512 + 11 * 256          # "A": per column 4 plane pairs (b64) + 11 A combos (b32)
+
+
+def a_off(slot, c, part, i):
+    """share "A" LDS offsets: part 0 = plane pair i (lane*8 addressing), part 1 = A combo i
+    (lane*4 addressing, stored after the pairs)"""
+    base = (slot * NW + c) * A_COL
+    return base + (i * 512 if part == 0 else 4 * 512 + i * 256)
+
+
+def ab_off(c, i):
+    """share "AB" LDS offsets (one slot): 15 b64 pairs per column -- pairs 0..3 planes (2i, 2i+1),
+    pairs 4..14 the combinations (A[m], B[m]) of MULTI[i - 4]"""
+    return (c * 15 + i) * 512
+
+
+def role_asm(G, k, m, w, probe=None, cfg=DEFAULT):
     noload, nocompute, nolds = probe == "noload", probe == "nocompute", probe == "nolds"
+    NS = cfg.nslot
     rows = m // NW
     r0 = w * rows
     steps = k // NW
@@ -180,42 +309,47 @@ def role_asm(G, k, m, w, probe=None):
         if noload:
             return []
         col = NW * step + w
-        rs = ring_slot(step % 2)
+        rs = cfg.ring_slot(step % NS)
         out = [f"s_mul_i32 s{S_COL}, %[ss], {col}"]
         for q in range(4):
             out.append(f"buffer_load_dwordx2 v[{rs[2 * q]}:{rs[2 * q + 1]}], {offs[q]}, s[{S_LRS}:{S_LRS + 3}], s{S_COL} offen")
         return out
 
-    L += loads(0)
-    if steps > 1:
-        L += loads(1)
+    for s in range(min(NS, steps)):
+        L += loads(s)
     for s in range(steps):
         slot = s % 2
-        own = ring_slot(slot)
-        pending_next = s + 1 < steps  # step s+1's loads are in flight behind ours
+        own = cfg.ring_slot(s % NS)
+        pending = min(steps, s + NS) - (s + 1)  # later steps' loads in flight behind ours
         if not noload:
-            L.append(f"s_waitcnt vmcnt({4 if pending_next else 0})")
+            L.append(f"s_waitcnt vmcnt({4 * pending})")
         if nocompute:
             for i in range(8):  # keep the loaded data live
                 L.append(f"v_xor_b32 v{acc_reg(0, i)}, v{own[i]}, v{acc_reg(0, i)}")
-            if s + 2 < steps:
-                L += loads(s + 2)
+            if s + NS < steps:
+                L += loads(s + NS)
             continue
-        L += transpose(own, combo_temps())
+        L += transpose(own, combo_temps(cfg))
         if nolds:
             for c in range(NW):
-                L += column_code(G, r0, rows, NW * s + c, own, first=(s == 0 and c == 0))
-            if s + 2 < steps:
-                L += loads(s + 2)
+                L += column_code(G, r0, rows, NW * s + c, own, first=(s == 0 and c == 0), cfg=cfg)
+            if s + NS < steps:
+                L += loads(s + NS)
+            continue
+        others = [(w + d) % NW for d in range(1, NW)]
+        if cfg.share in ("A", "AB"):
+            L += shared_step(G, r0, rows, s, w, own, others, cfg)
+            if s + NS < steps:
+                # issued at the end of the step: the ring slot's planes are dead only then
+                L += loads(s + NS)
             continue
         for i in range(4):
             L.append(f"ds_write_b64 %[la], v[{own[2 * i]}:{own[2 * i + 1]}] offset:{lds_off(slot, w, i)}")
-        L += column_code(G, r0, rows, NW * s + w, own, first=(s == 0))
-        if s + 2 < steps:
-            L += loads(s + 2)
+        L += column_code(G, r0, rows, NW * s + w, own, first=(s == 0), cfg=cfg)
+        if s + NS < steps:
+            L += loads(s + NS)
         L.append("s_waitcnt lgkmcnt(0)")
         L.append("s_barrier")
-        others = [(w + d) % NW for d in range(1, NW)]
 
         def reads(c, buf):
             p = pbuf(buf)
@@ -227,15 +361,15 @@ def role_asm(G, k, m, w, probe=None):
             buf = t % 2
             more = t + 1 < len(others)  # the next column's reads are in flight
             L.append(f"s_waitcnt lgkmcnt({4 if more else 0})")
-            L += column_code(G, r0, rows, NW * s + c, pbuf(buf), first=False)
+            L += column_code(G, r0, rows, NW * s + c, pbuf(buf), first=False, cfg=cfg)
             if t + 2 < len(others):
                 L += reads(others[t + 2], buf)
     # epilogue: planes back to bytes, optional accumulate, store
     for r in range(rows):
         acc = [acc_reg(r, i) for i in range(8)]
-        L += transpose(acc, epi_temps())
+        L += transpose(acc, epi_temps(cfg))
         L.append(f"s_mul_i32 s{S_ROW}, %[ss], {k + r0 + r}")
-        tmp = ring_slot(0)
+        tmp = cfg.ring_slot(0)
         L.append("s_cmp_eq_u32 %[acc], 0")
         L.append(f"s_cbranch_scc1 Lnoacc_{r}_%=")
         for q in range(4):
@@ -250,31 +384,112 @@ def role_asm(G, k, m, w, probe=None):
     return L
 
 
-def clobbers():
-    v = [f'"v{i}"' for i in range(4 * NQUAD) if i not in IN_REGS]
+def shared_step(G, r0, rows, s, w, own, others, cfg):
+    """one step of the shared-combination variants (after the own column's transpose)"""
+    L = []
+    j_own = NW * s + w
+    ups, need = column_ups(G, r0, rows, j_own)
+    # the owner builds every combination the other waves may need
+    full = [set(MULTI), set(MULTI) if cfg.share == "AB" else need[1]]
+    code, A, B = combos(own, full)
+    L += code
+    if cfg.share == "A":
+        slot = s % 2
+        for i in range(4):
+            L.append(f"ds_write_b64 %[la], v[{own[2 * i]}:{own[2 * i + 1]}] offset:{a_off(slot, w, 0, i)}")
+        for i, a in enumerate(MULTI):
+            L.append(f"ds_write_b32 %[la4], v{combo_reg(0, a)} offset:{a_off(slot, w, 1, i)}")
+        L += updates(ups, A, B, s == 0)
+        L.append("s_waitcnt lgkmcnt(0)")
+        L.append("s_barrier")
+
+        def reads(c, buf):
+            p = pbuf(buf)
+            return [f"ds_read_b64 v[{p[2 * i]}:{p[2 * i + 1]}], %[la] offset:{a_off(slot, c, 0, i)}" for i in range(4)]
+
+        def areads(c):
+            return [f"ds_read_b32 v{combo_reg(0, a)}, %[la4] offset:{a_off(slot, c, 1, i)}" for i, a in enumerate(MULTI)]
+
+        L += reads(others[0], 0) + areads(others[0])
+        L += reads(others[1], 1)
+        for t, c in enumerate(others):
+            buf = t % 2
+            # in flight behind this column's reads: the next column's planes (4)
+            L.append(f"s_waitcnt lgkmcnt({4 if t + 1 < len(others) else 0})")
+            p = pbuf(buf)
+            u, nd = column_ups(G, r0, rows, NW * s + c)
+            code, _, Bc = combos(p, [set(), nd[1]])
+            Ac = {1 << q: p[2 * q] for q in range(4)}
+            Ac.update({a: combo_reg(0, a) for a in MULTI})
+            L += code
+            L += updates(u, Ac, Bc, False)
+            if t + 1 < len(others):
+                L += areads(others[t + 1])
+            if t + 2 < len(others):
+                L += reads(others[t + 2], buf)
+        return L
+    # "AB": one slot; the barrier before the write keeps it from overwriting what the other
+    # waves still read of the previous step
+    pairs = [(own[2 * i], own[2 * i + 1]) for i in range(4)] + [(combo_reg(0, a), combo_reg(1, a)) for a in MULTI]
+    L.append("s_barrier")
+    for i, (x, y) in enumerate(pairs):
+        L.append(f"ds_write_b64 %[la], v[{x}:{y}] offset:{ab_off(w, i)}")
+    L += updates(ups, A, B, s == 0)
+    L.append("s_waitcnt lgkmcnt(0)")
+    L.append("s_barrier")
+    for t, c in enumerate(others):
+        p = pbuf(t % 2)
+        if t == 0:
+            L += [f"ds_read_b64 v[{p[2 * i]}:{p[2 * i + 1]}], %[la] offset:{ab_off(c, i)}" for i in range(4)]
+        L += [f"ds_read_b64 v[{combo_reg(0, a)}:{combo_reg(1, a)}], %[la] offset:{ab_off(c, 4 + i)}"
+              for i, a in enumerate(MULTI)]
+        if t + 1 < len(others):
+            q = pbuf((t + 1) % 2)
+            L += [f"ds_read_b64 v[{q[2 * i]}:{q[2 * i + 1]}], %[la] offset:{ab_off(others[t + 1], i)}" for i in range(4)]
+        L.append(f"s_waitcnt lgkmcnt({4 if t + 1 < len(others) else 0})")
+        u, _ = column_ups(G, r0, rows, NW * s + c)
+        Ac = {1 << q: p[2 * q] for q in range(4)}
+        Bc = {1 << q: p[2 * q + 1] for q in range(4)}
+        Ac.update({a: combo_reg(0, a) for a in MULTI})
+        Bc.update({a: combo_reg(1, a) for a in MULTI})
+        L += updates(u, Ac, Bc, False)
+    return L
+
+
+def clobbers(cfg):
+    v = [f'"v{i}"' for i in range(4 * NQUAD) if i not in cfg.in_regs]
     s = [f'"s{i}"' for i in range(S_LRS, S_ROW + 1)]
     return ", ".join(v + s + ['"scc"', '"memory"'])
 
 
-def gen_kernel(k, m, G=None, prefix="rs8_q4_enc", probe=None, suffix=""):
+def lds_bytes(cfg):
+    if cfg.share == "A":
+        return 2 * NW * A_COL
+    if cfg.share == "AB":
+        return NW * 15 * 512
+    return 2 * SLOT_BYTES
+
+
+def gen_kernel(k, m, G=None, prefix="rs8_q4_enc", probe=None, suffix="", cfg=DEFAULT):
     assert k % NW == 0 and m % NW == 0
     G = G if G is not None else generator(k, m)
     K = f"{prefix}{suffix}_k{k}_m{m}"
     out = []
+    la4 = ', [la4] "v"(la4)' if cfg.share == "A" else ""
     for w in range(NW):
-        body = role_asm(G, k, m, w, probe)
+        body = role_asm(G, k, m, w, probe, cfg)
         s = "\\n\"\n        \"".join(body)
-        out.append(f"""__device__ __forceinline__ void {K}_role{w}(const bs::EncArgs& a, const bs::Items& it, const uint32_t o[4], uint32_t la)
+        out.append(f"""__device__ __forceinline__ void {K}_role{w}(const bs::EncArgs& a, const bs::Items& it, const uint32_t o[4], uint32_t la, uint32_t la4)
 {{
     asm volatile(
         "{s}\\n"
         :
         : [ib] "s"(it.wbase), [ob] "s"(it.obase), [ss] "s"(a.seg_stride), [acc] "s"(a.accumulate),
-          [o0] "v"(o[0]), [o1] "v"(o[1]), [o2] "v"(o[2]), [o3] "v"(o[3]), [la] "v"(la)
-        : {clobbers()});
+          [o0] "v"(o[0]), [o1] "v"(o[1]), [o2] "v"(o[2]), [o3] "v"(o[3]), [la] "v"(la){la4}
+        : {clobbers(cfg)});
 }}""")
     body = [f"__global__ __launch_bounds__({64 * NW}, {NW}) void {K}(bs::EncArgs a)", "{"]
-    body.append(f"    __shared__ uint32_t lds[{2 * SLOT_BYTES // 4}];")
+    body.append(f"    __shared__ uint32_t lds[{lds_bytes(cfg) // 4}];")
     body.append("    const uint32_t lane = threadIdx.x & 63;")
     body.append("    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);")
     body.append("    bs::Items it;")
@@ -283,10 +498,11 @@ def gen_kernel(k, m, G=None, prefix="rs8_q4_enc", probe=None, suffix=""):
     body.append("    uint32_t o[4];")
     body.append("#pragma unroll")
     body.append("    for (int i = 0; i < 4; ++i) o[i] = it.nbytes[i] == 8 ? it.off[i] : 0x80000000u;")
-    body.append("    const uint32_t la = bs::lds_addr(lds) + lane * 8u;")
+    body.append("    const uint32_t la = bs::lds_addr(lds) + lane * 8u;   // b64 rows: 8 bytes per lane")
+    body.append("    const uint32_t la4 = bs::lds_addr(lds) + lane * 4u;  // b32 rows")
     for w in range(NW):
         kw = "if" if w == 0 else "else if"
-        body.append(f"    {kw} (wave == {w}) {K}_role{w}(a, it, o, la);")
+        body.append(f"    {kw} (wave == {w}) {K}_role{w}(a, it, o, la, la4);")
     body.append("}")
     out.append("\n".join(body))
     out.append(f"""
@@ -320,6 +536,8 @@ def main():
         if (k, m) == (64, 32):
             for v, probe in PROBES.items():
                 parts.append(gen_kernel(k, m, probe=probe, suffix=f"_probe_{probe}"))
+            for v, cfg in VARIANTS.items():
+                parts.append(gen_kernel(k, m, suffix=f"_v{v}", cfg=cfg))
     for k, m in MDP_SHAPES:
         parts.append(gen_kernel(k, m, G=mdp_matrix(k, m), prefix="mdp_q4_enc"))
     parts.append("}  // namespace")
@@ -335,6 +553,8 @@ def main():
     parts.append("{")
     for v, probe in PROBES.items():
         parts.append(f"    if (k == 64 && m == 32 && q4_variant() == {v}) return launch_rs8_q4_enc_probe_{probe}_k64_m32(a, s);")
+    for v in VARIANTS:
+        parts.append(f"    if (k == 64 && m == 32 && q4_variant() == {v}) return launch_rs8_q4_enc_v{v}_k64_m32(a, s);")
     for k, m in SHAPES:
         parts.append(f"    if (k == {k} && m == {m}) return launch_rs8_q4_enc_k{k}_m{m}(a, s);")
     parts.append("    return NFEC_ENOTSUP;")
