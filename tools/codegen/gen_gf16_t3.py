@@ -57,16 +57,17 @@ def acc(r, p, h):
     return 2 * (16 * r + p) + (1 - h)
 
 
-T_BASE = 128             # 4 planes in flight x (quad tA|tB + pair tC): v128..v151
-A_BASE = 152             # 12 address registers v152..v163
-V_B0, V_B1 = 164, 165    # lane*8 + buffer base (0 / 64 KiB)
-V_LOFF = 166             # lane*64 + OFF_LDS: the lane's piece offsets
+T_BASE = 128
+DEPTH = 4                # planes whose table reads are in flight beyond the one computed
+NSLOT = DEPTH + 1        # read-target slots: quads v128.., pairs after them
+A_BASE = T_BASE + 6 * NSLOT          # 4 rotating address registers
+V_B0, V_B1 = A_BASE + 4, A_BASE + 5  # lane*8 + buffer base (0 / 64 KiB), pinned inputs
 
 
 def row_slot(pp):
-    """(tA, tB, tC) register pairs for plane slot pp (0..3): tA banks (0,1), tB (2,3)"""
-    quad = T_BASE + 4 * pp           # v128, 132, 136, 140: tA = (q, q+1), tB = (q+2, q+3)
-    tc = T_BASE + 16 + 2 * pp        # v144, 146, 148, 150
+    """(tA, tB, tC) register pairs for read slot pp: tA banks (0,1), tB (2,3), tC even pair"""
+    quad = T_BASE + 4 * pp
+    tc = T_BASE + 4 * NSLOT + 2 * pp
     return (quad, quad + 1), (quad + 2, quad + 3), (tc, tc + 1)
 
 
@@ -217,35 +218,54 @@ def row_asm():
     L += sload(sb[0]) + advance(0) + ["s_waitcnt lgkmcnt(0)", "s_barrier", f"s_mov_b32 s{S_CNT}, 0"]
 
     def column(buf):
+        """the column's 4 rows x 16 planes as one pipeline: the three table reads of plane
+        i + DEPTH are issued before plane i is applied (counted lgkmcnt waits; LDS returns in
+        order, and the offsets' scalar loads in flight only make a count wait longer)"""
         out = []
         vb = V_B0 if buf == 0 else V_B1
-        for r in range(ROWS):
+        seq = [(r, p) for r in range(ROWS) for p in range(16)]
+        n = len(seq)
+        areg = [0]
+
+        def issue(i):
+            r, p = seq[i]
             cur = sb[r % 2]
-            nxt = sb[(r + 1) % 2]
-            for bt in range(4):
-                for pp in range(4):
-                    p = 4 * bt + pp
-                    ta, tb, tc = row_slot(pp)
-                    for g, t in enumerate((ta, tb, tc)):
-                        idx = 3 * p + g
-                        a = A_BASE + 3 * pp + g
-                        out.append(f"v_add_u32_sdwa v{a}, s{cur + idx // 2}, v{vb} dst_sel:DWORD dst_unused:UNUSED_PAD "
-                                   f"src0_sel:WORD_{idx % 2} src1_sel:DWORD")
-                        out.append(f"ds_read_b64 v[{t[0]}:{t[1]}], v{a}")
-                if bt == 1:
-                    # next (column, row) offsets: lands during the remaining batches
-                    out += sload(nxt)
-                    out += advance((r + 1) % ROWS)
-                out.append("s_waitcnt lgkmcnt(0)")
-                for pp in range(4):
-                    p = 4 * bt + pp
-                    ta, tb, tc = row_slot(pp)
-                    for h in (0, 1):
-                        a_ = acc(r, p, h)
-                        out.append(f"v_bitop3_b32 v{a_}, v{a_}, v{ta[h]}, v{tb[h]} bitop3:0x96")
-                    for h in (0, 1):
-                        a_ = acc(r, p, h)
-                        out.append(f"v_xor_b32 v{a_}, v{tc[h]}, v{a_}")
+            o = []
+            for g, t in enumerate(row_slot(i % NSLOT)):
+                idx = 3 * p + g
+                a = A_BASE + areg[0] % 4
+                areg[0] += 1
+                o.append(f"v_add_u32_sdwa v{a}, s{cur + idx // 2}, v{vb} dst_sel:DWORD dst_unused:UNUSED_PAD "
+                         f"src0_sel:WORD_{idx % 2} src1_sel:DWORD")
+                o.append(f"ds_read_b64 v[{t[0]}:{t[1]}], v{a}")
+            if p == 0:
+                # this row's offsets are in use: fetch the next (column, row)'s into the other buffer
+                o += sload(sb[(r + 1) % 2]) + advance((r + 1) % ROWS)
+            return o
+
+        def compute(i):
+            r, p = seq[i]
+            ta, tb, tc = row_slot(i % NSLOT)
+            o = []
+            for h in (0, 1):
+                a_ = acc(r, p, h)
+                o.append(f"v_bitop3_b32 v{a_}, v{a_}, v{ta[h]}, v{tb[h]} bitop3:0x96")
+            for h in (0, 1):
+                a_ = acc(r, p, h)
+                o.append(f"v_xor_b32 v{a_}, v{tc[h]}, v{a_}")
+            return o
+
+        for i in range(min(DEPTH, n)):
+            out += issue(i)
+        for i in range(n):
+            j = i + DEPTH
+            if j < n:
+                if j % 16 == 0:
+                    out.append("s_waitcnt lgkmcnt(0)")  # row j // 16's offsets (and all reads)
+                out += issue(j)
+            ahead = min(j, n - 1) - i
+            out.append(f"s_waitcnt lgkmcnt({3 * ahead})")
+            out += compute(i)
         return out
 
     for par in (0, 1):
@@ -261,10 +281,12 @@ def row_asm():
     L += mask_init()
     # epilogue: piece offsets from LDS, inverse transposes, stores of valid rows
     offv = list(range(T_BASE, T_BASE + 16))          # piece offsets v128..v143
+    lo = T_BASE + 16                                 # lane*64 + OFF_LDS (from vb0 = lane*8 + base)
+    L += [f"v_lshlrev_b32 v{lo}, 3, v{V_B0}", f"v_add_u32 v{lo}, %[loadj], v{lo}"]
     for i in range(4):
-        L.append(f"ds_read_b128 v[{offv[4 * i]}:{offv[4 * i + 3]}], v{V_LOFF} offset:{16 * i}")
+        L.append(f"ds_read_b128 v[{offv[4 * i]}:{offv[4 * i + 3]}], v{lo} offset:{16 * i}")
     L.append("s_waitcnt lgkmcnt(0)")
-    tmp = list(range(144, 152)) + list(range(A_BASE, A_BASE + 12))
+    tmp = list(range(T_BASE + 16, T_BASE + 24))
     for r in range(ROWS):
         L += [f"s_add_u32 s{S_T0}, %[row0], {r}", "s_cmp_ge_u32 s%d, %%[m]" % S_T0, f"s_cbranch_scc1 Lr_skip{r}_%="]
         L += [f"s_add_u32 s{S_T0}, s{S_T0}, %[k]", f"s_mul_i32 s{S_T1}, s{S_T0}, %[ss]"]
@@ -285,7 +307,7 @@ def row_asm():
 
 
 def row_clobbers():
-    v = [f'"v{i}"' for i in range(164)]
+    v = [f'"v{i}"' for i in range(V_B0)]
     s = [f'"s{i}"' for i in range(S_SB[0], S_LAST + 1)]
     return ", ".join(v + s + ['"scc"', '"memory"'])
 
@@ -337,13 +359,14 @@ __global__ __launch_bounds__({64 * NWAVES}, 1) void gf16_t3_encode_kernel(Gf16T3
         const uint32_t row0 = pass * {RP}u + (wave - 1u) * {ROWS}u;
         const uint8_t* op = reinterpret_cast<const uint8_t*>(a.offs) + (uint64_t)row0 * 96u;
         const uint32_t cstep = (a.m_pad - {ROWS - 1}u) * 96u;   // last row of a column -> first row of the next
-        const uint32_t vb0 = lbase + lane * 8u, vb1 = vb0 + {BUF}u, vloff = lbase + {OFF_LDS}u + lane * 64u;
+        const uint32_t vb0 = lbase + lane * 8u, vb1 = vb0 + {BUF}u;
+        const uint32_t loadj = lbase + {OFF_LDS}u - 8u * lbase;   // 8 * vb0 + loadj = piece offsets of the lane
         asm volatile(
         "{rb}\\n"
         :
         : [wb] "s"(wb), [op] "s"(op), [ss] "s"(a.seg_stride), [k] "s"(a.k), [m] "s"(a.m), [row0] "s"(row0),
-          [cstep] "s"(cstep), [acc] "s"(a.accumulate), [vb0] "{{v{V_B0}}}"(vb0), [vb1] "{{v{V_B1}}}"(vb1),
-          [vloff] "{{v{V_LOFF}}}"(vloff)
+          [cstep] "s"(cstep), [acc] "s"(a.accumulate), [loadj] "s"(loadj), [vb0] "{{v{V_B0}}}"(vb0),
+          [vb1] "{{v{V_B1}}}"(vb1)
         : {row_clobbers()});
     }}
 }}
