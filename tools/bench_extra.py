@@ -87,6 +87,27 @@ def main():
         "encode_ms": round(enc_ms, 3),
         "encode_GiBps": round(k * vec * nb / (enc_ms * 1e-3) / 2**30, 2),
     }
+    if kind == na.NFEC_RS16 and os.environ.get("NFEC_GF16_T3", "1") != "0" and vec % 8 == 0:
+        # op roofline of the shared-table RS16 encode (gen_gf16_t3.hip), counted from its code:
+        # per (item group of 64 lanes x 64 symbols, pass of 44 rows, source column) the 11 row
+        # waves issue 44 x 16 planes x 3 ds_read_b64 (512 B each) and 7 VALU per plane, the
+        # builder 506 VALU and 125 ds_write_b64
+        groups = -(-nb * vec // 8192)
+        passes = -(-m // 44)
+        units = groups * passes * k
+        lds_bytes = units * 44 * 16 * 3 * 512
+        valu = units * (44 * 16 * 7 + 506)
+        t = enc_ms * 1e-3
+        out["op_roofline"] = {
+            "kernel": "gf16_t3_encode_kernel",
+            "gf16_macs_per_s": float("%.4g" % (k * m * (vec // 2) * nb / t)),
+            "lds": {"achieved": float("%.4g" % (lds_bytes / t)), "peak": 256 * 256 * 2.4e9, "unit": "B/s",
+                    "frac": round(lds_bytes / t / (256 * 256 * 2.4e9), 4),
+                    "note": "table reads only (ds_read_b64, 256 B/clk/CU); the bound of this kernel"},
+            "valu": {"achieved": float("%.4g" % (valu * 64 / t)), "peak": 7.86e13, "unit": "lane-ops/s",
+                     "frac": round(valu * 64 / t / 7.86e13, 4), "insts_per_launch": valu},
+            "lds_insts_per_launch": units * (44 * 16 * 3 + 125),
+        }
     if er:
         dec_ms = timed(lambda: dec.decode_blocks(blocks, locs, counts, status=status, stream=stream), a.steps)
         keep = blocks.clone()

@@ -39,9 +39,10 @@ def main(root):
     json.dump(out, sys.stdout, indent=1, sort_keys=True)
     print()
     # traffic summary for bench.py (encode kernel, bench workload)
-    # the encode kernel of the bench workload (assembly kernel by default, else the compiler-built one)
+    # the encode kernel of the bench workload (the 4-role q4 kernel by default, then the 2-role
+    # assembly kernel, then the compiler-built one)
     names = sorted((k_ for k_, v in out.items() if "enc" in k_ and "k64_m32" in k_ and "FETCH_SIZE" in v),
-                   key=lambda n: "asm" not in n)
+                   key=lambda n: ("q4" not in n, "asm" not in n))
     enc = [out[n] for n in names]
     if enc and len(sys.argv) > 2:
         e = enc[0]
