@@ -766,6 +766,11 @@ int decode_device(nfec_codec* c, const nfec_block_batch* b, const uint16_t* locs
                 f.out_slots = c->w_oslots.p;
                 f.slots_stride = c->k;
                 f.accumulate = acc;
+                static const bool lane_major = [] {
+                    const char* e = std::getenv("NFEC_FDEC_LANEMAJOR");
+                    return !(e && e[0] == '0');
+                }();
+                f.lane_major = lane_major;
                 rc = launch_rs8_fused_decode(c->k, c->m, f, s);
                 if (rc != NFEC_OK && rc != NFEC_ENOTSUP) return fail(rc, "fused decode launch failed");
                 if (rc == NFEC_OK) gate = c->w_gate.p;

@@ -277,6 +277,7 @@ struct FdecArgs {
     const uint16_t* out_slots = nullptr; // [b][slots_stride]: erased source slots
     uint32_t slots_stride = 0;
     uint32_t accumulate = 0;
+    uint32_t lane_major = 0;             // lane L holds items 4L..4L+3; lanes without one exit
 };
 int launch_rs8_fused_decode(uint32_t k, uint32_t m, const FdecArgs& a, hipStream_t s);
 

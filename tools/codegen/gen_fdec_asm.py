@@ -283,10 +283,14 @@ def gen_kernel(k, m):
         a.rows[blk] = 0;
         a.psel[2 * (uint64_t)blk] = 0;
     }}
+    // lane-major items (lane L holds items 4L..4L+3): a 1400-byte segment then occupies lanes
+    // 0..43 and the lanes past it drop out of every instruction (EXEC) instead of computing
+    // garbage bytes, a third of the VALU lane work
+    if (a.lane_major && lane * 4u >= a.ips) return;
     uint32_t o[4], so[4];
 #pragma unroll
     for (int q = 0; q < 4; ++q) {{
-        const uint32_t item = (uint32_t)q * 64u + lane;
+        const uint32_t item = a.lane_major ? lane * 4u + (uint32_t)q : (uint32_t)q * 64u + lane;
         const bool ok = item < a.ips;
         o[q] = ok ? item * 8u : 0u;
         so[q] = ok ? item * 8u : 0x80000000u;  // past the store descriptor's records: dropped
