@@ -119,7 +119,9 @@ def fdec_asm(k, m):
     offs = ["%[o0]", "%[o1]", "%[o2]", "%[o3]"]
     soffs = ["%[s0]", "%[s1]", "%[s2]", "%[s3]"]
     ncol = k + nr
-    L += [f"s_mov_b64 s[{S_LRS}:{S_LRS + 1}], %[base]", f"s_mov_b32 s{S_LRS + 2}, -1",
+    # load records 2^31: item offsets with bit 31 set (items past the segment) read as zero
+    # without a memory access; erased columns switch the records to 0
+    L += [f"s_mov_b64 s[{S_LRS}:{S_LRS + 1}], %[base]", f"s_mov_b32 s{S_LRS + 2}, 0x80000000",
           f"s_mov_b32 s{S_LRS + 3}, 0x00020000",
           f"s_mov_b64 s[{S_SRS}:{S_SRS + 1}], %[base]", f"s_mov_b32 s{S_SRS + 2}, 0x80000000",
           f"s_mov_b32 s{S_SRS + 3}, 0x00020000",
@@ -137,9 +139,9 @@ def fdec_asm(k, m):
         """column c: source slot c (c < k) or parity row c - k (slot c); unused ones read nothing"""
         w = slot_regs(c % NSLOT)
         if c < k:
-            out = [f"s_bitcmp1_b64 s[{S_EM}:{S_EM + 1}], {c}", f"s_cselect_b32 s{S_LRS + 2}, 0, -1"]
+            out = [f"s_bitcmp1_b64 s[{S_EM}:{S_EM + 1}], {c}", f"s_cselect_b32 s{S_LRS + 2}, 0, 0x80000000"]
         else:
-            out = [f"s_cmp_lt_u32 {c - k}, %[e]", f"s_cselect_b32 s{S_LRS + 2}, -1, 0"]
+            out = [f"s_cmp_lt_u32 {c - k}, %[e]", f"s_cselect_b32 s{S_LRS + 2}, 0x80000000, 0"]
         out.append(f"s_mul_i32 s{S_COL}, %[ss], {c}")
         for q in range(4):
             out.append(f"buffer_load_dwordx2 v[{w[2 * q]}:{w[2 * q + 1]}], {offs[q]}, s[{S_LRS}:{S_LRS + 3}], s{S_COL} offen")
@@ -286,13 +288,13 @@ def gen_kernel(k, m):
     // lane-major items (lane L holds items 4L..4L+3): a 1400-byte segment then occupies lanes
     // 0..43 and the lanes past it drop out of every instruction (EXEC) instead of computing
     // garbage bytes, a third of the VALU lane work
-    if (a.lane_major && lane * 4u >= a.ips) return;
+    if (a.lane_major && lane * 4u >= a.ips) return;  // measured slower (strided loads); off by default
     uint32_t o[4], so[4];
 #pragma unroll
     for (int q = 0; q < 4; ++q) {{
         const uint32_t item = a.lane_major ? lane * 4u + (uint32_t)q : (uint32_t)q * 64u + lane;
         const bool ok = item < a.ips;
-        o[q] = ok ? item * 8u : 0u;
+        o[q] = ok ? item * 8u : 0x80000000u;  // past the load records: zeros, no memory access
         so[q] = ok ? item * 8u : 0x80000000u;  // past the store descriptor's records: dropped
     }}
     const uint8_t* base = a.base + (uint64_t)blk * a.block_stride;
