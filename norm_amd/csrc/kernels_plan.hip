@@ -112,18 +112,21 @@ __global__ __launch_bounds__(kWave) void rs_plan_kernel(RsPlanArgs a)
         if (listP[0] == 0xffff) { ok = false; status = 0; }
     }
     const uint32_t e = ok ? es : 0;
+    // stage 1 by encode: the substitute parities are rows 0..e-1 (listP ascending from nd)
+    const bool by_encode = a.rows1 && e > 0 && nd == k && listP[e - 1] == nd + e - 1;
     if (lane == 0) {
         if (a.status) a.status[b] = status;
         a.rows[b] = (int32_t)e;
         a.cols2[b] = (uint16_t)e;
+        if (a.rows1) a.rows1[b] = by_encode ? 0 : (int32_t)e;
     }
     if (e == 0) return;
 
     // ---- stage-1 gather matrix and slots ----
     const E* gp = reinterpret_cast<const E*>(a.gen_parity);
-    E* coef1 = reinterpret_cast<E*>(a.coef1) + (uint64_t)b * k * cs;
-    uint16_t* islots = a.in_slots1 + (uint64_t)b * k;
-    for (uint32_t c = lane; c < nd; c += kWave) {
+    for (uint32_t c = lane; c < nd && !by_encode; c += kWave) {
+        E* coef1 = reinterpret_cast<E*>(a.coef1) + (uint64_t)b * k * cs;
+        uint16_t* islots = a.in_slots1 + (uint64_t)b * k;
         // is c erased? (E sorted: binary search)
         int32_t s_idx = -1;
         {
@@ -235,6 +238,16 @@ __global__ __launch_bounds__(kWave) void rs_plan_kernel(RsPlanArgs a)
     }
     uint16_t* oslots = a.out_slots2 + (uint64_t)b * k;
     for (uint32_t s = lane; s < e; s += kWave) oslots[s] = listE[s];
+    if (by_encode) {
+        // the stage-1 encode reads every source slot: the erased ones must read as zero
+        if (lane == 0) atomicMax(a.rmax, e);
+        uint8_t* blk = a.zero_base + (uint64_t)b * a.zero_block_stride;
+        const uint32_t words = a.zero_vec >> 3;
+        for (uint32_t s = 0; s < e; ++s) {
+            uint2* p = reinterpret_cast<uint2*>(blk + (uint64_t)listE[s] * a.zero_seg_stride);
+            for (uint32_t w = lane; w < words; w += kWave) p[w] = make_uint2(0u, 0u);
+        }
+    }
 }
 
 

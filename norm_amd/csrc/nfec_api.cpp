@@ -207,7 +207,8 @@ struct nfec_codec {
 
     // decode workspace (guarded by mu)
     std::mutex mu;
-    DevBuf<int32_t> w_status, w_rows;
+    DevBuf<int32_t> w_status, w_rows, w_rows1;
+    DevBuf<uint32_t> w_rmax;
     DevBuf<uint16_t> w_islots, w_oslots, w_cols;
     DevBuf<uint8_t> w_coef1, w_coef2, w_z, w_work, w_pmap;
     DevBuf<uint32_t> w_emask, w_psel, w_gate;
@@ -241,6 +242,8 @@ struct nfec_codec {
         w_gate.release();
         w_status.release();
         w_rows.release();
+        w_rows1.release();
+        w_rmax.release();
         w_islots.release();
         w_oslots.release();
         w_cols.release();
@@ -656,6 +659,13 @@ int decode_device(nfec_codec* c, const nfec_block_batch* b, const uint16_t* locs
         if ((rc = c->w_z.reserve((size_t)sb * dcs * zstride))) return rc;
         if (big_plan && (rc = c->w_work.reserve((size_t)sb * rs_plan_work_bytes(dcs, c->sym)))) return rc;
     }
+    // RS16 stage 1 by the shared-table encode for the blocks whose substitute parities are rows
+    // 0..e-1 (RsPlanArgs::rows1): overwrite semantics only, since it zeroes the erased source
+    const bool t3dec = c->kind == NFEC_RS16 && c->d_t3off.p && !b->num_data && !acc && (c->vec % 8) == 0;
+    if (t3dec) {
+        if ((rc = c->w_rows1.reserve(sb))) return rc;
+        if ((rc = c->w_rmax.reserve(1))) return rc;
+    }
     const bool fast = c->kind == NFEC_RS8 && !b->num_data && c->m <= 32 && c->k <= 64 && !force_generic() &&
                       has_bitsliced(c->k, c->m) && bs::offsets_fit(b->block_stride, b->seg_stride);
     if (fast) {
@@ -880,7 +890,44 @@ int decode_device(nfec_codec* c, const nfec_block_batch* b, const uint16_t* locs
         p.coef2 = c->w_coef2.p;
         p.work = big_plan ? c->w_work.p : nullptr;
         p.work_block_bytes = rs_plan_work_bytes(dcs, c->sym);
+        if (t3dec) {
+            NFEC_HIP(hipMemsetAsync(c->w_rmax.p, 0, sizeof(uint32_t), s));
+            p.rows1 = c->w_rows1.p;
+            p.rmax = c->w_rmax.p;
+            p.zero_base = blocks;
+            p.zero_block_stride = b->block_stride;
+            p.zero_seg_stride = b->seg_stride;
+            p.zero_vec = c->vec & ~1u;
+        }
         if ((rc = launch_rs_plan(p, s))) return rc;
+        if (t3dec) {
+            // z_t = (encode row t of the block, erased source zeroed) ^ received parity t, for
+            // t below the plan's largest such e; the gather stage then overwrites the z rows of
+            // the other blocks
+            Gf16T3Args t;
+            t.base = blocks;
+            t.block_stride = b->block_stride;
+            t.seg_stride = b->seg_stride;
+            t.nblocks = nb;
+            t.k = c->k;
+            t.m = c->m;
+            t.m_pad = gf16_t3_rows_padded(c->m);
+            t.vec_bytes = c->vec & ~1u;
+            t.offs = c->d_t3off.p;
+            t.accumulate = 1;
+            t.out_base = c->w_z.p;
+            t.out_block_stride = (uint64_t)dcs * zstride;
+            t.out_seg_stride = zstride;
+            t.out_slot0 = 0;
+            t.acc_base = blocks;
+            t.acc_block_stride = b->block_stride;
+            t.acc_seg_stride = b->seg_stride;
+            t.acc_slot0 = c->k;
+            t.rows_lim = c->w_rmax.p;
+            rc = launch_gf16_t3_encode(t, s);
+            if (rc == NFEC_ENOTSUP) return fail(rc, "t3 decode stage 1: layout not covered");
+            if (rc) return rc;
+        }
         // stage 1: z_t = parity(P_t) ^ sum_{present c} G[P_t][c] d_c  -> scratch rows
         // stage 2: d_E = A^-1 z                                          -> erased slots
         if (c->kind == NFEC_RS8) {
@@ -937,7 +984,7 @@ int decode_device(nfec_codec* c, const nfec_block_batch* b, const uint16_t* locs
             a.out_block_stride = (uint64_t)dcs * zstride;
             a.out_seg_stride = zstride;
             a.out_slot_mode = OUT_SLOT_ROW;
-            a.row_count = c->w_rows.p;
+            a.row_count = t3dec ? c->w_rows1.p : c->w_rows.p;
             a.slots_stride = c->k;
             a.coef = reinterpret_cast<const uint16_t*>(c->w_coef1.p);
             a.coef_block_stride = (uint64_t)c->k * dcs;
@@ -958,6 +1005,7 @@ int decode_device(nfec_codec* c, const nfec_block_batch* b, const uint16_t* locs
             a2.out_seg_stride = b->seg_stride;
             a2.out_slots = c->w_oslots.p;
             a2.out_slot_mode = OUT_SLOT_LIST;
+            a2.row_count = c->w_rows.p;
             a2.coef = reinterpret_cast<const uint16_t*>(c->w_coef2.p);
             a2.coef_block_stride = (uint64_t)dcs * dcs;
             a2.accumulate = acc;

@@ -184,6 +184,15 @@ struct Gf16T3Args {
     const uint16_t* offs = nullptr;      // [k + 1][m_pad][48] LDS offsets (gf16_t3_offsets)
     uint32_t accumulate = 0;
     uint32_t passes = 0;                 // set by the launcher
+    // output and accumulate-source layouts (null: parity in place, slot k + r, as encode does);
+    // decode stage 1 writes z rows (slot r of a z batch) XORed with the received parity row
+    uint8_t* out_base = nullptr;
+    uint64_t out_block_stride = 0;
+    uint32_t out_seg_stride = 0, out_slot0 = 0;
+    const uint8_t* acc_base = nullptr;
+    uint64_t acc_block_stride = 0;
+    uint32_t acc_seg_stride = 0, acc_slot0 = 0;
+    const uint32_t* rows_lim = nullptr;  // device word: rows needed (<= m), null: m
 };
 inline uint32_t gf16_t3_rows_padded(uint32_t m) { return (m + 43u) / 44u * 44u; }
 int launch_gf16_t3_encode(const Gf16T3Args& a, hipStream_t s);  // NFEC_ENOTSUP: shape not covered
@@ -216,6 +225,15 @@ struct RsPlanArgs {
     void* work = nullptr;                    // [b] work_block_bytes: e x 2e matrix, then the E/P
                                              // lists and pivot factors (used when e > 64 / > 256)
     uint64_t work_block_bytes = 0;
+    // stage 1 by encode (RS16, gen_gf16_t3.hip): blocks whose substitute parities are rows
+    // 0..e-1 get z_t = encode row t of the block with its erased source zeroed ^ parity t.  For
+    // them the plan writes rows1 = 0 (the gather stage skips them), no gather matrix, raises
+    // *rmax to e and zeroes the erased source slots (zero_*: the batch).  Others: rows1 = e.
+    int32_t* rows1 = nullptr;
+    uint32_t* rmax = nullptr;
+    uint8_t* zero_base = nullptr;
+    uint64_t zero_block_stride = 0;
+    uint32_t zero_seg_stride = 0, zero_vec = 0;   // zero_vec: bytes, multiple of 8
 };
 // per-block scratch of launch_rs_plan for decode row stride cs (elements of sym bytes)
 inline uint64_t rs_plan_work_bytes(uint32_t cs, uint32_t sym)

@@ -38,7 +38,9 @@ NWAVES = RWAVES + 1
 GROUPS = [(0, 6, 0), (6, 5, 64), (11, 5, 96)]   # (first plane, planes, first table row)
 TROWS = 128
 BUF = TROWS * 512        # one table buffer: 128 rows x 64 lanes x 8 bytes
-OFF_LDS = 2 * BUF        # piece offsets (epilogue): 64 lanes x 16 dwords
+OFF_LDS = 2 * BUF        # piece offsets in the output layout (epilogue stores): 64 lanes x 16 dwords
+OFF_ACC = OFF_LDS + 4096 # ... and in the accumulate-source layout
+S_ODESC, S_ADESC = 60, 64  # row-wave epilogue: output / accumulate-source descriptors (over S_SB[1])
 MASKS = {8: 0x00FF00FF, 4: 0x0F0F0F0F, 2: 0x33333333, 1: 0x55555555}
 
 # ---- SGPRs used inside the asm bodies (clobbered) ----
@@ -279,17 +281,25 @@ def row_asm():
     # the prefetched offsets load past the last column may still be in flight
     L.append("s_waitcnt lgkmcnt(0)")
     L += mask_init()
-    # epilogue: piece offsets from LDS, inverse transposes, stores of valid rows
+    # epilogue: piece offsets (output layout) from LDS, inverse transposes, stores of the rows
+    # below the limit; with accumulate the old bytes come from the accumulate-source layout
+    # (encode: the parity slot itself; decode stage 1: the received parity row, output z)
+    L += [f"s_mov_b64 s[{S_ODESC}:{S_ODESC + 1}], %[ob]", f"s_mov_b32 s{S_ODESC + 2}, 0x80000000",
+          f"s_mov_b32 s{S_ODESC + 3}, 0x00020000",
+          f"s_mov_b64 s[{S_ADESC}:{S_ADESC + 1}], %[ab]", f"s_mov_b32 s{S_ADESC + 2}, 0x80000000",
+          f"s_mov_b32 s{S_ADESC + 3}, 0x00020000"]
     offv = list(range(T_BASE, T_BASE + 16))          # piece offsets v128..v143
     lo = T_BASE + 16                                 # lane*64 + OFF_LDS (from vb0 = lane*8 + base)
     L += [f"v_lshlrev_b32 v{lo}, 3, v{V_B0}", f"v_add_u32 v{lo}, %[loadj], v{lo}"]
     for i in range(4):
         L.append(f"ds_read_b128 v[{offv[4 * i]}:{offv[4 * i + 3]}], v{lo} offset:{16 * i}")
     L.append("s_waitcnt lgkmcnt(0)")
-    tmp = list(range(T_BASE + 16, T_BASE + 24))
+    ao = T_BASE + 17
+    tmp = list(range(T_BASE + 18, T_BASE + 26))
     for r in range(ROWS):
-        L += [f"s_add_u32 s{S_T0}, %[row0], {r}", "s_cmp_ge_u32 s%d, %%[m]" % S_T0, f"s_cbranch_scc1 Lr_skip{r}_%="]
-        L += [f"s_add_u32 s{S_T0}, s{S_T0}, %[k]", f"s_mul_i32 s{S_T1}, s{S_T0}, %[ss]"]
+        L += [f"s_add_u32 s{S_T0}, %[row0], {r}", "s_cmp_ge_u32 s%d, %%[rlim]" % S_T0, f"s_cbranch_scc1 Lr_skip{r}_%="]
+        L += [f"s_add_u32 s{S_T1}, s{S_T0}, %[aslot]", f"s_mul_i32 s{S_CNT}, s{S_T1}, %[ass]",
+              f"s_add_u32 s{S_T0}, s{S_T0}, %[oslot]", f"s_mul_i32 s{S_T1}, s{S_T0}, %[oss]"]
         for h in (0, 1):
             x = [acc(r, p, h) for p in range(16)]
             L += transpose16(x, tmp[:4])
@@ -298,10 +308,11 @@ def row_asm():
                 d0, d1 = tmp[4], tmp[5]
                 L += [f"v_mov_b32 v{d0}, v{x[2 * i]}", f"v_mov_b32 v{d1}, v{x[2 * i + 1]}"]
                 L += ["s_cmp_eq_u32 %[acc], 0", f"s_cbranch_scc1 Lr_na{r}_{piece}_%="]
-                L += [f"buffer_load_dwordx2 v[{tmp[6]}:{tmp[7]}], v{offv[piece]}, s[{S_DESC}:{S_DESC + 3}], s{S_T1} offen",
+                L += [f"ds_read_b32 v{ao}, v{lo} offset:{OFF_ACC - OFF_LDS + 4 * piece}", "s_waitcnt lgkmcnt(0)",
+                      f"buffer_load_dwordx2 v[{tmp[6]}:{tmp[7]}], v{ao}, s[{S_ADESC}:{S_ADESC + 3}], s{S_CNT} offen",
                       "s_waitcnt vmcnt(0)", f"v_xor_b32 v{d0}, v{d0}, v{tmp[6]}", f"v_xor_b32 v{d1}, v{d1}, v{tmp[7]}"]
                 L.append(f"Lr_na{r}_{piece}_%=:")
-                L.append(f"buffer_store_dwordx2 v[{d0}:{d1}], v{offv[piece]}, s[{S_DESC}:{S_DESC + 3}], s{S_T1} offen")
+                L.append(f"buffer_store_dwordx2 v[{d0}:{d1}], v{offv[piece]}, s[{S_ODESC}:{S_ODESC + 3}], s{S_T1} offen")
         L.append(f"Lr_skip{r}_%=:")
     return L
 
@@ -327,11 +338,16 @@ namespace {{
 
 __global__ __launch_bounds__({64 * NWAVES}, 1) void gf16_t3_encode_kernel(Gf16T3Args a)
 {{
-    __shared__ uint32_t lds[{(OFF_LDS + 64 * 64) // 4}];
+    __shared__ uint32_t lds[{(OFF_ACC + 64 * 64) // 4}];
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t wg = bs::wg_index(1);
     const uint32_t group = wg / a.passes, pass = wg - group * a.passes;
+    // rows actually needed (decode stage 1: the largest erasure count among the blocks it
+    // serves, written by the plan); passes past them leave at once, every wave together
+    uint32_t rlim = a.m;
+    if (a.rows_lim) rlim = min(rlim, __builtin_amdgcn_readfirstlane(*a.rows_lim));
+    if (pass * {RP}u >= rlim) return;
     const uint64_t total = (uint64_t)a.nblocks * a.vec_bytes;   // flat bytes over blocks
     const uint64_t f0 = (uint64_t)group * 8192u;
     const uint32_t b0 = __builtin_amdgcn_readfirstlane((uint32_t)(min(f0, total - 1) / a.vec_bytes));
@@ -339,16 +355,18 @@ __global__ __launch_bounds__({64 * NWAVES}, 1) void gf16_t3_encode_kernel(Gf16T3
     const uint32_t lbase = bs::lds_addr(lds);
     if (wave == 0) {{
         uint32_t off[16];
+        uint32_t* po = lds + {OFF_LDS // 4} + lane * 16;
+        uint32_t* pa = lds + {OFF_ACC // 4} + lane * 16;
 #pragma unroll
         for (int i = 0; i < 16; ++i) {{
             const uint64_t f = f0 + (uint64_t)i * 512u + lane * 8u;
             const uint32_t b = (uint32_t)(f / a.vec_bytes);
             const uint32_t p = (uint32_t)(f - (uint64_t)b * a.vec_bytes);
-            off[i] = f < total ? (uint32_t)((uint64_t)(b - b0) * a.block_stride) + p : 0x80000000u;
+            const bool ok = f < total;
+            off[i] = ok ? (uint32_t)((uint64_t)(b - b0) * a.block_stride) + p : 0x80000000u;
+            po[i] = ok ? (uint32_t)((uint64_t)(b - b0) * a.out_block_stride) + p : 0x80000000u;
+            pa[i] = ok ? (uint32_t)((uint64_t)(b - b0) * a.acc_block_stride) + p : 0x80000000u;
         }}
-        uint4* po = reinterpret_cast<uint4*>(lds + {OFF_LDS // 4} + lane * 16);
-#pragma unroll
-        for (int i = 0; i < 4; ++i) po[i] = make_uint4(off[4 * i], off[4 * i + 1], off[4 * i + 2], off[4 * i + 3]);
         const uint32_t lb0 = lbase + lane * 8u, lb1 = lb0 + {BUF}u;
         asm volatile(
         "{bb}\\n"
@@ -361,12 +379,16 @@ __global__ __launch_bounds__({64 * NWAVES}, 1) void gf16_t3_encode_kernel(Gf16T3
         const uint32_t cstep = (a.m_pad - {ROWS - 1}u) * 96u;   // last row of a column -> first row of the next
         const uint32_t vb0 = lbase + lane * 8u, vb1 = vb0 + {BUF}u;
         const uint32_t loadj = lbase + {OFF_LDS}u - 8u * lbase;   // 8 * vb0 + loadj = piece offsets of the lane
+        rlim = __builtin_amdgcn_readfirstlane(rlim);  // uniform: keep it in an SGPR for the asm
+        const uint8_t* ob = a.out_base + (uint64_t)b0 * a.out_block_stride;
+        const uint8_t* ab = a.acc_base + (uint64_t)b0 * a.acc_block_stride;
         asm volatile(
         "{rb}\\n"
         :
-        : [wb] "s"(wb), [op] "s"(op), [ss] "s"(a.seg_stride), [k] "s"(a.k), [m] "s"(a.m), [row0] "s"(row0),
-          [cstep] "s"(cstep), [acc] "s"(a.accumulate), [loadj] "s"(loadj), [vb0] "{{v{V_B0}}}"(vb0),
-          [vb1] "{{v{V_B1}}}"(vb1)
+        : [wb] "s"(wb), [op] "s"(op), [k] "s"(a.k), [rlim] "s"(rlim), [row0] "s"(row0),
+          [cstep] "s"(cstep), [acc] "s"(a.accumulate), [loadj] "s"(loadj), [ob] "s"(ob), [ab] "s"(ab),
+          [oslot] "s"(a.out_slot0), [oss] "s"(a.out_seg_stride), [aslot] "s"(a.acc_slot0),
+          [ass] "s"(a.acc_seg_stride), [vb0] "{{v{V_B0}}}"(vb0), [vb1] "{{v{V_B1}}}"(vb1)
         : {row_clobbers()});
     }}
 }}
@@ -380,10 +402,25 @@ int launch_gf16_t3_encode(const Gf16T3Args& a, hipStream_t s)
         a.m_pad != (a.m + {RP - 1}u) / {RP}u * {RP}u)
         return NFEC_ENOTSUP;
     // every piece offset of a group (8 KiB of flat positions) plus slot offsets within 2^31
-    const uint64_t span = (8192u / a.vec_bytes + 2u) * a.block_stride + (uint64_t)(a.k + a.m) * a.seg_stride;
-    if (span >= (1ull << 31)) return NFEC_ENOTSUP;
+    const uint64_t nbg = 8192u / a.vec_bytes + 2u;
+    if (nbg * a.block_stride + (uint64_t)(a.k + a.m) * a.seg_stride >= (1ull << 31) ||
+        (a.out_base && nbg * a.out_block_stride + (uint64_t)(a.out_slot0 + a.m) * a.out_seg_stride >= (1ull << 31)) ||
+        (a.acc_base && nbg * a.acc_block_stride + (uint64_t)(a.acc_slot0 + a.m) * a.acc_seg_stride >= (1ull << 31)))
+        return NFEC_ENOTSUP;
     const uint64_t total = (uint64_t)a.nblocks * a.vec_bytes;
     Gf16T3Args b = a;
+    if (!b.out_base) {{  // encode: parity in place, slot k + r; accumulate against it
+        b.out_base = const_cast<uint8_t*>(a.base);
+        b.out_block_stride = a.block_stride;
+        b.out_seg_stride = a.seg_stride;
+        b.out_slot0 = a.k;
+    }}
+    if (!b.acc_base) {{
+        b.acc_base = b.out_base;
+        b.acc_block_stride = b.out_block_stride;
+        b.acc_seg_stride = b.out_seg_stride;
+        b.acc_slot0 = b.out_slot0;
+    }}
     b.passes = (a.m + {RP - 1}u) / {RP}u;
     const uint64_t groups = (total + 8191u) / 8192u;
     if (groups * b.passes >= (1ull << 31)) return NFEC_ENOTSUP;
