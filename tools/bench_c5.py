@@ -1,8 +1,9 @@
 """BASELINE C5: mixed RS8/RS16 block stream striped over the GPUs of one node, segments in pinned
 host memory (NORM's socket buffers), H2D / compute / D2H overlapped.
 
-    python tools/bench_c5.py [--blocks 1048576] [--steps 2]            # one GPU: blocks / 8 by default
-    torchrun --nproc-per-node 8 tools/bench_c5.py --blocks 1048576     # the full C5 shape
+    python tools/bench_c5.py [--steps 2]                       # one GPU: 131,072 blocks (1M / 8)
+    torchrun --nproc-per-node 8 tools/bench_c5.py               # weak: 131,072 blocks per GPU = C5
+    torchrun --nproc-per-node N tools/bench_c5.py --strong      # strong: 1,048,576 blocks over N GPUs
 
 Block b of the stream is RS16 (k=400, m=100, vec=1400: the fecTest shape) when
 splitmix64(seed ^ b) % 8 == 0, otherwise RS8 (k=64, m=32, vec=1400).  Rank r owns the contiguous
@@ -11,8 +12,9 @@ One step = encode every block, then repair 16 (RS8) / 50 (RS16) random source er
 block.  The RS8 and RS16 sub-streams run concurrently from two host threads, each through the
 codec's pinned-staging pipeline (nfec_encode_host / nfec_decode_host).
 
-Reported: host-resident GiB/s (source bytes through encode + decode, all ranks / max time), and
-the device-resident GiB/s of the same mix with the blocks already in HBM.
+Reported as one JSON line in bench.py's schema: value = host-resident GiB/s (source bytes
+through encode + decode, all ranks / max-over-ranks time), plus the device-resident GiB/s of the
+same mix with the blocks already in HBM.
 """
 import argparse
 import json
@@ -44,7 +46,9 @@ def main():
     import torch
 
     p = argparse.ArgumentParser()
-    p.add_argument("--blocks", type=int, default=0, help="stream length over all ranks (default: 1M / 8 x ranks)")
+    p.add_argument("--blocks", type=int, default=0,
+                   help="blocks per GPU (weak; default 1M / 8), or in total with --strong (default 1M)")
+    p.add_argument("--strong", action="store_true", help="a fixed total split over the ranks")
     p.add_argument("--steps", type=int, default=2)
     p.add_argument("--warmup", type=int, default=1)
     p.add_argument("--serial", action="store_true", help="run the RS8 and RS16 sub-streams one after the other")
@@ -62,8 +66,12 @@ def main():
     dev = torch.device("cuda", local)
     import norm_amd as na
 
-    total = a.blocks or (1 << 20) // 8 * world
-    lo, hi = rank * total // world, (rank + 1) * total // world
+    from norm_amd.dist import shard
+
+    per = a.blocks or ((1 << 20) if a.strong else (1 << 20) // 8)
+    first, nmine = shard(per, world, rank, a.strong)
+    total = per if a.strong else per * world
+    lo, hi = first, first + nmine
     ids = np.arange(lo, hi, dtype=np.uint64)
     is16 = (splitmix64(np.uint64(SEED) ^ ids) % np.uint64(8)) == 0
     counts = {"RS8": int((~is16).sum()), "RS16": int(is16.sum())}
@@ -172,11 +180,17 @@ def main():
     src_all = float(src_all.item())
     if rank == 0:
         print(json.dumps({
-            "workload": "C5 mixed RS8(64,32)/RS16(400,100) stream, vec=1400, pinned host segments",
-            "blocks_total": total, "n_gpus": world, "rank0_blocks": counts,
-            "host_resident_GiBps": round(src_all / host_s / 2**30, 2), "host_ms_per_step": round(host_s * 1e3, 1),
-            "device_resident_GiBps": round(src_all / dev_s / 2**30, 2), "device_ms_per_step": round(dev_s * 1e3, 2),
-            "steps": a.steps, "status_ok": host_ok, "sample_round_trip_ok": sample_ok,
+            "metric": "FEC encode+erasure-decode GiB/s (host-resident, pinned H2D/D2H), C5 mixed RS8/RS16 stream",
+            "value": round(src_all / host_s / 2**30, 2), "unit": "GiB/s", "n_gpus": world,
+            "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(host_s * 1e3, 1),
+            "higher_is_better": True, "scaling": "strong" if a.strong else "weak", "vs_baseline": None,
+            "dtype": "u8", "data": "synthetic (splitmix64 source segments, reference generators)",
+            "config": {"workload": "C5 mixed RS8(64,32)/RS16(400,100) stream, vec=1400, pinned host segments",
+                       "blocks_total": total, "rank0_blocks": counts,
+                       "parallelism": f"block-striped x{world} (no collective)"},
+            "device_resident": {"value": round(src_all / dev_s / 2**30, 2), "unit": "GiB/s",
+                                "ms_per_step": round(dev_s * 1e3, 2)},
+            "status_ok": host_ok, "sample_round_trip_ok": sample_ok,
             "rank0_host_s": {j["name"]: [round(j["host_enc_s"], 3), round(j["host_dec_s"], 3)] for j in jobs},
             "note": "one step = encode + 16 (RS8) / 50 (RS16) source-erasure repair of every block; "
                     "GiB/s counts source bytes, all ranks / max-over-ranks time",
