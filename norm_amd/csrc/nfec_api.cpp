@@ -781,7 +781,14 @@ int decode_device(nfec_codec* c, const nfec_block_batch* b, const uint16_t* locs
                     return e && e[0] == '1';
                 }();
                 f.lane_major = lane_major;
-                rc = launch_rs8_fused_decode(c->k, c->m, f, s);
+                // NFEC_FDEC_Q2=1: two waves per block (A/B only; measured slower: 2.19 vs 2.01 ms,
+                // DESIGN.md section 4)
+                static const bool q2 = [] {
+                    const char* e = std::getenv("NFEC_FDEC_Q2");
+                    return e && e[0] == '1';
+                }();
+                rc = q2 && !lane_major ? launch_rs8_fused_decode_q2(c->k, c->m, f, s)
+                                       : launch_rs8_fused_decode(c->k, c->m, f, s);
                 if (rc != NFEC_OK && rc != NFEC_ENOTSUP) return fail(rc, "fused decode launch failed");
                 if (rc == NFEC_OK) gate = c->w_gate.p;
             }

@@ -298,6 +298,9 @@ struct FdecArgs {
     uint32_t lane_major = 0;             // lane L holds items 4L..4L+3; lanes without one exit
 };
 int launch_rs8_fused_decode(uint32_t k, uint32_t m, const FdecArgs& a, hipStream_t s);
+// The same repair with two waves per block sharing each column's transpose through LDS
+// (gen_fdec_q2.hip, 168 VGPRs: 3 waves per SIMD instead of 2).
+int launch_rs8_fused_decode_q2(uint32_t k, uint32_t m, const FdecArgs& a, hipStream_t s);
 
 // MDP decode planning: per block one-stage coefficient matrix over the surviving slots.
 struct MdpPlanArgs {

@@ -112,7 +112,7 @@ def snippets(regs):
     return out
 
 
-def fdec_asm(k, m):
+def fdec_asm(k, m, probe=None):
     G = generator(k, m)
     nr = min(NCOLS_PAR, m)  # z rows that can be in use (e <= m)
     L = []
@@ -137,6 +137,8 @@ def fdec_asm(k, m):
 
     def loads(c):
         """column c: source slot c (c < k) or parity row c - k (slot c); unused ones read nothing"""
+        if probe == "noload":
+            return []
         w = slot_regs(c % NSLOT)
         if c < k:
             out = [f"s_bitcmp1_b64 s[{S_EM}:{S_EM + 1}], {c}", f"s_cselect_b32 s{S_LRS + 2}, 0, 0x80000000"]
@@ -157,8 +159,12 @@ def fdec_asm(k, m):
     # ---- stage 1: z_t for rows 0..15 (rows >= e are computed but unused) ----
     for c in range(ncol):
         w = slot_regs(c % NSLOT)
-        L.append(f"s_waitcnt vmcnt({4 * (issued - c)})")
-        if c < k:
+        if probe != "noload":
+            L.append(f"s_waitcnt vmcnt({4 * (issued - c)})")
+        if probe == "nos1":
+            for i in range(8):  # keep the loaded data live
+                L.append(f"v_xor_b32 v{acc_reg(0, i)}, v{w[i]}, v{acc_reg(0, i)}")
+        elif c < k:
             L += [f"s_bitcmp1_b64 s[{S_EM}:{S_EM + 1}], {c}", f"s_cbranch_scc1 Lskip{c}_%="]
             L += transpose(w, ring_temps())
             ups, need = [], [set(), set()]
@@ -194,14 +200,14 @@ def fdec_asm(k, m):
     win = win_regs()
     cbuf = [S_COEF1, S_COEF2]
     tmp = [4 * (WIN_P0 + p) + h for p in range(4) for h in (0, 1)]
-    regs = None
+    regs = all_tables(win)[1]
     for h in range(2):
         if h == 1:
             L += ["s_cmp_le_u32 %[e], 8", "s_cbranch_scc1 Ldone_%="]
         for sl in range(8):
             for i in range(8):
                 L.append(f"v_mov_b32 v{d_reg(sl, i)}, 0")
-        for t in range(16):
+        for t in range(0 if probe == "nos2" else 16):
             L += [f"s_cmp_le_u32 %[e], {t}", f"s_cbranch_scc1 Lrows{h}_%="]
             cur = cbuf[t % 2]
             L.append("s_waitcnt lgkmcnt(0)")
@@ -262,9 +268,14 @@ def clobbers():
     return ", ".join(v + s + ['"m0"', '"scc"', '"memory"'])
 
 
-def gen_kernel(k, m):
-    K = f"rs8_fdec_k{k}_m{m}"
-    body = "\\n\"\n        \"".join(fdec_asm(k, m))
+# A/B probes of the (64, 32) kernel, NFEC_FDEC_VARIANT=<id> (never the default): no stage-2 solve,
+# no stage-1 arithmetic (loads only), no stage-1 loads
+PROBES = {1: "nos2", 2: "nos1", 3: "noload"}
+
+
+def gen_kernel(k, m, probe=None):
+    K = f"rs8_fdec_k{k}_m{m}" + (f"_probe_{probe}" if probe else "")
+    body = "\\n\"\n        \"".join(fdec_asm(k, m, probe))
     return f"""__global__ __launch_bounds__(256, 2) void {K}(FdecArgs a)
 {{
     const uint32_t lane = threadIdx.x & 63;
@@ -321,6 +332,7 @@ def main():
         "// GENERATED by tools/codegen/gen_fdec_asm.py -- do not edit by hand.",
         "// Fused RS8 erasure repair (re-encode + e x e solve in registers, one wave per block) for",
         "// (k, m) in: " + ", ".join(f"({k},{m})" for k, m in shapes),
+        "#include <cstdlib>",
         '#include "nfec_internal.hpp"',
         "",
         "namespace nfec {",
@@ -328,7 +340,16 @@ def main():
     ]
     for k, m in shapes:
         parts.append(gen_kernel(k, m))
+        if (k, m) == (64, 32):
+            for probe in PROBES.values():
+                parts.append(gen_kernel(k, m, probe))
     parts.append("}  // namespace")
+    parts.append("")
+    parts.append("static int fdec_variant()")
+    parts.append("{")
+    parts.append("    static const int v = [] { const char* e = std::getenv(\"NFEC_FDEC_VARIANT\"); return e ? std::atoi(e) : 0; }();")
+    parts.append("    return v;")
+    parts.append("}")
     parts.append("")
     parts.append("// NFEC_ENOTSUP when (k, m) has no fused kernel or the batch shape needs the unfused path")
     parts.append("int launch_rs8_fused_decode(uint32_t k, uint32_t m, const FdecArgs& a, hipStream_t s)")
@@ -337,6 +358,11 @@ def main():
     parts.append("    if ((a.vec & 7u) || a.vec > 2048 || a.coef_col_stride != 32 || (a.coef_block_stride & 15) ||")
     parts.append("        (a.slots_stride & 1) || (uint64_t)a.seg_stride * (k + 16) + a.vec >= (1ull << 31))")
     parts.append("        return NFEC_ENOTSUP;")
+    for v, probe in PROBES.items():
+        parts.append(f"    if (k == 64 && m == 32 && fdec_variant() == {v}) {{")
+        parts.append(f"        hipLaunchKernelGGL(rs8_fdec_k64_m32_probe_{probe}, dim3((a.nblocks + 3) / 4), dim3(256), 0, s, a);")
+        parts.append("        return hipGetLastError() == hipSuccess ? NFEC_OK : NFEC_EDEVICE;")
+        parts.append("    }")
     for k, m in shapes:
         parts.append(f"    if (k == {k} && m == {m}) {{")
         parts.append(f"        hipLaunchKernelGGL(rs8_fdec_k{k}_m{m}, dim3((a.nblocks + 3) / 4), dim3(256), 0, s, a);")
