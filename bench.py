@@ -75,9 +75,12 @@ def parse():
                         "capped by a cgroup CPU quota when one is set)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--verify", action="store_true", help="check the round trip after timing")
-    p.add_argument("--host-steps", type=int, default=0,
-                   help="also time K steps with the batch in pinned host memory (PCIe-inclusive, reported "
-                        "under 'host_resident'; never the headline value)")
+    p.add_argument("--host-steps", type=int, default=2,
+                   help="also time K steps with blocks in pinned host memory (PCIe-inclusive, reported "
+                        "under 'host_resident'; never the headline value; 0: skip)")
+    p.add_argument("--host-blocks", type=int, default=16384,
+                   help="blocks per GPU in the pinned host batch of --host-steps (the first ones of the "
+                        "device batch; the rate is link-bound, so a quarter of the batch measures it)")
     return p.parse_args()
 
 
@@ -160,11 +163,12 @@ def main():
     if a.host_steps > 0:
         import numpy as np
 
-        hblocks = torch.empty(blocks.shape, dtype=torch.uint8, pin_memory=True)
-        hblocks.copy_(blocks)
+        hb = min(nb, a.host_blocks) if a.host_blocks > 0 else nb
+        hblocks = torch.empty((hb,) + tuple(blocks.shape[1:]), dtype=torch.uint8, pin_memory=True)
+        hblocks.copy_(blocks[:hb])
         hnp = hblocks.numpy()
-        hlocs = locs.cpu().numpy().view(np.uint16)
-        hcounts = counts.cpu().numpy().view(np.uint16)
+        hlocs = locs[:hb].cpu().numpy().view(np.uint16)
+        hcounts = counts[:hb].cpu().numpy().view(np.uint16)
 
         def hstep():
             enc.encode_blocks_host(hnp)
@@ -183,7 +187,8 @@ def main():
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             he = float(t.item())
         host = {
-            "value": round(k * vec * (a.blocks if a.strong else nb * world) / (he / a.host_steps) / 2**30, 2),
+            "value": round(k * vec * hb * world / (he / a.host_steps) / 2**30, 2),
+            "blocks_per_gpu": hb,
             "unit": "GiB/s",
             "steps": a.host_steps,
             "ms_per_step": round(he / a.host_steps * 1e3, 2),

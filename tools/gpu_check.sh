@@ -14,7 +14,7 @@ timeout -k 10 600 python3 bench.py ${BENCH_ARGS:-} > gpurun_out/bench_$TAG.log 2
 tail -1 gpurun_out/bench_$TAG.log
 if [ -n "${PROFILE:-1}" ]; then
   export TMPDIR=/tmp
-  timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$TAG -o run --output-format csv -- python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline > gpurun_out/prof_$TAG.log 2>&1 || { echo rocprof failed; tail -20 gpurun_out/prof_$TAG.log; exit 5; }
+  timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$TAG -o run --output-format csv -- python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --host-steps 0 > gpurun_out/prof_$TAG.log 2>&1 || { echo rocprof failed; tail -20 gpurun_out/prof_$TAG.log; exit 5; }
   find gpurun_out/prof_$TAG -name '*kernel_stats.csv' | head -1 | xargs -r head -20
 fi
 exit $rc

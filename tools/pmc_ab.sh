@@ -11,7 +11,7 @@ for v in ${VARIANTS:-"NFEC_Q4_VARIANT=0"}; do
   for grp in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_ACTIVE_INST_ANY" \
              "GRBM_GUI_ACTIVE GRBM_COUNT" "SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_ACTIVE_INST_VMEM"; do
     i=$((i+1))
-    env ${v//,/ } timeout -s KILL 120 rocprofv3 --pmc $grp --output-format csv -d $OUT/p$i -o pmc -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline > $OUT/p$i.log 2>&1 || { echo "$v pass $i failed"; tail -5 $OUT/p$i.log; exit 1; }
+    env ${v//,/ } timeout -s KILL 120 rocprofv3 --pmc $grp --output-format csv -d $OUT/p$i -o pmc -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --host-steps 0 > $OUT/p$i.log 2>&1 || { echo "$v pass $i failed"; tail -5 $OUT/p$i.log; exit 1; }
   done
   python3 - "$OUT" "$v" <<'PY'
 import csv, glob, sys, collections

@@ -7,7 +7,7 @@ OUT=gpurun_out/sq_$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
 timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_ACTIVE_INST_ANY \
-  --output-format csv -d $OUT -o pmc -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline > $OUT/run.log 2>&1 || { echo "pmc failed"; tail -5 $OUT/run.log; exit 1; }
+  --output-format csv -d $OUT -o pmc -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --host-steps 0 > $OUT/run.log 2>&1 || { echo "pmc failed"; tail -5 $OUT/run.log; exit 1; }
 python3 - "$OUT" <<'PY'
 import csv, glob, sys, collections
 f = glob.glob(sys.argv[1] + "/**/*counter_collection.csv", recursive=True)[0]
