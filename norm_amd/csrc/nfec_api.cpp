@@ -1478,6 +1478,43 @@ static int run_host_batch(nfec_codec* c, const nfec_block_batch* hb, const uint1
         dn.emplace_back(dn_off, dn_len);
     const bool pinned = host_is_pinned(hb->blocks);
     uint8_t* const hbase = static_cast<uint8_t*>(hb->blocks);
+    // RS decode reads the source slots and only the first e surviving parities of a block (P,
+    // normEncoderRS8.cpp:680-700), so a chunk's upload stops after the last parity slot any of
+    // its blocks uses: [0, k + 16) instead of the whole span for RS8(64,32) with 16 source
+    // erasures.  MDP decode reads every surviving vector (normEncoderMDP.cpp:346-361).
+    // The download then covers [0, max numData) of the chunk, which the upload always includes
+    // (slots past the upload hold another chunk's bytes and must not travel back).
+    auto decode_up_len = [&](uint32_t b0, uint32_t nb, uint64_t& down) -> uint64_t {
+        down = dn_len;
+        if (c->kind == NFEC_MDP) return span;
+        uint32_t top = 0, ndmax = 0;  // slots [0, top) are read by some block of the chunk
+        std::vector<uint8_t> erased(c->k + c->m);
+        for (uint32_t b = b0; b < b0 + nb; ++b) {
+            const uint32_t nd = hb->num_data ? hb->num_data[b] : c->k;
+            const uint32_t ec = std::min<uint32_t>(counts[b], lstride);
+            const uint16_t* l = locs + (uint64_t)b * lstride;
+            const uint32_t nvec = nd + c->m;
+            if (nd == 0 || nd > c->k) return span;
+            ndmax = std::max(ndmax, nd);
+            std::fill(erased.begin(), erased.begin() + nvec, 0);
+            uint32_t es = 0;
+            for (uint32_t i = 0; i < ec; ++i) {
+                if (l[i] >= nvec) return span;  // invalid list: the plan rejects it, stay safe
+                erased[l[i]] = 1;
+                es += l[i] < nd;
+            }
+            uint32_t used = 0, end = nd;
+            for (uint32_t v = nd; v < nvec && used < es; ++v)
+                if (!erased[v]) {
+                    ++used;
+                    end = v + 1;
+                }
+            if (used < es) return span;  // undecodable: nothing is read, but keep it simple
+            top = std::max(top, end);
+        }
+        down = (uint64_t)(ndmax - 1) * ss + c->vec;
+        return (uint64_t)(top - 1) * ss + c->vec;  // top >= ndmax >= 1
+    };
 
     const uint32_t chunk = host_chunk(c, dbs, hb->nblocks);
     const uint32_t used = std::min<uint32_t>(kHostSlots, (hb->nblocks + chunk - 1) / chunk);
@@ -1489,6 +1526,7 @@ static int run_host_batch(nfec_codec* c, const nfec_block_batch* hb, const uint1
             return rc;
     struct Job {
         uint32_t b0 = 0, nb = 0;
+        uint64_t dl = 0;  // decode: download length of the chunk's single piece
         bool busy = false;
     } jobs[kHostSlots];
     auto finish = [&](uint32_t i) -> int {
@@ -1498,7 +1536,8 @@ static int run_host_batch(nfec_codec* c, const nfec_block_batch* hb, const uint1
         j.busy = false;
         NFEC_HIP(hipEventSynchronize(s.done));
         if (!pinned)
-            for (const auto& pc : dn) copy2d(hbase + (uint64_t)j.b0 * hbs + pc.first, hbs, s.pin + pc.first, dbs, pc.second, j.nb);
+            for (const auto& pc : dn)
+                copy2d(hbase + (uint64_t)j.b0 * hbs + pc.first, hbs, s.pin + pc.first, dbs, decode ? j.dl : pc.second, j.nb);
         if (decode && status) std::memcpy(status + j.b0, s.hstat, (size_t)j.nb * 4);
         return NFEC_OK;
     };
@@ -1515,12 +1554,15 @@ static int run_host_batch(nfec_codec* c, const nfec_block_batch* hb, const uint1
         j.b0 = b0;
         j.nb = std::min(chunk, hb->nblocks - b0);
         uint8_t* hsrc = hbase + (uint64_t)b0 * hbs;
+        uint64_t dl = dn_len;
+        const uint64_t ul = decode ? decode_up_len(b0, j.nb, dl) : up_len;
+        j.dl = dl;
         hipError_t ae;
         if (pinned) {
-            ae = hipMemcpy2DAsync(s.dev + up_off, dbs, hsrc + up_off, hbs, up_len, j.nb, hipMemcpyHostToDevice, s.st);
+            ae = hipMemcpy2DAsync(s.dev + up_off, dbs, hsrc + up_off, hbs, ul, j.nb, hipMemcpyHostToDevice, s.st);
         } else {
-            copy2d(s.pin + up_off, dbs, hsrc + up_off, hbs, up_len, j.nb);
-            ae = hipMemcpyAsync(s.dev, s.pin, (size_t)(j.nb - 1) * dbs + up_off + up_len, hipMemcpyHostToDevice, s.st);
+            copy2d(s.pin + up_off, dbs, hsrc + up_off, hbs, ul, j.nb);
+            ae = hipMemcpyAsync(s.dev, s.pin, (size_t)(j.nb - 1) * dbs + up_off + ul, hipMemcpyHostToDevice, s.st);
         }
         uint16_t* dnd = nullptr;
         if (hb->num_data) {
@@ -1560,11 +1602,11 @@ static int run_host_batch(nfec_codec* c, const nfec_block_batch* hb, const uint1
         if (rc) return bail(rc);
         if (pinned)
             for (size_t q = 0; q < dn.size() && ae == hipSuccess; ++q)
-                ae = hipMemcpy2DAsync(hsrc + dn[q].first, hbs, s.dev + dn[q].first, dbs, dn[q].second, j.nb,
-                                      hipMemcpyDeviceToHost, s.st);
+                ae = hipMemcpy2DAsync(hsrc + dn[q].first, hbs, s.dev + dn[q].first, dbs, decode ? dl : dn[q].second,
+                                      j.nb, hipMemcpyDeviceToHost, s.st);
         else
-            ae = hipMemcpyAsync(s.pin + dn_off, s.dev + dn_off, (size_t)(j.nb - 1) * dbs + dn_len, hipMemcpyDeviceToHost,
-                                s.st);
+            ae = hipMemcpyAsync(s.pin + dn_off, s.dev + dn_off, (size_t)(j.nb - 1) * dbs + (decode ? dl : dn_len),
+                                hipMemcpyDeviceToHost, s.st);
         if (ae == hipSuccess && decode && status)
             ae = hipMemcpyAsync(s.hstat, s.dstat, (size_t)j.nb * 4, hipMemcpyDeviceToHost, s.st);
         if (ae == hipSuccess) ae = hipEventRecord(s.done, s.st);
@@ -1643,6 +1685,7 @@ static int run_host_vectors(nfec_codec* c, void* const* vecs, uint32_t nblocks, 
             return rc;
     struct Job {
         uint32_t b0 = 0, nb = 0;
+        uint64_t dl = 0;  // decode: download length of the chunk's single piece
         bool busy = false;
     } jobs[kHostSlots];
     const uint64_t blk_bytes = (uint64_t)n * c->vec;

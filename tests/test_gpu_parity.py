@@ -320,6 +320,61 @@ def test_host_batch_pipeline(orc, kind, k, m, vec, stride, nb, pinned, monkeypat
     assert np.all(host[:, :, vec:] == 0xA5)
 
 
+@pytest.mark.parametrize("pinned", [False, True])
+@pytest.mark.parametrize("kind", [NFEC_RS8, NFEC_RS16, NFEC_MDP])
+def test_host_decode_windows(orc, kind, pinned, monkeypatch):
+    """RS host decode uploads only [0, the last parity slot a block of the chunk uses) and
+    downloads [0, max numData).  Chunks with different windows (16 / 2 / 0 source erasures,
+    parity erasures, shortened blocks, an undecodable block) take turns on the pipeline's device
+    slots, so a window that is too short would decode from, or write back, another chunk's
+    bytes.  Every byte the reference leaves alone must come back unchanged, including the
+    unused parity slots, which hold garbage here (the decoder never reads them)."""
+    k, m, vec, nb = 24, 16, 504, 48
+    monkeypatch.setenv("NFEC_HOST_CHUNK_BLOCKS", "8")  # 6 chunks over the pipeline's slots
+    _, dec = _codecs(kind, k, m, vec)
+    nd = np.full(nb, k, np.uint16)
+    nd[8:16] = [24, 5, 17, 24, 1, 9, 24, 12]
+    host = orc.encode_blocks(kind, k, m, vec, orc.make_blocks(k, m, vec, nb, num_data=nd), nd)
+    locs = np.zeros((nb, m), np.uint16)
+    counts = np.zeros(nb, np.uint16)
+    plan = [(16, 0), (3, 2), (2, 0), (0, 0), (5, 4), (15, 1)]  # (source, parity) erasures per chunk
+    for b in range(nb):
+        ns, npar = plan[b // 8]
+        ns = min(ns, int(nd[b]))
+        src = orc.erasure_pattern(b, int(nd[b]), ns) if ns else np.zeros(0, np.uint16)
+        par = (int(nd[b]) + orc.erasure_pattern(b + 500, m, npar)).astype(np.uint16) if npar else np.zeros(0, np.uint16)
+        allp = np.concatenate([src, par]).astype(np.uint16)
+        counts[b] = len(allp)
+        locs[b, :len(allp)] = allp
+    counts[47] = m + 1  # undecodable (more erasures than parity): untouched, status 0
+    _erase(host, locs, np.minimum(counts, m))
+    ref = host.copy()
+    st_ref = orc.decode_blocks(kind, k, m, vec, ref, locs, np.minimum(counts, m).astype(np.uint16), nd)
+    st_ref[47] = 0
+    ref[47] = host[47]
+    if kind != NFEC_MDP:
+        # garbage in the parity slots no decode reads (past the first e surviving parities)
+        for b in range(nb):
+            n = int(nd[b])
+            es = int(np.sum(locs[b, :min(counts[b], m)] < n))
+            er = set(int(x) for x in locs[b, :min(counts[b], m)])
+            used = 0
+            for v in range(n, n + m):
+                if v in er:
+                    continue
+                if used >= es or b == 47:
+                    host[b, v, :vec] = 0x77
+                    ref[b, v, :vec] = 0x77
+                used += 1
+    if pinned:
+        buf = torch.empty(host.shape, dtype=torch.uint8).pin_memory().numpy()
+        buf[...] = host
+        host = buf
+    st = dec.decode_blocks_host(host, locs, counts, num_data=nd)
+    assert np.array_equal(st, st_ref)
+    assert np.array_equal(host, ref)
+
+
 def test_device_workload_generators_match_oracle(orc):
     k, m, vec, nb = 64, 32, 1400, 9
     dev = torch.zeros((nb, k + m, 1400), dtype=torch.uint8, device="cuda")
