@@ -252,6 +252,151 @@ __global__ __launch_bounds__(kWave) void rs_plan_kernel(RsPlanArgs a)
 
 
 // ---------------------------------------------------------------------------------
+// RS16 plan in closed form: the outputs of rs_plan_kernel<uint16_t> (status, rows, the stage-1
+// gather matrix or the by-encode marking, the erased slots) with A^-1 from the Cauchy form of
+// the Lagrange generator instead of Gauss-Jordan (the same algebra as rs_plan2_kernel; the
+// inverse is unique, so the coefficients are identical):
+//     A^-1[s][t] = exp(lA[s] + lB[t] - log(x_s ^ y_t))
+//     lA[s] = log W'(x_s) + sum_t log(x_s ^ y_t) - sum_{s' != s} log(x_s ^ x_s')
+//     lB[t] = -log W(y_t) + sum_s log(y_t ^ x_s) - sum_{t' != t} log(y_t ^ y_t')
+// O(e^2) table terms per block instead of O(e^3).  One wavefront per block, e <= kPlanCfMaxE;
+// the GF(2^16) log / exp tables are read through L2.
+// ---------------------------------------------------------------------------------
+__global__ __launch_bounds__(kWave) void rs16_plan_cf_kernel(RsPlanArgs a)
+{
+    __shared__ uint16_t listE[kPlanCfMaxE], listP[kPlanCfMaxE];
+    __shared__ uint16_t xs[kPlanCfMaxE], yt[kPlanCfMaxE];
+    __shared__ int32_t lA[kPlanCfMaxE], lB[kPlanCfMaxE];
+    __shared__ uint32_t np_s;
+    const uint32_t lane = threadIdx.x;
+    const uint32_t b = blockIdx.x;
+    const uint16_t* ex = reinterpret_cast<const uint16_t*>(a.exp_tab);  // 2q entries
+    const uint16_t* lg = a.log_tab;                                      // lg[0] = q
+    constexpr int32_t q = 65535;
+    const uint32_t k = a.k, m = a.m;
+    const uint32_t nd = a.num_data ? uni(a.num_data[b]) : k;
+    const uint32_t ec = uni(a.erasure_counts[b]);
+    const uint16_t* locs = a.erasure_locs + (uint64_t)b * a.erasure_stride;
+    int32_t status = (int32_t)ec;
+
+    // ---- validate (lane-parallel: sorted, in range) and count source erasures ----
+    bool ok = nd >= 1 && nd <= k && ec <= a.erasure_stride && ec <= m;
+    uint32_t es = 0;
+    if (ok) {
+        bool bad = false;
+        uint32_t nsrc = 0;
+        for (uint32_t i = lane; i < ec; i += kWave) {
+            const uint32_t l = locs[i];
+            if (l >= nd + m || (i > 0 && l <= locs[i - 1])) bad = true;
+            nsrc += l < nd;
+        }
+        for (int off = 32; off > 0; off >>= 1) nsrc += __shfl_xor(nsrc, off);
+        ok = !__any(bad);
+        es = uni(nsrc);
+    }
+    if (ok && es > kPlanCfMaxE) ok = false;  // launch_rs_plan only picks this kernel when e fits
+    if (!ok) status = 0;
+    if (ok && es > 0) {
+        // surviving parities in ascending slot order (reference scan normEncoderRS8.cpp:660-718)
+        if (lane == 0) {
+            uint32_t next = es, np = 0;
+            for (uint32_t s = nd; s < nd + m && np < es; ++s) {
+                if (next < ec && locs[next] == s) { ++next; continue; }
+                listP[np++] = (uint16_t)s;
+            }
+            np_s = np;
+        }
+        for (uint32_t i = lane; i < es; i += kWave) listE[i] = locs[i];
+        __syncthreads();
+        if (np_s < es) { ok = false; status = 0; }
+    }
+    const uint32_t e = ok ? es : 0;
+    const bool by_encode = a.rows1 && e > 0 && nd == k && listP[e - 1] == nd + e - 1;
+    if (lane == 0) {
+        if (a.status) a.status[b] = status;
+        a.rows[b] = (int32_t)e;
+        a.cols2[b] = (uint16_t)e;
+        if (a.rows1) a.rows1[b] = by_encode ? 0 : (int32_t)e;
+    }
+    if (e == 0) return;
+
+    // ---- stage-1 gather matrix and slots (blocks not repaired by encode) ----
+    const uint32_t cs = a.coef_stride;
+    const uint16_t* gp = reinterpret_cast<const uint16_t*>(a.gen_parity);
+    for (uint32_t c = lane; c < nd && !by_encode; c += kWave) {
+        uint16_t* coef1 = reinterpret_cast<uint16_t*>(a.coef1) + (uint64_t)b * k * cs;
+        uint16_t* islots = a.in_slots1 + (uint64_t)b * k;
+        int32_t s_idx = -1;
+        {
+            uint32_t lo = 0, hi = e;  // first index with listE[i] >= c
+            while (lo < hi) {
+                const uint32_t mid = (lo + hi) >> 1;
+                if (listE[mid] < c) lo = mid + 1;
+                else hi = mid;
+            }
+            if (lo < e && listE[lo] == c) s_idx = (int32_t)lo;
+        }
+        islots[c] = s_idx >= 0 ? listP[s_idx] : (uint16_t)c;
+        for (uint32_t t = 0; t < cs; ++t) {
+            uint16_t v = 0;
+            if (t < e) {
+                if (s_idx >= 0) v = (uint16_t)((uint32_t)s_idx == t);
+                else v = gp[(uint64_t)(listP[t] - nd) * k + c];
+            }
+            coef1[(uint64_t)c * cs + t] = v;
+        }
+    }
+
+    // ---- A^-1 in closed form ----
+    for (uint32_t i = lane; i < e; i += kWave) {
+        const uint32_t s = listE[i];
+        xs[i] = s == 0 ? (uint16_t)0 : ex[(s - 1) % (uint32_t)q];
+        yt[i] = ex[(k - 1 + (listP[i] - nd)) % (uint32_t)q];  // parity row p: point alpha^(k+p-1)
+    }
+    __syncthreads();
+    for (uint32_t i = lane; i < e; i += kWave) {
+        const uint32_t x = xs[i], y = yt[i];
+        int32_t acc = (int32_t)a.lwp[listE[i]], bcc = -(int32_t)a.lw[listP[i] - nd];
+#pragma unroll 4
+        for (uint32_t t = 0; t < e; ++t) {
+            acc += (int32_t)lg[x ^ yt[t]] - (int32_t)lg[x ^ xs[t]];
+            bcc += (int32_t)lg[y ^ xs[t]] - (int32_t)lg[y ^ yt[t]];
+        }
+        // the t == i terms subtract lg[0] = q (x ^ x, y ^ y), which is 0 mod q
+        acc %= q;
+        bcc %= q;
+        lA[i] = acc < 0 ? acc + q : acc;
+        lB[i] = bcc < 0 ? bcc + q : bcc;
+    }
+    __syncthreads();
+    uint16_t* coef2 = reinterpret_cast<uint16_t*>(a.coef2) + (uint64_t)b * cs * cs;
+    for (uint32_t idx = lane; idx < cs * cs; idx += kWave) {
+        const uint32_t t = idx / cs, s = idx % cs;  // column t (input z_t), row s (output)
+        uint16_t v = 0;
+        if (t < e && s < e) {
+            int32_t l = lA[s] + lB[t] - (int32_t)lg[xs[s] ^ yt[t]];
+            l %= q;
+            if (l < 0) l += q;
+            v = ex[l];
+        }
+        coef2[idx] = v;
+    }
+    uint16_t* oslots = a.out_slots2 + (uint64_t)b * k;
+    for (uint32_t s = lane; s < e; s += kWave) oslots[s] = listE[s];
+    if (by_encode) {
+        // the stage-1 encode reads every source slot: the erased ones must read as zero
+        if (lane == 0) atomicMax(a.rmax, e);
+        uint8_t* blk = a.zero_base + (uint64_t)b * a.zero_block_stride;
+        const uint32_t words = a.zero_vec >> 3;
+        for (uint32_t s = 0; s < e; ++s) {
+            uint2* p = reinterpret_cast<uint2*>(blk + (uint64_t)listE[s] * a.zero_seg_stride);
+            for (uint32_t w = lane; w < words; w += kWave) p[w] = make_uint2(0u, 0u);
+        }
+    }
+}
+
+
+// ---------------------------------------------------------------------------------
 // MDP plan: one wavefront per block.
 // ---------------------------------------------------------------------------------
 __global__ __launch_bounds__(kWave) void mdp_plan_kernel(MdpPlanArgs a)
@@ -408,7 +553,9 @@ __global__ __launch_bounds__(kWave) void mdp_plan_kernel(MdpPlanArgs a)
 int launch_rs_plan(const RsPlanArgs& a, hipStream_t s)
 {
     if (a.nblocks == 0) return NFEC_OK;
-    if (a.bits == 8) hipLaunchKernelGGL(rs_plan_kernel<uint8_t>, dim3(a.nblocks), dim3(kWave), 0, s, a);
+    if (a.bits == 16 && a.lwp && a.lw && std::min(a.k, a.m) <= kPlanCfMaxE)
+        hipLaunchKernelGGL(rs16_plan_cf_kernel, dim3(a.nblocks), dim3(kWave), 0, s, a);
+    else if (a.bits == 8) hipLaunchKernelGGL(rs_plan_kernel<uint8_t>, dim3(a.nblocks), dim3(kWave), 0, s, a);
     else hipLaunchKernelGGL(rs_plan_kernel<uint16_t>, dim3(a.nblocks), dim3(kWave), 0, s, a);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return hip_fail(e, "rs_plan launch");

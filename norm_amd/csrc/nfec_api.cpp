@@ -361,18 +361,21 @@ int build_codec(nfec_codec* c)
             if ((rc = c->d_t3off.reserve(off.size()))) return rc;
             NFEC_HIP(hipMemcpy(c->d_t3off.p, off.data(), off.size() * 2, hipMemcpyHostToDevice));
         }
-        if (!wide) {
-            // log W'(x_j) over the k source points and log W(y_p) at the parity points
+        if (!wide || std::min(c->k, c->m) <= kPlanCfMaxE) {
+            // log W'(x_j) over the k source points and log W(y_p) at the parity points (the
+            // closed-form plans: rs_plan2_kernel for RS8, rs16_plan_cf_kernel for RS16)
             std::vector<uint16_t> lwp(c->k), lw(c->m);
+            std::vector<uint32_t> pt(c->k + c->m);
+            for (uint32_t j = 0; j < c->k + c->m; ++j) pt[j] = rs_point(f, j);
             for (uint32_t j = 0; j < c->k; ++j) {
                 uint64_t acc = 0;
                 for (uint32_t l = 0; l < c->k; ++l)
-                    if (l != j) acc += f.log[rs_point(f, j) ^ rs_point(f, l)];
+                    if (l != j) acc += f.log[pt[j] ^ pt[l]];
                 lwp[j] = (uint16_t)(acc % f.q);
             }
             for (uint32_t p = 0; p < c->m; ++p) {
                 uint64_t acc = 0;
-                for (uint32_t l = 0; l < c->k; ++l) acc += f.log[rs_point(f, c->k + p) ^ rs_point(f, l)];
+                for (uint32_t l = 0; l < c->k; ++l) acc += f.log[pt[c->k + p] ^ pt[l]];
                 lw[p] = (uint16_t)(acc % f.q);
             }
             if ((rc = c->d_lwp.reserve(c->k))) return rc;
@@ -897,6 +900,15 @@ int decode_device(nfec_codec* c, const nfec_block_batch* b, const uint16_t* locs
         p.coef2 = c->w_coef2.p;
         p.work = big_plan ? c->w_work.p : nullptr;
         p.work_block_bytes = rs_plan_work_bytes(dcs, c->sym);
+        // RS16: the closed-form inverse when every block's e fits it (NFEC_RS16_CF=0: Gauss-Jordan)
+        static const bool use_cf16 = [] {
+            const char* e = std::getenv("NFEC_RS16_CF");
+            return !(e && e[0] == '0');
+        }();
+        if (c->kind == NFEC_RS16 && use_cf16 && c->d_lwp.p && std::min(c->k, c->m) <= kPlanCfMaxE) {
+            p.lwp = c->d_lwp.p;
+            p.lw = c->d_lw.p;
+        }
         if (t3dec) {
             NFEC_HIP(hipMemsetAsync(c->w_rmax.p, 0, sizeof(uint32_t), s));
             p.rows1 = c->w_rows1.p;

@@ -234,7 +234,12 @@ struct RsPlanArgs {
     uint8_t* zero_base = nullptr;
     uint64_t zero_block_stride = 0;
     uint32_t zero_seg_stride = 0, zero_vec = 0;   // zero_vec: bytes, multiple of 8
+    // RS16 closed form (rs16_plan_cf_kernel, when both are set and min(k, m) <= kPlanCfMaxE):
+    // A^-1 from the Cauchy form of the Lagrange generator instead of Gauss-Jordan
+    const uint16_t* lwp = nullptr;      // [k] log W'(x_j)
+    const uint16_t* lw = nullptr;       // [m] log W(y_p)
 };
+constexpr uint32_t kPlanCfMaxE = 256;
 // per-block scratch of launch_rs_plan for decode row stride cs (elements of sym bytes)
 inline uint64_t rs_plan_work_bytes(uint32_t cs, uint32_t sym)
 {
