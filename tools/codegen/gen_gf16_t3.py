@@ -375,6 +375,10 @@ __global__ __launch_bounds__({64 * NWAVES}, 1) void gf16_t3_encode_kernel(Gf16T3
         : {builder_clobbers()});
     }} else {{
         const uint32_t row0 = pass * {RP}u + (wave - 1u) * {ROWS}u;
+        // a row wave whose rows are all past the limit (the last pass of m = 100, decode stage 1
+        // with e = 50) leaves before its first barrier: the builder and the other row waves
+        // synchronise among the waves still running, and its SIMD's issue slots go to them
+        if (row0 >= rlim) return;
         const uint8_t* op = reinterpret_cast<const uint8_t*>(a.offs) + (uint64_t)row0 * 96u;
         const uint32_t cstep = (a.m_pad - {ROWS - 1}u) * 96u;   // last row of a column -> first row of the next
         const uint32_t vb0 = lbase + lane * 8u, vb1 = vb0 + {BUF}u;
