@@ -654,6 +654,7 @@ __global__ __launch_bounds__(64 * kPlan2Waves) void rs_plan2_kernel(RsPlan2Args 
     uint32_t rank = (uint32_t)__popcll(surv & ((1ull << lane) - 1ull));
     const bool used = e > 0 && lane < m && ((surv >> lane) & 1ull) && rank < e;
     const uint64_t pused = __ballot(used);
+    const bool fused = a.fused_rows && e > 0 && e <= 16 && (pused >> a.fused_rows) == 0ull;
     if (lane < m) a.pmap[(uint64_t)b * m + lane] = used ? (uint8_t)rank : (uint8_t)0xff;
     // erased-source bitmap (k <= 64 for the specialised kernels; others ignore it)
     const uint64_t em = e > 0 ? __ballot(lane < k && ers[lane]) : 0ull;
@@ -663,8 +664,8 @@ __global__ __launch_bounds__(64 * kPlan2Waves) void rs_plan2_kernel(RsPlan2Args 
         psel[0] = (uint32_t)pused;
         psel[1] = (uint32_t)(pused >> 32);
         // a block the fused repair kernel will not take (it takes 1..16 source erasures
-        // repaired from parity rows 0..e-1) opens this call's gate for the unfused kernels
-        if (a.gate && e > 0 && (e > 16 || pused != ((1ull << e) - 1ull))) a.gate[0] = a.gate_gen;
+        // repaired from parity rows below fused_rows) opens this call's gate for the unfused kernels
+        if (a.gate && e > 0 && !fused) a.gate[0] = a.gate_gen;
     }
     if (e == 0) return;
     if (used) {
@@ -698,12 +699,29 @@ __global__ __launch_bounds__(64 * kPlan2Waves) void rs_plan2_kernel(RsPlan2Args 
     }
     wave_lds_sync();
     uint8_t* coef = a.coef2 + (uint64_t)b * cs * cs;
-    for (uint32_t idx = lane; idx < e * e; idx += 64) {
-        const uint32_t t = idx / e, s = idx % e;
-        int32_t l = lA[s] + lB[t] - (int32_t)lg[xs[s] ^ yt[t]];
-        l %= 255;
-        if (l < 0) l += 255;
-        coef[(uint64_t)t * cs + s] = ex[l];
+    if (fused) {
+        // by parity row: 16 x 16 bytes, row sP[t] holds z_t's coefficients, unused rows zero (the
+        // fused kernel applies rows 0..max used row; a zero coefficient's snippet is empty)
+        for (uint32_t idx = lane; idx < 16 * 16; idx += 64) {
+            const uint32_t row = idx >> 4, s = idx & 15;
+            const uint32_t t = (uint32_t)__popcll(pused & ((1ull << row) - 1ull));  // rank of row
+            uint8_t v = 0;
+            if (((pused >> row) & 1ull) && s < e) {
+                int32_t l = lA[s] + lB[t] - (int32_t)lg[xs[s] ^ yt[t]];
+                l %= 255;
+                if (l < 0) l += 255;
+                v = ex[l];
+            }
+            coef[(uint64_t)row * cs + s] = v;
+        }
+    } else {
+        for (uint32_t idx = lane; idx < e * e; idx += 64) {
+            const uint32_t t = idx / e, s = idx % e;
+            int32_t l = lA[s] + lB[t] - (int32_t)lg[xs[s] ^ yt[t]];
+            l %= 255;
+            if (l < 0) l += 255;
+            coef[(uint64_t)t * cs + s] = ex[l];
+        }
     }
     if (lane < e) a.out_slots2[(uint64_t)b * k + lane] = sE[lane];
 }

@@ -753,47 +753,42 @@ int decode_device(nfec_codec* c, const nfec_block_batch* b, const uint16_t* locs
                 const char* e = std::getenv("NFEC_FUSED");
                 return !(e && e[0] == '0');
             }();
+            FdecArgs f;
+            f.base = blocks;
+            f.block_stride = b->block_stride;
+            f.seg_stride = b->seg_stride;
+            f.nblocks = nb;
+            f.vec = c->vec;
+            f.ips = c->vec / 8;
+            f.rows = c->w_rows.p;
+            f.psel = c->w_psel.p;
+            f.emask = c->w_emask.p;
+            f.coef = c->w_coef2.p;
+            f.coef_block_stride = (uint64_t)dcs * dcs;
+            f.coef_col_stride = dcs;
+            f.out_slots = c->w_oslots.p;
+            f.slots_stride = c->k;
+            f.accumulate = acc;
+            static const bool lane_major = [] {
+                const char* e = std::getenv("NFEC_FDEC_LANEMAJOR");  // A/B only: 2.16 vs 2.02 ms
+                return e && e[0] == '1';
+            }();
+            f.lane_major = lane_major;
+            const bool fused = use_fused && rs8_fused_decode_covers(c->k, c->m, f);
             // gate: the plan writes this pass's generation into w_gate when some block needs the
             // unfused kernels; when the fused kernel ran they skip their whole launch otherwise
             const uint32_t gen = ++c->gate_gen;
-            if (use_fused) {
+            if (fused) {
                 p2.gate = c->w_gate.p;
                 p2.gate_gen = gen;
+                p2.fused_rows = std::min(16u, c->m);  // the inverse of the blocks it takes, by row
             }
             if ((rc = launch_rs_plan2(p2, s))) return rc;
             const uint32_t* gate = nullptr;
-            if (use_fused) {
-                FdecArgs f;
-                f.base = blocks;
-                f.block_stride = b->block_stride;
-                f.seg_stride = b->seg_stride;
-                f.nblocks = nb;
-                f.vec = c->vec;
-                f.ips = c->vec / 8;
-                f.rows = c->w_rows.p;
-                f.psel = c->w_psel.p;
-                f.emask = c->w_emask.p;
-                f.coef = c->w_coef2.p;
-                f.coef_block_stride = (uint64_t)dcs * dcs;
-                f.coef_col_stride = dcs;
-                f.out_slots = c->w_oslots.p;
-                f.slots_stride = c->k;
-                f.accumulate = acc;
-                static const bool lane_major = [] {
-                    const char* e = std::getenv("NFEC_FDEC_LANEMAJOR");  // A/B only: 2.16 vs 2.02 ms
-                    return e && e[0] == '1';
-                }();
-                f.lane_major = lane_major;
-                // NFEC_FDEC_Q2=1: two waves per block (A/B only; measured slower: 2.19 vs 2.01 ms,
-                // DESIGN.md section 4)
-                static const bool q2 = [] {
-                    const char* e = std::getenv("NFEC_FDEC_Q2");
-                    return e && e[0] == '1';
-                }();
-                rc = q2 && !lane_major ? launch_rs8_fused_decode_q2(c->k, c->m, f, s)
-                                       : launch_rs8_fused_decode(c->k, c->m, f, s);
-                if (rc != NFEC_OK && rc != NFEC_ENOTSUP) return fail(rc, "fused decode launch failed");
-                if (rc == NFEC_OK) gate = c->w_gate.p;
+            if (fused) {
+                rc = launch_rs8_fused_decode(c->k, c->m, f, s);
+                if (rc != NFEC_OK) return fail(rc == NFEC_ENOTSUP ? NFEC_EDEVICE : rc, "fused decode launch failed");
+                gate = c->w_gate.p;
             }
             bs::DecArgs d;
             d.base = blocks;

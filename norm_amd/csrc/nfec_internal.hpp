@@ -278,11 +278,16 @@ struct RsPlan2Args {
     // The generation changes per call, so the word never needs clearing.
     uint32_t* gate = nullptr;
     uint32_t gate_gen = 0;
+    // fused repair runs after the plan (gen_fdec_asm.hip, rows fused_rows = min(16, m)): for a
+    // block with e <= 16 whose substitute parities are all below fused_rows the inverse is
+    // written by parity ROW ([row][s], zero rows for unused rows) instead of by rank, and the
+    // block does not open the gate.  0: no fused kernel follows.
+    uint32_t fused_rows = 0;
 };
 int launch_rs_plan2(const RsPlan2Args& a, hipStream_t s);
 
 // Fused RS8 repair (gen_fdec_asm.hip): re-encode + e x e solve in registers, one wave per block,
-// for blocks with e <= 16 repaired from parity rows 0..e-1.  Marks the blocks it repaired
+// for blocks with e <= 16 whose substitute parities are rows below min(16, m).  Marks the blocks it repaired
 // (rows = 0, psel = 0) so the unfused kernels that follow skip them.
 struct FdecArgs {
     uint8_t* base = nullptr;
@@ -303,9 +308,7 @@ struct FdecArgs {
     uint32_t lane_major = 0;             // lane L holds items 4L..4L+3; lanes without one exit
 };
 int launch_rs8_fused_decode(uint32_t k, uint32_t m, const FdecArgs& a, hipStream_t s);
-// The same repair with two waves per block sharing each column's transpose through LDS
-// (gen_fdec_q2.hip, 168 VGPRs: 3 waves per SIMD instead of 2).
-int launch_rs8_fused_decode_q2(uint32_t k, uint32_t m, const FdecArgs& a, hipStream_t s);
+bool rs8_fused_decode_covers(uint32_t k, uint32_t m, const FdecArgs& a);
 
 // MDP decode planning: per block one-stage coefficient matrix over the surviving slots.
 struct MdpPlanArgs {

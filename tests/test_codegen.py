@@ -10,7 +10,7 @@ import sys
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-GENERATORS = ["rs8_asm", "rs8_bitsliced", "rs8_q4", "fdec_asm", "fdec_q2", "solve_asm", "gf16_t3"]
+GENERATORS = ["rs8_asm", "rs8_bitsliced", "rs8_q4", "fdec_asm", "solve_asm", "gf16_t3"]
 
 
 @pytest.mark.parametrize("name", GENERATORS)

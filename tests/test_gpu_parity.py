@@ -454,6 +454,34 @@ def test_fused_decode_mixed_batch(orc, m, accumulate):
     assert np.array_equal(dev.cpu().numpy(), expect)
 
 
+@pytest.mark.parametrize("m,ne", [(32, 16), (32, 24), (16, 16), (16, 9), (8, 8), (8, 5)])
+def test_fused_decode_random_loss(orc, m, ne):
+    """NORM loses source and parity segments alike: ne erasures drawn uniformly over all k + m
+    slots.  The fused kernel takes every block whose substitute parities (the first e surviving
+    rows, reference scan normEncoderRS8.cpp:660-718) lie below min(16, m) -- for m <= 16 all of
+    them -- with the inverse written by parity row; the rest go unfused.  Bytes and statuses
+    must match the reference decode."""
+    k, vec, nb = 64, 1400, 96
+    enc, dec = _codecs(NFEC_RS8, k, m, vec)
+    clean = orc.encode_blocks(NFEC_RS8, k, m, vec, orc.make_blocks(k, m, vec, nb))
+    rng = np.random.default_rng(1000 + 10 * m + ne)
+    locs = np.zeros((nb, m), np.uint16)
+    counts = np.full(nb, ne, np.uint16)
+    for b in range(nb):
+        locs[b, :ne] = np.sort(rng.choice(k + m, ne, replace=False))
+    rx = clean.copy()
+    _erase(rx, locs, counts)
+    ref = rx.copy()
+    st_ref = orc.decode_blocks(NFEC_RS8, k, m, vec, ref, locs, counts)
+    dev = torch.from_numpy(rx).cuda()
+    st = dec.decode_blocks(dev, torch.from_numpy(locs.astype(np.int16)).cuda(),
+                           torch.from_numpy(counts.astype(np.int16)).cuda())
+    torch.cuda.synchronize()
+    assert np.array_equal(st.cpu().numpy(), st_ref)
+    assert np.array_equal(dev.cpu().numpy(), ref)
+    assert np.array_equal(ref[:, :k], clean[:, :k])
+
+
 @pytest.mark.parametrize("m", [32, 8])
 def test_unfused_gate_across_calls(orc, m):
     """The unfused stage 1 + solve run only when the plan opened this call's gate word (some

@@ -142,8 +142,8 @@ def fdec_asm(k, m, probe=None):
         w = slot_regs(c % NSLOT)
         if c < k:
             out = [f"s_bitcmp1_b64 s[{S_EM}:{S_EM + 1}], {c}", f"s_cselect_b32 s{S_LRS + 2}, 0, 0x80000000"]
-        else:
-            out = [f"s_cmp_lt_u32 {c - k}, %[e]", f"s_cselect_b32 s{S_LRS + 2}, 0x80000000, 0"]
+        else:  # parity row c - k: read when the block uses it (bit of the parity-row mask)
+            out = [f"s_bitcmp1_b32 %[ps], {c - k}", f"s_cselect_b32 s{S_LRS + 2}, 0x80000000, 0"]
         out.append(f"s_mul_i32 s{S_COL}, %[ss], {c}")
         for q in range(4):
             out.append(f"buffer_load_dwordx2 v[{w[2 * q]}:{w[2 * q + 1]}], {offs[q]}, s[{S_LRS}:{S_LRS + 3}], s{S_COL} offen")
@@ -188,7 +188,7 @@ def fdec_asm(k, m, probe=None):
                     L.append(f"v_xor_b32 v{acc}, v{B[b]}, v{acc}")
         else:
             t = c - k
-            L += [f"s_cmp_le_u32 %[e], {t}", f"s_cbranch_scc1 Lskip{c}_%="]
+            L += [f"s_bitcmp0_b32 %[ps], {t}", f"s_cbranch_scc1 Lskip{c}_%="]
             L += transpose(w, ring_temps())
             for i in range(8):
                 L.append(f"v_xor_b32 v{acc_reg(t, i)}, v{w[i]}, v{acc_reg(t, i)}")
@@ -208,7 +208,7 @@ def fdec_asm(k, m, probe=None):
             for i in range(8):
                 L.append(f"v_mov_b32 v{d_reg(sl, i)}, 0")
         for t in range(0 if probe == "nos2" else 16):
-            L += [f"s_cmp_le_u32 %[e], {t}", f"s_cbranch_scc1 Lrows{h}_%="]
+            L += [f"s_cmp_le_u32 %[tmax], {t}", f"s_cbranch_scc1 Lrows{h}_%="]
             cur = cbuf[t % 2]
             L.append("s_waitcnt lgkmcnt(0)")
             # next coefficient row (after row 15: row 0 again, for the second half)
@@ -275,6 +275,7 @@ PROBES = {1: "nos2", 2: "nos1", 3: "noload"}
 
 def gen_kernel(k, m, probe=None):
     K = f"rs8_fdec_k{k}_m{m}" + (f"_probe_{probe}" if probe else "")
+    nr = min(NCOLS_PAR, m)
     body = "\\n\"\n        \"".join(fdec_asm(k, m, probe))
     return f"""__global__ __launch_bounds__(256, 2) void {K}(FdecArgs a)
 {{
@@ -284,9 +285,11 @@ def gen_kernel(k, m, probe=None):
     const int32_t rows = (int32_t)__builtin_amdgcn_readfirstlane((uint32_t)a.rows[blk]);
     const uint32_t ps0 = __builtin_amdgcn_readfirstlane(a.psel[2 * (uint64_t)blk]);
     const uint32_t ps1 = __builtin_amdgcn_readfirstlane(a.psel[2 * (uint64_t)blk + 1]);
-    // qualifies: 1..16 source erasures repaired from parity rows 0..e-1
-    if (rows <= 0 || rows > 16 || ps1 != 0 || ps0 != ((1u << rows) - 1u)) return;
+    // qualifies: 1..16 source erasures repaired from parity rows below {nr} (the z rows this
+    // kernel computes); the plan then wrote the inverse by parity row, zero for unused rows
+    if (rows <= 0 || rows > 16 || ps1 != 0 || (ps0 >> {nr}) != 0u) return;
     const uint32_t e = (uint32_t)rows;
+    const uint32_t tmax = 32u - (uint32_t)__builtin_clz(ps0);  // highest used parity row + 1
     // (readfirstlane yields int: widen through uint32_t, or bit 31 would sign-extend into the
     // high word)
     const uint64_t em = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane(a.emask[2 * (uint64_t)blk]) |
@@ -315,7 +318,7 @@ def gen_kernel(k, m, probe=None):
         "{body}\\n"
         :
         : [base] "s"(base), [em] "s"(em), [cp] "s"(cp), [sp] "s"(sp), [e] "s"(e), [ss] "s"(a.seg_stride),
-          [acc] "s"(a.accumulate),
+          [acc] "s"(a.accumulate), [ps] "s"(ps0), [tmax] "s"(tmax),
           [o0] "v"(o[0]), [o1] "v"(o[1]), [o2] "v"(o[2]), [o3] "v"(o[3]),
           [s0] "v"(so[0]), [s1] "v"(so[1]), [s2] "v"(so[2]), [s3] "v"(so[3])
         : {clobbers()});
@@ -351,13 +354,21 @@ def main():
     parts.append("    return v;")
     parts.append("}")
     parts.append("")
+    parts.append("// true when launch_rs8_fused_decode runs a kernel for this shape and layout (the plan then")
+    parts.append("// writes the inverse of the blocks it will take by parity row)")
+    parts.append("bool rs8_fused_decode_covers(uint32_t k, uint32_t m, const FdecArgs& a)")
+    parts.append("{")
+    parts.append("    if ((a.vec & 7u) || a.vec > 2048 || a.coef_col_stride != 32 || (a.coef_block_stride & 15) ||")
+    parts.append("        (a.slots_stride & 1) || (uint64_t)a.seg_stride * (k + 16) + a.vec >= (1ull << 31))")
+    parts.append("        return false;")
+    parts.append("    return " + " || ".join(f"(k == {k} && m == {m})" for k, m in shapes) + ";")
+    parts.append("}")
+    parts.append("")
     parts.append("// NFEC_ENOTSUP when (k, m) has no fused kernel or the batch shape needs the unfused path")
     parts.append("int launch_rs8_fused_decode(uint32_t k, uint32_t m, const FdecArgs& a, hipStream_t s)")
     parts.append("{")
     parts.append("    if (a.nblocks == 0) return NFEC_OK;")
-    parts.append("    if ((a.vec & 7u) || a.vec > 2048 || a.coef_col_stride != 32 || (a.coef_block_stride & 15) ||")
-    parts.append("        (a.slots_stride & 1) || (uint64_t)a.seg_stride * (k + 16) + a.vec >= (1ull << 31))")
-    parts.append("        return NFEC_ENOTSUP;")
+    parts.append("    if (!rs8_fused_decode_covers(k, m, a)) return NFEC_ENOTSUP;")
     for v, probe in PROBES.items():
         parts.append(f"    if (k == 64 && m == 32 && fdec_variant() == {v}) {{")
         parts.append(f"        hipLaunchKernelGGL(rs8_fdec_k64_m32_probe_{probe}, dim3((a.nblocks + 3) / 4), dim3(256), 0, s, a);")
