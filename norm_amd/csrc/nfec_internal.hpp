@@ -194,7 +194,11 @@ struct Gf16T3Args {
     uint32_t acc_seg_stride = 0, acc_slot0 = 0;
     const uint32_t* rows_lim = nullptr;  // device word: rows needed (<= m), null: m
 };
-inline uint32_t gf16_t3_rows_padded(uint32_t m) { return (m + 43u) / 44u * 44u; }
+constexpr uint32_t kGf16T3RowsPerPass = 44;  // 11 row waves x 4 rows (gen_gf16_t3.py asserts it)
+constexpr uint32_t gf16_t3_rows_padded(uint32_t m)
+{
+    return (m + kGf16T3RowsPerPass - 1) / kGf16T3RowsPerPass * kGf16T3RowsPerPass;
+}
 int launch_gf16_t3_encode(const Gf16T3Args& a, hipStream_t s);  // NFEC_ENOTSUP: shape not covered
 void gf16_t3_offsets(const std::vector<uint32_t>& parity_rows, uint32_t k, uint32_t m, uint16_t* out);
 int launch_gf16_bs_encode(const Gf16BsEncArgs& a, hipStream_t s);  // NFEC_ENOTSUP: layout not 8-byte aligned

@@ -102,14 +102,15 @@ def main():
     }
     if kind == na.NFEC_RS16 and os.environ.get("NFEC_GF16_T3", "1") != "0" and vec % 8 == 0:
         # op roofline of the shared-table RS16 encode (gen_gf16_t3.hip), counted from its code:
-        # per (item group of 64 lanes x 64 symbols, pass of 44 rows, source column) the 11 row
-        # waves issue 44 x 16 planes x 3 ds_read_b64 (512 B each) and 7 VALU per plane, the
-        # builder 506 VALU and 125 ds_write_b64
+        # per (item group of 64 lanes x 64 symbols, pass of RP rows, source column) the row
+        # waves issue RP x 16 planes x 3 ds_read_b64 (512 B each) and 7 VALU per plane, the
+        # builder 506 VALU and 125 ds_write_b64 (RP = 44: 11 row waves x 4 rows)
         groups = -(-nb * vec // 8192)
-        passes = -(-m // 44)
+        RP = 44
+        passes = -(-m // RP)
         units = groups * passes * k
-        lds_bytes = units * 44 * 16 * 3 * 512
-        valu = units * (44 * 16 * 7 + 506)
+        lds_bytes = units * RP * 16 * 3 * 512
+        valu = units * (RP * 16 * 7 + 506)
         t = enc_ms * 1e-3
         out["op_roofline"] = {
             "kernel": "gf16_t3_encode_kernel",
@@ -119,7 +120,7 @@ def main():
                     "note": "table reads only (ds_read_b64, counted at 256 B/clk/CU)"},
             "valu": {"achieved": float("%.4g" % (valu * 64 / t)), "peak": 7.86e13, "unit": "lane-ops/s",
                      "frac": round(valu * 64 / t / 7.86e13, 4), "insts_per_launch": valu},
-            "lds_insts_per_launch": units * (44 * 16 * 3 + 125),
+            "lds_insts_per_launch": units * (RP * 16 * 3 + 125),
         }
     if er:
         dec_ms = timed(lambda: dec.decode_blocks(blocks, locs, counts, status=status, stream=stream), a.steps)

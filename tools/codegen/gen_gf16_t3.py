@@ -32,7 +32,7 @@ Usage: gen_gf16_t3.py OUT.hip
 import sys
 
 ROWS = 4                 # parity rows per row wave
-RWAVES = 11              # row waves per workgroup
+RWAVES = 11              # row waves per workgroup (15 x 3 rows at 4 waves/SIMD measured no faster)
 RP = ROWS * RWAVES       # rows per pass
 NWAVES = RWAVES + 1
 GROUPS = [(0, 6, 0), (6, 5, 64), (11, 5, 96)]   # (first plane, planes, first table row)
@@ -59,7 +59,7 @@ def acc(r, p, h):
     return 2 * (16 * r + p) + (1 - h)
 
 
-T_BASE = 128
+T_BASE = 32 * ROWS
 DEPTH = 4                # planes whose table reads are in flight beyond the one computed
 NSLOT = DEPTH + 1        # read-target slots: quads v128.., pairs after them
 A_BASE = T_BASE + 6 * NSLOT          # 4 rotating address registers
@@ -334,6 +334,7 @@ def main():
 #include "bitslice.hpp"
 
 namespace nfec {{
+static_assert(kGf16T3RowsPerPass == {RP}u, "gen_gf16_t3.py and nfec_internal.hpp disagree on the rows per pass");
 namespace {{
 
 __global__ __launch_bounds__({64 * NWAVES}, 1) void gf16_t3_encode_kernel(Gf16T3Args a)
