@@ -652,8 +652,9 @@ int decode_device(nfec_codec* c, const nfec_block_batch* b, const uint16_t* locs
     if ((rc = c->w_rows.reserve(sb))) return rc;
     if ((rc = c->w_cols.reserve(sb))) return rc;
     if (!status && (rc = c->w_status.reserve(sb))) return rc;
-    if ((rc = c->w_islots.reserve((size_t)sb * n))) return rc;
-    if ((rc = c->w_oslots.reserve((size_t)sb * n))) return rc;
+    // + 128: the bit-sliced solves' scalar loads read up to 128 slots past a block's list
+    if ((rc = c->w_islots.reserve((size_t)sb * n + 128))) return rc;
+    if ((rc = c->w_oslots.reserve((size_t)sb * n + 128))) return rc;
     if (c->kind == NFEC_MDP) {
         if ((rc = c->w_coef1.reserve((size_t)sb * n * dcs))) return rc;
     } else {
@@ -703,6 +704,29 @@ int decode_device(nfec_codec* c, const nfec_block_batch* b, const uint16_t* locs
             p.coef_stride = dcs;
             p.coef = c->w_coef1.p;
             if ((rc = launch_mdp_plan(p, s))) return rc;
+            // blocks with <= 16 erased source vectors: the snippet solve (NFEC_MDP_BS=0: off)
+            static const bool use_mdp_bs = [] {
+                const char* e = std::getenv("NFEC_MDP_BS");
+                return !(e && e[0] == '0');
+            }();
+            if (use_mdp_bs) {
+                MdpSolveArgs ms;
+                ms.base = blocks;
+                ms.block_stride = b->block_stride;
+                ms.seg_stride = b->seg_stride;
+                ms.nblocks = nb;
+                ms.vec = c->vec;
+                ms.rows = c->w_rows.p;
+                ms.cols = c->w_cols.p;
+                ms.in_slots = c->w_islots.p;
+                ms.out_slots = c->w_oslots.p;
+                ms.slots_stride = n;
+                ms.coef = c->w_coef1.p;
+                ms.coef_block_stride = (uint64_t)n * dcs;
+                ms.coef_col_stride = dcs;
+                rc = launch_mdp_solve_bs(ms, s);
+                if (rc != NFEC_OK && rc != NFEC_ENOTSUP) return fail(rc, "MDP solve launch failed");
+            }
             Gf8MatmulArgs a;
             a.in_base = blocks;
             a.in_block_stride = b->block_stride;

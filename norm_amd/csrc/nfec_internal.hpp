@@ -333,6 +333,28 @@ struct MdpPlanArgs {
 };
 int launch_mdp_plan(const MdpPlanArgs& a, hipStream_t s);
 
+// MDP decode, bit-sliced snippet solve (gen_solve_asm.hip): erased source r = XOR_j C[r][j] v_j
+// over the block's surviving vectors, for blocks with rows (source erasures) <= 16 and cols
+// (survivors) <= 96; marks them done (rows = 0) so the generic kernel that follows skips them.
+// The scalar loads of the slot lists read up to 128 entries past a block's list: the lists'
+// allocation must be padded by that much.
+struct MdpSolveArgs {
+    uint8_t* base = nullptr;             // the batch (inputs and outputs in place)
+    uint64_t block_stride = 0;
+    uint32_t seg_stride = 0;
+    uint32_t nblocks = 0;
+    uint32_t vec = 0;
+    int32_t* rows = nullptr;             // plan outputs (consumed and cleared)
+    const uint16_t* cols = nullptr;
+    const uint16_t* in_slots = nullptr;  // [b][slots_stride]
+    const uint16_t* out_slots = nullptr; // [b][slots_stride]
+    uint32_t slots_stride = 0;
+    const uint8_t* coef = nullptr;       // [b][j][r], column stride 32
+    uint64_t coef_block_stride = 0;
+    uint32_t coef_col_stride = 0;
+};
+int launch_mdp_solve_bs(const MdpSolveArgs& a, hipStream_t s);
+
 // utilities
 int launch_fill(uint8_t* base, uint64_t block_stride, uint32_t seg_stride, uint32_t nblocks,
                 const uint16_t* num_data, uint32_t k, uint32_t vec, uint64_t seed, uint64_t first_block,

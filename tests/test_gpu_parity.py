@@ -482,6 +482,44 @@ def test_fused_decode_random_loss(orc, m, ne):
     assert np.array_equal(ref[:, :k], clean[:, :k])
 
 
+@pytest.mark.parametrize("m,codeword", [(32, True), (32, False), (16, True), (16, False)])
+def test_mdp_snippet_solve(orc, m, codeword):
+    """MDP decode through the bit-sliced snippet solve (gen_solve_asm.hip, blocks with <= 16
+    erased source vectors and <= 96 survivors) and, for the rest of the batch, the generic
+    kernel.  Erasures over source and parity, shortened blocks, and (codeword=False) survivors
+    that are not a codeword: the reference's syndrome / Forney chain is a fixed linear map of
+    all survivors, so the bytes must match it for any input."""
+    k, vec, nb = 64, 1400, 40
+    _, dec = _codecs(NFEC_MDP, k, m, vec)
+    nd = np.full(nb, k, np.uint16)
+    nd[5], nd[17], nd[30] = 40, 9, 63
+    blocks = orc.make_blocks(k, m, vec, nb, num_data=nd)
+    if codeword:
+        blocks = orc.encode_blocks(NFEC_MDP, k, m, vec, blocks, nd)
+    else:
+        rng0 = np.random.default_rng(5)
+        for b in range(nb):
+            blocks[b, : int(nd[b]) + m] = rng0.integers(0, 256, (int(nd[b]) + m, vec), dtype=np.uint8)
+    rng = np.random.default_rng(77 + m)
+    locs = np.zeros((nb, m), np.uint16)
+    counts = np.zeros(nb, np.uint16)
+    for b in range(nb):
+        n = int(nd[b]) + m
+        ne = min(m, 1 + b % 20)  # 1..20 erasures: e > 16 source ones go to the generic kernel
+        locs[b, :ne] = np.sort(rng.choice(n, ne, replace=False))
+        counts[b] = ne
+    _erase(blocks, locs, counts)
+    ref = blocks.copy()
+    st_ref = orc.decode_blocks(NFEC_MDP, k, m, vec, ref, locs, counts, nd)
+    dev = torch.from_numpy(blocks).cuda()
+    st = dec.decode_blocks(dev, torch.from_numpy(locs.astype(np.int16)).cuda(),
+                           torch.from_numpy(counts.astype(np.int16)).cuda(),
+                           num_data=torch.from_numpy(nd.astype(np.int16)).cuda())
+    torch.cuda.synchronize()
+    assert np.array_equal(st.cpu().numpy(), st_ref)
+    assert np.array_equal(dev.cpu().numpy(), ref)
+
+
 @pytest.mark.parametrize("m", [32, 8])
 def test_unfused_gate_across_calls(orc, m):
     """The unfused stage 1 + solve run only when the plan opened this call's gate word (some
