@@ -56,6 +56,8 @@ ENC_CASES = [
     # kind, k, m, vec, seg_stride, nblocks
     (NFEC_RS8, 64, 32, 1400, 1400, 37),
     (NFEC_RS8, 64, 32, 1400, 1408, 5),
+    (NFEC_RS8, 64, 16, 1408, 1408, 29),  # NORM's canonical code at its real vector size (segment + 8)
+    (NFEC_RS8, 64, 8, 1408, 1408, 13),   # NORM's default parity count
     (NFEC_RS8, 64, 16, 1400, 1400, 9),
     (NFEC_RS8, 64, 8, 1400, 1400, 7),
     (NFEC_RS8, 64, 32, 1397, 1400, 6),   # segment tail (vec % 8 != 0)
@@ -122,6 +124,8 @@ def test_encode_accumulates_like_reference(orc, kind, k, m, vec, nb):
 DEC_CASES = [
     # kind, k, m, vec, nblocks, source erasures, parity erasures
     (NFEC_RS8, 64, 32, 1400, 23, 16, 0),
+    (NFEC_RS8, 64, 16, 1408, 19, 11, 5),   # NORM (64, 16), vector = segment + 8, source + parity lost
+    (NFEC_RS8, 64, 8, 1408, 11, 6, 2),
     (NFEC_RS8, 64, 32, 1400, 9, 32, 0),
     (NFEC_RS8, 64, 32, 1400, 9, 20, 12),
     (NFEC_RS8, 64, 32, 1400, 5, 0, 7),
