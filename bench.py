@@ -159,6 +159,16 @@ def main():
     dec_ms = timed(lambda: dec.decode_blocks(blocks, locs, counts, status=status, stream=stream), n_k)
     torch.cuda.synchronize(dev)
 
+    # achievable HBM rate on this box (report it beside the 8 TB/s spec): a 4 GiB
+    # device-to-device copy, read + write bytes over its time
+    with torch.cuda.stream(stream):
+        csrc = torch.empty(1 << 32, dtype=torch.uint8, device=dev)
+        cdst = torch.empty_like(csrc)
+        cdst.copy_(csrc)
+    copy_ms = timed(lambda: cdst.copy_(csrc), 5)
+    copy_gbs = 2 * csrc.numel() / (copy_ms * 1e-3) / 1e9
+    del csrc, cdst
+
     host = None
     if a.host_steps > 0:
         import numpy as np
@@ -294,6 +304,8 @@ def main():
             "kernel": encode_kernel_name(k, m, vec),
             "algorithmic_bytes_per_launch": enc_bytes,
             "read_only_frac": round(k * vec * nb / (enc_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+            "achievable_copy": {"GBps": round(copy_gbs, 1), "frac": round(achieved / copy_gbs, 4),
+                                "note": "4 GiB device-to-device copy on this GPU, read + write bytes"},
             "valu": valu,
         },
         "kernels_ms": {"encode": round(enc_ms, 4), "decode": round(dec_ms, 4)},
