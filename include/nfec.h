@@ -200,7 +200,9 @@ int nfec_decode_vectors(nfec_codec* codec, void* const* vector_list, uint32_t nu
  *       word w of (block b, slot s) = mix(seed ^ ((b0+b)<<20) ^ s + (w+1)*0x9E3779B97F4A7C15).
  * erasures: per block `count` sorted distinct indices in [0, range), Fisher-Yates over the
  *           counter stream mix(seed ^ 0xE7A5E7A500000000 ^ (b0+b) + (i+1)*gamma).
- * zero: zero the listed slots of every block (the receiver's zero-fill, normObject.cpp:1579). */
+ * zero: zero the listed slots of every block (the receiver's zero-fill, normObject.cpp:1579).
+ * stream_copy: device-to-device copy of `bytes` (16-byte aligned pointers and size) by a
+ *       streaming kernel, for the bench's achievable-HBM-rate figure. */
 int nfec_util_fill(const nfec_block_batch* batch, uint32_t num_data, uint32_t vector_size,
                    uint64_t seed, uint64_t first_block, void* stream);
 int nfec_util_erasures(uint16_t* erasure_locs, uint32_t erasure_stride, uint16_t* erasure_counts,
@@ -209,6 +211,7 @@ int nfec_util_erasures(uint16_t* erasure_locs, uint32_t erasure_stride, uint16_t
 int nfec_util_zero_slots(const nfec_block_batch* batch, const uint16_t* erasure_locs,
                          uint32_t erasure_stride, const uint16_t* erasure_counts,
                          uint32_t vector_size, void* stream);
+int nfec_util_stream_copy(void* dst, const void* src, uint64_t bytes, void* stream);
 
 /* ---- NORM wire format on the FEC path (host only; no device work) ----
  * The FEC Object Transmission Information header extension (type 64) a sender attaches to

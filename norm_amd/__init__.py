@@ -8,7 +8,7 @@ surface (include/normEncoder.h:38-54) plus batch entry points for device-residen
 from ._native import NFEC_RS8, NFEC_RS16, NFEC_MDP, NFEC_ACCUMULATE, NfecError, lib  # noqa: F401
 from .codec import (  # noqa: F401
     NormEncoderRS8, NormDecoderRS8, NormEncoderRS16, NormDecoderRS16, NormEncoderMDP, NormDecoderMDP,
-    BlockLayout, build_generator, device_count, fill_blocks, make_erasures, zero_erasures,
+    BlockLayout, build_generator, device_count, fill_blocks, make_erasures, stream_copy, zero_erasures,
 )
 
 __version__ = "0.1.0"

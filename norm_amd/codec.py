@@ -366,6 +366,15 @@ def fill_blocks(blocks, num_data, vector_size, seed, first_block=0, per_block_nu
             "nfec_util_fill")
 
 
+def stream_copy(dst, src, stream=None):
+    """dst[:] = src through the streaming copy kernel (bench's achievable-HBM figure)."""
+    if dst.numel() * dst.element_size() != src.numel() * src.element_size():
+        raise ValueError("stream_copy: size mismatch")
+    N.check(N.lib().nfec_util_stream_copy(ctypes.c_void_p(dst.data_ptr()), ctypes.c_void_p(src.data_ptr()),
+                                          src.numel() * src.element_size(), _stream_handle(stream)),
+            "nfec_util_stream_copy")
+
+
 def make_erasures(nblocks, range_, count, seed, stride, first_block=0, device="cuda", stream=None):
     import torch
 

@@ -1966,4 +1966,10 @@ int nfec_util_zero_slots(const nfec_block_batch* b, const uint16_t* locs, uint32
                              stride, counts, vector_size, static_cast<hipStream_t>(stream));
 }
 
+int nfec_util_stream_copy(void* dst, const void* src, uint64_t bytes, void* stream)
+{
+    if ((!dst || !src) && bytes) return fail(NFEC_EINVAL, "null argument");
+    return launch_stream_copy(dst, src, bytes, static_cast<hipStream_t>(stream));
+}
+
 }  // extern "C"

@@ -361,6 +361,7 @@ int launch_fill(uint8_t* base, uint64_t block_stride, uint32_t seg_stride, uint3
                 hipStream_t s);
 int launch_erasures(uint16_t* locs, uint32_t stride, uint16_t* counts, uint32_t nblocks, uint32_t range,
                     uint32_t count, uint64_t seed, uint64_t first_block, hipStream_t s);
+int launch_stream_copy(void* dst, const void* src, uint64_t bytes, hipStream_t s);
 int launch_zero_slots(uint8_t* base, uint64_t block_stride, uint32_t seg_stride, uint32_t nblocks,
                       const uint16_t* locs, uint32_t stride, const uint16_t* counts, uint32_t vec,
                       hipStream_t s);

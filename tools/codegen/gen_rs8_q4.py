@@ -60,8 +60,9 @@ class Cfg:
            the 11 group-A combinations), "AB" (all combinations: one slot, two barriers per
            step)"""
 
-    def __init__(self, nslot=2, lazy=False, share="planes"):
+    def __init__(self, nslot=2, lazy=False, share="planes", lpol="", spol=""):
         self.nslot, self.lazy, self.share = nslot, lazy, share
+        self.lpol, self.spol = lpol, spol  # cache-policy suffixes of the source loads / parity stores
         assert share == "planes" or not lazy
         if lazy:
             # 4 item offsets + LDS address in freed A-combination registers (bank 0)
@@ -89,7 +90,8 @@ class Cfg:
 
 DEFAULT = Cfg(2, False)
 # variants of the (64, 32) kernel selectable with NFEC_Q4_VARIANT=<id> for A/B runs
-VARIANTS = {1: Cfg(3, True), 2: Cfg(2, True), 3: Cfg(2, share="A"), 4: Cfg(2, share="AB")}
+VARIANTS = {1: Cfg(3, True), 2: Cfg(2, True), 3: Cfg(2, share="A"), 4: Cfg(2, share="AB"),
+            5: Cfg(lpol=" nt"), 6: Cfg(spol=" nt"), 7: Cfg(lpol=" nt", spol=" nt")}
 S_LRS, S_SRS = 64, 68        # load / store buffer descriptors
 S_MASK = 72                  # s72..s77 transpose masks (gen_rs8_asm.transpose reads them here)
 S_COL, S_ROW = 78, 79
@@ -312,7 +314,7 @@ def role_asm(G, k, m, w, probe=None, cfg=DEFAULT):
         rs = cfg.ring_slot(step % NS)
         out = [f"s_mul_i32 s{S_COL}, %[ss], {col}"]
         for q in range(4):
-            out.append(f"buffer_load_dwordx2 v[{rs[2 * q]}:{rs[2 * q + 1]}], {offs[q]}, s[{S_LRS}:{S_LRS + 3}], s{S_COL} offen")
+            out.append(f"buffer_load_dwordx2 v[{rs[2 * q]}:{rs[2 * q + 1]}], {offs[q]}, s[{S_LRS}:{S_LRS + 3}], s{S_COL} offen{cfg.lpol}")
         return out
 
     for s in range(min(NS, steps)):
@@ -380,7 +382,7 @@ def role_asm(G, k, m, w, probe=None, cfg=DEFAULT):
             L.append(f"v_xor_b32 v{acc[2 * q + 1]}, v{tmp[2 * q + 1]}, v{acc[2 * q + 1]}")
         L.append(f"Lnoacc_{r}_%=:")
         for q in range(4):
-            L.append(f"buffer_store_dwordx2 v[{acc[2 * q]}:{acc[2 * q + 1]}], {offs[q]}, s[{S_SRS}:{S_SRS + 3}], s{S_ROW} offen")
+            L.append(f"buffer_store_dwordx2 v[{acc[2 * q]}:{acc[2 * q + 1]}], {offs[q]}, s[{S_SRS}:{S_SRS + 3}], s{S_ROW} offen{cfg.spol}")
     return L
 
 
