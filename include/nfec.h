@@ -113,6 +113,11 @@ int nfec_codec_create(int device, int kind, uint32_t num_data, uint32_t num_pari
                       uint32_t vector_size, nfec_codec** out);
 void nfec_codec_destroy(nfec_codec* codec);
 int nfec_codec_get_info(const nfec_codec* codec, nfec_codec_info* out);
+/* Encode paths the codec chose at creation (bit mask, < 0 on error):
+ *   NFEC_FEATURE_RS16_TOEPLITZ: unshortened, overwriting RS16 encodes use the Toeplitz split of
+ *   the generator (three (m/2)-row products over k/2 columns). */
+#define NFEC_FEATURE_RS16_TOEPLITZ 1
+int nfec_codec_features(const nfec_codec* codec);
 /* Copies the m x k parity rows of the systematic generator (row p = generator row k+p),
  * row-major, elements of symbol_bytes each.  MDP: the m x k matrix of the LFSR code for a
  * full block of k source symbols.  bytes must be >= m*k*symbol_bytes. */

@@ -15,6 +15,7 @@ HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "nfec.h")
 NFEC_RS8, NFEC_RS16, NFEC_MDP = 1, 2, 3
 NFEC_OK, NFEC_EINVAL, NFEC_ENOMEM, NFEC_EDEVICE, NFEC_ERANGE, NFEC_ENOTSUP = 0, -1, -2, -3, -4, -5
 NFEC_ACCUMULATE = 1
+NFEC_FEATURE_RS16_TOEPLITZ = 1
 
 
 class NfecError(RuntimeError):
@@ -103,6 +104,7 @@ _SIGS = {
     "nfec_codec_create": (_I, [_I, _I, _U32, _U32, _U32, ctypes.POINTER(_P)]),
     "nfec_codec_destroy": (None, [_P]),
     "nfec_codec_get_info": (_I, [_P, ctypes.POINTER(CodecInfo)]),
+    "nfec_codec_features": (_I, [_P]),
     "nfec_codec_get_generator": (_I, [_P, _P, ctypes.c_size_t]),
     "nfec_encode": (_I, [_P, ctypes.POINTER(BlockBatch), _P]),
     "nfec_decode": (_I, [_P, ctypes.POINTER(BlockBatch), _P, _U32, _P, _P, _P]),

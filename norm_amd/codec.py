@@ -148,6 +148,13 @@ class _Codec:
         N.check(N.lib().nfec_codec_get_generator(self._h, out.ctypes.data, out.nbytes), "nfec_codec_get_generator")
         return out
 
+    def features(self):
+        """Bit mask of the encode paths the codec chose (NFEC_FEATURE_*, include/nfec.h)."""
+        self._need()
+        rc = N.lib().nfec_codec_features(self._h)
+        N.check(min(rc, 0), "nfec_codec_features")
+        return rc
+
     def _need(self):
         if not self._h:
             raise RuntimeError("codec not initialised (call Init)")

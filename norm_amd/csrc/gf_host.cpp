@@ -182,3 +182,77 @@ void gf16_t3_offsets(const std::vector<uint32_t>& parity_rows, uint32_t k, uint3
 }
 
 }  // namespace nfec
+
+namespace nfec {
+
+// 16 row masks of x -> c * x over GF(2^16): M[p] bit q = bit p of c * 2^q (gf16_bs.hpp)
+static void gf16_bitmatrix(const Field& f, uint32_t c, uint16_t* M)
+{
+    for (int p = 0; p < 16; ++p) M[p] = 0;
+    for (int q = 0; q < 16; ++q) {
+        const uint32_t v = f.mul(c, 1u << q);
+        for (int p = 0; p < 16; ++p) M[p] |= (uint16_t)(((v >> p) & 1u) << q);
+    }
+}
+
+// The Toeplitz split of the RS16 generator (kernels_tmvp.hip): G[p][j] = W(y_p) T[p][j] c_j for
+// j >= 1 with T[p][j] = 1 / (1 + alpha^(k+p-j)).  Builds the three cw x (k/2) product matrices
+// (row-major, virtual column q*cw + i for the column pair a = 2q*cw + i, b = a + cw):
+//   prod[0] = A       = T[p][a]
+//   prod[1] = (B-A) c = (T[p][b] + T[p][a]) c_b
+//   prod[2] = (C-A) c = (T[p+cw][a] + T[p][a]) c_a      (c_0 = 0)
+// and the row masks of c_j, W(y_p) and G[p][0].  Every G[p][j] is re-derived from the factors
+// and compared with the generator; false (and nothing used) on any mismatch or shape the split
+// does not cover (m even, m/2 a power of two, k a multiple of m).
+bool rs16_tmvp_plan(uint32_t k, uint32_t m, const std::vector<uint32_t>& gen, std::vector<uint32_t> prod[3],
+                    std::vector<uint16_t>& cmat, std::vector<uint16_t>& wmat, std::vector<uint16_t>& gmat)
+{
+    const uint32_t cw = m / 2;
+    if (m < 2 || (m & 1u) || (cw & (cw - 1u)) || k % m || gen.size() != (size_t)m * k) return false;
+    const Field& f = gf16();
+    const uint32_t q = f.q;
+    std::vector<uint32_t> x(k);
+    for (uint32_t j = 0; j < k; ++j) x[j] = rs_point(f, j);
+    std::vector<uint32_t> c(k, 0), w(m), h(k + m, 0);
+    for (uint32_t j = 1; j < k; ++j) {
+        uint64_t lwp = 0;  // log W'(x_j)
+        for (uint32_t l = 0; l < k; ++l)
+            if (l != j) lwp += f.log[x[j] ^ x[l]];
+        c[j] = f.exp[(2ull * q - (j - 1) % q - lwp % q) % q];
+    }
+    for (uint32_t p = 0; p < m; ++p) {
+        const uint32_t y = rs_point(f, k + p);
+        uint64_t lw = 0;
+        for (uint32_t l = 0; l < k; ++l) lw += f.log[y ^ x[l]];
+        w[p] = f.exp[lw % q];
+    }
+    for (uint32_t t = 1; t < k + m; ++t) {
+        const uint32_t d = 1u ^ f.exp[t % q];
+        if (d == 0) return false;
+        h[t] = f.exp[(q - f.log[d]) % q];
+    }
+    for (uint32_t p = 0; p < m; ++p)
+        for (uint32_t j = 1; j < k; ++j)
+            if (gen[(size_t)p * k + j] != f.mul(w[p], f.mul(h[k + p - j], c[j]))) return false;
+    const uint32_t half = k / 2;
+    for (int e = 0; e < 3; ++e) prod[e].assign((size_t)cw * half, 0);
+    for (uint32_t p = 0; p < cw; ++p)
+        for (uint32_t v = 0; v < half; ++v) {
+            const uint32_t a = 2 * (v / cw) * cw + v % cw, b = a + cw;
+            const uint32_t ta = h[k + p - a];
+            prod[0][(size_t)p * half + v] = ta;
+            prod[1][(size_t)p * half + v] = f.mul(h[k + p - b] ^ ta, c[b]);
+            prod[2][(size_t)p * half + v] = f.mul(h[k + p + cw - a] ^ ta, c[a]);
+        }
+    cmat.assign((size_t)k * 16, 0);
+    wmat.assign((size_t)m * 16, 0);
+    gmat.assign((size_t)m * 16, 0);
+    for (uint32_t j = 0; j < k; ++j) gf16_bitmatrix(f, c[j], &cmat[(size_t)j * 16]);
+    for (uint32_t p = 0; p < m; ++p) {
+        gf16_bitmatrix(f, w[p], &wmat[(size_t)p * 16]);
+        gf16_bitmatrix(f, gen[(size_t)p * k], &gmat[(size_t)p * 16]);
+    }
+    return true;
+}
+
+}  // namespace nfec

@@ -1,0 +1,150 @@
+// RS16 encode by the Toeplitz split of the generator (rs16_tmvp in nfec_api.cpp).
+//
+// The RS16 generator of NormEncoderRS16::Init (src/common/normEncoderRS16.cpp:399-461) is the
+// Lagrange basis of the points x_0 = 0, x_j = alpha^(j-1) evaluated at y_p = alpha^(k-1+p):
+//   G[p][j] = W(y_p) / ((y_p + x_j) W'(x_j)),  W(z) = prod_l (z + x_l),
+// and for j >= 1, y_p + x_j = alpha^(j-1) (1 + alpha^(k+p-j)), so
+//   G[p][j] = W(y_p) * T[p][j] * c_j,  T[p][j] = 1 / (1 + alpha^(k+p-j)),  c_j = alpha^-(j-1) / W'(x_j):
+// a row scaling, a Toeplitz matrix and a column scaling.  With the rows split in halves R0, R1
+// of cw = m/2 and the columns in chunk pairs (C0, C1) of cw each, T's blocks are [[A, B], [C, A]]
+// and one Karatsuba step needs three products instead of four:
+//   P0 = A (v_C0 + v_C1)  (v = c * d, the prescaled data: prescale_kernel)
+//   P1 = (B - A) c_C1 d_C1,  P2 = (C - A) c_C0 d_C0   (coefficients absorb c)
+//   parity_R0 = W (P0 + P1) + G[.][0] d_0,  parity_R1 = W (P0 + P2) + G[.][0] d_0  (postscale_kernel)
+// The three products run on the shared-table kernel (gen_gf16_t3.hip) in one launch; these two
+// kernels are the elementwise steps around it: bit-sliced multiplies by wave-uniform constants.
+#include "nfec_internal.hpp"
+#include "gf16_bs.hpp"
+
+namespace nfec {
+namespace {
+
+// items of 8 bytes (4 symbols), 8 per lane, 512 per wave: item j of the lane is
+// chunk * 512 + j * 64 + lane, flat over (block, position in the segment)
+struct ItemMap {
+    uint32_t ok[8];
+    uint64_t blk[8];
+    uint32_t off[8];
+};
+
+__device__ __forceinline__ void map_items(uint32_t chunk, uint32_t lane, uint32_t items, uint32_t ipb, ItemMap& m)
+{
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const uint32_t it = chunk * 512u + (uint32_t)j * 64u + lane;
+        m.ok[j] = it < items;
+        const uint32_t b = it / ipb;
+        m.blk[j] = b;
+        m.off[j] = (it - b * ipb) * 8u;
+    }
+}
+
+__device__ __forceinline__ void load16(uint32_t x[16], const uint8_t* col, uint64_t block_stride, const ItemMap& m)
+{
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        uint2 v = make_uint2(0u, 0u);
+        if (m.ok[j]) v = *reinterpret_cast<const uint2*>(col + m.blk[j] * block_stride + m.off[j]);
+        x[2 * j] = v.x;
+        x[2 * j + 1] = v.y;
+    }
+}
+
+__device__ __forceinline__ void store16(const uint32_t x[16], uint8_t* col, uint64_t block_stride, const ItemMap& m)
+{
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+        if (m.ok[j]) *reinterpret_cast<uint2*>(col + m.blk[j] * block_stride + m.off[j]) = make_uint2(x[2 * j], x[2 * j + 1]);
+}
+
+// v = c_a d_a + c_b d_b for every chunk pair: virtual column q*cw + i from columns
+// a = 2q*cw + i and b = a + cw (c_0 = 0: column 0 is added by the postscale)
+__global__ __launch_bounds__(256, 4) void tmvp_prescale_kernel(Rs16TmvpArgs a)
+{
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t wid = __builtin_amdgcn_readfirstlane(blockIdx.x * 4u + (threadIdx.x >> 6));
+    const uint32_t half = a.k / 2;
+    const uint32_t v = wid % half, chunk = wid / half;
+    const uint32_t ipb = a.vec / 8u, items = a.nblocks * ipb;
+    if (chunk * 512u >= items) return;
+    const uint32_t q = v / a.cw, i = v - q * a.cw;
+    const uint32_t ca = 2u * q * a.cw + i, cb = ca + a.cw;
+    ItemMap m;
+    map_items(chunk, lane, items, ipb, m);
+    uint32_t x[16], y[16], z[16];
+    load16(x, a.base + (uint64_t)ca * a.seg_stride, a.block_stride, m);
+    load16(y, a.base + (uint64_t)cb * a.seg_stride, a.block_stride, m);
+    bs16::transpose(x);
+    bs16::transpose(y);
+#pragma unroll
+    for (int p = 0; p < 16; ++p) z[p] = 0;
+    bs16::mulc_acc(x, z, a.cmat + 16u * ca);
+    bs16::mulc_acc(y, z, a.cmat + 16u * cb);
+    bs16::transpose(z);
+    store16(z, a.s + (uint64_t)v * a.vec, a.s_block_stride, m);
+}
+
+// parity row p < cw and p + cw from P0 (parity row p), P1 (x row p), P2 (parity row cw + p)
+// and source column 0
+__global__ __launch_bounds__(256, 4) void tmvp_postscale_kernel(Rs16TmvpArgs a)
+{
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t wid = __builtin_amdgcn_readfirstlane(blockIdx.x * 4u + (threadIdx.x >> 6));
+    const uint32_t p = wid % a.cw, chunk = wid / a.cw;
+    const uint32_t ipb = a.vec / 8u, items = a.nblocks * ipb;
+    if (chunk * 512u >= items) return;
+    ItemMap m;
+    map_items(chunk, lane, items, ipb, m);
+    uint8_t* r0 = const_cast<uint8_t*>(a.base) + (uint64_t)(a.k + p) * a.seg_stride;
+    uint8_t* r1 = const_cast<uint8_t*>(a.base) + (uint64_t)(a.k + a.cw + p) * a.seg_stride;
+    uint32_t t0[16], t1[16], d0[16], o[16];
+    load16(t0, r0, a.block_stride, m);
+    load16(d0, a.base, a.block_stride, m);
+    load16(t1, a.x + (uint64_t)p * a.vec, a.x_block_stride, m);
+#pragma unroll
+    for (int j = 0; j < 16; ++j) t1[j] ^= t0[j];  // P0 + P1
+    bs16::transpose(t1);
+    bs16::transpose(d0);
+#pragma unroll
+    for (int j = 0; j < 16; ++j) o[j] = 0;
+    bs16::mulc_acc(t1, o, a.wmat + 16u * p);
+    bs16::mulc_acc(d0, o, a.gmat + 16u * p);
+    bs16::transpose(o);
+    load16(t1, r1, a.block_stride, m);
+    store16(o, r0, a.block_stride, m);
+#pragma unroll
+    for (int j = 0; j < 16; ++j) t1[j] ^= t0[j];  // P0 + P2
+    bs16::transpose(t1);
+#pragma unroll
+    for (int j = 0; j < 16; ++j) o[j] = 0;
+    bs16::mulc_acc(t1, o, a.wmat + 16u * (a.cw + p));
+    bs16::mulc_acc(d0, o, a.gmat + 16u * (a.cw + p));
+    bs16::transpose(o);
+    store16(o, r1, a.block_stride, m);
+}
+
+}  // namespace
+
+int launch_tmvp_prescale(const Rs16TmvpArgs& a, hipStream_t s)
+{
+    const uint64_t items = (uint64_t)a.nblocks * (a.vec / 8u);
+    const uint64_t waves = (items + 511) / 512 * (a.k / 2);
+    if (items >= (1ull << 32) || waves >= (1ull << 32)) return NFEC_ENOTSUP;
+    if (waves == 0) return NFEC_OK;
+    hipLaunchKernelGGL(tmvp_prescale_kernel, dim3((uint32_t)((waves + 3) / 4)), dim3(256), 0, s, a);
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? NFEC_OK : hip_fail(e, "tmvp prescale launch");
+}
+
+int launch_tmvp_postscale(const Rs16TmvpArgs& a, hipStream_t s)
+{
+    const uint64_t items = (uint64_t)a.nblocks * (a.vec / 8u);
+    const uint64_t waves = (items + 511) / 512 * a.cw;
+    if (items >= (1ull << 32) || waves >= (1ull << 32)) return NFEC_ENOTSUP;
+    if (waves == 0) return NFEC_OK;
+    hipLaunchKernelGGL(tmvp_postscale_kernel, dim3((uint32_t)((waves + 3) / 4)), dim3(256), 0, s, a);
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? NFEC_OK : hip_fail(e, "tmvp postscale launch");
+}
+
+}  // namespace nfec

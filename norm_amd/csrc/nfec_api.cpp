@@ -204,6 +204,13 @@ struct nfec_codec {
     DevBuf<uint16_t> d_lwp, d_lw;  // RS8 closed-form plan constants: log W'(x_j), log W(y_p)
     DevBuf<uint16_t> d_sel16;      // RS16 bit-sliced encode table offsets [k][m][64] (may be absent)
     DevBuf<uint16_t> d_t3off;      // RS16 shared-table encode LDS offsets [k+1][m_pad][48]
+    // RS16 encode by the Toeplitz split (kernels_tmvp.hip): offsets of the three products, each
+    // [k/2+1][m_pad(m/2)][48], then the constants' row masks (c_j [k][16], W [m][16], G0 [m][16])
+    bool tmvp = false;
+    DevBuf<uint16_t> d_tmvp_off, d_tmvp_mat;
+    std::mutex tmvp_mu;            // one Toeplitz encode at a time per codec: they share w_tmvp
+    DevBuf<uint8_t> w_tmvp;        // prescaled pair sums + P1 rows of a sub-batch
+    hipEvent_t tmvp_done = nullptr;  // the last Toeplitz encode's end, on its stream
 
     // decode workspace (guarded by mu)
     std::mutex mu;
@@ -228,8 +235,11 @@ struct nfec_codec {
         async.shutdown();  // outstanding async requests complete before the codec goes away
         DeviceGuard g(device);
         stage.release();
-        for (auto* b : {&d_coef, &d_gen, &d_exp, &w_coef1, &w_coef2, &w_z, &w_work, &s_block, &d_mdp_step})
+        for (auto* b : {&d_coef, &d_gen, &d_exp, &w_coef1, &w_coef2, &w_z, &w_work, &s_block, &d_mdp_step, &w_tmvp})
             b->release();
+        d_tmvp_off.release();
+        d_tmvp_mat.release();
+        if (tmvp_done) (void)hipEventDestroy(tmvp_done);
         d_vtab.release();
         d_log.release();
         d_lwp.release();
@@ -361,6 +371,34 @@ int build_codec(nfec_codec* c)
             if ((rc = c->d_t3off.reserve(off.size()))) return rc;
             NFEC_HIP(hipMemcpy(c->d_t3off.p, off.data(), off.size() * 2, hipMemcpyHostToDevice));
         }
+        // RS16: the Toeplitz split of the generator, three (m/2)-row products over k/2 columns
+        // instead of one m-row product over k (kernels_tmvp.hip), where its passes are fewer:
+        // NFEC_RS16_TMVP=0 never, =1 whenever the shape allows it (tests), unset when it pays
+        if (wide && use_gf16_t3() && (c->vec % 8) == 0) {
+            const char* ev = std::getenv("NFEC_RS16_TMVP");
+            const int mode = ev ? std::atoi(ev) : -1;
+            const uint32_t cw = c->m / 2;
+            const bool pays = 3ull * ((cw + kGf16T3RowsPerPass - 1) / kGf16T3RowsPerPass) * (c->k / 2) <
+                              (uint64_t)((c->m + kGf16T3RowsPerPass - 1) / kGf16T3RowsPerPass) * c->k;
+            std::vector<uint32_t> prod[3];
+            std::vector<uint16_t> cm, wm, gm;
+            if (mode != 0 && (mode == 1 || pays) && rs16_tmvp_plan(c->k, c->m, c->gen, prod, cm, wm, gm)) {
+                const uint32_t half = c->k / 2, mp = gf16_t3_rows_padded(cw);
+                const size_t one = (size_t)(half + 1) * mp * 48;
+                std::vector<uint16_t> off(3 * one);
+                for (int e = 0; e < 3; ++e) gf16_t3_offsets(prod[e], half, cw, off.data() + e * one);
+                std::vector<uint16_t> mat;
+                mat.insert(mat.end(), cm.begin(), cm.end());
+                mat.insert(mat.end(), wm.begin(), wm.end());
+                mat.insert(mat.end(), gm.begin(), gm.end());
+                if ((rc = c->d_tmvp_off.reserve(off.size()))) return rc;
+                if ((rc = c->d_tmvp_mat.reserve(mat.size()))) return rc;
+                NFEC_HIP(hipMemcpy(c->d_tmvp_off.p, off.data(), off.size() * 2, hipMemcpyHostToDevice));
+                NFEC_HIP(hipMemcpy(c->d_tmvp_mat.p, mat.data(), mat.size() * 2, hipMemcpyHostToDevice));
+                NFEC_HIP(hipEventCreateWithFlags(&c->tmvp_done, hipEventDisableTiming));
+                c->tmvp = true;
+            }
+        }
         if (!wide || std::min(c->k, c->m) <= kPlanCfMaxE) {
             // log W'(x_j) over the k source points and log W(y_p) at the parity points (the
             // closed-form plans: rs_plan2_kernel for RS8, rs16_plan_cf_kernel for RS16)
@@ -474,6 +512,88 @@ static bool use_asm()
 }
 
 // ---- encode on a device batch ----
+// RS16 encode by the Toeplitz split (kernels_tmvp.hip): per sub-batch the prescale of the chunk
+// pairs, the three shared-table products in one launch, and the postscale into the parity.
+// The sub-batch scratch is the codec's, so calls are ordered: each waits (on its stream) for
+// the previous one's end.
+int rs16_tmvp_encode(nfec_codec* c, const nfec_block_batch* b, hipStream_t s)
+{
+    const uint32_t k = c->k, m = c->m, cw = m / 2, half = k / 2, vec = c->vec;
+    const uint64_t per_block = (uint64_t)(half + cw) * vec;
+    const uint32_t sb = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(b->nblocks, (8ull << 30) / per_block));
+    std::lock_guard<std::mutex> lk(c->tmvp_mu);
+    int rc = c->w_tmvp.reserve((size_t)sb * per_block);
+    if (rc) return rc;
+    NFEC_HIP(hipStreamWaitEvent(s, c->tmvp_done, 0));
+    const uint32_t mp = gf16_t3_rows_padded(cw);
+    const size_t one = (size_t)(half + 1) * mp * 48;
+    uint32_t shift = 0;
+    while ((1u << shift) < cw) ++shift;
+    for (uint32_t b0 = 0; b0 < b->nblocks; b0 += sb) {
+        const uint32_t nb = std::min(sb, b->nblocks - b0);
+        uint8_t* blocks = static_cast<uint8_t*>(b->blocks) + (uint64_t)b0 * b->block_stride;
+        Rs16TmvpArgs a;
+        a.base = blocks;
+        a.block_stride = b->block_stride;
+        a.seg_stride = b->seg_stride;
+        a.nblocks = nb;
+        a.vec = vec;
+        a.k = k;
+        a.cw = cw;
+        a.s = c->w_tmvp.p;
+        a.s_block_stride = (uint64_t)half * vec;
+        a.x = c->w_tmvp.p + (uint64_t)sb * half * vec;
+        a.x_block_stride = (uint64_t)cw * vec;
+        a.cmat = c->d_tmvp_mat.p;
+        a.wmat = c->d_tmvp_mat.p + (size_t)k * 16;
+        a.gmat = c->d_tmvp_mat.p + (size_t)(k + m) * 16;
+        Gf16T3Args e[3];
+        for (int i = 0; i < 3; ++i) {
+            e[i].nblocks = nb;
+            e[i].k = half;
+            e[i].m = cw;
+            e[i].m_pad = mp;
+            e[i].vec_bytes = vec;
+            e[i].offs = c->d_tmvp_off.p + i * one;
+            e[i].base = blocks;
+            e[i].block_stride = b->block_stride;
+            e[i].seg_stride = b->seg_stride;
+            e[i].out_base = blocks;
+            e[i].out_block_stride = b->block_stride;
+            e[i].out_seg_stride = b->seg_stride;
+        }
+        // P0 = A (pair sums) -> parity rows [k, k + cw)
+        e[0].base = a.s;
+        e[0].block_stride = a.s_block_stride;
+        e[0].seg_stride = vec;
+        e[0].out_slot0 = k;
+        // P1 over the second column of every pair -> x rows
+        e[1].col_shift = shift;
+        e[1].col_mask = cw - 1;
+        e[1].col_chunk = 2 * cw;
+        e[1].col_base = cw;
+        e[1].in_slots = k + m;
+        e[1].out_base = a.x;
+        e[1].out_block_stride = a.x_block_stride;
+        e[1].out_seg_stride = vec;
+        e[1].out_slot0 = 0;
+        // P2 over the first column of every pair -> parity rows [k + cw, k + m)
+        e[2].col_shift = shift;
+        e[2].col_mask = cw - 1;
+        e[2].col_chunk = 2 * cw;
+        e[2].col_base = 0;
+        e[2].in_slots = k + m;
+        e[2].out_slot0 = k + cw;
+        // a shape the kernels do not cover shows on the first sub-batch, before any parity byte
+        // is written: NFEC_ENOTSUP then hands the batch to the one-product encode
+        if ((rc = launch_tmvp_prescale(a, s))) return rc == NFEC_ENOTSUP && b0 == 0 ? rc : fail(rc, "tmvp prescale");
+        if ((rc = launch_gf16_t3_multi(e, 3, s))) return rc == NFEC_ENOTSUP && b0 == 0 ? rc : fail(rc, "tmvp products");
+        if ((rc = launch_tmvp_postscale(a, s))) return fail(rc, "tmvp postscale");
+    }
+    NFEC_HIP(hipEventRecord(c->tmvp_done, s));
+    return NFEC_OK;
+}
+
 int encode_device(nfec_codec* c, const nfec_block_batch* b, hipStream_t s)
 {
     const bool acc = b->flags & NFEC_ACCUMULATE;
@@ -528,6 +648,10 @@ int encode_device(nfec_codec* c, const nfec_block_batch* b, hipStream_t s)
             const char* e = std::getenv("NFEC_GF16_BS");
             return !(e && e[0] == '0');
         }();
+        if (c->tmvp && !b->num_data && !acc) {
+            const int rc = rs16_tmvp_encode(c, b, s);
+            if (rc != NFEC_ENOTSUP) return rc;
+        }
         if (c->d_t3off.p && !b->num_data) {
             Gf16T3Args t;
             t.base = static_cast<const uint8_t*>(b->blocks);
@@ -1147,6 +1271,12 @@ int nfec_codec_get_info(const nfec_codec* c, nfec_codec_info* out)
     out->vector_size = c->vec;
     out->symbol_bytes = c->sym;
     return NFEC_OK;
+}
+
+int nfec_codec_features(const nfec_codec* c)
+{
+    if (!c) return fail(NFEC_EINVAL, "null argument");
+    return c->tmvp ? NFEC_FEATURE_RS16_TOEPLITZ : 0;
 }
 
 int nfec_codec_get_generator(const nfec_codec* c, void* host_out, size_t bytes)

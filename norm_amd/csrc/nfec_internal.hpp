@@ -193,13 +193,41 @@ struct Gf16T3Args {
     uint64_t acc_block_stride = 0;
     uint32_t acc_seg_stride = 0, acc_slot0 = 0;
     const uint32_t* rows_lim = nullptr;  // device word: rows needed (<= m), null: m
+    // column map: column c is read from slot ((c >> col_shift) * col_chunk + (c & col_mask) +
+    // col_base) (identity by default); in_slots bounds the slots read (0: k + m)
+    uint32_t col_shift = 31, col_mask = 0xFFFFFFFFu, col_chunk = 0, col_base = 0, in_slots = 0;
+};
+struct Gf16T3Multi {
+    Gf16T3Args e[3];
+    uint32_t wg_end[3] = {0, 0, 0};
 };
 constexpr uint32_t kGf16T3RowsPerPass = 44;  // 11 row waves x 4 rows (gen_gf16_t3.py asserts it)
 constexpr uint32_t gf16_t3_rows_padded(uint32_t m)
 {
     return (m + kGf16T3RowsPerPass - 1) / kGf16T3RowsPerPass * kGf16T3RowsPerPass;
 }
+// RS16 encode by the Toeplitz split of the generator (kernels_tmvp.hip): the elementwise steps
+// around the three shared-table products
+struct Rs16TmvpArgs {
+    const uint8_t* base = nullptr;  // batch: source slots [0, k), parity slots [k, k + m)
+    uint64_t block_stride = 0;
+    uint32_t seg_stride = 0, nblocks = 0;
+    uint32_t vec = 0;               // bytes, multiple of 8
+    uint32_t k = 0, cw = 0;         // cw = m / 2 (chunk width and half the parity rows)
+    uint8_t* s = nullptr;           // prescaled chunk-pair sums: block b, virtual column v at s + b*s_block_stride + v*vec
+    uint64_t s_block_stride = 0;
+    uint8_t* x = nullptr;           // P1 rows: block b, row p at x + b*x_block_stride + p*vec
+    uint64_t x_block_stride = 0;
+    const uint16_t* cmat = nullptr; // [k][16] row masks of c_j (c_0 = 0)
+    const uint16_t* wmat = nullptr; // [m][16] of W(y_p)
+    const uint16_t* gmat = nullptr; // [m][16] of G[p][0]
+};
+bool rs16_tmvp_plan(uint32_t k, uint32_t m, const std::vector<uint32_t>& gen, std::vector<uint32_t> prod[3],
+                    std::vector<uint16_t>& cmat, std::vector<uint16_t>& wmat, std::vector<uint16_t>& gmat);
+int launch_tmvp_prescale(const Rs16TmvpArgs& a, hipStream_t s);
+int launch_tmvp_postscale(const Rs16TmvpArgs& a, hipStream_t s);
 int launch_gf16_t3_encode(const Gf16T3Args& a, hipStream_t s);  // NFEC_ENOTSUP: shape not covered
+int launch_gf16_t3_multi(const Gf16T3Args* e, uint32_t n, hipStream_t s);  // n <= 3 independent products
 void gf16_t3_offsets(const std::vector<uint32_t>& parity_rows, uint32_t k, uint32_t m, uint16_t* out);
 int launch_gf16_bs_encode(const Gf16BsEncArgs& a, hipStream_t s);  // NFEC_ENOTSUP: layout not 8-byte aligned
 void gf16_bs_selectors(const std::vector<uint32_t>& parity_rows, uint32_t k, uint32_t m, uint16_t* sel);

@@ -1,0 +1,107 @@
+"""RS16 encode by the Toeplitz split (kernels_tmvp.hip + gen_gf16_t3.hip multi launch) against
+the oracle on the GPU, bit-exact.  NFEC_RS16_TMVP=1 forces the split for shapes where it is
+allowed but not chosen by default; (256, 64) and C4 take it by default."""
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+from norm_amd import NFEC_RS16, NormDecoderRS16, NormEncoderRS16  # noqa: E402
+from norm_amd._native import NFEC_FEATURE_RS16_TOEPLITZ  # noqa: E402
+
+
+def _encoder(k, m, vec, force):
+    old = os.environ.get("NFEC_RS16_TMVP")
+    if force is not None:
+        os.environ["NFEC_RS16_TMVP"] = force
+    try:
+        enc = NormEncoderRS16()
+        assert enc.Init(k, m, vec)
+    finally:
+        if old is None:
+            os.environ.pop("NFEC_RS16_TMVP", None)
+        else:
+            os.environ["NFEC_RS16_TMVP"] = old
+    return enc
+
+
+CASES = [
+    # k, m, vec, seg_stride, nblocks, force, expect split
+    (64, 16, 1400, 1400, 5, "1", True),
+    (128, 32, 64, 64, 37, "1", True),     # several item groups, short segments
+    (128, 32, 1408, 1416, 3, "1", True),  # padded segment stride
+    (256, 64, 1400, 1400, 4, None, True),  # chosen by default (3 x 1 pass of 128 columns < 2 x 256)
+    (256, 64, 1400, 1400, 4, "0", False),
+    (512, 128, 64, 64, 2, "1", True),     # three passes of 44 rows per product
+    (96, 24, 1400, 1400, 3, "1", False),  # m / 2 not a power of two: not allowed
+    (100, 20, 1400, 1400, 3, "1", False),  # k not a multiple of m
+]
+
+
+@pytest.mark.parametrize("k,m,vec,stride,nb,force,split", CASES)
+def test_toeplitz_encode_matches_oracle(orc, k, m, vec, stride, nb, force, split):
+    enc = _encoder(k, m, vec, force)
+    assert bool(enc.features() & NFEC_FEATURE_RS16_TOEPLITZ) == split
+    host = orc.make_blocks(k, m, vec, nb, seg_stride=stride)
+    host[:, k:, :] = 0xA5  # overwrite semantics: stale parity must not leak through
+    ref = orc.encode_blocks(orc.RS16, k, m, vec, host.copy())  # zeroes the parity, then Encode()s
+    dev = torch.from_numpy(host).cuda()
+    enc.encode_blocks(dev)
+    torch.cuda.synchronize()
+    got = dev.cpu().numpy()
+    assert np.array_equal(got[:, :, :vec], ref[:, :, :vec])
+    assert np.array_equal(got[:, :, vec:], host[:, :, vec:])  # stride padding untouched
+
+
+def test_toeplitz_encode_twice_and_accumulate(orc):
+    """Back-to-back calls share the codec's scratch; accumulate mode takes the one-product path."""
+    k, m, vec, nb = 128, 32, 1400, 6
+    enc = _encoder(k, m, vec, "1")
+    host = orc.make_blocks(k, m, vec, nb)
+    ref = orc.encode_blocks(orc.RS16, k, m, vec, host.copy())
+    a = torch.from_numpy(host).cuda()
+    b = torch.from_numpy(orc.make_blocks(k, m, vec, nb, first_block=100)).cuda()
+    ref_b = orc.encode_blocks(orc.RS16, k, m, vec, b.cpu().numpy().copy())
+    s2 = torch.cuda.Stream()
+    enc.encode_blocks(a)
+    with torch.cuda.stream(s2):
+        enc.encode_blocks(b, stream=s2)
+    torch.cuda.synchronize()
+    assert np.array_equal(a.cpu().numpy(), ref)
+    assert np.array_equal(b.cpu().numpy(), ref_b)
+    enc.encode_blocks(a, accumulate=True)  # parity ^= parity: zero
+    torch.cuda.synchronize()
+    assert not a[:, k:, :].any()
+
+
+def test_toeplitz_round_trip_c4_shape(orc):
+    """C4's code (4096, 256) at a reduced block count: encode through the split, erase 40
+    source segments per block, decode, compare; sampled block against the oracle's encode."""
+    k, m, vec, nb = 4096, 256, 1400, 6
+    enc = _encoder(k, m, vec, None)
+    assert enc.features() & NFEC_FEATURE_RS16_TOEPLITZ
+    host = orc.make_blocks(k, m, vec, nb)
+    dev = torch.from_numpy(host).cuda()
+    enc.encode_blocks(dev)
+    torch.cuda.synchronize()
+    got = dev.cpu().numpy()
+    ref0 = orc.encode_blocks(orc.RS16, k, m, vec, host[:1].copy())
+    assert np.array_equal(got[:1], ref0)
+    dec = NormDecoderRS16()
+    assert dec.Init(k, m, vec)
+    locs = np.zeros((nb, m), np.int16)
+    counts = np.full(nb, 40, np.int16)
+    for b in range(nb):
+        locs[b, :40] = orc.erasure_pattern(b, k, 40)
+    rx = got.copy()
+    for b in range(nb):
+        rx[b, locs[b, :40]] = 0
+    d = torch.from_numpy(rx).cuda()
+    st = dec.decode_blocks(d, torch.from_numpy(locs).cuda(), torch.from_numpy(counts).cuda())
+    torch.cuda.synchronize()
+    assert (st.cpu().numpy() == 40).all()
+    assert np.array_equal(d.cpu().numpy()[:, :k], got[:, :k])

@@ -49,6 +49,7 @@ S_DESC = 84              # buffer descriptor (4)
 S_PTR = 88               # row waves: offsets pointer (2)
 S_CNT = 90               # column counter
 S_T0, S_T1 = 91, 92      # scratch
+S_T2 = 93                # builder: column-map scratch
 S_MASK = 36              # s36..s43 transpose masks (builder; row waves: epilogue, over S_SB[0])
 S_LAST = 92
 
@@ -116,8 +117,11 @@ def builder_asm():
     offs = [f"%[o{i}]" for i in range(16)]
 
     def loads(slot):
-        # column index in S_T0 (set by the caller): s_T1 = col * seg_stride
-        out = [f"s_mul_i32 s{S_T1}, s{S_T0}, %[ss]"]
+        # column index in S_T0 (set by the caller) -> byte offset in S_T1 through the column
+        # map: ((c >> csh) * cck + (c & cmk) * ss + cbb; identity: csh 31, cck 0, cmk ~0, cbb 0)
+        out = [f"s_lshr_b32 s{S_T2}, s{S_T0}, %[csh]", f"s_mul_i32 s{S_T2}, s{S_T2}, %[cck]",
+               f"s_and_b32 s{S_T1}, s{S_T0}, %[cmk]", f"s_mul_i32 s{S_T1}, s{S_T1}, %[ss]",
+               f"s_add_u32 s{S_T1}, s{S_T1}, s{S_T2}", f"s_add_u32 s{S_T1}, s{S_T1}, %[cbb]"]
         base = B_RING[slot]
         for i in range(16):
             out.append(f"buffer_load_dwordx2 v[{base + 2 * i}:{base + 2 * i + 1}], {offs[i]}, s[{S_DESC}:{S_DESC + 3}], s{S_T1} offen")
@@ -190,7 +194,7 @@ def builder_asm():
 
 def builder_clobbers():
     v = [f'"v{i}"' for i in range(74)]
-    s = [f'"s{i}"' for i in range(S_DESC, S_LAST + 1)]
+    s = [f'"s{i}"' for i in range(S_DESC, S_T2 + 1)]
     return ", ".join(v + s + ['"scc"', '"memory"'])
 
 
@@ -337,12 +341,11 @@ namespace nfec {{
 static_assert(kGf16T3RowsPerPass == {RP}u, "gen_gf16_t3.py and nfec_internal.hpp disagree on the rows per pass");
 namespace {{
 
-__global__ __launch_bounds__({64 * NWAVES}, 1) void gf16_t3_encode_kernel(Gf16T3Args a)
+__device__ __forceinline__ void t3_body(const Gf16T3Args& a, uint32_t wg)
 {{
     __shared__ uint32_t lds[{(OFF_ACC + 64 * 64) // 4}];
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const uint32_t wg = bs::wg_index(1);
     const uint32_t group = wg / a.passes, pass = wg - group * a.passes;
     // rows actually needed (decode stage 1: the largest erasure count among the blocks it
     // serves, written by the plan); passes past them leave at once, every wave together
@@ -372,7 +375,9 @@ __global__ __launch_bounds__({64 * NWAVES}, 1) void gf16_t3_encode_kernel(Gf16T3
         asm volatile(
         "{bb}\\n"
         :
-        : [wb] "s"(wb), [ss] "s"(a.seg_stride), [k] "s"(a.k), [lb0] "v"(lb0), [lb1] "v"(lb1), {ins}
+        : [wb] "s"(wb), [ss] "s"(a.seg_stride), [k] "s"(a.k), [lb0] "v"(lb0), [lb1] "v"(lb1),
+          [csh] "s"(a.col_shift), [cmk] "s"(a.col_mask), [cck] "s"(a.col_chunk * a.seg_stride),
+          [cbb] "s"(a.col_base * a.seg_stride), {ins}
         : {builder_clobbers()});
     }} else {{
         const uint32_t row0 = pass * {RP}u + (wave - 1u) * {ROWS}u;
@@ -398,22 +403,36 @@ __global__ __launch_bounds__({64 * NWAVES}, 1) void gf16_t3_encode_kernel(Gf16T3
     }}
 }}
 
-}}  // namespace
-
-int launch_gf16_t3_encode(const Gf16T3Args& a, hipStream_t s)
+__global__ __launch_bounds__({64 * NWAVES}, 1) void gf16_t3_encode_kernel(Gf16T3Args a)
 {{
-    if (a.nblocks == 0) return NFEC_OK;
+    t3_body(a, bs::wg_index(1));
+}}
+
+// several independent products in one grid (the RS16 Toeplitz split, rs16_tmvp): workgroup
+// ranges [wg_end[i-1], wg_end[i]) run problem i, so their tails share one launch
+__global__ __launch_bounds__({64 * NWAVES}, 1) void gf16_t3_multi_kernel(Gf16T3Multi mm)
+{{
+    const uint32_t wg = bs::wg_index(1);
+    if (wg < mm.wg_end[0]) t3_body(mm.e[0], wg);
+    else if (wg < mm.wg_end[1]) t3_body(mm.e[1], wg - mm.wg_end[0]);
+    else t3_body(mm.e[2], wg - mm.wg_end[1]);
+}}
+
+// checks the shape, fills the default output / accumulate layouts and the pass count
+int t3_prepare(const Gf16T3Args& a, Gf16T3Args& b, uint64_t& wgs)
+{{
     if ((a.vec_bytes & 7u) || a.vec_bytes == 0 || !a.offs || a.num_data ||
         a.m_pad != (a.m + {RP - 1}u) / {RP}u * {RP}u)
         return NFEC_ENOTSUP;
     // every piece offset of a group (8 KiB of flat positions) plus slot offsets within 2^31
     const uint64_t nbg = 8192u / a.vec_bytes + 2u;
-    if (nbg * a.block_stride + (uint64_t)(a.k + a.m) * a.seg_stride >= (1ull << 31) ||
+    const uint64_t in_slots = a.in_slots ? a.in_slots : (uint64_t)a.k + a.m;
+    if (nbg * a.block_stride + in_slots * a.seg_stride >= (1ull << 31) ||
         (a.out_base && nbg * a.out_block_stride + (uint64_t)(a.out_slot0 + a.m) * a.out_seg_stride >= (1ull << 31)) ||
         (a.acc_base && nbg * a.acc_block_stride + (uint64_t)(a.acc_slot0 + a.m) * a.acc_seg_stride >= (1ull << 31)))
         return NFEC_ENOTSUP;
     const uint64_t total = (uint64_t)a.nblocks * a.vec_bytes;
-    Gf16T3Args b = a;
+    b = a;
     if (!b.out_base) {{  // encode: parity in place, slot k + r; accumulate against it
         b.out_base = const_cast<uint8_t*>(a.base);
         b.out_block_stride = a.block_stride;
@@ -428,8 +447,41 @@ int launch_gf16_t3_encode(const Gf16T3Args& a, hipStream_t s)
     }}
     b.passes = (a.m + {RP - 1}u) / {RP}u;
     const uint64_t groups = (total + 8191u) / 8192u;
-    if (groups * b.passes >= (1ull << 31)) return NFEC_ENOTSUP;
-    hipLaunchKernelGGL(gf16_t3_encode_kernel, dim3((uint32_t)(groups * b.passes)), dim3({64 * NWAVES}), 0, s, b);
+    wgs = groups * b.passes;
+    return wgs >= (1ull << 31) ? NFEC_ENOTSUP : NFEC_OK;
+}}
+
+}}  // namespace
+
+int launch_gf16_t3_multi(const Gf16T3Args* e, uint32_t n, hipStream_t s)
+{{
+    if (n == 0 || n > 3) return NFEC_EINVAL;
+    Gf16T3Multi mm;
+    uint64_t end = 0;
+    for (uint32_t i = 0; i < 3; ++i) {{
+        uint64_t w = 0;
+        if (i < n && e[i].nblocks) {{
+            const int rc = t3_prepare(e[i], mm.e[i], w);
+            if (rc) return rc;
+        }}
+        end += w;
+        if (end >= (1ull << 31)) return NFEC_ENOTSUP;
+        mm.wg_end[i] = (uint32_t)end;
+    }}
+    if (end == 0) return NFEC_OK;
+    hipLaunchKernelGGL(gf16_t3_multi_kernel, dim3((uint32_t)end), dim3({64 * NWAVES}), 0, s, mm);
+    const hipError_t err = hipGetLastError();
+    return err == hipSuccess ? NFEC_OK : hip_fail(err, "gf16 t3 multi launch");
+}}
+
+int launch_gf16_t3_encode(const Gf16T3Args& a, hipStream_t s)
+{{
+    if (a.nblocks == 0) return NFEC_OK;
+    Gf16T3Args b;
+    uint64_t wgs = 0;
+    const int rc = t3_prepare(a, b, wgs);
+    if (rc) return rc;
+    hipLaunchKernelGGL(gf16_t3_encode_kernel, dim3((uint32_t)wgs), dim3({64 * NWAVES}), 0, s, b);
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? NFEC_OK : hip_fail(e, "gf16 t3 encode launch");
 }}
