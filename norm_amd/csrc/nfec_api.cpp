@@ -519,8 +519,12 @@ static bool use_asm()
 int rs16_tmvp_encode(nfec_codec* c, const nfec_block_batch* b, hipStream_t s)
 {
     const uint32_t k = c->k, m = c->m, cw = m / 2, half = k / 2, vec = c->vec;
+    // sub-batches of at most 16 GiB of scratch (C4's 4,096 blocks: one, 12.5 GB), of equal size
+    // so no launch runs a small tail batch
     const uint64_t per_block = (uint64_t)(half + cw) * vec;
-    const uint32_t sb = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(b->nblocks, (8ull << 30) / per_block));
+    const uint64_t cap = std::max<uint64_t>(1, (16ull << 30) / per_block);
+    const uint64_t nsub = (b->nblocks + cap - 1) / cap;
+    const uint32_t sb = (uint32_t)std::max<uint64_t>(1, (b->nblocks + nsub - 1) / std::max<uint64_t>(nsub, 1));
     std::lock_guard<std::mutex> lk(c->tmvp_mu);
     int rc = c->w_tmvp.reserve((size_t)sb * per_block);
     if (rc) return rc;

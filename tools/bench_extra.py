@@ -102,25 +102,33 @@ def main():
     }
     if kind == na.NFEC_RS16 and os.environ.get("NFEC_GF16_T3", "1") != "0" and vec % 8 == 0:
         # op roofline of the shared-table RS16 encode (gen_gf16_t3.hip), counted from its code:
-        # per (item group of 64 lanes x 64 symbols, pass of RP rows, source column) the row
-        # waves issue RP x 16 planes x 3 ds_read_b64 (512 B each) and 7 VALU per plane, the
-        # builder 506 VALU and 125 ds_write_b64 (RP = 44: 11 row waves x 4 rows)
+        # per (item group of 64 lanes x 64 symbols, source column) every live parity row issues
+        # 16 planes x 3 ds_read_b64 (512 B each) and 7 VALU per plane, and per pass of up to RP
+        # rows the builder issues 506 VALU and 125 ds_write_b64 (RP = 44: 11 row waves x 4 rows;
+        # row waves past the last row leave).  With the Toeplitz split (features bit 0) the
+        # products are three of m/2 rows over k/2 columns instead of one of m rows over k.
         groups = -(-nb * vec // 8192)
         RP = 44
-        passes = -(-m // RP)
-        units = groups * passes * k
-        lds_bytes = units * RP * 16 * 3 * 512
-        valu = units * (RP * 16 * 7 + 506)
+        split = bool(enc.features() & na.NFEC_FEATURE_RS16_TOEPLITZ)
+        nprod, ncols, rows = (3, k // 2, m // 2) if split else (1, k, m)
+        passes = -(-rows // RP)
+        rows4 = -(-rows // 4) * 4
+        units = groups * ncols * nprod
+        lds_bytes = units * rows4 * 16 * 3 * 512
+        valu = units * (rows4 * 16 * 7 + passes * 506)
         t = enc_ms * 1e-3
         out["op_roofline"] = {
-            "kernel": "gf16_t3_encode_kernel",
+            "kernel": "gf16_t3_multi_kernel (Toeplitz split: 3 products of m/2 rows over k/2 columns)"
+                      if split else "gf16_t3_encode_kernel",
             "gf16_macs_per_s": float("%.4g" % (k * m * (vec // 2) * nb / t)),
+            "macs_note": "k*m*symbols of the generator product per second (the split computes 3/4 of them)"
+                         if split else "k*m*symbols per second",
             "lds": {"achieved": float("%.4g" % (lds_bytes / t)), "peak": 256 * 256 * 2.4e9, "unit": "B/s",
                     "frac": round(lds_bytes / t / (256 * 256 * 2.4e9), 4),
-                    "note": "table reads only (ds_read_b64, counted at 256 B/clk/CU)"},
+                    "note": "table reads only (ds_read_b64, counted at 256 B/clk/CU), over the whole encode time"},
             "valu": {"achieved": float("%.4g" % (valu * 64 / t)), "peak": 7.86e13, "unit": "lane-ops/s",
                      "frac": round(valu * 64 / t / 7.86e13, 4), "insts_per_launch": valu},
-            "lds_insts_per_launch": units * (RP * 16 * 3 + 125),
+            "lds_insts_per_launch": units * rows4 * 16 * 3 + groups * nprod * passes * ncols * 125,
         }
     if er:
         dec_ms = timed(lambda: dec.decode_blocks(blocks, locs, counts, status=status, stream=stream), a.steps)
