@@ -109,8 +109,39 @@ B_CUR = [(68, 69), (70, 71)]   # Gray-code running values (ping-pong), half 0 / 
 B_ZERO = (72, 73)
 
 
-def builder_asm():
+# builder variants (NFEC_T3_VARIANT=<id> for A/B runs; add them to BUILDER_VARIANTS to build):
+#   "prio"    raise the builder's issue priority above the row waves on its SIMD
+#   "ilp"     build the three groups' Gray-code chains interleaved (6 independent XOR chains)
+#   "deep"    three source columns in flight instead of two
+#   "nochain" / "notr": timing probes (wrong parity): no Gray-code XORs / no transposes
+# Measured on C4 (4,096 blocks, Toeplitz split, one MI355X): default 179.2-180.2 ms; prio 179.9,
+# ilp 180.0, prio+ilp 180.3, deep 180.4, deep+ilp 180.0; nochain 188.8, notr 176.1, both 175.6.
+# The builder does not set the column step: the row waves' VALU does (7 per row, plane and
+# 64 symbols: 3 address adds for the table reads, a bitop3 and a xor per half), DESIGN.md RS16.
+BUILDER_VARIANTS = {0: ()}
+T3_DEFAULT = 0
+B_CUR3 = [[(68, 69), (70, 71)], [(74, 75), (76, 77)], [(78, 79), (80, 81)]]  # per group (ilp)
+# "deep" register map: three 32-register slots v0..v95, then temporaries (four slots leave the
+# compiler too few registers for the asm's inputs)
+D_NS = 3
+D_RING = [0, 32, 64]
+D_TMP = [96, 97, 98, 99]
+D_CUR = [(100, 101), (102, 103)]
+D_CUR3 = [[(100, 101), (102, 103)], [(104, 105), (106, 107)], [(108, 109), (110, 111)]]
+D_ZERO = (112, 113)
+
+
+def builder_regs(flags):
+    if "deep" in flags:
+        return D_RING, D_TMP, D_CUR, D_CUR3, D_ZERO
+    return B_RING, B_TMP, B_CUR, B_CUR3, B_ZERO
+
+
+def builder_asm(flags=()):
+    ring, tmp, bcur, bcur3, bzero = builder_regs(flags)
     L = []
+    if "prio" in flags:
+        L.append("s_setprio 3")
     L += [f"s_mov_b64 s[{S_DESC}:{S_DESC + 1}], %[wb]", f"s_mov_b32 s{S_DESC + 2}, 0x80000000",
           f"s_mov_b32 s{S_DESC + 3}, 0x00020000"]
     L += mask_init()
@@ -122,7 +153,7 @@ def builder_asm():
         out = [f"s_lshr_b32 s{S_T2}, s{S_T0}, %[csh]", f"s_mul_i32 s{S_T2}, s{S_T2}, %[cck]",
                f"s_and_b32 s{S_T1}, s{S_T0}, %[cmk]", f"s_mul_i32 s{S_T1}, s{S_T1}, %[ss]",
                f"s_add_u32 s{S_T1}, s{S_T1}, s{S_T2}", f"s_add_u32 s{S_T1}, s{S_T1}, %[cbb]"]
-        base = B_RING[slot]
+        base = ring[slot]
         for i in range(16):
             out.append(f"buffer_load_dwordx2 v[{base + 2 * i}:{base + 2 * i + 1}], {offs[i]}, s[{S_DESC}:{S_DESC + 3}], s{S_T1} offen")
         return out
@@ -130,33 +161,57 @@ def builder_asm():
     def build(slot, buf):
         """transpose the slot, write its tables into LDS buffer buf"""
         out = []
-        base = B_RING[slot]
+        base = ring[slot]
         halves = [[base + d for d in range(16)], [base + 16 + d for d in range(16)]]
         for h in (0, 1):
-            out += transpose16(halves[h], B_TMP)
+            if "notr" not in flags:
+                out += transpose16(halves[h], tmp)
         lb = "%[lb0]" if buf == 0 else "%[lb1]"
-        for first, n, row0 in GROUPS:
-            prev, k = 0, 0
+
+        def chain(gi):
+            """(instructions of one Gray-code step) for group gi, in order"""
+            first, n, row0 = GROUPS[gi]
+            cur = bcur3[gi] if "ilp" in flags else bcur
+            steps, prev, k = [], 0, 0
             for i in range(1, 1 << n):
                 g = i ^ (i >> 1)
                 q = (g ^ prev).bit_length() - 1
-                dst = B_CUR[k % 2]
-                srcp = B_CUR[(k + 1) % 2]
+                dst, srcp = cur[k % 2], cur[(k + 1) % 2]
+                st = []
                 for h in (0, 1):
                     plane = halves[h][first + q]
+                    if "nochain" in flags:
+                        continue
                     if prev == 0:
-                        out.append(f"v_mov_b32 v{dst[h]}, v{plane}")
+                        st.append(f"v_mov_b32 v{dst[h]}, v{plane}")
                     else:
-                        out.append(f"v_xor_b32 v{dst[h]}, v{srcp[h]}, v{plane}")
-                out.append(f"ds_write_b64 {lb}, v[{dst[0]}:{dst[1]}] offset:{(row0 + g) * 512}")
+                        st.append(f"v_xor_b32 v{dst[h]}, v{srcp[h]}, v{plane}")
+                st.append(f"ds_write_b64 {lb}, v[{dst[0]}:{dst[1]}] offset:{(row0 + g) * 512}")
+                steps.append(st)
                 prev, k = g, k + 1
+            return steps
+
+        chains = [chain(gi) for gi in range(len(GROUPS))]
+        if "ilp" in flags:
+            # round-robin over the groups: the 63-step chain of group 0 with the two 31-step
+            # chains of groups 1 and 2 beside it
+            for i in range(max(len(c) for c in chains)):
+                for c in chains:
+                    if i < len(c):
+                        out += c[i]
+        else:
+            for c in chains:
+                for st in c:
+                    out += st
         return out
 
     # zero rows of both buffers; piece offsets for the row waves' epilogue
-    L += [f"v_mov_b32 v{B_ZERO[0]}, 0", f"v_mov_b32 v{B_ZERO[1]}, 0"]
+    L += [f"v_mov_b32 v{bzero[0]}, 0", f"v_mov_b32 v{bzero[1]}, 0"]
     for lb in ("%[lb0]", "%[lb1]"):
         for _, _, row0 in GROUPS:
-            L.append(f"ds_write_b64 {lb}, v[{B_ZERO[0]}:{B_ZERO[1]}] offset:{row0 * 512}")
+            L.append(f"ds_write_b64 {lb}, v[{bzero[0]}:{bzero[1]}] offset:{row0 * 512}")
+    if "deep" in flags:
+        return L + deep_loop(loads, build)
     # prologue: column 0 -> slot 0 (wait), column 1 -> slot 1 (in flight), build column 0
     L += [f"s_mov_b32 s{S_T0}, 0"] + loads(0)
     L += ["s_cmp_gt_u32 %[k], 1", "s_cbranch_scc0 Lb_one_%=", f"s_mov_b32 s{S_T0}, 1"] + loads(1)
@@ -192,8 +247,59 @@ def builder_asm():
     return L
 
 
-def builder_clobbers():
-    v = [f'"v{i}"' for i in range(74)]
+def deep_loop(loads, build):
+    """D_NS slots: column j in slot j % D_NS, tables in buffer j % 2; at column step c the
+    builder builds column c + 1, then loads column c + 1 + D_NS into the slot c + 1 just left"""
+    ns = D_NS
+    L = []
+    # prologue: columns 0..ns-1 in flight, wait for column 0, build it, load column ns
+    L += [f"s_mov_b32 s{S_T0}, 0"] + loads(0)
+    for j in range(1, ns):
+        L += [f"s_cmp_gt_u32 %[k], {j}", f"s_cbranch_scc0 Lb_pl{j}_%=", f"s_mov_b32 s{S_T0}, {j}"] + loads(j)
+        L.append(f"Lb_pl{j}_%=:")
+    L += wait_for(f"s_sub_u32 s{S_T1}, %[k], 1", "p", ns - 1)
+    L += build(0, 0)
+    L += [f"s_cmp_gt_u32 %[k], {ns}", f"s_cbranch_scc0 Lb_pln_%=", f"s_mov_b32 s{S_T0}, {ns}"] + loads(0) + ["Lb_pln_%=:"]
+    L += ["s_waitcnt lgkmcnt(0)", "s_barrier", f"s_mov_b32 s{S_CNT}, 0"]
+    unroll = ns * 2 // (2 if ns % 2 == 0 else 1)  # lcm(ns, 2)
+    for u in range(unroll):
+        L.append(f"Lb_it{u}_%=:")
+        nslot, nbuf = (u + 1) % ns, (u + 1) % 2
+        L += [f"s_add_u32 s{S_T0}, s{S_CNT}, 1", "s_cmp_ge_u32 s%d, %%[k]" % S_T0, "s_cbranch_scc1 Lb_tail_%="]
+        # columns issued beyond c+1: c+2 .. min(k-1, c+ns), i.e. clamp(k - c - 2, 0, ns-1)
+        L += wait_for(f"s_sub_u32 s{S_T1}, %[k], s{S_CNT}", f"i{u}", ns - 1, extra=[f"s_sub_u32 s{S_T1}, s{S_T1}, 2"])
+        L += build(nslot, nbuf)
+        L += [f"s_add_u32 s{S_T0}, s{S_CNT}, {1 + ns}", "s_cmp_lt_u32 s%d, %%[k]" % S_T0, f"s_cbranch_scc0 Lb_nl_{u}_%="]
+        L += loads(nslot)
+        L.append(f"Lb_nl_{u}_%=:")
+        L += ["s_waitcnt lgkmcnt(0)", "s_barrier", f"s_add_u32 s{S_CNT}, s{S_CNT}, 1"]
+    L.append("s_branch Lb_it0_%=")
+    L += ["Lb_tail_%=:", "s_waitcnt vmcnt(0)", "s_barrier"]
+    return L
+
+
+def wait_for(first, tag, nmax, extra=()):
+    """s_waitcnt vmcnt(16 * n) with n = clamp(S_T1, 0, nmax) computed by `first` (+ `extra`):
+    the loads of the n columns issued after the one needed may stay in flight (S_T1 is a
+    signed count; the comparisons are signed)"""
+    L = [first] + list(extra)
+    L += [f"s_cmp_ge_i32 s{S_T1}, {nmax}", f"s_cbranch_scc1 Lb_w{nmax}{tag}_%="]
+    for n in range(nmax - 1, 0, -1):
+        L += [f"s_cmp_eq_i32 s{S_T1}, {n}", f"s_cbranch_scc1 Lb_w{n}{tag}_%="]
+    L += ["s_waitcnt vmcnt(0)", f"s_branch Lb_wd{tag}_%="]
+    for n in range(1, nmax + 1):
+        L += [f"Lb_w{n}{tag}_%=:", f"s_waitcnt vmcnt({16 * n})"]
+        if n < nmax:
+            L.append(f"s_branch Lb_wd{tag}_%=")
+    L.append(f"Lb_wd{tag}_%=:")
+    return L
+
+
+def builder_clobbers(flags=()):
+    if "deep" in flags:
+        return ", ".join([f'"v{i}"' for i in range(D_ZERO[1] + 1)] + [f'"s{i}"' for i in range(S_DESC, S_T2 + 1)] +
+                         ['"scc"', '"memory"'])
+    v = [f'"v{i}"' for i in range(82)]
     s = [f'"s{i}"' for i in range(S_DESC, S_T2 + 1)]
     return ", ".join(v + s + ['"scc"', '"memory"'])
 
@@ -329,11 +435,30 @@ def row_clobbers():
 
 def main():
     path = sys.argv[1]
-    bb = "\\n\"\n        \"".join(builder_asm())
+    bbs = {v: "\\n\"\n        \"".join(builder_asm(f)) for v, f in BUILDER_VARIANTS.items()}
     rb = "\\n\"\n        \"".join(row_asm())
     ins = ", ".join(f'[o{i}] "v"(off[{i}])' for i in range(16))
+    blocks = []
+    for v in BUILDER_VARIANTS:
+        kw = "if constexpr" if v == 0 else "else if constexpr"
+        blocks.append(f"""        {kw} (V == {v}) {{
+            asm volatile(
+            "{bbs[v]}\\n"
+            :
+            : [wb] "s"(wb), [ss] "s"(a.seg_stride), [k] "s"(a.k), [lb0] "v"(lb0), [lb1] "v"(lb1),
+              [csh] "s"(a.col_shift), [cmk] "s"(a.col_mask), [cck] "s"(cck), [cbb] "s"(cbb), {ins}
+            : {builder_clobbers(BUILDER_VARIANTS[v])});
+        }}""")
+    builder_blocks = "\n".join(blocks)
+    multi_cases = "\n".join(
+        f"    case {v}: hipLaunchKernelGGL(gf16_t3_multi_kernel<{v}>, dim3((uint32_t)end), dim3({64 * NWAVES}), 0, s, mm); break;"
+        for v in BUILDER_VARIANTS)
+    enc_cases = "\n".join(
+        f"    case {v}: hipLaunchKernelGGL(gf16_t3_encode_kernel<{v}>, dim3((uint32_t)wgs), dim3({64 * NWAVES}), 0, s, b); break;"
+        for v in BUILDER_VARIANTS)
     src = f"""// GENERATED by tools/codegen/gen_gf16_t3.py -- do not edit by hand.
 // RS16 encode: bit-sliced, three shared four-Russians tables per source column in LDS.
+#include <cstdlib>
 #include "nfec_internal.hpp"
 #include "bitslice.hpp"
 
@@ -341,6 +466,7 @@ namespace nfec {{
 static_assert(kGf16T3RowsPerPass == {RP}u, "gen_gf16_t3.py and nfec_internal.hpp disagree on the rows per pass");
 namespace {{
 
+template <int V>
 __device__ __forceinline__ void t3_body(const Gf16T3Args& a, uint32_t wg)
 {{
     __shared__ uint32_t lds[{(OFF_ACC + 64 * 64) // 4}];
@@ -372,13 +498,8 @@ __device__ __forceinline__ void t3_body(const Gf16T3Args& a, uint32_t wg)
             pa[i] = ok ? (uint32_t)((uint64_t)(b - b0) * a.acc_block_stride) + p : 0x80000000u;
         }}
         const uint32_t lb0 = lbase + lane * 8u, lb1 = lb0 + {BUF}u;
-        asm volatile(
-        "{bb}\\n"
-        :
-        : [wb] "s"(wb), [ss] "s"(a.seg_stride), [k] "s"(a.k), [lb0] "v"(lb0), [lb1] "v"(lb1),
-          [csh] "s"(a.col_shift), [cmk] "s"(a.col_mask), [cck] "s"(a.col_chunk * a.seg_stride),
-          [cbb] "s"(a.col_base * a.seg_stride), {ins}
-        : {builder_clobbers()});
+        const uint32_t cck = a.col_chunk * a.seg_stride, cbb = a.col_base * a.seg_stride;
+{builder_blocks}
     }} else {{
         const uint32_t row0 = pass * {RP}u + (wave - 1u) * {ROWS}u;
         // a row wave whose rows are all past the limit (the last pass of m = 100, decode stage 1
@@ -403,19 +524,31 @@ __device__ __forceinline__ void t3_body(const Gf16T3Args& a, uint32_t wg)
     }}
 }}
 
+template <int V>
 __global__ __launch_bounds__({64 * NWAVES}, 1) void gf16_t3_encode_kernel(Gf16T3Args a)
 {{
-    t3_body(a, bs::wg_index(1));
+    t3_body<V>(a, bs::wg_index(1));
 }}
 
 // several independent products in one grid (the RS16 Toeplitz split, rs16_tmvp): workgroup
 // ranges [wg_end[i-1], wg_end[i]) run problem i, so their tails share one launch
+template <int V>
 __global__ __launch_bounds__({64 * NWAVES}, 1) void gf16_t3_multi_kernel(Gf16T3Multi mm)
 {{
     const uint32_t wg = bs::wg_index(1);
-    if (wg < mm.wg_end[0]) t3_body(mm.e[0], wg);
-    else if (wg < mm.wg_end[1]) t3_body(mm.e[1], wg - mm.wg_end[0]);
-    else t3_body(mm.e[2], wg - mm.wg_end[1]);
+    if (wg < mm.wg_end[0]) t3_body<V>(mm.e[0], wg);
+    else if (wg < mm.wg_end[1]) t3_body<V>(mm.e[1], wg - mm.wg_end[0]);
+    else t3_body<V>(mm.e[2], wg - mm.wg_end[1]);
+}}
+
+int t3_variant()
+{{
+    static const int v = [] {{
+        const char* e = std::getenv("NFEC_T3_VARIANT");
+        const int x = e ? std::atoi(e) : {T3_DEFAULT};
+        return x >= 0 && x < {len(BUILDER_VARIANTS)} ? x : {T3_DEFAULT};
+    }}();
+    return v;
 }}
 
 // checks the shape, fills the default output / accumulate layouts and the pass count
@@ -469,7 +602,9 @@ int launch_gf16_t3_multi(const Gf16T3Args* e, uint32_t n, hipStream_t s)
         mm.wg_end[i] = (uint32_t)end;
     }}
     if (end == 0) return NFEC_OK;
-    hipLaunchKernelGGL(gf16_t3_multi_kernel, dim3((uint32_t)end), dim3({64 * NWAVES}), 0, s, mm);
+    switch (t3_variant()) {{
+{multi_cases}
+    }}
     const hipError_t err = hipGetLastError();
     return err == hipSuccess ? NFEC_OK : hip_fail(err, "gf16 t3 multi launch");
 }}
@@ -481,7 +616,9 @@ int launch_gf16_t3_encode(const Gf16T3Args& a, hipStream_t s)
     uint64_t wgs = 0;
     const int rc = t3_prepare(a, b, wgs);
     if (rc) return rc;
-    hipLaunchKernelGGL(gf16_t3_encode_kernel, dim3((uint32_t)wgs), dim3({64 * NWAVES}), 0, s, b);
+    switch (t3_variant()) {{
+{enc_cases}
+    }}
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? NFEC_OK : hip_fail(e, "gf16 t3 encode launch");
 }}
