@@ -137,8 +137,11 @@ int launch_stream_copy(void* dst, const void* src, uint64_t bytes, hipStream_t s
     if ((reinterpret_cast<uintptr_t>(dst) | reinterpret_cast<uintptr_t>(src) | bytes) & 15)
         return fail(NFEC_EINVAL, "stream_copy: pointers and size must be multiples of 16 bytes");
     const uint64_t n16 = bytes / 16;
-    // 8 workgroups of 4 waves per CU, grid-stride beyond that
-    const uint32_t grid = (uint32_t)std::min<uint64_t>((n16 + 1023) / 1024, 256 * 8);
+    // one 4 KiB piece per wave, no grid-stride loop: 6.29 TB/s on a 4 GiB copy, against
+    // 5.5-5.8 TB/s with 1-16 K resident workgroups looping (tools/diag/copy_rate.hip,
+    // profiles/r02/copy_rate.jsonl)
+    if ((n16 + 1023) / 1024 >= (1ull << 31)) return fail(NFEC_EINVAL, "stream_copy: size too large");
+    const uint32_t grid = (uint32_t)((n16 + 1023) / 1024);
     hipLaunchKernelGGL(stream_copy_kernel, dim3(grid), dim3(256), 0, s, static_cast<u32x4*>(dst),
                        static_cast<const u32x4*>(src), n16);
     hipError_t e = hipGetLastError();
