@@ -921,9 +921,12 @@ int decode_device(nfec_codec* c, const nfec_block_batch* b, const uint16_t* locs
             f.out_slots = c->w_oslots.p;
             f.slots_stride = c->k;
             f.accumulate = acc;
-            static const bool lane_major = [] {
-                const char* e = std::getenv("NFEC_FDEC_LANEMAJOR");  // A/B only: 2.16 vs 2.02 ms
-                return e && e[0] == '1';
+            static const uint32_t lane_major = [] {
+                // 2 (default) = compact lane-major items, idle lanes out of EXEC (1.981-1.985 vs
+                // 1.989-1.998 ms, r02g); 0 = item q*64 + lane; 1 = lane L holds items 4L..4L+3
+                // (strided loads: 2.16 vs 2.02 ms).  NFEC_FDEC_LANEMAJOR overrides (A/B).
+                const char* e = std::getenv("NFEC_FDEC_LANEMAJOR");
+                return e ? (uint32_t)std::atoi(e) : 2u;
             }();
             f.lane_major = lane_major;
             const bool fused = use_fused && rs8_fused_decode_covers(c->k, c->m, f);

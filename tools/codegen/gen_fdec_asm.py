@@ -318,14 +318,18 @@ def gen_kernel(k, m, probe=None):
         a.rows[blk] = 0;
         a.psel[2 * (uint64_t)blk] = 0;
     }}
-    // lane-major items (lane L holds items 4L..4L+3): a 1400-byte segment then occupies lanes
-    // 0..43 and the lanes past it drop out of every instruction (EXEC) instead of computing
-    // garbage bytes, a third of the VALU lane work
-    if (a.lane_major && lane * 4u >= a.ips) return;  // measured slower (strided loads); off by default
+    // lane-major items: a 1400-byte segment occupies lanes 0..43 and the lanes past it drop out
+    // of every instruction (EXEC) instead of computing garbage bytes, a third of the lane work.
+    // lane_major 1: lane L holds items 4L..4L+3 (strided loads; measured slower, off);
+    // lane_major 2: item q*L4 + L with L4 = ceil(items / 4), so each load stays contiguous
+    const uint32_t l4 = (a.ips + 3u) / 4u;
+    if ((a.lane_major == 1u && lane * 4u >= a.ips) || (a.lane_major == 2u && lane >= l4)) return;
     uint32_t o[4], so[4];
 #pragma unroll
     for (int q = 0; q < 4; ++q) {{
-        const uint32_t item = a.lane_major ? lane * 4u + (uint32_t)q : (uint32_t)q * 64u + lane;
+        const uint32_t item = a.lane_major == 1u   ? lane * 4u + (uint32_t)q
+                              : a.lane_major == 2u ? (uint32_t)q * l4 + lane
+                                                   : (uint32_t)q * 64u + lane;
         const bool ok = item < a.ips;
         o[q] = ok ? item * 8u : 0x80000000u;  // past the load records: zeros, no memory access
         so[q] = ok ? item * 8u : 0x80000000u;  // past the store descriptor's records: dropped
