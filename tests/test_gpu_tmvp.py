@@ -105,3 +105,19 @@ def test_toeplitz_round_trip_c4_shape(orc):
     torch.cuda.synchronize()
     assert (st.cpu().numpy() == 40).all()
     assert np.array_equal(d.cpu().numpy()[:, :k], got[:, :k])
+
+
+def test_stream_copy_matches_source():
+    """nfec_util_stream_copy (the bench's achievable-copy kernel): exact bytes, odd sizes
+    rejected, one-piece-per-wave grid covers the tail."""
+    from norm_amd import stream_copy
+    from norm_amd._native import NfecError
+
+    for n in (16, 4096 + 16, (1 << 20) + 48):
+        src = torch.randint(0, 256, (n,), dtype=torch.uint8, device="cuda")
+        dst = torch.zeros_like(src)
+        stream_copy(dst, src)
+        torch.cuda.synchronize()
+        assert torch.equal(dst, src)
+    with pytest.raises(NfecError):
+        stream_copy(torch.zeros(24, dtype=torch.uint8, device="cuda"), torch.zeros(24, dtype=torch.uint8, device="cuda"))
