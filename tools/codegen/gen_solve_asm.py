@@ -372,10 +372,14 @@ __global__ __launch_bounds__(256, 2) void mdp_solve_bs_kernel(MdpSolveArgs a, ui
     if (rows <= 0 || rows > 16 || ns > {MDP_NT}u) return;  // the generic kernel that follows takes it
     const uint32_t e = (uint32_t)rows;
     if (lane == 0) a.rows[blk] = 0;  // hand the block off: the generic kernel skips it
+    // lane-major items, ceil(items / 4) lanes per load (item q*l4 + lane): the lanes past the
+    // segment leave EXEC instead of computing garbage bytes (as the fused RS8 repair does)
+    const uint32_t l4 = (ips + 3u) / 4u;
+    if (lane >= l4) return;
     uint32_t o[4], so[4];
 #pragma unroll
     for (int q = 0; q < 4; ++q) {{
-        const uint32_t item = (uint32_t)q * 64u + lane;
+        const uint32_t item = (uint32_t)q * l4 + lane;
         const bool ok = item < ips;
         o[q] = ok ? item * 8u : 0u;
         so[q] = ok ? item * 8u : 0x80000000u;   // past the output descriptor's records: dropped
