@@ -157,6 +157,8 @@ def fdec_asm(k, m, probe=None, e16=False):
         L += loads(c)
         issued = c
     # ---- stage 1: z_t for rows 0..15 (rows >= e are computed but unused) ----
+    if probe == "prio1":
+        L.append("s_setprio 2")  # A/B: the loading stage ahead of the other wave's solve
     for c in range(ncol):
         w = slot_regs(c % NSLOT)
         if probe != "noload":
@@ -197,6 +199,10 @@ def fdec_asm(k, m, probe=None, e16=False):
             L += loads(c + NSLOT)
             issued = c + NSLOT
     # ---- stage 2: d_s = sum_t c[s][t] z_t, outputs in two halves of 8 ----
+    if probe == "prio1":
+        L.append("s_setprio 0")
+    if probe == "prio2":
+        L.append("s_setprio 2")  # A/B: the solve ahead of the other wave's loading stage
     win = win_regs()
     cbuf = [S_COEF1, S_COEF2]
     tmp = [4 * (WIN_P0 + p) + h for p in range(4) for h in (0, 1)]
@@ -286,6 +292,8 @@ def clobbers():
 # A/B probes of the (64, 32) kernel, NFEC_FDEC_VARIANT=<id> (never the default): no stage-2 solve,
 # no stage-1 arithmetic (loads only), no stage-1 loads, no e = 16 specialisation of stage 2
 # (measured: 1.992 ms without it, 1.981 with it, 64k blocks)
+# Also generable (add to PROBES): "prio1" (stage 1 at issue priority 2: 2.12-2.14 ms, slower) and
+# "prio2" (stage 2 at priority 2: 1.993-1.996 ms, no change against 1.989-1.992).
 PROBES = {1: "nos2", 2: "nos1", 3: "noload", 4: "gen"}
 
 
@@ -294,7 +302,8 @@ def gen_kernel(k, m, probe=None):
     nr = min(NCOLS_PAR, m)
     # e = 16 blocks (every output live) get a copy of stage 2 without the bound checks; m < 16
     # codes never have them
-    asm = fdec_asm(k, m, None if probe == "gen" else probe, e16=(probe is None and nr == 16))
+    asm = fdec_asm(k, m, None if probe == "gen" else probe,
+                   e16=(probe in (None, "prio1", "prio2") and nr == 16))
     body = "\\n\"\n        \"".join(asm)
     return f"""__global__ __launch_bounds__(256, 2) void {K}(FdecArgs a)
 {{
