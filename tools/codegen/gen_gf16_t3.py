@@ -118,6 +118,8 @@ B_ZERO = (72, 73)
 # ilp 180.0, prio+ilp 180.3, deep 180.4, deep+ilp 180.0; nochain 188.8, notr 176.1, both 175.6.
 # The builder does not set the column step: the row waves' VALU does (7 per row, plane and
 # 64 symbols: 3 address adds for the table reads, a bitop3 and a xor per half), DESIGN.md RS16.
+#   "nodrain" (row waves): timing probe without the lgkmcnt(0) at each row start that waits for
+#             the row's scalar-loaded offsets: 178.6-178.8 against 179.8-180.2 ms, under 1 %.
 BUILDER_VARIANTS = {0: ()}
 T3_DEFAULT = 0
 B_CUR3 = [[(68, 69), (70, 71)], [(74, 75), (76, 77)], [(78, 79), (80, 81)]]  # per group (ilp)
@@ -305,7 +307,7 @@ def builder_clobbers(flags=()):
 
 
 # ---- row waves ----
-def row_asm():
+def row_asm(flags=()):
     L = []
     L += [f"s_mov_b64 s[{S_DESC}:{S_DESC + 1}], %[wb]", f"s_mov_b32 s{S_DESC + 2}, 0x80000000",
           f"s_mov_b32 s{S_DESC + 3}, 0x00020000"]
@@ -372,7 +374,7 @@ def row_asm():
         for i in range(n):
             j = i + DEPTH
             if j < n:
-                if j % 16 == 0:
+                if j % 16 == 0 and "nodrain" not in flags:
                     out.append("s_waitcnt lgkmcnt(0)")  # row j // 16's offsets (and all reads)
                 out += issue(j)
             ahead = min(j, n - 1) - i
@@ -436,7 +438,7 @@ def row_clobbers():
 def main():
     path = sys.argv[1]
     bbs = {v: "\\n\"\n        \"".join(builder_asm(f)) for v, f in BUILDER_VARIANTS.items()}
-    rb = "\\n\"\n        \"".join(row_asm())
+    rbs = {v: "\\n\"\n        \"".join(row_asm(f)) for v, f in BUILDER_VARIANTS.items()}
     ins = ", ".join(f'[o{i}] "v"(off[{i}])' for i in range(16))
     blocks = []
     for v in BUILDER_VARIANTS:
@@ -450,6 +452,20 @@ def main():
             : {builder_clobbers(BUILDER_VARIANTS[v])});
         }}""")
     builder_blocks = "\n".join(blocks)
+    rblocks = []
+    for v in BUILDER_VARIANTS:
+        kw = "if constexpr" if v == 0 else "else if constexpr"
+        rblocks.append(f"""        {kw} (V == {v}) {{
+            asm volatile(
+            "{rbs[v]}\\n"
+            :
+            : [wb] "s"(wb), [op] "s"(op), [k] "s"(a.k), [rlim] "s"(rlim), [row0] "s"(row0),
+              [cstep] "s"(cstep), [acc] "s"(a.accumulate), [loadj] "s"(loadj), [ob] "s"(ob), [ab] "s"(ab),
+              [oslot] "s"(a.out_slot0), [oss] "s"(a.out_seg_stride), [aslot] "s"(a.acc_slot0),
+              [ass] "s"(a.acc_seg_stride), [vb0] "{{v{V_B0}}}"(vb0), [vb1] "{{v{V_B1}}}"(vb1)
+            : {row_clobbers()});
+        }}""")
+    row_blocks = "\n".join(rblocks)
     multi_cases = "\n".join(
         f"    case {v}: hipLaunchKernelGGL(gf16_t3_multi_kernel<{v}>, dim3((uint32_t)end), dim3({64 * NWAVES}), 0, s, mm); break;"
         for v in BUILDER_VARIANTS)
@@ -513,14 +529,7 @@ __device__ __forceinline__ void t3_body(const Gf16T3Args& a, uint32_t wg)
         rlim = __builtin_amdgcn_readfirstlane(rlim);  // uniform: keep it in an SGPR for the asm
         const uint8_t* ob = a.out_base + (uint64_t)b0 * a.out_block_stride;
         const uint8_t* ab = a.acc_base + (uint64_t)b0 * a.acc_block_stride;
-        asm volatile(
-        "{rb}\\n"
-        :
-        : [wb] "s"(wb), [op] "s"(op), [k] "s"(a.k), [rlim] "s"(rlim), [row0] "s"(row0),
-          [cstep] "s"(cstep), [acc] "s"(a.accumulate), [loadj] "s"(loadj), [ob] "s"(ob), [ab] "s"(ab),
-          [oslot] "s"(a.out_slot0), [oss] "s"(a.out_seg_stride), [aslot] "s"(a.acc_slot0),
-          [ass] "s"(a.acc_seg_stride), [vb0] "{{v{V_B0}}}"(vb0), [vb1] "{{v{V_B1}}}"(vb1)
-        : {row_clobbers()});
+{row_blocks}
     }}
 }}
 
