@@ -294,6 +294,9 @@ def clobbers():
 # (measured: 1.992 ms without it, 1.981 with it, 64k blocks)
 # Also generable (add to PROBES): "prio1" (stage 1 at issue priority 2: 2.12-2.14 ms, slower) and
 # "prio2" (stage 2 at priority 2: 1.993-1.996 ms, no change against 1.989-1.992).
+# "dephase" / "dephase2" (first-generation second workgroups start 30 / 17 us late, so the two
+# waves of a SIMD do not ramp their loads in phase): 1.999-2.002 / 1.984-1.987 ms against
+# 1.983-1.986, no gain; generable, not built.
 PROBES = {1: "nos2", 2: "nos1", 3: "noload", 4: "gen"}
 
 
@@ -302,15 +305,21 @@ def gen_kernel(k, m, probe=None):
     nr = min(NCOLS_PAR, m)
     # e = 16 blocks (every output live) get a copy of stage 2 without the bound checks; m < 16
     # codes never have them
-    asm = fdec_asm(k, m, None if probe == "gen" else probe,
-                   e16=(probe in (None, "prio1", "prio2") and nr == 16))
+    asm = fdec_asm(k, m, None if probe in ("gen", "dephase", "dephase2") else probe,
+                   e16=(probe in (None, "prio1", "prio2", "dephase", "dephase2") and nr == 16))
+    # A/B probe: the first generation's second workgroup per CU (dispatch order 256..511) starts
+    # ~half (dephase) / ~a quarter (dephase2) of a block later, so the two waves of a SIMD stop
+    # ramping their loads in phase
+    nsleep = {"dephase": 9, "dephase2": 5}.get(probe, 0)
+    dephase = (f"    if (blockIdx.x >= 256u && blockIdx.x < 512u)\n"
+               f"        for (int i = 0; i < {nsleep}; ++i) __builtin_amdgcn_s_sleep(127);\n") if nsleep else ""
     body = "\\n\"\n        \"".join(asm)
     return f"""__global__ __launch_bounds__(256, 2) void {K}(FdecArgs a)
 {{
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t blk = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
     if (blk >= a.nblocks) return;
-    const int32_t rows = (int32_t)__builtin_amdgcn_readfirstlane((uint32_t)a.rows[blk]);
+{dephase}    const int32_t rows = (int32_t)__builtin_amdgcn_readfirstlane((uint32_t)a.rows[blk]);
     const uint32_t ps0 = __builtin_amdgcn_readfirstlane(a.psel[2 * (uint64_t)blk]);
     const uint32_t ps1 = __builtin_amdgcn_readfirstlane(a.psel[2 * (uint64_t)blk + 1]);
     // qualifies: 1..16 source erasures repaired from parity rows below {nr} (the z rows this
