@@ -37,6 +37,11 @@ CASES = [
     (256, 64, 1400, 1400, 4, None, True),  # chosen by default (3 x 1 pass of 128 columns < 2 x 256)
     (256, 64, 1400, 1400, 4, "0", False),
     (512, 128, 64, 64, 2, "1", True),     # three passes of 44 rows per product
+    (32, 8, 8, 8, 7, "1", True),          # one item per segment, chunk width 4
+    (96, 16, 72, 72, 5, "1", True),       # three chunk pairs
+    (1024, 64, 1400, 1400, 2, "1", True),
+    (2048, 128, 64, 64, 2, "1", True),    # same pass count either way: forced
+    (1024, 64, 64, 64, 3, None, True),    # chosen by default (3 x 1 pass of 512 < 2 x 1024)
     (96, 24, 1400, 1400, 3, "1", False),  # m / 2 not a power of two: not allowed
     (100, 20, 1400, 1400, 3, "1", False),  # k not a multiple of m
 ]
