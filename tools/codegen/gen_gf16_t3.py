@@ -120,6 +120,10 @@ B_ZERO = (72, 73)
 # 64 symbols: 3 address adds for the table reads, a bitop3 and a xor per half), DESIGN.md RS16.
 #   "nodrain" (row waves): timing probe without the lgkmcnt(0) at each row start that waits for
 #             the row's scalar-loaded offsets: 178.6-178.8 against 179.8-180.2 ms, under 1 %.
+#   "timed"   probe: s_memtime around the builder's phases, printf from workgroup 0
+#             (profiles/r02/t3_builder_timing.txt): per column the builder's build + table-write
+#             drain takes ~5,000 shader clocks and it then waits ~2,500 (44 rows) / ~1,600 (20
+#             rows) at the barrier for the row waves; loads wait ~130.
 BUILDER_VARIANTS = {0: ()}
 T3_DEFAULT = 0
 B_CUR3 = [[(68, 69), (70, 71)], [(74, 75), (76, 77)], [(78, 79), (80, 81)]]  # per group (ilp)
@@ -137,6 +141,12 @@ def builder_regs(flags):
     if "deep" in flags:
         return D_RING, D_TMP, D_CUR, D_CUR3, D_ZERO
     return B_RING, B_TMP, B_CUR, B_CUR3, B_ZERO
+
+
+def STAMP(acc):
+    """timing probe: add the shader clocks since the last stamp to s<acc>"""
+    return ["s_memtime s[94:95]", "s_waitcnt lgkmcnt(0)", "s_sub_u32 s100, s94, s99",
+            f"s_add_u32 s{acc}, s{acc}, s100", "s_mov_b32 s99, s94"]
 
 
 def builder_asm(flags=()):
@@ -222,6 +232,10 @@ def builder_asm(flags=()):
     # column 2 into the slot column 0 just left
     L += ["s_cmp_gt_u32 %[k], 2", "s_cbranch_scc0 Lb_no2_%=", f"s_mov_b32 s{S_T0}, 2"] + loads(0) + ["Lb_no2_%=:"]
     L += ["s_waitcnt lgkmcnt(0)", "s_barrier"]
+    timed = "timed" in flags
+    if timed:  # probe: s96 load wait, s97 build + table-write drain, s98 barrier (shader clocks)
+        L += ["s_memtime s[94:95]", "s_waitcnt lgkmcnt(0)", "s_mov_b32 s99, s94", "s_mov_b32 s96, 0",
+              "s_mov_b32 s97, 0", "s_mov_b32 s98, 0"]
     # loop: at column c build c+1 (slot (c+1)%2, buffer (c+1)%2), load c+3 into slot c%2...
     # unrolled by two so slots and buffers are compile-time: iteration A has c even.
     L += [f"s_mov_b32 s{S_CNT}, 0"]
@@ -234,13 +248,21 @@ def builder_asm(flags=()):
         L += [f"s_add_u32 s{S_T1}, s{S_CNT}, 2", "s_cmp_lt_u32 s%d, %%[k]" % S_T1,
               f"s_cbranch_scc0 Lb_w0_{par}_%=", "s_waitcnt vmcnt(16)", f"s_branch Lb_w1_{par}_%=",
               f"Lb_w0_{par}_%=:", "s_waitcnt vmcnt(0)", f"Lb_w1_{par}_%=:"]
+        if timed:
+            L += STAMP(96)
         L += build(nxt, nxt)
         # column c+3 into slot (c+1)%2 ... no: slot of column c+3 is (c+3)%2 = (c+1)%2, which
         # holds column c+1 until its tables are written: issue after the build
         L += [f"s_add_u32 s{S_T0}, s{S_CNT}, 3", "s_cmp_lt_u32 s%d, %%[k]" % S_T0, f"s_cbranch_scc0 Lb_nl_{par}_%="]
         L += loads(nxt)
         L.append(f"Lb_nl_{par}_%=:")
-        L += ["s_waitcnt lgkmcnt(0)", "s_barrier", f"s_add_u32 s{S_CNT}, s{S_CNT}, 1"]
+        L += ["s_waitcnt lgkmcnt(0)"]
+        if timed:
+            L += STAMP(97)
+        L += ["s_barrier"]
+        if timed:
+            L += STAMP(98)
+        L += [f"s_add_u32 s{S_CNT}, s{S_CNT}, 1"]
         if par == 0:
             pass
         else:
@@ -302,7 +324,7 @@ def builder_clobbers(flags=()):
         return ", ".join([f'"v{i}"' for i in range(D_ZERO[1] + 1)] + [f'"s{i}"' for i in range(S_DESC, S_T2 + 1)] +
                          ['"scc"', '"memory"'])
     v = [f'"v{i}"' for i in range(82)]
-    s = [f'"s{i}"' for i in range(S_DESC, S_T2 + 1)]
+    s = [f'"s{i}"' for i in range(S_DESC, (100 if "timed" in flags else S_T2) + 1)]
     return ", ".join(v + s + ['"scc"', '"memory"'])
 
 
@@ -437,19 +459,26 @@ def row_clobbers():
 
 def main():
     path = sys.argv[1]
-    bbs = {v: "\\n\"\n        \"".join(builder_asm(f)) for v, f in BUILDER_VARIANTS.items()}
+    bbs = {v: "\\n\"\n        \"".join(builder_asm(f) + (["s_mov_b32 %[oa], s96", "s_mov_b32 %[ob], s97",
+                                                                 "s_mov_b32 %[oc], s98"] if "timed" in f else []))
+           for v, f in BUILDER_VARIANTS.items()}
     rbs = {v: "\\n\"\n        \"".join(row_asm(f)) for v, f in BUILDER_VARIANTS.items()}
     ins = ", ".join(f'[o{i}] "v"(off[{i}])' for i in range(16))
     blocks = []
     for v in BUILDER_VARIANTS:
         kw = "if constexpr" if v == 0 else "else if constexpr"
+        timed = "timed" in BUILDER_VARIANTS[v]
+        outs = '[oa] "=s"(ta), [ob] "=s"(tb), [oc] "=s"(tc)' if timed else ""
+        decl = "uint32_t ta, tb, tc;\n            " if timed else ""
+        prt = ('\n            if (wg == 0 && lane == 0) printf("t3 builder k=%u m=%u: load wait %u, build+drain %u, '
+               'barrier %u shader clocks\\n", a.k, a.m, ta, tb, tc);') if timed else ""
         blocks.append(f"""        {kw} (V == {v}) {{
-            asm volatile(
+            {decl}asm volatile(
             "{bbs[v]}\\n"
-            :
+            : {outs}
             : [wb] "s"(wb), [ss] "s"(a.seg_stride), [k] "s"(a.k), [lb0] "v"(lb0), [lb1] "v"(lb1),
               [csh] "s"(a.col_shift), [cmk] "s"(a.col_mask), [cck] "s"(cck), [cbb] "s"(cbb), {ins}
-            : {builder_clobbers(BUILDER_VARIANTS[v])});
+            : {builder_clobbers(BUILDER_VARIANTS[v])});{prt}
         }}""")
     builder_blocks = "\n".join(blocks)
     rblocks = []
