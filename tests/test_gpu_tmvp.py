@@ -126,3 +126,22 @@ def test_stream_copy_matches_source():
         assert torch.equal(dst, src)
     with pytest.raises(NfecError):
         stream_copy(torch.zeros(24, dtype=torch.uint8, device="cuda"), torch.zeros(24, dtype=torch.uint8, device="cuda"))
+
+
+@pytest.mark.parametrize("pinned", [False, True])
+def test_toeplitz_host_pipeline_chunks(orc, pinned, monkeypatch):
+    """Host-resident encode through the split: four chunks over the three slot streams share
+    the codec's scratch (ordered by its event)."""
+    k, m, vec, nb = 256, 64, 1400, 10
+    enc = _encoder(k, m, vec, None)
+    assert enc.features() & NFEC_FEATURE_RS16_TOEPLITZ
+    host = orc.make_blocks(k, m, vec, nb)
+    ref = orc.encode_blocks(orc.RS16, k, m, vec, host.copy())
+    if pinned:
+        buf = torch.from_numpy(host).pin_memory()
+        arr = buf.numpy()
+    else:
+        arr = host
+    monkeypatch.setenv("NFEC_HOST_CHUNK_BLOCKS", "3")
+    enc.encode_blocks_host(arr)
+    assert np.array_equal(arr, ref)
