@@ -694,8 +694,12 @@ __global__ __launch_bounds__(64 * kPlan2Waves) void rs_plan2_kernel(RsPlan2Args 
         }
         acc += (int32_t)lg[0];
         bcc += (int32_t)lg[0];
-        lA[lane] = acc;
-        lB[lane] = bcc;
+        // reduced to [0, 255) once here, so a coefficient's exponent lA + lB - log(x ^ y) lies in
+        // (-255, 510) and needs one conditional add before the doubled exp table, not a modulo
+        acc %= 255;
+        bcc %= 255;
+        lA[lane] = acc < 0 ? acc + 255 : acc;
+        lB[lane] = bcc < 0 ? bcc + 255 : bcc;
     }
     wave_lds_sync();
     uint8_t* coef = a.coef2 + (uint64_t)b * cs * cs;
@@ -708,7 +712,6 @@ __global__ __launch_bounds__(64 * kPlan2Waves) void rs_plan2_kernel(RsPlan2Args 
             uint8_t v = 0;
             if (((pused >> row) & 1ull) && s < e) {
                 int32_t l = lA[s] + lB[t] - (int32_t)lg[xs[s] ^ yt[t]];
-                l %= 255;
                 if (l < 0) l += 255;
                 v = ex[l];
             }
@@ -718,7 +721,6 @@ __global__ __launch_bounds__(64 * kPlan2Waves) void rs_plan2_kernel(RsPlan2Args 
         for (uint32_t idx = lane; idx < e * e; idx += 64) {
             const uint32_t t = idx / e, s = idx % e;
             int32_t l = lA[s] + lB[t] - (int32_t)lg[xs[s] ^ yt[t]];
-            l %= 255;
             if (l < 0) l += 255;
             coef[(uint64_t)t * cs + s] = ex[l];
         }
