@@ -591,7 +591,7 @@ __device__ __forceinline__ void wave_lds_sync()
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-constexpr uint32_t kPlan2Waves = 4;  // blocks per workgroup, one wave each: they share the tables
+constexpr uint32_t kPlan2Waves = 4;  // blocks per workgroup, one wave each: they share the tables (8: 63.6 vs 65.4 us, noise)
 
 __global__ __launch_bounds__(64 * kPlan2Waves) void rs_plan2_kernel(RsPlan2Args a)
 {
