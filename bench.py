@@ -1,6 +1,12 @@
 """Headline benchmark: RS8 k=64/m=32, 1400-byte segments, encode + 16-erasure decode, in HBM.
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
+
+`--gpus N` without a launcher starts N rank processes of this script itself (one per GPU,
+before anything touches the GPU); under a launcher --gpus must equal WORLD_SIZE.  `--dry-run`
+exercises the same launch, barrier, max-over-ranks timing and JSON line on the CPU (gloo, no
+GPU, no FEC work) for the launcher's tests.
 
 One step = one pass of the hot path over one batch resident in HBM: parity generation for
 65,536 blocks (BASELINE C2) followed by erasure repair of 16 random source symbols in each of
@@ -31,12 +37,10 @@ VALU_PEAK = 7.86e13    # 256 CU x 4 SIMD x 32 lanes x 2.4 GHz, 32-bit bitwise op
 
 def encode_kernel_name(k, m, vec):
     """the kernel nfec_encode dispatches for this shape (nfec_api.cpp encode_device)"""
-    if (k, m) not in ((64, 32), (64, 16), (64, 8)) or os.environ.get("NFEC_FORCE_GENERIC", "0") not in ("", "0"):
+    if (k, m) not in ((64, 32), (64, 16), (64, 8)):
         return "gf8_matmul_kernel (RS8 encode, generic)"
-    if os.environ.get("NFEC_ASM", "1") != "0" and vec % 8 == 0:
-        if os.environ.get("NFEC_Q4", "1") != "0":
-            return f"nfec::rs8_q4_enc_k{k}_m{m} (RS8 encode, 4 role waves sharing each column's transpose through LDS)"
-        return f"nfec::rs8_asm_enc_k{k}_m{m} (RS8 encode, hand-allocated assembly body)"
+    if vec % 8 == 0:
+        return f"nfec::rs8_q4_enc_k{k}_m{m} (RS8 encode, 4 role waves sharing each column's transpose through LDS)"
     return f"nfec::rs8_enc_k{k}_m{m} (RS8 encode, compiler-allocated)"
 
 
@@ -58,7 +62,10 @@ def host_cores():
 
 def parse():
     p = argparse.ArgumentParser()
-    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--gpus", type=int, default=None,
+                   help="GPUs = ranks (default 1, or WORLD_SIZE under a launcher)")
+    p.add_argument("--dry-run", action="store_true",
+                   help="CPU rehearsal of the multi-rank launch and reporting (gloo; no GPU, no FEC work)")
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--blocks", type=int, default=65536,
@@ -84,13 +91,69 @@ def parse():
     return p.parse_args()
 
 
+def dry_run(a, world, rank):
+    """The multi-rank skeleton of main() on the CPU: gloo barrier, exactly K timed steps of a
+    stand-in workload (a byte XOR-reduce of this rank's share, no FEC), max over ranks, one
+    JSON line from rank 0 with n_gpus = the number of ranks that reported."""
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    if world > 1:
+        dist.init_process_group("gloo")
+    from norm_amd.dist import shard
+
+    first, nb = shard(a.blocks, world, rank, a.strong)
+    buf = np.random.default_rng(first).integers(0, 256, size=(min(nb, 64), a.k * a.vec), dtype=np.uint8)
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    for _ in range(a.warmup):
+        np.bitwise_xor.reduce(buf, axis=0)
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        np.bitwise_xor.reduce(buf, axis=0)
+    elapsed = time.perf_counter() - t0
+    barrier()
+    ranks = 1
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        one = torch.ones(1)
+        dist.all_reduce(one)
+        ranks = int(one.item())
+    if rank == 0:
+        print(json.dumps({"metric": METRIC, "value": None, "unit": "GiB/s", "n_gpus": ranks, "steps": a.steps,
+                          "warmup": a.warmup, "ms_per_step": round(elapsed / a.steps * 1e3, 4),
+                          "higher_is_better": True, "scaling": "strong" if a.strong else "weak",
+                          "dry_run": True, "world_size": world,
+                          "config": {"workload": "dry run: launch and reporting only, no FEC work",
+                                     "blocks_total": a.blocks if a.strong else a.blocks * world}}))
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main():
     a = parse()
-    import torch
+    from norm_amd.dist import launch_local_ranks, plan_launch
 
+    n = plan_launch(a.gpus)
+    if n:
+        # no launcher: one child process per GPU, started before this process touches the GPU
+        sys.exit(launch_local_ranks(n, os.path.abspath(__file__), sys.argv[1:]))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if a.dry_run:
+        return dry_run(a, world, rank)
+    import torch
+
+    if world > torch.cuda.device_count():
+        raise SystemExit(f"{world} ranks but {torch.cuda.device_count()} visible GPUs: one rank per GPU")
     dist = None
     if world > 1:
         import torch.distributed as dist

@@ -199,6 +199,10 @@ int nfec_encode_segment(nfec_codec* codec, uint32_t segment_id, const void* data
 /* NormDecoder::Decode: returns erasure_count on success, 0 when undecodable, <0 on error. */
 int nfec_decode_vectors(nfec_codec* codec, void* const* vector_list, uint32_t num_data,
                         uint32_t erasure_count, const uint32_t* erasure_locs);
+/* sizeof() of the drop-in class NormEncoder<kind> (decoder = 0) or NormDecoder<kind>
+ * (decoder = 1) as the library was compiled (include/norm_fec/normEncoder*.h), 0 for an
+ * unknown kind: a NORM build can check that its translation units see the same layout. */
+size_t nfec_dropin_sizeof(int kind, int decoder);
 
 /* ---- synthetic workload utilities (device kernels; SURVEY.md 8d definitions) ----
  * fill: source slots [0, numData) of every block with the splitmix64 stream

@@ -1,0 +1,38 @@
+// nfecCodecBase.h -- the state every GPU-backed NORM codec class carries (one nfec codec
+// handle plus the Init parameters), and the batch extensions beyond the reference surface.
+//
+// Included by normEncoderRS8.h, normEncoderRS16.h and normEncoderMDP.h of this directory.  The
+// library (norm_amd/csrc/norm_codecs.cpp) and every NORM translation unit compile the codec
+// classes from these same headers, so their layout is one definition everywhere.
+#ifndef NFEC_CODEC_BASE_H
+#define NFEC_CODEC_BASE_H
+
+#include "normEncoder.h"
+#include "../nfec.h"
+
+class NfecCodecBase
+{
+  public:
+    // GPU used by codecs created afterwards in this process (one process per GPU)
+    static void SetDevice(int device) { default_device = device; }
+    static int GetDevice() { return default_device; }
+    nfec_codec* Handle() const { return codec; }
+    // Batched device-resident calls (see nfec_encode / nfec_decode): the throughput path for
+    // block-at-once call sites such as NormObject::CalculateBlockParity (normObject.cpp:2203-2229).
+    int EncodeBlocks(const nfec_block_batch* batch, void* stream);
+    int DecodeBlocks(const nfec_block_batch* batch, const uint16_t* erasureLocs, uint32_t erasureStride,
+                     const uint16_t* erasureCounts, int32_t* status, void* stream);
+
+  protected:
+    NfecCodecBase() : codec(0), ndata(0), npar(0), vector_size(0) {}
+    ~NfecCodecBase() {}
+    bool InitCodec(int kind, unsigned int numData, unsigned int numParity, UINT16 vectorSize);
+    void DestroyCodec();
+    nfec_codec* codec;
+    unsigned int ndata;        // max data pkts per block (k)
+    unsigned int npar;         // No. of parity packets (n-k)
+    unsigned int vector_size;  // Size of biggest vector to encode
+    static int default_device;
+};
+
+#endif  // NFEC_CODEC_BASE_H

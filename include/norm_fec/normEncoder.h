@@ -1,15 +1,25 @@
 // normEncoder.h -- NormEncoder / NormDecoder plugin surface for the MI355X FEC engine.
 //
-// Same abstract interface as the reference (include/normEncoder.h:38-54): a NORM engine
-// built against this header (or against its own normEncoder.h, which declares the same
-// classes) can construct the GPU-backed codecs below in place of the CPU ones at
-// src/common/normSession.cpp:842-883 and src/common/normNode.cpp:295-357.
-#ifndef NFEC_NORM_ENCODER_H
-#define NFEC_NORM_ENCODER_H
+// Replaces the reference's include/normEncoder.h (abstract bases at normEncoder.h:38-54) under
+// the same file name and the same include guard, so a NORM tree compiled with
+// -I<nfec>/include/norm_fec ahead of its own include/ picks this header up wherever it writes
+// #include "normEncoder.h" (normSession.h:7, normObject.h:5, normNode.h:6 and the codec headers),
+// and never sees a second definition of these classes.  The declarations are token-for-token
+// the reference's.
+#ifndef _NORM_ENCODER
+#define _NORM_ENCODER
 
-#ifdef NFEC_WITH_PROTOLIB
-#include "protokit.h"  // inside a NORM tree: protolib supplies UINT8/UINT16/UINT32
-#else
+// Inside a NORM tree protolib supplies UINT8/UINT16/UINT32 (the reference includes protokit.h
+// here, normEncoder.h:36); standalone builds (the tests, a non-NORM host) get the same types.
+#if defined(NFEC_WITH_PROTOLIB)
+#include "protokit.h"
+#elif defined(__has_include)
+#if __has_include("protokit.h")
+#include "protokit.h"
+#define NFEC_WITH_PROTOLIB 1
+#endif
+#endif
+#ifndef NFEC_WITH_PROTOLIB
 #include <stdint.h>
 typedef uint8_t UINT8;
 typedef uint16_t UINT16;
@@ -23,7 +33,7 @@ class NormEncoder
     virtual bool Init(unsigned int numData, unsigned int numParity, UINT16 vectorSize) = 0;
     virtual void Destroy() = 0;
     virtual void Encode(unsigned int segmentId, const char* dataVector, char** parityVectorList) = 0;
-};
+};  // end class NormEncoder
 
 class NormDecoder
 {
@@ -33,6 +43,6 @@ class NormDecoder
     virtual void Destroy() = 0;
     virtual int Decode(char** vectorList, unsigned int numData, unsigned int erasureCount,
                        unsigned int* erasureLocs) = 0;
-};
+};  // end class NormDecoder
 
-#endif
+#endif  // _NORM_ENCODER

@@ -9,7 +9,10 @@ import os
 import re
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "_lib", "libnfec.so")
+# NFEC_LIBRARY selects another build of the same ABI: the diagnostic library with the A/B
+# variants and probes of the kernels (make -C norm_amd diag -> _lib/libnfec_diag.so)
+PRODUCT_LIB_PATH = os.path.join(_HERE, "_lib", "libnfec.so")
+LIB_PATH = os.environ.get("NFEC_LIBRARY") or PRODUCT_LIB_PATH
 HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "nfec.h")
 
 NFEC_RS8, NFEC_RS16, NFEC_MDP = 1, 2, 3
@@ -118,6 +121,7 @@ _SIGS = {
     "nfec_request_wait": (_I, [_P]),
     "nfec_encode_segment": (_I, [_P, _U32, _P, _P]),
     "nfec_decode_vectors": (_I, [_P, _P, _U32, _U32, _P]),
+    "nfec_dropin_sizeof": (ctypes.c_size_t, [_I, _I]),
     "nfec_util_fill": (_I, [ctypes.POINTER(BlockBatch), _U32, _U32, _U64, _U64, _P]),
     "nfec_util_erasures": (_I, [_P, _U32, _P, _U32, _U32, _U32, _U64, _U64, _P]),
     "nfec_util_zero_slots": (_I, [ctypes.POINTER(BlockBatch), _P, _U32, _P, _U32, _P]),

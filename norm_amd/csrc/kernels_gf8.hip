@@ -388,11 +388,8 @@ int launch_gf8_solve(const Gf8SolveArgs& a, uint32_t max_rows, uint32_t max_cols
     if (a.nblocks == 0 || a.vec_bytes == 0) return NFEC_OK;
     if (max_cols > 32) return NFEC_ENOTSUP;
     const uint32_t ni = (((a.vec_bytes + 7) / 8) + kWave - 1) / kWave;
-    // NFEC_SOLVE_CFG (A/B runs): 1 = 8-row bands, 2 = tables two rows ahead
-    static const int cfg = [] {
-        const char* v = std::getenv("NFEC_SOLVE_CFG");
-        return v ? std::atoi(v) : 0;
-    }();
+    // NFEC_SOLVE_CFG (A/B runs, diagnostic library): 1 = 8-row bands, 2 = tables two rows ahead
+    static const int cfg = (int)diag_knob("NFEC_SOLVE_CFG", 0, 0, 2);
     hipError_t e;
     if (max_rows <= 8 || cfg == 1) e = ni <= 2 ? launch_solve<2, 8>(a, s) : launch_solve<3, 8>(a, s);
     else if (cfg == 2) e = ni <= 2 ? launch_solve<2, 16, 2>(a, s) : launch_solve<3, 16, 2>(a, s);

@@ -71,13 +71,10 @@ constexpr uint32_t kRowPad = 32;       // coefficient rows padded (kernel row ch
 // decode blocks per planning pass: bounds the workspace (stage-1 rows z, plan matrices).
 // Larger passes measured faster (fewer, fuller launches: 16k -> 64k blocks took
 // decode from 2.92 to 2.77 ms per 64k blocks), so a pass is as large as 4 GiB of z allows.
-// NFEC_SUBBATCH overrides (A/B runs).
+// NFEC_SUBBATCH overrides (A/B runs, diagnostic library).
 static uint32_t sub_batch(uint64_t ws_bytes_per_block)
 {
-    static const long env = [] {
-        const char* e = std::getenv("NFEC_SUBBATCH");
-        return e ? std::atol(e) : 0L;
-    }();
+    static const long env = diag_knob("NFEC_SUBBATCH", 0, 0, 1L << 20);
     if (env > 0) return (uint32_t)std::max(256L, std::min(env, 1L << 20));
     const uint64_t cap = (4ull << 30) / std::max<uint64_t>(ws_bytes_per_block, 1);
     return (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(65536, cap));
@@ -285,13 +282,10 @@ int check_batch(const nfec_codec* c, const nfec_block_batch* b)
     return NFEC_OK;
 }
 
-// NFEC_GF16_T3=0 disables the shared-table RS16 encode (A/B runs)
+// NFEC_GF16_T3=0 disables the shared-table RS16 encode (A/B runs, diagnostic library)
 bool use_gf16_t3()
 {
-    static const bool v = [] {
-        const char* e = std::getenv("NFEC_GF16_T3");
-        return !(e && *e == '0');
-    }();
+    static const bool v = diag_knob("NFEC_GF16_T3", 1) != 0;
     return v;
 }
 
@@ -451,13 +445,10 @@ int build_codec(nfec_codec* c)
     return NFEC_OK;
 }
 
-// NFEC_FORCE_GENERIC=1 disables the generated bit-sliced kernels (A/B measurements)
+// NFEC_FORCE_GENERIC=1 disables the generated bit-sliced kernels (A/B runs, diagnostic library)
 bool force_generic()
 {
-    static const bool v = [] {
-        const char* e = std::getenv("NFEC_FORCE_GENERIC");
-        return e && *e && *e != '0';
-    }();
+    static const bool v = diag_knob("NFEC_FORCE_GENERIC", 0) != 0;
     return v;
 }
 
@@ -484,30 +475,22 @@ bool has_bitsliced(uint32_t k, uint32_t m)
 // so one XCD's L2 fetches them once; encode 2.38 -> 2.35 ms), bit 1 nontemporal parity stores
 static uint32_t bs_flags()
 {
-    static const uint32_t f = [] {
-        const char* e = std::getenv("NFEC_BS_FLAGS");
-        return e ? (uint32_t)std::strtoul(e, nullptr, 0) : 1u;
-    }();
+    static const uint32_t f = (uint32_t)diag_knob("NFEC_BS_FLAGS", 1, 0, 3);
     return f;
 }
 
-// NFEC_Q4=0 disables the 4-role-wave encode kernels (gen_rs8_q4.hip; A/B runs), falling
-// back to the 2-role assembly kernels
+// NFEC_Q4=0 (diagnostic library) replaces the 4-role-wave encode kernels (gen_rs8_q4.hip) by
+// the round-1 2-role assembly kernels, which only the diagnostic library builds
 static bool use_q4()
 {
-    static const bool v = [] {
-        const char* e = std::getenv("NFEC_Q4");
-        return !(e && *e == '0');
-    }();
+    static const bool v = diag_knob("NFEC_Q4", 1) != 0;
     return v;
 }
 
+// NFEC_ASM=0 (diagnostic library): compiler-allocated bit-sliced kernels only
 static bool use_asm()
 {
-    static const bool v = [] {
-        const char* e = std::getenv("NFEC_ASM");
-        return !(e && *e == '0');
-    }();
+    static const bool v = diag_knob("NFEC_ASM", 1) != 0;
     return v;
 }
 
@@ -519,16 +502,35 @@ static bool use_asm()
 int rs16_tmvp_encode(nfec_codec* c, const nfec_block_batch* b, hipStream_t s)
 {
     const uint32_t k = c->k, m = c->m, cw = m / 2, half = k / 2, vec = c->vec;
-    // sub-batches of at most 16 GiB of scratch (C4's 4,096 blocks: one, 12.5 GB), of equal size
-    // so no launch runs a small tail batch
+    // sub-batches of at most 16 GiB of scratch (C4's 4,096 blocks: one, 12.5 GB) and at most
+    // half of the device memory free now (plus the scratch this codec already holds), of equal
+    // size so no launch runs a small tail batch
     const uint64_t per_block = (uint64_t)(half + cw) * vec;
-    const uint64_t cap = std::max<uint64_t>(1, (16ull << 30) / per_block);
+    std::lock_guard<std::mutex> lk(c->tmvp_mu);
+    size_t free_b = 0, total_b = 0;
+    if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) {
+        (void)hipGetLastError();
+        free_b = 0;
+    }
+    const uint64_t budget = std::min<uint64_t>(16ull << 30, ((uint64_t)free_b + c->w_tmvp.n) / 2);
+    const uint64_t cap = std::max<uint64_t>(1, budget / per_block);
     const uint64_t nsub = (b->nblocks + cap - 1) / cap;
     const uint32_t sb = (uint32_t)std::max<uint64_t>(1, (b->nblocks + nsub - 1) / std::max<uint64_t>(nsub, 1));
-    std::lock_guard<std::mutex> lk(c->tmvp_mu);
-    int rc = c->w_tmvp.reserve((size_t)sb * per_block);
-    if (rc) return rc;
+    // no room for the scratch: the one-product shared-table encode (no scratch) takes the batch
+    if (c->w_tmvp.reserve((size_t)sb * per_block) != NFEC_OK) {
+        (void)hipGetLastError();
+        return NFEC_ENOTSUP;
+    }
     NFEC_HIP(hipStreamWaitEvent(s, c->tmvp_done, 0));
+    // once a kernel that writes the scratch is queued, every exit records tmvp_done after it, so
+    // the next Toeplitz encode (any stream) waits for it even when this one hands over
+    bool queued = false;
+    auto leave = [&](int code) {
+        if (queued && hipEventRecord(c->tmvp_done, s) != hipSuccess && code == NFEC_OK)
+            code = hip_fail(hipGetLastError(), "tmvp event");
+        return code;
+    };
+    int rc;
     const uint32_t mp = gf16_t3_rows_padded(cw);
     const size_t one = (size_t)(half + 1) * mp * 48;
     uint32_t shift = 0;
@@ -590,12 +592,14 @@ int rs16_tmvp_encode(nfec_codec* c, const nfec_block_batch* b, hipStream_t s)
         e[2].out_slot0 = k + cw;
         // a shape the kernels do not cover shows on the first sub-batch, before any parity byte
         // is written: NFEC_ENOTSUP then hands the batch to the one-product encode
-        if ((rc = launch_tmvp_prescale(a, s))) return rc == NFEC_ENOTSUP && b0 == 0 ? rc : fail(rc, "tmvp prescale");
-        if ((rc = launch_gf16_t3_multi(e, 3, s))) return rc == NFEC_ENOTSUP && b0 == 0 ? rc : fail(rc, "tmvp products");
-        if ((rc = launch_tmvp_postscale(a, s))) return fail(rc, "tmvp postscale");
+        if ((rc = launch_tmvp_prescale(a, s)))
+            return leave(rc == NFEC_ENOTSUP && b0 == 0 ? rc : fail(rc, "tmvp prescale"));
+        queued = true;
+        if ((rc = launch_gf16_t3_multi(e, 3, s)))
+            return leave(rc == NFEC_ENOTSUP && b0 == 0 ? rc : fail(rc, "tmvp products"));
+        if ((rc = launch_tmvp_postscale(a, s))) return leave(fail(rc, "tmvp postscale"));
     }
-    NFEC_HIP(hipEventRecord(c->tmvp_done, s));
-    return NFEC_OK;
+    return leave(NFEC_OK);
 }
 
 int encode_device(nfec_codec* c, const nfec_block_batch* b, hipStream_t s)
@@ -620,10 +624,12 @@ int encode_device(nfec_codec* c, const nfec_block_batch* b, hipStream_t s)
             const int rc = launch_rs8_q4_encode(c->k, c->m, e, s);
             if (rc != NFEC_ENOTSUP) return rc == NFEC_OK ? NFEC_OK : fail(rc, "q4 encode launch failed");
         }
+#ifdef NFEC_DIAG
         if (use_asm()) {
             const int rc = launch_rs8_asm_encode(c->k, c->m, e, s);
             if (rc != NFEC_ENOTSUP) return rc == NFEC_OK ? NFEC_OK : fail(rc, "assembly encode launch failed");
         }
+#endif
         const int rc = launch_rs8_bitsliced_encode(c->k, c->m, e, s);
         if (rc != NFEC_ENOTSUP) return rc == NFEC_OK ? NFEC_OK : fail(rc, "bit-sliced encode launch failed");
     }
@@ -648,10 +654,7 @@ int encode_device(nfec_codec* c, const nfec_block_batch* b, hipStream_t s)
         return launch_gf8_matmul(a, true, s);
     }
     if (c->kind == NFEC_RS16) {
-        static const bool use_bs16 = [] {
-            const char* e = std::getenv("NFEC_GF16_BS");
-            return !(e && e[0] == '0');
-        }();
+        static const bool use_bs16 = diag_knob("NFEC_GF16_BS", 1) != 0;
         if (c->tmvp && !b->num_data && !acc) {
             const int rc = rs16_tmvp_encode(c, b, s);
             if (rc != NFEC_ENOTSUP) return rc;
@@ -730,8 +733,10 @@ int encode_device(nfec_codec* c, const nfec_block_batch* b, hipStream_t s)
             const int rc = launch_mdp_q4_encode(c->k, c->m, e, s);
             if (rc != NFEC_ENOTSUP) return rc == NFEC_OK ? NFEC_OK : fail(rc, "MDP q4 encode launch failed");
         }
+#ifdef NFEC_DIAG
         const int rc = launch_mdp_asm_encode(c->k, c->m, e, s);
         if (rc != NFEC_ENOTSUP) return rc == NFEC_OK ? NFEC_OK : fail(rc, "MDP assembly encode launch failed");
+#endif
     }
     Gf8MatmulArgs a;
     a.in_base = static_cast<const uint8_t*>(b->blocks);
@@ -793,7 +798,36 @@ int decode_device(nfec_codec* c, const nfec_block_batch* b, const uint16_t* locs
     }
     // RS16 stage 1 by the shared-table encode for the blocks whose substitute parities are rows
     // 0..e-1 (RsPlanArgs::rows1): overwrite semantics only, since it zeroes the erased source
-    const bool t3dec = c->kind == NFEC_RS16 && c->d_t3off.p && !b->num_data && !acc && (c->vec % 8) == 0;
+    // z_t = (encode row t of the block, erased source zeroed) ^ received parity t
+    auto t3_stage1 = [&](uint8_t* blocks, uint32_t nb) {
+        Gf16T3Args t;
+        t.base = blocks;
+        t.block_stride = b->block_stride;
+        t.seg_stride = b->seg_stride;
+        t.nblocks = nb;
+        t.k = c->k;
+        t.m = c->m;
+        t.m_pad = gf16_t3_rows_padded(c->m);
+        t.vec_bytes = c->vec & ~1u;
+        t.offs = c->d_t3off.p;
+        t.accumulate = 1;
+        t.out_base = c->w_z.p;
+        t.out_block_stride = (uint64_t)dcs * zstride;
+        t.out_seg_stride = zstride;
+        t.out_slot0 = 0;
+        t.acc_base = blocks;
+        t.acc_block_stride = b->block_stride;
+        t.acc_seg_stride = b->seg_stride;
+        t.acc_slot0 = c->k;
+        t.rows_lim = c->w_rmax.p;
+        return t;
+    };
+    // the plan marks blocks for this stage 1 only when the kernel takes the batch's layout
+    // (t3_prepare's 2^31 offset bounds); otherwise every block keeps the gather stage
+    bool t3dec = c->kind == NFEC_RS16 && c->d_t3off.p && !b->num_data && !acc && (c->vec % 8) == 0;
+    if (t3dec) {
+        t3dec = gf16_t3_covers(t3_stage1(static_cast<uint8_t*>(b->blocks), sb));
+    }
     if (t3dec) {
         if ((rc = c->w_rows1.reserve(sb))) return rc;
         if ((rc = c->w_rmax.reserve(1))) return rc;
@@ -833,10 +867,7 @@ int decode_device(nfec_codec* c, const nfec_block_batch* b, const uint16_t* locs
             p.coef = c->w_coef1.p;
             if ((rc = launch_mdp_plan(p, s))) return rc;
             // blocks with <= 16 erased source vectors: the snippet solve (NFEC_MDP_BS=0: off)
-            static const bool use_mdp_bs = [] {
-                const char* e = std::getenv("NFEC_MDP_BS");
-                return !(e && e[0] == '0');
-            }();
+            static const bool use_mdp_bs = diag_knob("NFEC_MDP_BS", 1) != 0;
             if (use_mdp_bs) {
                 MdpSolveArgs ms;
                 ms.base = blocks;
@@ -901,10 +932,7 @@ int decode_device(nfec_codec* c, const nfec_block_batch* b, const uint16_t* locs
             p2.coef2 = c->w_coef2.p;
             // fused per-block repair for the blocks it qualifies for (NFEC_FUSED=0: off); the
             // unfused stage 1 and solve below skip the blocks it marked
-            static const bool use_fused = [] {
-                const char* e = std::getenv("NFEC_FUSED");
-                return !(e && e[0] == '0');
-            }();
+            static const bool use_fused = diag_knob("NFEC_FUSED", 1) != 0;
             FdecArgs f;
             f.base = blocks;
             f.block_stride = b->block_stride;
@@ -921,13 +949,10 @@ int decode_device(nfec_codec* c, const nfec_block_batch* b, const uint16_t* locs
             f.out_slots = c->w_oslots.p;
             f.slots_stride = c->k;
             f.accumulate = acc;
-            static const uint32_t lane_major = [] {
-                // 2 (default) = compact lane-major items, idle lanes out of EXEC (1.981-1.985 vs
-                // 1.989-1.998 ms, r02g); 0 = item q*64 + lane; 1 = lane L holds items 4L..4L+3
-                // (strided loads: 2.16 vs 2.02 ms).  NFEC_FDEC_LANEMAJOR overrides (A/B).
-                const char* e = std::getenv("NFEC_FDEC_LANEMAJOR");
-                return e ? (uint32_t)std::atoi(e) : 2u;
-            }();
+            // 2 (default) = compact lane-major items, idle lanes out of EXEC (1.981-1.985 vs
+            // 1.989-1.998 ms, r02g); 0 = item q*64 + lane; 1 = lane L holds items 4L..4L+3
+            // (strided loads: 2.16 vs 2.02 ms).  NFEC_FDEC_LANEMAJOR overrides (diagnostic library).
+            static const uint32_t lane_major = (uint32_t)diag_knob("NFEC_FDEC_LANEMAJOR", 2, 0, 2);
             f.lane_major = lane_major;
             const bool fused = use_fused && rs8_fused_decode_covers(c->k, c->m, f);
             // gate: the plan writes this pass's generation into w_gate when some block needs the
@@ -961,10 +986,7 @@ int decode_device(nfec_codec* c, const nfec_block_batch* b, const uint16_t* locs
             d.gate = gate;
             d.gate_gen = gen;
             if ((rc = launch_rs8_bitsliced_reencode(c->k, c->m, d, s))) return fail(rc, "bit-sliced re-encode launch failed");
-            static const bool use_solve = [] {
-                const char* e = std::getenv("NFEC_SOLVE");
-                return !(e && e[0] == '0');
-            }();
+            static const bool use_solve = diag_knob("NFEC_SOLVE", 1) != 0;
             if (!use_solve) {
                 Gf8MatmulArgs g2;
                 g2.in_base = c->w_z.p;
@@ -1010,10 +1032,7 @@ int decode_device(nfec_codec* c, const nfec_block_batch* b, const uint16_t* locs
             a2.gate_gen = gen;
             // bit-sliced snippet-table solve for blocks with <= 16 erasures (NFEC_SOLVE_BS=0: off),
             // the v_perm kernel for the rest
-            static const bool use_bs = [] {
-                const char* e = std::getenv("NFEC_SOLVE_BS");
-                return !(e && e[0] == '0');
-            }();
+            static const bool use_bs = diag_knob("NFEC_SOLVE_BS", 1) != 0;
             if (use_bs) {
                 rc = launch_gf8_solve_bs(a2, s);
                 if (rc != NFEC_OK && rc != NFEC_ENOTSUP) return fail(rc, "bit-sliced solve launch failed");
@@ -1051,10 +1070,7 @@ int decode_device(nfec_codec* c, const nfec_block_batch* b, const uint16_t* locs
         p.work = big_plan ? c->w_work.p : nullptr;
         p.work_block_bytes = rs_plan_work_bytes(dcs, c->sym);
         // RS16: the closed-form inverse when every block's e fits it (NFEC_RS16_CF=0: Gauss-Jordan)
-        static const bool use_cf16 = [] {
-            const char* e = std::getenv("NFEC_RS16_CF");
-            return !(e && e[0] == '0');
-        }();
+        static const bool use_cf16 = diag_knob("NFEC_RS16_CF", 1) != 0;
         if (c->kind == NFEC_RS16 && use_cf16 && c->d_lwp.p && std::min(c->k, c->m) <= kPlanCfMaxE) {
             p.lwp = c->d_lwp.p;
             p.lw = c->d_lw.p;
@@ -1070,30 +1086,9 @@ int decode_device(nfec_codec* c, const nfec_block_batch* b, const uint16_t* locs
         }
         if ((rc = launch_rs_plan(p, s))) return rc;
         if (t3dec) {
-            // z_t = (encode row t of the block, erased source zeroed) ^ received parity t, for
-            // t below the plan's largest such e; the gather stage then overwrites the z rows of
-            // the other blocks
-            Gf16T3Args t;
-            t.base = blocks;
-            t.block_stride = b->block_stride;
-            t.seg_stride = b->seg_stride;
-            t.nblocks = nb;
-            t.k = c->k;
-            t.m = c->m;
-            t.m_pad = gf16_t3_rows_padded(c->m);
-            t.vec_bytes = c->vec & ~1u;
-            t.offs = c->d_t3off.p;
-            t.accumulate = 1;
-            t.out_base = c->w_z.p;
-            t.out_block_stride = (uint64_t)dcs * zstride;
-            t.out_seg_stride = zstride;
-            t.out_slot0 = 0;
-            t.acc_base = blocks;
-            t.acc_block_stride = b->block_stride;
-            t.acc_seg_stride = b->seg_stride;
-            t.acc_slot0 = c->k;
-            t.rows_lim = c->w_rmax.p;
-            rc = launch_gf16_t3_encode(t, s);
+            // z_t for t below the plan's largest such e; the gather stage then overwrites the z
+            // rows of the other blocks
+            rc = launch_gf16_t3_encode(t3_stage1(blocks, nb), s);
             if (rc == NFEC_ENOTSUP) return fail(rc, "t3 decode stage 1: layout not covered");
             if (rc) return rc;
         }
@@ -1235,6 +1230,7 @@ int nfec_codec_create(int device, int kind, uint32_t num_data, uint32_t num_pari
     c->k = num_data;
     c->m = num_parity;
     c->vec = vector_size;
+    c->async.device = device;  // fixed before any worker thread can read it
     int rc = build_codec(c.get());
     if (rc) return rc;
     *out = c.release();
@@ -1744,10 +1740,10 @@ static int run_host_batch(nfec_codec* c, const nfec_block_batch* hb, const uint1
         db.num_data = dnd;
         if (ae != hipSuccess) return bail(hip_fail(ae, "host batch upload"));
         if (decode) {
-            uint16_t* dl = s.dmeta + chunk;
-            uint16_t* dc = dl + (size_t)chunk * lstride;
-            ae = hipMemcpyAsync(dl, locs + (uint64_t)b0 * lstride, (size_t)j.nb * lstride * 2, hipMemcpyHostToDevice, s.st);
-            if (ae == hipSuccess) ae = hipMemcpyAsync(dc, counts + b0, (size_t)j.nb * 2, hipMemcpyHostToDevice, s.st);
+            uint16_t* dlocs = s.dmeta + chunk;
+            uint16_t* dcnt = dlocs + (size_t)chunk * lstride;
+            ae = hipMemcpyAsync(dlocs, locs + (uint64_t)b0 * lstride, (size_t)j.nb * lstride * 2, hipMemcpyHostToDevice, s.st);
+            if (ae == hipSuccess) ae = hipMemcpyAsync(dcnt, counts + b0, (size_t)j.nb * 2, hipMemcpyHostToDevice, s.st);
             if (ae != hipSuccess) return bail(hip_fail(ae, "host batch upload"));
             rc = split_full_runs(hb->num_data ? hb->num_data + b0 : nullptr, j.nb, c->k,
                                  [&](uint32_t o, uint32_t n, bool nd) {
@@ -1755,7 +1751,7 @@ static int run_host_batch(nfec_codec* c, const nfec_block_batch* hb, const uint1
                                      sb.blocks = s.dev + o * dbs;
                                      sb.nblocks = n;
                                      sb.num_data = nd ? dnd + o : nullptr;
-                                     return decode_serialized(c, &sb, dl + (uint64_t)o * lstride, lstride, dc + o, s, o);
+                                     return decode_serialized(c, &sb, dlocs + (uint64_t)o * lstride, lstride, dcnt + o, s, o);
                                  });
         } else {
             rc = split_full_runs(hb->num_data ? hb->num_data + b0 : nullptr, j.nb, c->k,
@@ -2033,7 +2029,6 @@ int submit_vectors(nfec_codec* c, void* const* vecs, uint32_t nblocks, const uin
                                 decode ? el->data() : nullptr, lstride, decode ? ec->data() : nullptr, status,
                                 flags, decode);
     };
-    c->async.device = c->device;
     c->async.submit(r.get());
     *out = r.release();
     return NFEC_OK;

@@ -5,6 +5,7 @@
 
 #include <cstddef>
 #include <cstdint>
+#include <cstdlib>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -25,6 +26,23 @@ int hip_fail(hipError_t e, const char* what);
         hipError_t e_ = (call);                           \
         if (e_ != hipSuccess) return ::nfec::hip_fail(e_, #call); \
     } while (0)
+
+// A/B switches between correct alternative paths (kernels on or off, tuning choices).  Only
+// the diagnostic library (make -C norm_amd diag, -DNFEC_DIAG) reads them from the
+// environment; the product library always takes the default, so no stray variable changes
+// what it runs.  Values outside [lo, hi] fall back to the default.
+inline long diag_knob(const char* name, long def, long lo = 0, long hi = 1)
+{
+#ifdef NFEC_DIAG
+    const char* e = std::getenv(name);
+    if (!e || !*e) return def;
+    const long v = std::strtol(e, nullptr, 0);
+    return v < lo || v > hi ? def : v;
+#else
+    (void)name, (void)lo, (void)hi;
+    return def;
+#endif
+}
 
 // ---------------------------------------------------------------------------------
 // Host field arithmetic (gf_host.cpp).  GF(2^8) on 0x11d and GF(2^16) on 0x1100B with
@@ -227,6 +245,7 @@ bool rs16_tmvp_plan(uint32_t k, uint32_t m, const std::vector<uint32_t>& gen, st
 int launch_tmvp_prescale(const Rs16TmvpArgs& a, hipStream_t s);
 int launch_tmvp_postscale(const Rs16TmvpArgs& a, hipStream_t s);
 int launch_gf16_t3_encode(const Gf16T3Args& a, hipStream_t s);  // NFEC_ENOTSUP: shape not covered
+bool gf16_t3_covers(const Gf16T3Args& a);  // launch_gf16_t3_encode would take it
 int launch_gf16_t3_multi(const Gf16T3Args* e, uint32_t n, hipStream_t s);  // n <= 3 independent products
 void gf16_t3_offsets(const std::vector<uint32_t>& parity_rows, uint32_t k, uint32_t m, uint16_t* out);
 int launch_gf16_bs_encode(const Gf16BsEncArgs& a, hipStream_t s);  // NFEC_ENOTSUP: layout not 8-byte aligned

@@ -1,5 +1,11 @@
 // norm_codecs.cpp -- NormEncoder/NormDecoder drop-in classes over the nfec C ABI.
-#include "../../include/norm_fec/nfecCodecs.h"
+//
+// Compiled from the reference-named headers (include/norm_fec/normEncoder*.h), exactly the
+// include lines of NORM's construction sites (normSession.cpp:3-5, normNode.cpp:4-6), so the
+// library and a NORM translation unit see one class layout.
+#include "../../include/norm_fec/normEncoderMDP.h"
+#include "../../include/norm_fec/normEncoderRS8.h"
+#include "../../include/norm_fec/normEncoderRS16.h"
 
 #include <cstdio>
 
@@ -30,6 +36,7 @@ void NfecCodecBase::DestroyCodec()
 {
     if (codec) nfec_codec_destroy(codec);
     codec = 0;
+    ndata = npar = vector_size = 0;
 }
 
 int NfecCodecBase::EncodeBlocks(const nfec_block_batch* batch, void* stream)
@@ -86,3 +93,13 @@ NFEC_DEFINE_ENCODER(NormEncoderRS16, NFEC_RS16)
 NFEC_DEFINE_DECODER(NormDecoderRS16, NFEC_RS16)
 NFEC_DEFINE_ENCODER(NormEncoderMDP, NFEC_MDP)
 NFEC_DEFINE_DECODER(NormDecoderMDP, NFEC_MDP)
+
+extern "C" size_t nfec_dropin_sizeof(int kind, int decoder)
+{
+    switch (kind) {
+        case NFEC_RS8: return decoder ? sizeof(NormDecoderRS8) : sizeof(NormEncoderRS8);
+        case NFEC_RS16: return decoder ? sizeof(NormDecoderRS16) : sizeof(NormEncoderRS16);
+        case NFEC_MDP: return decoder ? sizeof(NormDecoderMDP) : sizeof(NormEncoderMDP);
+        default: return 0;
+    }
+}

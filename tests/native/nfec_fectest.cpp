@@ -13,31 +13,102 @@
 //     NULLPAR  1: erased parity passed as NULL pointers (NORM's receiver), 0: zeroed (fecTest)
 //     LOC ...  sorted erasure locations in [0, NUMDATA+M)
 // Exit status 0 when every source segment came back byte for byte (fecTest step 8).
+//
+// The codec headers are included exactly as NORM's construction sites include them
+// (normSession.cpp:3-5), and tests/native/Makefile compiles this file with
+// -I../../include/norm_fec ahead of poison/, a directory holding #error stand-ins under the
+// reference's header names: it builds only if the engine's headers shadow the reference's.
+// The inline accessors (GetNumData() & co., compiled here, not in the library) and sizeof()
+// are checked against the library's own view of the classes (nfec_dropin_sizeof).
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <vector>
 
-#include "norm_fec/nfecCodecs.h"
+#include "normEncoderMDP.h"  // "legacy" MDP Reed-Solomon encoder
+#include "normEncoderRS8.h"  // 8-bit Reed-Solomon encoder of RFC 5510
+#include "normEncoderRS16.h" // 16-bit Reed-Solomon encoder of RFC 5510
 
-static NormEncoder* new_encoder(const char* kind)
+static int layout_errors = 0;
+
+static void expect(bool ok, const char* what)
 {
-    if (!std::strcmp(kind, "rs8")) return new NormEncoderRS8;
-    if (!std::strcmp(kind, "rs16")) return new NormEncoderRS16;
-    if (!std::strcmp(kind, "mdp")) return new NormEncoderMDP;
+    if (!ok) {
+        std::fprintf(stderr, "fect: %s\n", what);
+        ++layout_errors;
+    }
+}
+
+// new + Init through the concrete class, accessors read back, then handed out as the base
+template <class E>
+static NormEncoder* init_encoder(unsigned k, unsigned m, unsigned vec, int kind)
+{
+    E* e = new E;
+    expect(sizeof(E) == nfec_dropin_sizeof(kind, 0), "encoder sizeof differs from the library's");
+    if (!e->Init(k, m, (UINT16)vec)) {
+        delete e;
+        return 0;
+    }
+    expect(e->IsReady(), "encoder IsReady() false after Init");
+    expect(e->GetNumData() == k && e->GetNumParity() == m && e->GetVectorSize() == vec,
+           "encoder accessors do not return the Init parameters");
+    return e;
+}
+
+template <class D>
+static NormDecoder* init_decoder(unsigned k, unsigned m, unsigned vec, int kind)
+{
+    D* d = new D;
+    expect(sizeof(D) == nfec_dropin_sizeof(kind, 1), "decoder sizeof differs from the library's");
+    if (!d->Init(k, m, (UINT16)vec)) {
+        delete d;
+        return 0;
+    }
+    expect(d->GetNumParity() == m && d->GetVectorSize() == vec, "decoder accessors do not return the Init parameters");
+    return d;
+}
+
+static NormEncoder* new_encoder(const char* kind, unsigned k, unsigned m, unsigned vec)
+{
+    if (!std::strcmp(kind, "rs8")) return init_encoder<NormEncoderRS8>(k, m, vec, NFEC_RS8);
+    if (!std::strcmp(kind, "rs16")) return init_encoder<NormEncoderRS16>(k, m, vec, NFEC_RS16);
+    if (!std::strcmp(kind, "mdp")) return init_encoder<NormEncoderMDP>(k, m, vec, NFEC_MDP);
     return 0;
 }
 
-static NormDecoder* new_decoder(const char* kind)
+static NormDecoder* new_decoder(const char* kind, unsigned k, unsigned m, unsigned vec)
 {
-    if (!std::strcmp(kind, "rs8")) return new NormDecoderRS8;
-    if (!std::strcmp(kind, "rs16")) return new NormDecoderRS16;
-    if (!std::strcmp(kind, "mdp")) return new NormDecoderMDP;
+    if (!std::strcmp(kind, "rs8")) return init_decoder<NormDecoderRS8>(k, m, vec, NFEC_RS8);
+    if (!std::strcmp(kind, "rs16")) return init_decoder<NormDecoderRS16>(k, m, vec, NFEC_RS16);
+    if (!std::strcmp(kind, "mdp")) {
+        NormDecoder* d = init_decoder<NormDecoderMDP>(k, m, vec, NFEC_MDP);
+        // the reference MDP decoder's own accessors (normEncoderMDP.h:70-71)
+        if (d) expect(static_cast<NormDecoderMDP*>(d)->NumParity() == (int)m &&
+                          static_cast<NormDecoderMDP*>(d)->VectorSize() == (int)vec,
+                      "MDP decoder NumParity()/VectorSize() wrong");
+        return d;
+    }
     return 0;
+}
+
+// `nfec_fectest layout`: the sizeof() checks alone (no GPU needed)
+static int layout_only()
+{
+    expect(sizeof(NormEncoderRS8) == nfec_dropin_sizeof(NFEC_RS8, 0), "NormEncoderRS8 sizeof differs");
+    expect(sizeof(NormDecoderRS8) == nfec_dropin_sizeof(NFEC_RS8, 1), "NormDecoderRS8 sizeof differs");
+    expect(sizeof(NormEncoderRS16) == nfec_dropin_sizeof(NFEC_RS16, 0), "NormEncoderRS16 sizeof differs");
+    expect(sizeof(NormDecoderRS16) == nfec_dropin_sizeof(NFEC_RS16, 1), "NormDecoderRS16 sizeof differs");
+    expect(sizeof(NormEncoderMDP) == nfec_dropin_sizeof(NFEC_MDP, 0), "NormEncoderMDP sizeof differs");
+    expect(sizeof(NormDecoderMDP) == nfec_dropin_sizeof(NFEC_MDP, 1), "NormDecoderMDP sizeof differs");
+    std::printf("layout %zu %zu %zu %zu %zu %zu errors %d\n", sizeof(NormEncoderRS8), sizeof(NormDecoderRS8),
+                sizeof(NormEncoderRS16), sizeof(NormDecoderRS16), sizeof(NormEncoderMDP), sizeof(NormDecoderMDP),
+                layout_errors);
+    return layout_errors ? 1 : 0;
 }
 
 int main(int argc, char* argv[])
 {
+    if (argc == 2 && !std::strcmp(argv[1], "layout")) return layout_only();
     if (argc < 9) {
         std::fprintf(stderr, "usage: %s KIND K M VEC NUMDATA IN OUT NULLPAR [LOC ...]\n", argv[0]);
         return 2;
@@ -52,14 +123,15 @@ int main(int argc, char* argv[])
     for (int i = 9; i < argc; ++i) locs.push_back((unsigned)std::atoi(argv[i]));
     const unsigned n = nd + m;
 
-    NormEncoder* encoder = new_encoder(kind);
-    NormDecoder* decoder = new_decoder(kind);
-    if (!encoder || !decoder || nd == 0 || nd > k) return 2;
-    // Init / Destroy / Init again through the vtable: Destroy must leave the codec reusable
-    if (!encoder->Init(k, m, (UINT16)vec) || !decoder->Init(k, m, (UINT16)vec)) {
+    if (std::strcmp(kind, "rs8") && std::strcmp(kind, "rs16") && std::strcmp(kind, "mdp")) return 2;
+    if (nd == 0 || nd > k) return 2;
+    NormEncoder* encoder = new_encoder(kind, k, m, vec);
+    NormDecoder* decoder = new_decoder(kind, k, m, vec);
+    if (!encoder || !decoder) {
         std::fprintf(stderr, "fect: Init(%u, %u, %u) failed\n", k, m, vec);
         return 3;
     }
+    // Destroy / Init again through the vtable: Destroy must leave the codec reusable
     encoder->Destroy();
     if (!encoder->Init(k, m, (UINT16)vec)) return 3;
 
@@ -113,13 +185,13 @@ int main(int argc, char* argv[])
     std::fwrite(&status, sizeof(status), 1, f);
     for (unsigned i = 0; i < n; ++i) std::fwrite(rx[i], 1, vec, f);
     std::fclose(f);
-    std::fprintf(stderr, "fect: %s k=%u m=%u vec=%u numData=%u erasures=%zu Decode()=%d bad=%d\n", kind, k, m, vec,
-                 nd, locs.size(), status, bad);
+    std::fprintf(stderr, "fect: %s k=%u m=%u vec=%u numData=%u erasures=%zu Decode()=%d bad=%d layout_errors=%d\n",
+                 kind, k, m, vec, nd, locs.size(), status, bad, layout_errors);
     for (unsigned i = 0; i < n; ++i) {
         delete[] tx[i];
         delete[] rx[i];
     }
     delete encoder;  // through the base class: the virtual destructors release the GPU codec
     delete decoder;
-    return bad ? 1 : 0;
+    return (bad || layout_errors) ? 1 : 0;
 }

@@ -1,0 +1,3 @@
+// Poisoned stand-in for the reference header normEncoderRS8.h (test fixture): a drop-in build must find
+// include/norm_fec/ first; reaching this file means the reference header would be used.
+#error "reference header normEncoderRS8.h was picked up instead of include/norm_fec"

@@ -10,7 +10,8 @@ import sys
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-GENERATORS = ["rs8_asm", "rs8_bitsliced", "rs8_q4", "fdec_asm", "solve_asm", "gf16_t3"]
+# product kernels; gen_rs8_asm.py (the round-1 2-role encode) feeds the diagnostic library only
+GENERATORS = ["rs8_bitsliced", "rs8_q4", "fdec_asm", "solve_asm", "gf16_t3"]
 
 
 @pytest.mark.parametrize("name", GENERATORS)
@@ -27,3 +28,19 @@ def test_every_generated_source_has_a_generator():
     gen = sorted(f[4:-4] for f in os.listdir(os.path.join(ROOT, "norm_amd", "csrc"))
                  if f.startswith("gen_") and f.endswith(".hip"))
     assert gen == sorted(GENERATORS)
+
+
+def test_product_library_has_no_probe_or_variant_kernels():
+    """The A/B variants and timing probes (some compute wrong parity on purpose) are built into
+    the diagnostic library only (make -C norm_amd diag); the product library holds the default
+    kernels and reads no NFEC_*_VARIANT switch."""
+    import re
+
+    data = open(os.path.join(ROOT, "norm_amd", "_lib", "libnfec.so"), "rb").read()
+    assert b"_probe_" not in data
+    assert not re.search(rb"_v[0-9]+_k[0-9]+_m[0-9]+", data)
+    assert not re.search(rb"NFEC_[A-Z0-9]*VARIANT", data)
+    assert b"rs8_asm_enc" not in data
+    for name in GENERATORS:
+        src = open(os.path.join(ROOT, "norm_amd", "csrc", f"gen_{name}.hip")).read()
+        assert "getenv" not in src and "_probe_" not in src, name

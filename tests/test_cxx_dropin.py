@@ -1,4 +1,4 @@
-"""The C++ drop-in surface (include/norm_fec/nfecCodecs.h) exercised the way NORM uses it.
+"""The C++ drop-in surface (include/norm_fec/normEncoder*.h) exercised the way NORM uses it.
 
 tests/native/nfec_fectest is the reference's fecTest (src/common/fecTest.cpp:23-135) restated
 against the GPU classes: Init, per-segment Encode and whole-block Decode called through
@@ -24,6 +24,47 @@ def test_fectest_links_against_libnfec_only():
     assert r.returncode == 2 and "usage" in r.stderr
     ldd = subprocess.run(["ldd", EXE], capture_output=True, text=True).stdout
     assert "libnfec.so" in ldd and "not found" not in ldd
+
+
+NATIVE = os.path.join(ROOT, "tests", "native")
+SRC = os.path.join(NATIVE, "nfec_fectest.cpp")
+
+
+def _syntax(*incs):
+    return subprocess.run(["g++", "-std=c++11", "-fsyntax-only"] + [f"-I{i}" for i in incs] + [SRC],
+                          capture_output=True, text=True, timeout=120)
+
+
+def test_reference_named_headers_shadow_the_reference():
+    """NORM's call sites include normEncoderMDP.h / normEncoderRS8.h / normEncoderRS16.h by name
+    (normSession.cpp:3-5).  With include/norm_fec ahead of the tree's include/ (INTEGRATION.md
+    section 1) the engine's headers win; poison/ holds #error stand-ins under the reference
+    names, so the order is what makes the unit compile."""
+    good = _syntax(os.path.join(ROOT, "include", "norm_fec"), os.path.join(NATIVE, "poison"))
+    assert good.returncode == 0, good.stderr
+    bad = _syntax(os.path.join(NATIVE, "poison"), os.path.join(ROOT, "include", "norm_fec"))
+    assert bad.returncode != 0 and "was picked up instead of include/norm_fec" in bad.stderr
+
+
+def test_reference_include_guards():
+    """Same guards as the reference headers, so a stray second include of either is a no-op."""
+    want = {"normEncoder.h": "_NORM_ENCODER", "normEncoderRS8.h": "_NORM_ENCODER_RS8",
+            "normEncoderRS16.h": "_NORM_ENCODER_RS16", "normEncoderMDP.h": "_NORM_ENCODER_MDP"}
+    for name, guard in want.items():
+        text = open(os.path.join(ROOT, "include", "norm_fec", name)).read()
+        assert f"#ifndef {guard}\n#define {guard}\n" in text, name
+
+
+@pytest.mark.skipif(not os.path.isdir("/root/reference/include"), reason="reference tree absent (GPU box)")
+def test_headers_shadow_the_real_reference_include_dir():
+    r = _syntax(os.path.join(ROOT, "include", "norm_fec"), "/root/reference/include")
+    assert r.returncode == 0, r.stderr
+
+
+def test_dropin_layout_matches_library():
+    """sizeof() of the six classes as a NORM unit sees them equals the library's (no GPU)."""
+    r = subprocess.run([EXE, "layout"], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0 and "errors 0" in r.stdout, r.stdout + r.stderr
 
 
 KINDS = {"rs8": 1, "rs16": 2, "mdp": 3}
@@ -59,6 +100,7 @@ def test_fectest_matches_oracle(orc, tmp_path, kind, k, m, vec, nd, locs, nullpa
                        + [str(x) for x in locs], capture_output=True, text=True, timeout=120)
     dump = np.fromfile(out, np.uint8)
     assert dump.size == 2 * n * vec + 4, r.stderr
+    assert "layout_errors=0" in r.stderr, r.stderr  # inline accessors and sizeof agree with the library
     tx = dump[: n * vec].reshape(n, vec)
     status = int(dump[n * vec: n * vec + 4].view(np.int32)[0])
     rx = dump[n * vec + 4:].reshape(n, vec)

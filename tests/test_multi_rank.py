@@ -91,3 +91,51 @@ def test_two_rank_gloo_striping(orc, strong):
         assert [g[:2] for g in gathered] == [block_range(total, world, r) for r in range(world)]
         for lo, hi, digest in gathered:
             assert digest == hashlib.sha256(whole[lo:hi, k:].tobytes()).hexdigest()
+
+
+# ---- bench.py --gpus N: the launch itself (--gpus must produce N ranks) ----
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _bench(args, env_extra=None, timeout=300):
+    import json
+    import subprocess
+    import sys
+
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env.update(env_extra or {})
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + args, capture_output=True, text=True,
+                       timeout=timeout, env=env, cwd=ROOT)
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    return r, [json.loads(ln) for ln in lines]
+
+
+@pytest.mark.parametrize("n", [1, 2, 3])
+def test_bench_gpus_flag_starts_n_ranks(n):
+    """Without a launcher `bench.py --gpus N` starts N rank processes; rank 0 alone prints, and
+    the line counts every rank that joined the group (the dry run's all-reduce of ones)."""
+    r, out = _bench(["--gpus", str(n), "--dry-run", "--steps", "2", "--warmup", "1", "--blocks", "256"])
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert len(out) == 1, r.stdout
+    assert out[0]["n_gpus"] == n and out[0]["world_size"] == n and out[0]["steps"] == 2
+
+
+def test_bench_gpus_must_match_launcher_world():
+    r, out = _bench(["--gpus", "4", "--dry-run"], {"WORLD_SIZE": "2", "RANK": "0", "LOCAL_RANK": "0"}, timeout=120)
+    assert r.returncode != 0 and "WORLD_SIZE=2" in r.stderr and not out
+
+
+def test_plan_launch():
+    from norm_amd.dist import plan_launch
+
+    old = {k: os.environ.pop(k, None) for k in ("WORLD_SIZE",)}
+    try:
+        assert plan_launch(None) == 0 and plan_launch(1) == 0 and plan_launch(8) == 8
+        os.environ["WORLD_SIZE"] = "8"
+        assert plan_launch(8) == 0 and plan_launch(None) == 0
+        with pytest.raises(SystemExit):
+            plan_launch(1)
+    finally:
+        os.environ.pop("WORLD_SIZE", None)
+        if old["WORLD_SIZE"] is not None:
+            os.environ["WORLD_SIZE"] = old["WORLD_SIZE"]

@@ -2,6 +2,7 @@
 host memory (NORM's socket buffers), H2D / compute / D2H overlapped.
 
     python tools/bench_c5.py [--steps 2]                       # one GPU: 131,072 blocks (1M / 8)
+    python tools/bench_c5.py --gpus 8                           # 8 rank processes, no launcher
     torchrun --nproc-per-node 8 tools/bench_c5.py               # weak: 131,072 blocks per GPU = C5
     torchrun --nproc-per-node N tools/bench_c5.py --strong      # strong: 1,048,576 blocks over N GPUs
 
@@ -42,10 +43,9 @@ def splitmix64(x):
 
 
 def main():
-    import numpy as np
-    import torch
-
     p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=None,
+                   help="GPUs = ranks; without a launcher N > 1 starts N rank processes (bench.py's rule)")
     p.add_argument("--blocks", type=int, default=0,
                    help="blocks per GPU (weak; default 1M / 8), or in total with --strong (default 1M)")
     p.add_argument("--strong", action="store_true", help="a fixed total split over the ranks")
@@ -53,6 +53,13 @@ def main():
     p.add_argument("--warmup", type=int, default=1)
     p.add_argument("--serial", action="store_true", help="run the RS8 and RS16 sub-streams one after the other")
     a = p.parse_args()
+    from norm_amd.dist import launch_local_ranks, plan_launch
+
+    n = plan_launch(a.gpus)
+    if n:
+        sys.exit(launch_local_ranks(n, os.path.abspath(__file__), sys.argv[1:]))
+    import numpy as np
+    import torch
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))

@@ -368,10 +368,14 @@ def gen_kernel(k, m, probe=None):
 
 
 def main():
-    path = sys.argv[1]
+    # --diag: also emit the A/B probes and their NFEC_FDEC_VARIANT switch (the diagnostic
+    # library, make -C norm_amd diag); the product library ships the default kernels only
+    diag = "--diag" in sys.argv
+    argv = [a for a in sys.argv if a != "--diag"]
+    path = argv[1]
     shapes = DEFAULT_SHAPES
-    if len(sys.argv) > 2:
-        shapes = [tuple(int(v) for v in s.split(",")) for s in sys.argv[2:]]
+    if len(argv) > 2:
+        shapes = [tuple(int(v) for v in s.split(",")) for s in argv[2:]]
     parts = [
         "// GENERATED by tools/codegen/gen_fdec_asm.py -- do not edit by hand.",
         "// Fused RS8 erasure repair (re-encode + e x e solve in registers, one wave per block) for",
@@ -384,17 +388,18 @@ def main():
     ]
     for k, m in shapes:
         parts.append(gen_kernel(k, m))
-        if (k, m) == (64, 32):
+        if diag and (k, m) == (64, 32):
             for probe in PROBES.values():
                 parts.append(gen_kernel(k, m, probe))
     parts.append("}  // namespace")
     parts.append("")
-    parts.append("static int fdec_variant()")
-    parts.append("{")
-    parts.append("    static const int v = [] { const char* e = std::getenv(\"NFEC_FDEC_VARIANT\"); return e ? std::atoi(e) : 0; }();")
-    parts.append("    return v;")
-    parts.append("}")
-    parts.append("")
+    if diag:
+        parts.append("static int fdec_variant()")
+        parts.append("{")
+        parts.append("    static const int v = [] { const char* e = std::getenv(\"NFEC_FDEC_VARIANT\"); return e ? std::atoi(e) : 0; }();")
+        parts.append("    return v;")
+        parts.append("}")
+        parts.append("")
     parts.append("// true when launch_rs8_fused_decode runs a kernel for this shape and layout (the plan then")
     parts.append("// writes the inverse of the blocks it will take by parity row)")
     parts.append("bool rs8_fused_decode_covers(uint32_t k, uint32_t m, const FdecArgs& a)")
@@ -410,7 +415,7 @@ def main():
     parts.append("{")
     parts.append("    if (a.nblocks == 0) return NFEC_OK;")
     parts.append("    if (!rs8_fused_decode_covers(k, m, a)) return NFEC_ENOTSUP;")
-    for v, probe in PROBES.items():
+    for v, probe in (PROBES.items() if diag else ()):
         parts.append(f"    if (k == 64 && m == 32 && fdec_variant() == {v}) {{")
         parts.append(f"        hipLaunchKernelGGL(rs8_fdec_k64_m32_probe_{probe}, dim3((a.nblocks + 3) / 4), dim3(256), 0, s, a);")
         parts.append("        return hipGetLastError() == hipSuccess ? NFEC_OK : NFEC_EDEVICE;")

@@ -125,6 +125,7 @@ B_ZERO = (72, 73)
 #             drain takes ~5,000 shader clocks and it then waits ~2,500 (44 rows) / ~1,600 (20
 #             rows) at the barrier for the row waves; loads wait ~130.
 BUILDER_VARIANTS = {0: ()}
+DIAG_BUILDER_VARIANTS = {0: (), 1: ("timed",)}   # --diag (make -C norm_amd diag) only
 T3_DEFAULT = 0
 B_CUR3 = [[(68, 69), (70, 71)], [(74, 75), (76, 77)], [(78, 79), (80, 81)]]  # per group (ilp)
 # "deep" register map: three 32-register slots v0..v95, then temporaries (four slots leave the
@@ -458,7 +459,13 @@ def row_clobbers():
 
 
 def main():
-    path = sys.argv[1]
+    # --diag: build DIAG_BUILDER_VARIANTS with their NFEC_T3_VARIANT switch (the diagnostic
+    # library, make -C norm_amd diag); the product library ships the default builder only
+    global BUILDER_VARIANTS
+    diag = "--diag" in sys.argv
+    path = [a for a in sys.argv if a != "--diag"][1]
+    if diag:
+        BUILDER_VARIANTS = DIAG_BUILDER_VARIANTS
     bbs = {v: "\\n\"\n        \"".join(builder_asm(f) + (["s_mov_b32 %[oa], s96", "s_mov_b32 %[ob], s97",
                                                                  "s_mov_b32 %[oc], s98"] if "timed" in f else []))
            for v, f in BUILDER_VARIANTS.items()}
@@ -501,6 +508,18 @@ def main():
     enc_cases = "\n".join(
         f"    case {v}: hipLaunchKernelGGL(gf16_t3_encode_kernel<{v}>, dim3((uint32_t)wgs), dim3({64 * NWAVES}), 0, s, b); break;"
         for v in BUILDER_VARIANTS)
+    if diag:
+        t3_variant = f"""int t3_variant()
+{{
+    static const int v = [] {{
+        const char* e = std::getenv("NFEC_T3_VARIANT");
+        const int x = e ? std::atoi(e) : {T3_DEFAULT};
+        return x >= 0 && x < {len(BUILDER_VARIANTS)} ? x : {T3_DEFAULT};
+    }}();
+    return v;
+}}"""
+    else:
+        t3_variant = f"constexpr int t3_variant() {{ return {T3_DEFAULT}; }}"
     src = f"""// GENERATED by tools/codegen/gen_gf16_t3.py -- do not edit by hand.
 // RS16 encode: bit-sliced, three shared four-Russians tables per source column in LDS.
 #include <cstdlib>
@@ -579,15 +598,7 @@ __global__ __launch_bounds__({64 * NWAVES}, 1) void gf16_t3_multi_kernel(Gf16T3M
     else t3_body<V>(mm.e[2], wg - mm.wg_end[1]);
 }}
 
-int t3_variant()
-{{
-    static const int v = [] {{
-        const char* e = std::getenv("NFEC_T3_VARIANT");
-        const int x = e ? std::atoi(e) : {T3_DEFAULT};
-        return x >= 0 && x < {len(BUILDER_VARIANTS)} ? x : {T3_DEFAULT};
-    }}();
-    return v;
-}}
+{t3_variant}
 
 // checks the shape, fills the default output / accumulate layouts and the pass count
 int t3_prepare(const Gf16T3Args& a, Gf16T3Args& b, uint64_t& wgs)
@@ -623,6 +634,15 @@ int t3_prepare(const Gf16T3Args& a, Gf16T3Args& b, uint64_t& wgs)
 }}
 
 }}  // namespace
+
+// whether launch_gf16_t3_encode takes this shape and layout (decode asks before its plan marks
+// blocks for stage 1 by the encode kernel, so an uncovered layout keeps the gather stage)
+bool gf16_t3_covers(const Gf16T3Args& a)
+{{
+    Gf16T3Args b;
+    uint64_t wgs = 0;
+    return t3_prepare(a, b, wgs) == NFEC_OK;
+}}
 
 int launch_gf16_t3_multi(const Gf16T3Args* e, uint32_t n, hipStream_t s)
 {{

@@ -340,10 +340,13 @@ static int launch_{K}(const bs::EncArgs& a, hipStream_t s)
 
 
 def main():
-    path = sys.argv[1]
+    # the round-1 2-role encode is an A/B alternative to the q4 kernels: it is built into the
+    # diagnostic library only (make -C norm_amd diag), always with its probes
+    argv = [a for a in sys.argv if a != "--diag"]
+    path = argv[1]
     shapes = DEFAULT_SHAPES
-    if len(sys.argv) > 2:
-        shapes = [tuple(int(v) for v in s.split(",")) for s in sys.argv[2:]]
+    if len(argv) > 2:
+        shapes = [tuple(int(v) for v in s.split(",")) for s in argv[2:]]
     parts = [
         "// GENERATED by tools/codegen/gen_rs8_asm.py -- do not edit by hand.",
         "// Bit-sliced RS8 encode kernels with hand-allocated gfx950 assembly role bodies for",

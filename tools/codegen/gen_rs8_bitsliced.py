@@ -365,10 +365,14 @@ static int launch_{K}(const bs::EncArgs& a, hipStream_t s)
 
 
 def main():
-    path = sys.argv[1]
+    # --diag: also emit the (64, 32) A/B builds and probes and their NFEC_BS_VARIANT switch (the
+    # diagnostic library, make -C norm_amd diag); the product library ships the defaults only
+    diag = "--diag" in sys.argv
+    argv = [a for a in sys.argv if a != "--diag"]
+    path = argv[1]
     shapes = DEFAULT_SHAPES
-    if len(sys.argv) > 2:
-        shapes = [tuple(int(v) for v in s.split(",")) for s in sys.argv[2:]]
+    if len(argv) > 2:
+        shapes = [tuple(int(v) for v in s.split(",")) for s in argv[2:]]
     parts = [
         "// GENERATED by tools/codegen/gen_rs8_bitsliced.py -- do not edit by hand.",
         "// Bit-sliced RS8 encode / decode-stage-1 kernels specialised to the reference generator",
@@ -384,18 +388,19 @@ def main():
         parts.append(gen_kernel(k, m, DEFAULT))
         if m <= 32:
             parts.append(gen_dec_kernel(k, m, DEC_DEFAULT))
-        if (k, m) == (64, 32):
+        if diag and (k, m) == (64, 32):
             extra[(k, m)] = VARIANTS_64_32
             for v, cfg in VARIANTS_64_32.items():
                 parts.append(gen_kernel(k, m, cfg))
     parts.append("}  // namespace")
     parts.append("")
-    parts.append("static int bs_variant()")
-    parts.append("{")
-    parts.append("    static const int v = [] { const char* e = std::getenv(\"NFEC_BS_VARIANT\"); return e ? std::atoi(e) : 0; }();")
-    parts.append("    return v;")
-    parts.append("}")
-    parts.append("")
+    if diag:
+        parts.append("static int bs_variant()")
+        parts.append("{")
+        parts.append("    static const int v = [] { const char* e = std::getenv(\"NFEC_BS_VARIANT\"); return e ? std::atoi(e) : 0; }();")
+        parts.append("    return v;")
+        parts.append("}")
+        parts.append("")
     parts.append("// Returns NFEC_ENOTSUP when no specialised kernel exists for (k, m).")
     parts.append("int launch_rs8_bitsliced_encode(uint32_t k, uint32_t m, const bs::EncArgs& a, hipStream_t s)")
     parts.append("{")

@@ -522,7 +522,10 @@ static int launch_{K}(const bs::EncArgs& a, hipStream_t s)
 
 
 def main():
-    path = sys.argv[1]
+    # --diag: also emit the A/B variants and probes and their NFEC_Q4_VARIANT switch (the
+    # diagnostic library, make -C norm_amd diag); the product library ships the defaults only
+    diag = "--diag" in sys.argv
+    path = [a for a in sys.argv if a != "--diag"][1]
     parts = [
         "// GENERATED by tools/codegen/gen_rs8_q4.py -- do not edit by hand.",
         "// Bit-sliced RS8 / MDP encode: 4 role waves per workgroup share each column's transpose",
@@ -535,7 +538,7 @@ def main():
     ]
     for k, m in SHAPES:
         parts.append(gen_kernel(k, m))
-        if (k, m) == (64, 32):
+        if diag and (k, m) == (64, 32):
             for v, probe in PROBES.items():
                 parts.append(gen_kernel(k, m, probe=probe, suffix=f"_probe_{probe}"))
             for v, cfg in VARIANTS.items():
@@ -544,18 +547,19 @@ def main():
         parts.append(gen_kernel(k, m, G=mdp_matrix(k, m), prefix="mdp_q4_enc"))
     parts.append("}  // namespace")
     parts.append("")
-    parts.append("static int q4_variant()")
-    parts.append("{")
-    parts.append("    static const int v = [] { const char* e = std::getenv(\"NFEC_Q4_VARIANT\"); return e ? std::atoi(e) : 0; }();")
-    parts.append("    return v;")
-    parts.append("}")
-    parts.append("")
+    if diag:
+        parts.append("static int q4_variant()")
+        parts.append("{")
+        parts.append("    static const int v = [] { const char* e = std::getenv(\"NFEC_Q4_VARIANT\"); return e ? std::atoi(e) : 0; }();")
+        parts.append("    return v;")
+        parts.append("}")
+        parts.append("")
     parts.append("// NFEC_ENOTSUP when no kernel covers (k, m) or the batch (tails, shortened blocks)")
     parts.append("int launch_rs8_q4_encode(uint32_t k, uint32_t m, const bs::EncArgs& a, hipStream_t s)")
     parts.append("{")
-    for v, probe in PROBES.items():
+    for v, probe in (PROBES.items() if diag else ()):
         parts.append(f"    if (k == 64 && m == 32 && q4_variant() == {v}) return launch_rs8_q4_enc_probe_{probe}_k64_m32(a, s);")
-    for v in VARIANTS:
+    for v in (VARIANTS if diag else ()):
         parts.append(f"    if (k == 64 && m == 32 && q4_variant() == {v}) return launch_rs8_q4_enc_v{v}_k64_m32(a, s);")
     for k, m in SHAPES:
         parts.append(f"    if (k == {k} && m == {m}) return launch_rs8_q4_enc_k{k}_m{m}(a, s);")
