@@ -1,0 +1,127 @@
+// percall.cpp -- per-call latency of the drop-in classes (NORM's incremental sender path and
+// one-block receiver repair) next to the oracle's CPU restatement of the reference codec.
+//
+//   percall KIND K M VEC ERASURES ITERS      KIND: rs8 | rs16 | mdp
+//
+// Encode: the sender's per-segment call (normObject.cpp:2038-2052 -> NormEncoderRS8::Encode,
+// normEncoderRS8.cpp:473-483), cycling segmentId over 0..K-1 into zeroed parity.
+// Decode: one block, ERASURES source erasures (zero-filled, normObject.cpp:1579), through
+// NormDecoder::Decode (normEncoderRS8.cpp:652-757).  Prints one JSON line of microseconds per
+// call.  Built against libnfec.so (the drop-in headers, as NORM includes them) and the oracle
+// library (test infrastructure; its timing is the CPU reference per call).
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+
+#include "normEncoderMDP.h"
+#include "normEncoderRS8.h"
+#include "normEncoderRS16.h"
+
+extern "C" {
+int orc_rs8_generator(unsigned k, unsigned m, uint8_t* enc_out);
+int orc_rs16_generator(unsigned k, unsigned m, uint16_t* enc_out);
+void orc_rs8_encode(const uint8_t* enc, unsigned k, unsigned m, unsigned vec, unsigned segment_id,
+                    const uint8_t* data, uint8_t** parity);
+void orc_rs16_encode(const uint16_t* enc, unsigned k, unsigned m, unsigned vec, unsigned segment_id,
+                     const uint8_t* data, uint8_t** parity);
+int orc_rs8_decode(const uint8_t* enc, unsigned k, unsigned m, unsigned vec, uint8_t** vectors, unsigned num_data,
+                   unsigned erasure_count, const unsigned* erasure_locs);
+int orc_rs16_decode(const uint16_t* enc, unsigned k, unsigned m, unsigned vec, uint8_t** vectors,
+                    unsigned num_data, unsigned erasure_count, const unsigned* erasure_locs);
+}
+
+static double now_us()
+{
+    return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+int main(int argc, char** argv)
+{
+    if (argc < 7) {
+        std::fprintf(stderr, "usage: %s KIND K M VEC ERASURES ITERS\n", argv[0]);
+        return 2;
+    }
+    const char* kind = argv[1];
+    const unsigned k = std::atoi(argv[2]), m = std::atoi(argv[3]), vec = std::atoi(argv[4]);
+    const unsigned ne = std::atoi(argv[5]), iters = std::atoi(argv[6]);
+    const bool rs16 = !std::strcmp(kind, "rs16"), mdp = !std::strcmp(kind, "mdp");
+    NormEncoder* enc = rs16 ? (NormEncoder*)new NormEncoderRS16 : mdp ? (NormEncoder*)new NormEncoderMDP
+                                                                       : (NormEncoder*)new NormEncoderRS8;
+    NormDecoder* dec = rs16 ? (NormDecoder*)new NormDecoderRS16 : mdp ? (NormDecoder*)new NormDecoderMDP
+                                                                       : (NormDecoder*)new NormDecoderRS8;
+    if (!enc->Init(k, m, (UINT16)vec) || !dec->Init(k, m, (UINT16)vec)) return 3;
+    const unsigned n = k + m;
+    std::vector<std::vector<char>> seg(n, std::vector<char>(vec));
+    srand(7);
+    for (unsigned i = 0; i < k; ++i)
+        for (unsigned j = 0; j < vec; ++j) seg[i][j] = (char)rand();
+    std::vector<char*> list(n);
+    for (unsigned i = 0; i < n; ++i) list[i] = seg[i].data();
+
+    // ---- per-segment Encode ----
+    for (unsigned p = k; p < n; ++p) std::memset(list[p], 0, vec);
+    for (unsigned i = 0; i < 8; ++i) enc->Encode(i % k, list[i % k], list.data() + k);  // warm-up
+    for (unsigned p = k; p < n; ++p) std::memset(list[p], 0, vec);
+    double t0 = now_us();
+    for (unsigned i = 0; i < iters; ++i) enc->Encode(i % k, list[i % k], list.data() + k);
+    const double enc_us = (now_us() - t0) / iters;
+    // a clean encode of the block for the decode below
+    for (unsigned p = k; p < n; ++p) std::memset(list[p], 0, vec);
+    for (unsigned i = 0; i < k; ++i) enc->Encode(i, list[i], list.data() + k);
+
+    // ---- one-block Decode with ne source erasures ----
+    std::vector<unsigned> locs;
+    for (unsigned i = 0; i < ne; ++i) locs.push_back(i * (k / (ne ? ne : 1)));
+    std::vector<std::vector<char>> keep(ne);
+    for (unsigned i = 0; i < ne; ++i) keep[i] = seg[locs[i]];
+    double dec_us = 0;
+    int bad = 0, st = 0;
+    for (unsigned it = 0; it < iters + 2; ++it) {
+        for (unsigned i = 0; i < ne; ++i) std::memset(list[locs[i]], 0, vec);
+        const double t = now_us();
+        st = dec->Decode(list.data(), k, ne, locs.data());
+        if (it >= 2) dec_us += now_us() - t;
+        for (unsigned i = 0; i < ne; ++i) bad += std::memcmp(list[locs[i]], keep[i].data(), rs16 ? vec & ~1u : vec) != 0;
+    }
+    dec_us /= iters;
+
+    // ---- the oracle (CPU restatement of the reference codec), same calls ----
+    double orc_enc_us = -1, orc_dec_us = -1;
+    if (!mdp) {
+        std::vector<uint16_t> g16(rs16 ? (size_t)n * k : 1);
+        std::vector<uint8_t> g8(rs16 ? 1 : (size_t)n * k);
+        if (rs16) orc_rs16_generator(k, m, g16.data());
+        else orc_rs8_generator(k, m, g8.data());
+        uint8_t** ul = reinterpret_cast<uint8_t**>(list.data());
+        const unsigned oit = iters * 4;
+        t0 = now_us();
+        for (unsigned i = 0; i < oit; ++i) {
+            if (rs16) orc_rs16_encode(g16.data(), k, m, vec, i % k, ul[i % k], ul + k);
+            else orc_rs8_encode(g8.data(), k, m, vec, i % k, ul[i % k], ul + k);
+        }
+        orc_enc_us = (now_us() - t0) / oit;
+        for (unsigned p = k; p < n; ++p) std::memset(list[p], 0, vec);
+        for (unsigned i = 0; i < k; ++i) {
+            if (rs16) orc_rs16_encode(g16.data(), k, m, vec, i, ul[i], ul + k);
+            else orc_rs8_encode(g8.data(), k, m, vec, i, ul[i], ul + k);
+        }
+        orc_dec_us = 0;
+        for (unsigned it = 0; it < iters; ++it) {
+            for (unsigned i = 0; i < ne; ++i) std::memset(list[locs[i]], 0, vec);
+            const double t = now_us();
+            if (rs16) orc_rs16_decode(g16.data(), k, m, vec, ul, k, ne, locs.data());
+            else orc_rs8_decode(g8.data(), k, m, vec, ul, k, ne, locs.data());
+            orc_dec_us += now_us() - t;
+        }
+        orc_dec_us /= iters;
+    }
+    std::printf("{\"kind\": \"%s\", \"k\": %u, \"m\": %u, \"vec\": %u, \"erasures\": %u, \"iters\": %u, "
+                "\"encode_us_per_call\": %.2f, \"decode_us_per_call\": %.2f, \"decode_status\": %d, \"bad\": %d, "
+                "\"oracle_encode_us_per_call\": %.2f, \"oracle_decode_us_per_call\": %.2f}\n",
+                kind, k, m, vec, ne, iters, enc_us, dec_us, st, bad, orc_enc_us, orc_dec_us);
+    delete enc;
+    delete dec;
+    return bad ? 1 : 0;
+}
