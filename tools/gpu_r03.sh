@@ -30,8 +30,8 @@ for step in $STEPS; do
       find gpurun_out/prof_$TAG -name '*kernel_stats.csv' | head -1 | xargs -r head -8 ;;
     percall)
       : > gpurun_out/percall_$TAG.jsonl
-      for shape in "rs8 64 16 1408 16" "rs8 64 32 1408 16" "mdp 64 32 1408 16" "rs16 400 100 1408 50"; do
-        timeout -k 10 120 tools/percall/_build/percall $shape ${PERCALL_ITERS:-2000} >> gpurun_out/percall_$TAG.jsonl \
+      for shape in "rs8 64 16 1408 16 2000" "rs8 64 32 1408 16 2000" "mdp 64 32 1408 16 500" "rs16 400 100 1408 50 100"; do
+        timeout -k 10 120 tools/percall/_build/percall $shape >> gpurun_out/percall_$TAG.jsonl \
             2>> gpurun_out/percall_$TAG.err || { echo "percall $shape failed"; tail -5 gpurun_out/percall_$TAG.err; exit 7; }
       done
       cat gpurun_out/percall_$TAG.jsonl ;;
