@@ -2,11 +2,11 @@
 # Round-3 GPU session: -m gpu suite, smoke, bench, rocprofv3 kernel summary.  Each GPU step runs
 # under its own time limit and a failure ends the script (no retries).
 #   TAG=a bash tools/gpu_r03.sh            everything
-#   STEPS="tests bench" TAG=b ...          a subset (tests smoke bench prof)
+#   TAG=b bash tools/gpu_r03.sh tests bench  a subset (tests smoke bench prof percall, or tools/<x>.py)
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 TAG=${TAG:-a}
-STEPS=${STEPS:-tests smoke bench prof}
+STEPS=${*:-tests smoke bench prof}
 export TMPDIR=/tmp
 for step in $STEPS; do
   case $step in
