@@ -104,6 +104,83 @@ __global__ void zero_kernel(uint8_t* base, uint64_t block_stride, uint32_t seg_s
     }
 }
 
+// slot moves of the host-resident decode (launch_slot_move): one workgroup per block.  The
+// block's erasure list becomes an LDS bitmap; lane 0 of wave 0 finds the end of the parity
+// range the decode reads; then each wave copies every fourth selected slot, 8 bytes per lane
+// (slots are 8-byte aligned: NORM's segment pool rounds to 8, normSegment.cpp:25-27).
+constexpr uint32_t kMoveMaxSlots = 65536;
+
+__global__ __launch_bounds__(256) void slot_move_kernel(SlotMoveArgs a)
+{
+    __shared__ uint32_t erased[kMoveMaxSlots / 32];
+    __shared__ uint32_t sh_end, sh_bad, sh_es;
+    const uint32_t b = blockIdx.x;
+    const uint32_t nd = a.num_data ? a.num_data[b] : a.k;
+    const uint32_t nvec = nd + a.m;
+    const uint32_t words = (nvec + 31) / 32;
+    for (uint32_t w = threadIdx.x; w < words; w += blockDim.x) erased[w] = 0;
+    if (threadIdx.x == 0) {
+        sh_bad = (nd == 0 || nd > a.k || a.counts[b] > a.lstride) ? 1u : 0u;
+        sh_es = 0;
+    }
+    __syncthreads();
+    const uint32_t ec = min((uint32_t)a.counts[b], a.lstride);
+    const uint16_t* l = a.locs + (uint64_t)b * a.lstride;
+    for (uint32_t i = threadIdx.x; i < ec; i += blockDim.x) {
+        const uint32_t v = l[i];
+        if (v >= nvec) {
+            sh_bad = 1u;
+            continue;
+        }
+        atomicOr(&erased[v / 32], 1u << (v % 32));
+        if (v < nd) atomicAdd(&sh_es, 1u);
+    }
+    __syncthreads();
+    const bool bad = sh_bad != 0;
+    if (a.mode == SLOTS_OUT && (bad || !a.status || a.status[b] <= 0)) return;
+    if (threadIdx.x == 0) {
+        uint32_t end = nvec;
+        if (!bad && a.mode == SLOTS_RS_IN) {
+            // the first es surviving parities; fewer than es: undecodable, nothing is read,
+            // and copying every surviving slot is harmless
+            uint32_t used = 0;
+            end = nd;
+            for (uint32_t v = nd; v < nvec && used < sh_es; ++v)
+                if (!((erased[v / 32] >> (v % 32)) & 1u)) {
+                    ++used;
+                    end = v + 1;
+                }
+            if (used < sh_es) end = nvec;
+        }
+        sh_end = end;
+    }
+    __syncthreads();
+    const uint32_t end = a.mode == SLOTS_OUT ? nd : sh_end;
+    const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const uint8_t* sb = a.src + (uint64_t)b * a.src_block_stride;
+    uint8_t* db = a.dst + (uint64_t)b * a.dst_block_stride;
+    const uint32_t nw = a.bytes / 8, tail = a.bytes - nw * 8;
+    uint32_t pick = 0;  // selected slots seen so far: slot j goes to wave j % 4
+    for (uint32_t v = 0; v < end; ++v) {
+        const bool is_erased = (erased[v / 32] >> (v % 32)) & 1u;
+        bool sel;
+        if (bad) sel = a.mode != SLOTS_OUT;
+        else if (a.mode == SLOTS_OUT) sel = is_erased;                        // v < nd here
+        else if (v < nd) sel = !is_erased || (a.accumulate && a.mode == SLOTS_RS_IN);
+        else sel = !is_erased;
+        if (!sel) continue;
+        if ((pick++ & 3u) != wave) continue;
+        const uint64_t* s8 = reinterpret_cast<const uint64_t*>(sb + (uint64_t)v * a.src_seg_stride);
+        uint64_t* d8 = reinterpret_cast<uint64_t*>(db + (uint64_t)v * a.dst_seg_stride);
+        for (uint32_t i = lane; i < nw; i += 64) d8[i] = __builtin_nontemporal_load(s8 + i);
+        if (lane < tail) {
+            const uint8_t* s1 = sb + (uint64_t)v * a.src_seg_stride + nw * 8;
+            uint8_t* d1 = db + (uint64_t)v * a.dst_seg_stride + nw * 8;
+            d1[lane] = s1[lane];
+        }
+    }
+}
+
 // streaming copy for the bench's achievable-HBM figure: 16 bytes per lane, four loads in
 // flight per lane before the stores, grid-stride over 4 KiB per wave
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
@@ -170,6 +247,19 @@ int launch_erasures(uint16_t* locs, uint32_t stride, uint16_t* counts, uint32_t 
                        range, count, seed, first_block);
     hipError_t e = hipGetLastError();
     return e == hipSuccess ? NFEC_OK : hip_fail(e, "erasure launch");
+}
+
+int launch_slot_move(const SlotMoveArgs& a, hipStream_t s)
+{
+    if (a.nblocks == 0) return NFEC_OK;
+    if ((uint64_t)a.k + a.m > kMoveMaxSlots) return fail(NFEC_ENOTSUP, "slot_move: more than 65536 slots");
+    if (!a.src || !a.dst || !a.locs || !a.counts || a.lstride == 0) return fail(NFEC_EINVAL, "slot_move: bad arguments");
+    if ((reinterpret_cast<uintptr_t>(a.src) | reinterpret_cast<uintptr_t>(a.dst) | a.src_block_stride |
+         a.dst_block_stride | a.src_seg_stride | a.dst_seg_stride) & 7)
+        return fail(NFEC_EINVAL, "slot_move: slots must be 8-byte aligned");
+    hipLaunchKernelGGL(slot_move_kernel, dim3(a.nblocks), dim3(256), 0, s, a);
+    hipError_t e = hipGetLastError();
+    return e == hipSuccess ? NFEC_OK : hip_fail(e, "slot_move launch");
 }
 
 int launch_zero_slots(uint8_t* base, uint64_t block_stride, uint32_t seg_stride, uint32_t nblocks,

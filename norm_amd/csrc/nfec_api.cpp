@@ -88,6 +88,7 @@ constexpr uint32_t kHostSlots = 3;
 struct HostSlot {
     uint8_t* dev = nullptr;
     uint8_t* pin = nullptr;     // pinned staging (pageable callers, segment lists)
+    uint8_t* pin_dev = nullptr; // the same staging as the device addresses it (zero-copy kernels)
     uint16_t* dmeta = nullptr;  // num_data, erasure locs, counts
     int32_t* dstat = nullptr;
     int32_t* hstat = nullptr;   // pinned status readback
@@ -217,10 +218,13 @@ struct nfec_codec {
     DevBuf<uint8_t> w_coef1, w_coef2, w_z, w_work, w_pmap;
     DevBuf<uint32_t> w_emask, w_psel, w_gate;
     uint32_t gate_gen = 0;         // per-pass generation written into w_gate (RsPlan2Args)
-    // per-call staging (nfec_encode_segment / nfec_decode_vectors, guarded by mu)
+    // per-call staging (nfec_encode_segment / nfec_decode_vectors, guarded by mu): one device
+    // buffer and one pinned mirror of the same layout, and a stream of the codec's own, so a
+    // call is one gather, one H2D, the kernels, one D2H and one scatter
     DevBuf<uint8_t> s_block;
-    DevBuf<uint16_t> s_locs;
-    DevBuf<int32_t> s_status;
+    uint8_t* s_pin = nullptr;
+    size_t s_pin_bytes = 0;
+    hipStream_t s_stream = nullptr;
     // host-batch pipelines (slots, pinned staging, streams): one host-batch call at a time per
     // codec.  Separate from mu, which the decode kernels' workspace takes inside such a call.
     std::mutex stage_mu;
@@ -234,6 +238,11 @@ struct nfec_codec {
         stage.release();
         for (auto* b : {&d_coef, &d_gen, &d_exp, &w_coef1, &w_coef2, &w_z, &w_work, &s_block, &d_mdp_step, &w_tmvp})
             b->release();
+        if (s_stream) {
+            (void)hipStreamSynchronize(s_stream);
+            (void)hipStreamDestroy(s_stream);
+        }
+        if (s_pin) (void)hipHostFree(s_pin);
         d_tmvp_off.release();
         d_tmvp_mat.release();
         if (tmvp_done) (void)hipEventDestroy(tmvp_done);
@@ -254,8 +263,6 @@ struct nfec_codec {
         w_islots.release();
         w_oslots.release();
         w_cols.release();
-        s_locs.release();
-        s_status.release();
     }
 };
 
@@ -1314,27 +1321,72 @@ int nfec_decode(nfec_codec* codec, const nfec_block_batch* batch, const uint16_t
 }
 
 // ---- per-call NORM semantics (synchronous, host vectors) ----
+// One call = gather the caller's vectors into the codec's pinned staging (host memcpy), one
+// H2D copy, the kernels, one D2H copy of what the call writes, one synchronize, scatter.  The
+// staging layout (device and pinned alike):
+//   [0, 8)                 decode status (int32)
+//   [8, 8 + meta)          decode erasure list (m uint16), count, numData
+//   [data0, ...)           slots of round_up(vec, 8) bytes
+// Per call this is latency-bound ("per-call drop-in"): NORM's block-at-once
+// sites should use the batch calls instead.
+namespace {
+
+struct PerCall {
+    uint8_t* dev;
+    uint8_t* pin;
+    uint32_t stride, data0;
+};
+
+int per_call_stage(nfec_codec* c, uint32_t nslots, PerCall& pc)
+{
+    pc.stride = round_up(c->vec, 8);
+    pc.data0 = 8 + round_up((c->m + 2) * 2, 8);
+    const size_t bytes = pc.data0 + (size_t)nslots * pc.stride;
+    int rc = c->s_block.reserve(bytes);
+    if (rc) return rc;
+    if (c->s_pin_bytes < bytes) {
+        if (c->s_pin) (void)hipHostFree(c->s_pin);
+        c->s_pin = nullptr;
+        c->s_pin_bytes = 0;
+        if (hipHostMalloc(reinterpret_cast<void**>(&c->s_pin), bytes, hipHostMallocDefault) != hipSuccess)
+            return fail(NFEC_ENOMEM, "per-call pinned staging allocation failed");
+        c->s_pin_bytes = bytes;
+    }
+    if (!c->s_stream && hipStreamCreateWithFlags(&c->s_stream, hipStreamNonBlocking) != hipSuccess)
+        return fail(NFEC_ENOMEM, "per-call stream creation failed");
+    pc.dev = c->s_block.p;
+    pc.pin = c->s_pin;
+    return NFEC_OK;
+}
+
+}  // namespace
+
 int nfec_encode_segment(nfec_codec* c, uint32_t segment_id, const void* data, void* const* parity)
 {
     if (!c || !data || !parity) return fail(NFEC_EINVAL, "null argument");
     if (segment_id >= c->k) return fail(NFEC_EINVAL, "segmentId >= numData");
+    for (uint32_t i = 0; i < c->m; ++i)
+        if (!parity[i]) return fail(NFEC_EINVAL, "null parity vector");
     DeviceGuard g(c->device);
     std::lock_guard<std::mutex> lk(c->mu);
-    const uint32_t stride = round_up(c->vec, 8);
-    const uint32_t nslots = 2 * c->m + 1;
-    int rc = c->s_block.reserve((size_t)nslots * stride);
+    // slots: data, P0..P(m-1), and for MDP the new P(0..m-1) after them
+    const uint32_t nslots = c->kind == NFEC_MDP ? 2 * c->m + 1 : c->m + 1;
+    PerCall pc;
+    int rc = per_call_stage(c, nslots, pc);
     if (rc) return rc;
-    uint8_t* d = c->s_block.p;
-    NFEC_HIP(hipMemcpy(d, data, c->vec, hipMemcpyHostToDevice));
-    for (uint32_t i = 0; i < c->m; ++i)
-        NFEC_HIP(hipMemcpy(d + (size_t)(1 + i) * stride, parity[i], c->vec, hipMemcpyHostToDevice));
+    const hipStream_t st = c->s_stream;
+    uint8_t* hp = pc.pin + pc.data0;
+    uint8_t* d = pc.dev + pc.data0;
+    std::memcpy(hp, data, c->vec);
+    for (uint32_t i = 0; i < c->m; ++i) std::memcpy(hp + (size_t)(1 + i) * pc.stride, parity[i], c->vec);
+    NFEC_HIP(hipMemcpyAsync(d, hp, (size_t)(c->m + 1) * pc.stride, hipMemcpyHostToDevice, st));
     uint32_t out_first = 1;
     if (c->kind == NFEC_RS8 || c->kind == NFEC_MDP) {
         Gf8MatmulArgs a;
         a.in_base = d;
-        a.in_seg_stride = stride;
+        a.in_seg_stride = pc.stride;
         a.out_base = d;
-        a.out_seg_stride = stride;
+        a.out_seg_stride = pc.stride;
         a.out_slot_mode = OUT_SLOT_AFTER_INPUT;
         a.rows_const = c->m;
         a.coef_col_stride = c->cs;
@@ -1350,14 +1402,14 @@ int nfec_encode_segment(nfec_codec* c, uint32_t segment_id, const void* data, vo
             a.coef = c->d_mdp_step.p;
             out_first = c->m + 1;
         }
-        if ((rc = launch_gf8_matmul(a, false, nullptr))) return rc;
+        if ((rc = launch_gf8_matmul(a, false, st))) return rc;
     } else {
         Gf16MatmulArgs a;
         a.in_base = d;
-        a.in_seg_stride = stride;
+        a.in_seg_stride = pc.stride;
         a.cols_const = 1;
         a.out_base = d;
-        a.out_seg_stride = stride;
+        a.out_seg_stride = pc.stride;
         a.out_slot_mode = OUT_SLOT_AFTER_INPUT;
         a.rows_const = c->m;
         a.coef = reinterpret_cast<const uint16_t*>(c->d_coef.p) + (size_t)segment_id * c->cs;
@@ -1367,10 +1419,13 @@ int nfec_encode_segment(nfec_codec* c, uint32_t segment_id, const void* data, vo
         a.nblocks = 1;
         a.vec_bytes = c->vec & ~1u;
         a.accumulate = 1;
-        if ((rc = launch_gf16_matmul(a, nullptr))) return rc;
+        if ((rc = launch_gf16_matmul(a, st))) return rc;
     }
-    for (uint32_t i = 0; i < c->m; ++i)
-        NFEC_HIP(hipMemcpy(parity[i], d + (size_t)(out_first + i) * stride, c->vec, hipMemcpyDeviceToHost));
+    const size_t off = (size_t)out_first * pc.stride;
+    NFEC_HIP(hipMemcpyAsync(hp + off, d + off, (size_t)c->m * pc.stride, hipMemcpyDeviceToHost, st));
+    NFEC_HIP(hipStreamSynchronize(st));
+    // RS16 never writes an odd last byte: it came back unchanged from the upload
+    for (uint32_t i = 0; i < c->m; ++i) std::memcpy(parity[i], hp + off + (size_t)i * pc.stride, c->vec);
     return NFEC_OK;
 }
 
@@ -1381,48 +1436,50 @@ int nfec_decode_vectors(nfec_codec* c, void* const* vectors, uint32_t num_data, 
     if (num_data == 0 || num_data > c->k) return fail(NFEC_EINVAL, "numData out of range");
     if (erasure_count > c->m) return 0;
     DeviceGuard g(c->device);
-    const uint32_t stride = round_up(c->vec, 8);
     const uint32_t nslots = num_data + c->m;
-    // the whole call runs under mu: the staging block, list and status word are the codec's,
-    // and nfec_encode_segment may grow s_block concurrently otherwise
+    // the whole call runs under mu: the staging and the decode workspace are the codec's
     std::lock_guard<std::mutex> lk(c->mu);
-    int rc0 = c->s_block.reserve((size_t)(c->k + c->m) * stride + 64);
-    if (!rc0) rc0 = c->s_locs.reserve(c->m + 8);
-    if (!rc0) rc0 = c->s_status.reserve(1);
-    if (rc0) return rc0;
-    uint8_t* d = c->s_block.p;
-    uint16_t* dl = c->s_locs.p;
-    NFEC_HIP(hipMemset(d, 0, (size_t)nslots * stride));
-    for (uint32_t s = 0; s < nslots; ++s)
-        if (vectors[s]) NFEC_HIP(hipMemcpy(d + (size_t)s * stride, vectors[s], c->vec, hipMemcpyHostToDevice));
-    std::vector<uint16_t> hl(c->m + 4, 0);
+    PerCall pc;
+    int rc = per_call_stage(c, c->k + c->m, pc);
+    if (rc) return rc;
+    const hipStream_t st = c->s_stream;
+    uint16_t* hl = reinterpret_cast<uint16_t*>(pc.pin + 8);
+    std::memset(hl, 0, pc.data0 - 8);
     for (uint32_t i = 0; i < erasure_count; ++i) hl[i] = (uint16_t)erasure_locs[i];
     hl[c->m] = (uint16_t)erasure_count;
     hl[c->m + 1] = (uint16_t)num_data;
-    NFEC_HIP(hipMemcpy(dl, hl.data(), hl.size() * 2, hipMemcpyHostToDevice));
-    int32_t* dstatus = c->s_status.p;
+    // gather: present vectors as given (erased source arrives zero-filled, normObject.cpp:1579),
+    // missing (NULL) parity as zeros
+    uint8_t* hp = pc.pin + pc.data0;
+    for (uint32_t s = 0; s < nslots; ++s) {
+        if (vectors[s]) std::memcpy(hp + (size_t)s * pc.stride, vectors[s], c->vec);
+        else std::memset(hp + (size_t)s * pc.stride, 0, c->vec);
+    }
+    NFEC_HIP(hipMemcpyAsync(pc.dev + 8, pc.pin + 8, pc.data0 - 8 + (size_t)nslots * pc.stride, hipMemcpyHostToDevice, st));
+    uint16_t* dl = reinterpret_cast<uint16_t*>(pc.dev + 8);
+    int32_t* dstatus = reinterpret_cast<int32_t*>(pc.dev);
     nfec_block_batch b{};
-    b.blocks = d;
-    b.block_stride = (uint64_t)(c->k + c->m) * stride;
-    b.seg_stride = stride;
+    b.blocks = pc.dev + pc.data0;
+    b.block_stride = (uint64_t)(c->k + c->m) * pc.stride;
+    b.seg_stride = pc.stride;
     b.nblocks = 1;
     b.num_data = dl + c->m + 1;
     b.flags = c->kind == NFEC_MDP ? 0 : NFEC_ACCUMULATE;
-    int rc = decode_device(c, &b, dl, c->m, dl + c->m, dstatus, nullptr, true);
-    int32_t st = 0;
-    if (rc == NFEC_OK) {
-        hipError_t e = hipMemcpy(&st, dstatus, sizeof(st), hipMemcpyDeviceToHost);
-        if (e != hipSuccess) rc = hip_fail(e, "decode status copy");
-    }
-    if (rc) return rc;
-    if (st > 0) {
+    if ((rc = decode_device(c, &b, dl, c->m, dl + c->m, dstatus, st, true))) return rc;
+    // status and the source slots in one copy (the meta bytes between them ride along)
+    NFEC_HIP(hipMemcpyAsync(pc.pin, pc.dev, pc.data0 + (size_t)num_data * pc.stride, hipMemcpyDeviceToHost, st));
+    NFEC_HIP(hipStreamSynchronize(st));
+    int32_t status;
+    std::memcpy(&status, pc.pin, sizeof(status));
+    if (status > 0) {
+        const size_t out_bytes = c->sym == 2 ? (c->vec & ~1u) : c->vec;  // RS16: odd last byte untouched
         for (uint32_t i = 0; i < erasure_count; ++i) {
             const uint32_t s = erasure_locs[i];
             if (s >= num_data) break;  // parity is never filled (normEncoderRS8.cpp:732)
-            NFEC_HIP(hipMemcpy(vectors[s], d + (size_t)s * stride, c->vec, hipMemcpyDeviceToHost));
+            if (vectors[s]) std::memcpy(vectors[s], hp + (size_t)s * pc.stride, out_bytes);
         }
     }
-    return st;
+    return status;
 }
 
 // ---- host-resident batches: pinned staging, H2D || compute || D2H over two slots ----
@@ -1447,6 +1504,18 @@ bool host_is_pinned(const void* p)
         return false;
     }
     return at.type == hipMemoryTypeHost;
+}
+
+// the device's address of pinned host memory (kernels read and write it over PCIe), or null
+uint8_t* host_device_ptr(const void* p)
+{
+    hipPointerAttribute_t at;
+    std::memset(&at, 0, sizeof(at));
+    if (hipPointerGetAttributes(&at, p) != hipSuccess || at.type != hipMemoryTypeHost) {
+        (void)hipGetLastError();
+        return nullptr;
+    }
+    return static_cast<uint8_t*>(at.devicePointer);
 }
 
 unsigned host_copy_threads()
@@ -1524,12 +1593,14 @@ static int stage_slot(nfec_codec* c, uint32_t i, size_t dev_bytes, size_t pin_by
 {
     HostSlot& s = c->stage.slot[i];
     int rc;
+    const uint8_t* pin_before = s.pin;
     if ((rc = grow_dev(reinterpret_cast<void**>(&s.dev), s.dev_bytes, dev_bytes)) ||
         (pin_bytes && (rc = grow_pin(reinterpret_cast<void**>(&s.pin), s.pin_bytes, pin_bytes))) ||
         (rc = grow_dev(reinterpret_cast<void**>(&s.dmeta), s.meta_bytes, meta_bytes)) ||
         (rc = grow_dev(reinterpret_cast<void**>(&s.dstat), s.dstat_bytes, stat_bytes)) ||
         (rc = grow_pin(reinterpret_cast<void**>(&s.hstat), s.hstat_bytes, stat_bytes)))
         return rc;
+    if (s.pin != pin_before) s.pin_dev = s.pin ? host_device_ptr(s.pin) : nullptr;
     if (!s.st) {
         if (hipStreamCreateWithFlags(&s.st, hipStreamNonBlocking) != hipSuccess ||
             hipEventCreateWithFlags(&s.done, hipEventDisableTiming) != hipSuccess ||
@@ -1615,6 +1686,81 @@ static int decode_serialized(nfec_codec* c, const nfec_block_batch* db, const ui
     return NFEC_OK;
 }
 
+// One chunk of a host-resident decode with zero-copy slot moves (run_host_batch): metadata up
+// by DMA, the read slots gathered from host memory by a kernel (hdev: the caller's pinned
+// blocks as the device addresses them; null: a pageable caller, whose chunk is first copied
+// into the slot's pinned staging by host threads), the decode on the compute stream, the
+// repaired slots scattered back by a kernel, the status by DMA.  Ends with s.done recorded.
+static int host_decode_zc(nfec_codec* c, const nfec_block_batch* hb, HostSlot& s, uint32_t b0, uint32_t nb,
+                          uint32_t chunk, const uint16_t* locs, uint32_t lstride, const uint16_t* counts,
+                          uint8_t* hdev, uint64_t ul)
+{
+    const uint64_t hbs = hb->block_stride, ss = hb->seg_stride;
+    const uint64_t dbs = (uint64_t)(c->k + c->m) * ss;
+    uint8_t* hsrc = static_cast<uint8_t*>(hb->blocks) + (uint64_t)b0 * hbs;
+    uint16_t* dnd = hb->num_data ? s.dmeta : nullptr;
+    uint16_t* dlocs = s.dmeta + chunk;
+    uint16_t* dcnt = dlocs + (size_t)chunk * lstride;
+    hipError_t ae = hipMemcpyAsync(dlocs, locs + (uint64_t)b0 * lstride, (size_t)nb * lstride * 2,
+                                   hipMemcpyHostToDevice, s.st);
+    if (ae == hipSuccess) ae = hipMemcpyAsync(dcnt, counts + b0, (size_t)nb * 2, hipMemcpyHostToDevice, s.st);
+    if (ae == hipSuccess && dnd)
+        ae = hipMemcpyAsync(dnd, hb->num_data + b0, (size_t)nb * 2, hipMemcpyHostToDevice, s.st);
+    if (ae != hipSuccess) return hip_fail(ae, "host decode metadata upload");
+    SlotMoveArgs mv;
+    if (hdev) {
+        mv.src = hdev + (uint64_t)b0 * hbs;
+        mv.src_block_stride = hbs;
+    } else {
+        if (!s.pin_dev) return fail(NFEC_EDEVICE, "pinned staging is not device-mapped");
+        copy2d(s.pin, dbs, hsrc, hbs, ul, nb);
+        mv.src = s.pin_dev;
+        mv.src_block_stride = dbs;
+    }
+    mv.src_seg_stride = (uint32_t)ss;
+    mv.dst = s.dev;
+    mv.dst_block_stride = dbs;
+    mv.dst_seg_stride = (uint32_t)ss;
+    mv.nblocks = nb;
+    mv.k = c->k;
+    mv.m = c->m;
+    mv.bytes = c->vec;
+    mv.num_data = dnd;
+    mv.locs = dlocs;
+    mv.lstride = lstride;
+    mv.counts = dcnt;
+    mv.mode = c->kind == NFEC_MDP ? SLOTS_ALL_IN : SLOTS_RS_IN;
+    mv.accumulate = (hb->flags & NFEC_ACCUMULATE) ? 1u : 0u;
+    int rc = launch_slot_move(mv, s.st);
+    if (rc) return rc;
+    nfec_block_batch db = *hb;
+    db.blocks = s.dev;
+    db.block_stride = dbs;
+    db.nblocks = nb;
+    db.num_data = dnd;
+    rc = split_full_runs(hb->num_data ? hb->num_data + b0 : nullptr, nb, c->k, [&](uint32_t o, uint32_t n, bool nd) {
+        nfec_block_batch sb = db;
+        sb.blocks = s.dev + o * dbs;
+        sb.nblocks = n;
+        sb.num_data = nd ? dnd + o : nullptr;
+        return decode_serialized(c, &sb, dlocs + (uint64_t)o * lstride, lstride, dcnt + o, s, o);
+    });
+    if (rc) return rc;
+    // repaired source slots back (RS16 never writes an odd last byte, normEncoderRS16.cpp:733)
+    SlotMoveArgs out = mv;
+    out.src = s.dev;
+    out.src_block_stride = dbs;
+    out.dst = hdev ? hdev + (uint64_t)b0 * hbs : s.pin_dev;
+    out.dst_block_stride = hdev ? hbs : dbs;
+    out.bytes = c->sym == 2 ? (c->vec & ~1u) : c->vec;
+    out.status = s.dstat;
+    out.mode = SLOTS_OUT;
+    if ((rc = launch_slot_move(out, s.st))) return rc;
+    ae = hipMemcpyAsync(s.hstat, s.dstat, (size_t)nb * 4, hipMemcpyDeviceToHost, s.st);
+    if (ae == hipSuccess) ae = hipEventRecord(s.done, s.st);
+    return ae == hipSuccess ? NFEC_OK : hip_fail(ae, "host decode status");
+}
+
 static int run_host_batch(nfec_codec* c, const nfec_block_batch* hb, const uint16_t* locs, uint32_t lstride,
                           const uint16_t* counts, int32_t* status, bool decode)
 {
@@ -1642,6 +1788,14 @@ static int run_host_batch(nfec_codec* c, const nfec_block_batch* hb, const uint1
         dn.emplace_back(dn_off, dn_len);
     const bool pinned = host_is_pinned(hb->blocks);
     uint8_t* const hbase = static_cast<uint8_t*>(hb->blocks);
+    // Decode moves its bytes by zero-copy kernels (launch_slot_move): up only the slots the
+    // decode reads (surviving source + the first e surviving parities; an erased source slot
+    // only when accumulating), down only the repaired source slots of blocks with status > 0.
+    // Per RS8(64,32) block with 16 source erasures that is 64 segments up and 16 down, against
+    // 80 and 64 for the window DMA below, which stays for encode and for device setups where
+    // the host memory is not mapped.
+    uint8_t* const hbase_dev = pinned ? host_device_ptr(hb->blocks) : nullptr;
+    const bool zc = decode && (pinned ? hbase_dev != nullptr : true) && (uint64_t)c->k + c->m <= 65536;
     // RS decode reads the source slots and only the first e surviving parities of a block (P,
     // normEncoderRS8.cpp:680-700), so a chunk's upload stops after the last parity slot any of
     // its blocks uses: [0, k + 16) instead of the whole span for RS8(64,32) with 16 source
@@ -1722,6 +1876,13 @@ static int run_host_batch(nfec_codec* c, const nfec_block_batch* hb, const uint1
         const uint64_t ul = decode ? decode_up_len(b0, j.nb, dl) : up_len;
         j.dl = dl;
         hipError_t ae;
+        if (zc) {
+            if ((rc = host_decode_zc(c, hb, s, b0, j.nb, chunk, locs, lstride, counts, pinned ? hbase_dev : nullptr,
+                                     ul)))
+                return bail(rc);
+            j.busy = true;
+            continue;
+        }
         if (pinned) {
             ae = hipMemcpy2DAsync(s.dev + up_off, dbs, hsrc + up_off, hbs, ul, j.nb, hipMemcpyHostToDevice, s.st);
         } else {
@@ -1911,7 +2072,11 @@ static int run_host_vectors(nfec_codec* c, void* const* vecs, uint32_t nblocks, 
         j.b0 = b0;
         j.nb = std::min(chunk, nblocks - b0);
         gather(s, j);
-        hipError_t ae = hipMemcpyAsync(s.dev, s.pin, (size_t)j.nb * dbs, hipMemcpyHostToDevice, s.st);
+        // decode: the staged slots the decode reads go up by the zero-copy gather kernel (the
+        // erased source and unused parity stay on the host), the repaired ones come down by
+        // the scatter kernel (launch_slot_move, as in run_host_batch)
+        const bool zcv = decode && s.pin_dev && (uint64_t)n <= 65536;
+        hipError_t ae = zcv ? hipSuccess : hipMemcpyAsync(s.dev, s.pin, (size_t)j.nb * dbs, hipMemcpyHostToDevice, s.st);
         uint16_t* dnd = nullptr;
         if (num_data && ae == hipSuccess) {
             dnd = s.dmeta;
@@ -1932,6 +2097,26 @@ static int run_host_vectors(nfec_codec* c, void* const* vecs, uint32_t nblocks, 
             ae = hipMemcpyAsync(dl, locs + (uint64_t)b0 * lstride, (size_t)j.nb * lstride * 2, hipMemcpyHostToDevice, s.st);
             if (ae == hipSuccess) ae = hipMemcpyAsync(dc, counts + b0, (size_t)j.nb * 2, hipMemcpyHostToDevice, s.st);
             if (ae != hipSuccess) return bail(hip_fail(ae, "vector batch upload"));
+            SlotMoveArgs mv;
+            if (zcv) {
+                mv.src = s.pin_dev;
+                mv.src_block_stride = dbs;
+                mv.src_seg_stride = (uint32_t)ss;
+                mv.dst = s.dev;
+                mv.dst_block_stride = dbs;
+                mv.dst_seg_stride = (uint32_t)ss;
+                mv.nblocks = j.nb;
+                mv.k = c->k;
+                mv.m = c->m;
+                mv.bytes = c->vec;
+                mv.num_data = dnd;
+                mv.locs = dl;
+                mv.lstride = lstride;
+                mv.counts = dc;
+                mv.mode = c->kind == NFEC_MDP ? SLOTS_ALL_IN : SLOTS_RS_IN;
+                mv.accumulate = acc ? 1u : 0u;
+                if ((rc = launch_slot_move(mv, s.st))) return bail(rc);
+            }
             rc = split_full_runs(num_data ? num_data + b0 : nullptr, j.nb, c->k, [&](uint32_t o, uint32_t n, bool nd) {
                 nfec_block_batch sb = db;
                 sb.blocks = s.dev + o * dbs;
@@ -1939,6 +2124,15 @@ static int run_host_vectors(nfec_codec* c, void* const* vecs, uint32_t nblocks, 
                 sb.num_data = nd ? dnd + o : nullptr;
                 return decode_serialized(c, &sb, dl + (uint64_t)o * lstride, lstride, dc + o, s, o);
             });
+            if (!rc && zcv) {
+                SlotMoveArgs out = mv;
+                out.src = s.dev;
+                out.dst = s.pin_dev;
+                out.bytes = (uint32_t)out_bytes;
+                out.status = s.dstat;
+                out.mode = SLOTS_OUT;
+                rc = launch_slot_move(out, s.st);
+            }
             if (!rc) {
                 ae = hipMemcpyAsync(s.hstat, s.dstat, (size_t)j.nb * 4, hipMemcpyDeviceToHost, s.st);
                 if (ae != hipSuccess) return bail(hip_fail(ae, "vector batch status"));
@@ -1954,7 +2148,9 @@ static int run_host_vectors(nfec_codec* c, void* const* vecs, uint32_t nblocks, 
         }
         if (rc) return bail(rc);
         // unshortened encode: only the parity region of each block comes back
-        if (!decode && !num_data)
+        if (zcv)
+            ae = hipSuccess;
+        else if (!decode && !num_data)
             ae = hipMemcpy2DAsync(s.pin + (uint64_t)c->k * ss, dbs, s.dev + (uint64_t)c->k * ss, dbs, (uint64_t)c->m * ss,
                                   j.nb, hipMemcpyDeviceToHost, s.st);
         else

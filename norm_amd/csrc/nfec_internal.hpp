@@ -413,6 +413,38 @@ int launch_zero_slots(uint8_t* base, uint64_t block_stride, uint32_t seg_stride,
                       const uint16_t* locs, uint32_t stride, const uint16_t* counts, uint32_t vec,
                       hipStream_t s);
 
+// Host-resident decode transfers by kernels that read / write pinned host memory directly
+// (zero-copy: 55-57 GB/s either way on one MI355X, as fast as the DMA engine, but per segment,
+// tools/diag/zc_rate.hip).  Per block, the slots a mode selects from the block's erasure list:
+//   SLOTS_RS_IN:  surviving source slots [0, numData) (erased ones too when accumulating) and
+//                 the first e surviving parities -- what an RS decode reads (normEncoderRS8.cpp:
+//                 680-700: the erased source rows are replaced by the first surviving parities)
+//   SLOTS_ALL_IN: every surviving slot (MDP decode reads all of them, normEncoderMDP.cpp:346-361)
+//   SLOTS_OUT:    the erased source slots, for blocks whose status is > 0 (the only bytes a
+//                 decode writes, normEncoderRS8.cpp:732)
+// An invalid erasure list (a location >= numData + m, or more entries than the stride) moves
+// every slot [0, numData + m) in the IN modes and nothing in SLOTS_OUT.
+enum SlotMoveMode : uint32_t { SLOTS_RS_IN = 0, SLOTS_ALL_IN = 1, SLOTS_OUT = 2 };
+struct SlotMoveArgs {
+    const uint8_t* src = nullptr;
+    uint64_t src_block_stride = 0;
+    uint32_t src_seg_stride = 0;
+    uint8_t* dst = nullptr;
+    uint64_t dst_block_stride = 0;
+    uint32_t dst_seg_stride = 0;
+    uint32_t nblocks = 0;
+    uint32_t k = 0, m = 0;
+    uint32_t bytes = 0;                    // bytes per slot to move
+    const uint16_t* num_data = nullptr;    // device, per block (null: k)
+    const uint16_t* locs = nullptr;        // device [b * lstride + i]
+    uint32_t lstride = 0;
+    const uint16_t* counts = nullptr;      // device
+    const int32_t* status = nullptr;       // SLOTS_OUT: device decode status per block
+    uint32_t mode = SLOTS_RS_IN;
+    uint32_t accumulate = 0;
+};
+int launch_slot_move(const SlotMoveArgs& a, hipStream_t s);
+
 // npc segment checksums (kernels_crc.hip): CRC-32 of the first len bytes of every slot
 // (crc[b*slots + s], optional) and, optionally, whether it differs from the big-endian CRC
 // stored right after them (bad[b*slots + s]).

@@ -167,6 +167,26 @@ def test_decode_matches_oracle(orc, kind, k, m, vec, nb, es, ep):
     assert np.array_equal(dev.cpu().numpy(), ref)
 
 
+def test_rs16_decode_layout_past_the_t3_offset_bound(orc):
+    """RS16 decode stage 1 by the shared-table encode kernel needs every piece offset
+    of an 8 KiB item group below 2^31 (t3_prepare).  A padded seg_stride past that bound must
+    decode through the gather stage, not fail after the plan marked blocks for the encode path."""
+    k, m, vec, nb, es = 40, 10, 64, 3, 6
+    stride = 352 * 1024                       # 130 blocks x (50 x 352 KiB) > 2^31
+    enc, dec = _codecs(NFEC_RS16, k, m, vec)
+    host = orc.encode_blocks(NFEC_RS16, k, m, vec, orc.make_blocks(k, m, vec, nb, seg_stride=stride))
+    locs, counts = _erasures(orc, NFEC_RS16, k, m, nb, es, 0)
+    _erase(host, locs, counts)
+    ref = host.copy()
+    st_ref = orc.decode_blocks(NFEC_RS16, k, m, vec, ref, locs, counts)
+    dev = torch.from_numpy(host).cuda()
+    st = dec.decode_blocks(dev, torch.from_numpy(locs.astype(np.int16)).cuda(),
+                           torch.from_numpy(counts.astype(np.int16)).cuda())
+    torch.cuda.synchronize()
+    assert np.array_equal(st.cpu().numpy(), st_ref) and (st_ref == es).all()
+    assert np.array_equal(dev.cpu().numpy(), ref)
+
+
 @pytest.mark.parametrize("kind", [NFEC_RS8, NFEC_RS16, NFEC_MDP])
 def test_decode_shortened_blocks(orc, kind):
     k, m, vec, nb = 64, 16, 120, 6
