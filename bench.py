@@ -269,8 +269,9 @@ def main():
             "unit": "GiB/s",
             "steps": a.host_steps,
             "ms_per_step": round(he / a.host_steps * 1e3, 2),
-            "note": "same workload with the blocks in pinned host memory: nfec_encode_host + nfec_decode_host "
-                    "(H2D of the bytes read, D2H of the bytes written, overlapped with the kernels)",
+            "note": "same workload with the blocks in pinned host memory: nfec_encode_host (DMA: source up, "
+                    "parity down) + nfec_decode_host (zero-copy slot moves: the 48 surviving source and 16 "
+                    "substitute parity segments up, the 16 repaired segments down), overlapped with the kernels",
         }
         del hblocks, hnp
 

@@ -6,6 +6,8 @@
 //            identical to the oracle's full-array shuffle (orc_erasure_pattern).
 // zero:      the receiver's zero-fill of erased segments before Decode
 //            (reference src/common/normObject.cpp:1579).
+#include <algorithm>
+
 #include "nfec_internal.hpp"
 
 namespace nfec {
@@ -110,11 +112,9 @@ __global__ void zero_kernel(uint8_t* base, uint64_t block_stride, uint32_t seg_s
 // (slots are 8-byte aligned: NORM's segment pool rounds to 8, normSegment.cpp:25-27).
 constexpr uint32_t kMoveMaxSlots = 65536;
 
-__global__ __launch_bounds__(256) void slot_move_kernel(SlotMoveArgs a)
+__device__ void slot_move_block(const SlotMoveArgs& a, uint32_t b, uint32_t* erased, uint32_t& sh_end,
+                                uint32_t& sh_bad, uint32_t& sh_es)
 {
-    __shared__ uint32_t erased[kMoveMaxSlots / 32];
-    __shared__ uint32_t sh_end, sh_bad, sh_es;
-    const uint32_t b = blockIdx.x;
     const uint32_t nd = a.num_data ? a.num_data[b] : a.k;
     const uint32_t nvec = nd + a.m;
     const uint32_t words = (nvec + 31) / 32;
@@ -137,7 +137,10 @@ __global__ __launch_bounds__(256) void slot_move_kernel(SlotMoveArgs a)
     }
     __syncthreads();
     const bool bad = sh_bad != 0;
-    if (a.mode == SLOTS_OUT && (bad || !a.status || a.status[b] <= 0)) return;
+    if (a.mode == SLOTS_OUT && (bad || !a.status || a.status[b] <= 0)) {
+        __syncthreads();  // every thread leaves together: the LDS is reused by the next block
+        return;
+    }
     if (threadIdx.x == 0) {
         uint32_t end = nvec;
         if (!bad && a.mode == SLOTS_RS_IN) {
@@ -179,6 +182,20 @@ __global__ __launch_bounds__(256) void slot_move_kernel(SlotMoveArgs a)
             d1[lane] = s1[lane];
         }
     }
+    __syncthreads();
+}
+
+// A few hundred workgroups loop over the blocks: the copies are PCIe-bound (one workgroup per
+// CU already reaches the link's 55-57 GB/s, tools/diag/zc_rate.hip), and a grid of one
+// workgroup per block filled every CU with waves parked on PCIe reads, starving the decode
+// kernels of the other pipeline chunks (rs_plan2 1.5 ms instead of 0.07 per 2k blocks).
+constexpr uint32_t kMoveGrid = 256;
+
+__global__ __launch_bounds__(256) void slot_move_kernel(SlotMoveArgs a)
+{
+    __shared__ uint32_t erased[kMoveMaxSlots / 32];
+    __shared__ uint32_t sh_end, sh_bad, sh_es;
+    for (uint32_t b = blockIdx.x; b < a.nblocks; b += gridDim.x) slot_move_block(a, b, erased, sh_end, sh_bad, sh_es);
 }
 
 // streaming copy for the bench's achievable-HBM figure: 16 bytes per lane, four loads in
@@ -257,7 +274,9 @@ int launch_slot_move(const SlotMoveArgs& a, hipStream_t s)
     if ((reinterpret_cast<uintptr_t>(a.src) | reinterpret_cast<uintptr_t>(a.dst) | a.src_block_stride |
          a.dst_block_stride | a.src_seg_stride | a.dst_seg_stride) & 7)
         return fail(NFEC_EINVAL, "slot_move: slots must be 8-byte aligned");
-    hipLaunchKernelGGL(slot_move_kernel, dim3(a.nblocks), dim3(256), 0, s, a);
+    static const uint32_t g = (uint32_t)diag_knob("NFEC_MOVE_GRID", kMoveGrid, 1, 4096);
+    static const uint32_t go = (uint32_t)diag_knob("NFEC_MOVE_GRID_OUT", kMoveGrid, 1, 4096);
+    hipLaunchKernelGGL(slot_move_kernel, dim3(std::min(a.nblocks, a.mode == SLOTS_OUT ? go : g)), dim3(256), 0, s, a);
     hipError_t e = hipGetLastError();
     return e == hipSuccess ? NFEC_OK : hip_fail(e, "slot_move launch");
 }

@@ -90,11 +90,12 @@ struct HostSlot {
     uint8_t* pin = nullptr;     // pinned staging (pageable callers, segment lists)
     uint8_t* pin_dev = nullptr; // the same staging as the device addresses it (zero-copy kernels)
     uint16_t* dmeta = nullptr;  // num_data, erasure locs, counts
+    uint8_t* hmeta = nullptr;   // pinned mirror of dmeta (meta_up)
     int32_t* dstat = nullptr;
     int32_t* hstat = nullptr;   // pinned status readback
     hipStream_t st = nullptr;
     hipEvent_t done = nullptr, ev_up = nullptr, ev_cd = nullptr;
-    size_t dev_bytes = 0, pin_bytes = 0, meta_bytes = 0, dstat_bytes = 0, hstat_bytes = 0;
+    size_t dev_bytes = 0, pin_bytes = 0, meta_bytes = 0, dstat_bytes = 0, hstat_bytes = 0, hmeta_bytes = 0;
 };
 
 // host-batch pipeline resources cached per codec (run_host_batch / run_host_vectors)
@@ -108,6 +109,7 @@ struct HostStage {
             if (s.dev) (void)hipFree(s.dev);
             if (s.pin) (void)hipHostFree(s.pin);
             if (s.dmeta) (void)hipFree(s.dmeta);
+            if (s.hmeta) (void)hipHostFree(s.hmeta);
             if (s.dstat) (void)hipFree(s.dstat);
             if (s.hstat) (void)hipHostFree(s.hstat);
             if (s.done) (void)hipEventDestroy(s.done);
@@ -1597,21 +1599,43 @@ static int stage_slot(nfec_codec* c, uint32_t i, size_t dev_bytes, size_t pin_by
     if ((rc = grow_dev(reinterpret_cast<void**>(&s.dev), s.dev_bytes, dev_bytes)) ||
         (pin_bytes && (rc = grow_pin(reinterpret_cast<void**>(&s.pin), s.pin_bytes, pin_bytes))) ||
         (rc = grow_dev(reinterpret_cast<void**>(&s.dmeta), s.meta_bytes, meta_bytes)) ||
+        (rc = grow_pin(reinterpret_cast<void**>(&s.hmeta), s.hmeta_bytes, meta_bytes)) ||
         (rc = grow_dev(reinterpret_cast<void**>(&s.dstat), s.dstat_bytes, stat_bytes)) ||
         (rc = grow_pin(reinterpret_cast<void**>(&s.hstat), s.hstat_bytes, stat_bytes)))
         return rc;
     if (s.pin != pin_before) s.pin_dev = s.pin ? host_device_ptr(s.pin) : nullptr;
     if (!s.st) {
-        if (hipStreamCreateWithFlags(&s.st, hipStreamNonBlocking) != hipSuccess ||
+        const hipError_t se = hipStreamCreateWithFlags(&s.st, hipStreamNonBlocking);
+        if (se != hipSuccess ||
             hipEventCreateWithFlags(&s.done, hipEventDisableTiming) != hipSuccess ||
             hipEventCreateWithFlags(&s.ev_up, hipEventDisableTiming) != hipSuccess ||
             hipEventCreateWithFlags(&s.ev_cd, hipEventDisableTiming) != hipSuccess)
             return fail(NFEC_ENOMEM, "staging stream creation failed");
     }
-    if (!c->stage.cst && hipStreamCreateWithFlags(&c->stage.cst, hipStreamNonBlocking) != hipSuccess)
-        return fail(NFEC_ENOMEM, "staging stream creation failed");
+    if (!c->stage.cst) {
+        // the decode kernels run at the highest stream priority: the slot moves of the other
+        // chunks are PCIe-bound and must not hold the CUs the compute waits for
+        int least = 0, greatest = 0;
+        if (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess) {
+            (void)hipGetLastError();
+            greatest = 0;
+        }
+        if (hipStreamCreateWithPriority(&c->stage.cst, hipStreamNonBlocking, greatest) != hipSuccess)
+            return fail(NFEC_ENOMEM, "staging stream creation failed");
+    }
     out = &s;
     return NFEC_OK;
+}
+
+// Per-chunk metadata (numData, erasure lists, counts) goes up through the slot's pinned mirror:
+// an async copy straight from the caller's pageable arrays is staged by the runtime and
+// blocks the host thread until the link drains, which stalls the pipeline behind the other
+// chunks' transfers.  (The slot is reused only after its previous chunk completed.)
+static hipError_t meta_up(HostSlot& s, uint16_t* dev, const uint16_t* src, size_t count)
+{
+    const size_t off = reinterpret_cast<uint8_t*>(dev) - reinterpret_cast<uint8_t*>(s.dmeta);
+    std::memcpy(s.hmeta + off, src, count * 2);
+    return hipMemcpyAsync(dev, s.hmeta + off, count * 2, hipMemcpyHostToDevice, s.st);
 }
 
 // Blocks per pipeline chunk: about 256 MiB, but never fewer than the blocks it takes to fill
@@ -1701,11 +1725,10 @@ static int host_decode_zc(nfec_codec* c, const nfec_block_batch* hb, HostSlot& s
     uint16_t* dnd = hb->num_data ? s.dmeta : nullptr;
     uint16_t* dlocs = s.dmeta + chunk;
     uint16_t* dcnt = dlocs + (size_t)chunk * lstride;
-    hipError_t ae = hipMemcpyAsync(dlocs, locs + (uint64_t)b0 * lstride, (size_t)nb * lstride * 2,
-                                   hipMemcpyHostToDevice, s.st);
-    if (ae == hipSuccess) ae = hipMemcpyAsync(dcnt, counts + b0, (size_t)nb * 2, hipMemcpyHostToDevice, s.st);
+    hipError_t ae = meta_up(s, dlocs, locs + (uint64_t)b0 * lstride, (size_t)nb * lstride);
+    if (ae == hipSuccess) ae = meta_up(s, dcnt, counts + b0, nb);
     if (ae == hipSuccess && dnd)
-        ae = hipMemcpyAsync(dnd, hb->num_data + b0, (size_t)nb * 2, hipMemcpyHostToDevice, s.st);
+        ae = meta_up(s, dnd, hb->num_data + b0, nb);
     if (ae != hipSuccess) return hip_fail(ae, "host decode metadata upload");
     SlotMoveArgs mv;
     if (hdev) {
@@ -1738,7 +1761,11 @@ static int host_decode_zc(nfec_codec* c, const nfec_block_batch* hb, HostSlot& s
     db.block_stride = dbs;
     db.nblocks = nb;
     db.num_data = dnd;
-    rc = split_full_runs(hb->num_data ? hb->num_data + b0 : nullptr, nb, c->k, [&](uint32_t o, uint32_t n, bool nd) {
+    // timing probes (diagnostic library): 1 no decode, 2 no scatter, 3 neither.  Measured (16k
+    // blocks RS8(64,32), tools/host_rate.py): 33.1 / 29.3 / 29.9 / 29.1 ms; a window DMA for the
+    // download instead of the scatter: 51 ms (DMA writes and zero-copy reads share the link badly)
+    static const long probe = diag_knob("NFEC_ZC_PROBE", 0, 0, 3);
+    if (!(probe & 1)) rc = split_full_runs(hb->num_data ? hb->num_data + b0 : nullptr, nb, c->k, [&](uint32_t o, uint32_t n, bool nd) {
         nfec_block_batch sb = db;
         sb.blocks = s.dev + o * dbs;
         sb.nblocks = n;
@@ -1755,7 +1782,7 @@ static int host_decode_zc(nfec_codec* c, const nfec_block_batch* hb, HostSlot& s
     out.bytes = c->sym == 2 ? (c->vec & ~1u) : c->vec;
     out.status = s.dstat;
     out.mode = SLOTS_OUT;
-    if ((rc = launch_slot_move(out, s.st))) return rc;
+    if (!(probe & 2) && (rc = launch_slot_move(out, s.st))) return rc;
     ae = hipMemcpyAsync(s.hstat, s.dstat, (size_t)nb * 4, hipMemcpyDeviceToHost, s.st);
     if (ae == hipSuccess) ae = hipEventRecord(s.done, s.st);
     return ae == hipSuccess ? NFEC_OK : hip_fail(ae, "host decode status");
@@ -1892,7 +1919,7 @@ static int run_host_batch(nfec_codec* c, const nfec_block_batch* hb, const uint1
         uint16_t* dnd = nullptr;
         if (hb->num_data) {
             dnd = s.dmeta;
-            if (ae == hipSuccess) ae = hipMemcpyAsync(dnd, hb->num_data + b0, (size_t)j.nb * 2, hipMemcpyHostToDevice, s.st);
+            if (ae == hipSuccess) ae = meta_up(s, dnd, hb->num_data + b0, j.nb);
         }
         nfec_block_batch db = *hb;
         db.blocks = s.dev;
@@ -1903,8 +1930,8 @@ static int run_host_batch(nfec_codec* c, const nfec_block_batch* hb, const uint1
         if (decode) {
             uint16_t* dlocs = s.dmeta + chunk;
             uint16_t* dcnt = dlocs + (size_t)chunk * lstride;
-            ae = hipMemcpyAsync(dlocs, locs + (uint64_t)b0 * lstride, (size_t)j.nb * lstride * 2, hipMemcpyHostToDevice, s.st);
-            if (ae == hipSuccess) ae = hipMemcpyAsync(dcnt, counts + b0, (size_t)j.nb * 2, hipMemcpyHostToDevice, s.st);
+            ae = meta_up(s, dlocs, locs + (uint64_t)b0 * lstride, j.nb * lstride);
+            if (ae == hipSuccess) ae = meta_up(s, dcnt, counts + b0, j.nb);
             if (ae != hipSuccess) return bail(hip_fail(ae, "host batch upload"));
             rc = split_full_runs(hb->num_data ? hb->num_data + b0 : nullptr, j.nb, c->k,
                                  [&](uint32_t o, uint32_t n, bool nd) {
@@ -2080,7 +2107,7 @@ static int run_host_vectors(nfec_codec* c, void* const* vecs, uint32_t nblocks, 
         uint16_t* dnd = nullptr;
         if (num_data && ae == hipSuccess) {
             dnd = s.dmeta;
-            ae = hipMemcpyAsync(dnd, num_data + b0, (size_t)j.nb * 2, hipMemcpyHostToDevice, s.st);
+            ae = meta_up(s, dnd, num_data + b0, j.nb);
         }
         if (ae != hipSuccess) return bail(hip_fail(ae, "vector batch upload"));
         nfec_block_batch db;
@@ -2094,8 +2121,8 @@ static int run_host_vectors(nfec_codec* c, void* const* vecs, uint32_t nblocks, 
         if (decode) {
             uint16_t* dl = s.dmeta + chunk;
             uint16_t* dc = dl + (size_t)chunk * lstride;
-            ae = hipMemcpyAsync(dl, locs + (uint64_t)b0 * lstride, (size_t)j.nb * lstride * 2, hipMemcpyHostToDevice, s.st);
-            if (ae == hipSuccess) ae = hipMemcpyAsync(dc, counts + b0, (size_t)j.nb * 2, hipMemcpyHostToDevice, s.st);
+            ae = meta_up(s, dl, locs + (uint64_t)b0 * lstride, j.nb * lstride);
+            if (ae == hipSuccess) ae = meta_up(s, dc, counts + b0, j.nb);
             if (ae != hipSuccess) return bail(hip_fail(ae, "vector batch upload"));
             SlotMoveArgs mv;
             if (zcv) {

@@ -30,6 +30,25 @@ __global__ __launch_bounds__(256) void copy_k(u32x4* __restrict__ dst, const u32
     }
 }
 
+// the host decode's access pattern: per block of 96 slots x 1400 B, copy `nsel` slots (the first
+// nsel of every 3-slot group pattern when skip, else the first nsel), one wave per slot, W-byte
+// lane accesses
+template <typename T>
+__global__ __launch_bounds__(256) void seg_k(uint8_t* __restrict__ dst, const uint8_t* __restrict__ src,
+                                            uint32_t nblocks, uint32_t skip)
+{
+    const uint32_t wave = (blockIdx.x * 256 + threadIdx.x) >> 6, nwaves = (gridDim.x * 256) >> 6;
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t nw = 1400 / sizeof(T);
+    for (uint32_t job = wave; job < nblocks * 64; job += nwaves) {
+        const uint32_t b = job / 64, j = job % 64;
+        const uint32_t slot = skip ? (j / 2) * 3 + (j & 1) : j;  // 64 of 96 slots
+        const T* s8 = reinterpret_cast<const T*>(src + (uint64_t)b * 134400 + slot * 1400);
+        T* d8 = reinterpret_cast<T*>(dst + (uint64_t)b * 134400 + slot * 1400);
+        for (uint32_t i = lane; i < nw; i += 64) d8[i] = __builtin_nontemporal_load(s8 + i);
+    }
+}
+
 static float timed(hipStream_t s, hipEvent_t e0, hipEvent_t e1, void (*fn)(void*), void* arg, int reps)
 {
     fn(arg);
@@ -114,6 +133,31 @@ int main()
                    bytes / (ms * 1e-3) / 1e9);
             fflush(stdout);
         }
+    {
+        const uint32_t nb = (uint32_t)(bytes / 134400);
+        for (int skip : {0, 1})
+            for (uint32_t grid : {256u, 1024u}) {
+                for (int w : {8, 16}) {
+                    (void)hipDeviceSynchronize();
+                    (void)hipEventRecord(e0, s);
+                    for (int r = 0; r < 3; ++r) {
+                        if (w == 8)
+                            hipLaunchKernelGGL(seg_k<uint64_t>, dim3(grid), dim3(256), 0, s, (uint8_t*)d, (const uint8_t*)hdev,
+                                               nb, (uint32_t)skip);
+                        else
+                            hipLaunchKernelGGL(seg_k<u32x4>, dim3(grid), dim3(256), 0, s, (uint8_t*)d, (const uint8_t*)hdev,
+                                               nb, (uint32_t)skip);
+                    }
+                    (void)hipEventRecord(e1, s);
+                    (void)hipEventSynchronize(e1);
+                    (void)hipEventElapsedTime(&ms, e0, e1);
+                    ms /= 3;
+                    printf("{\"what\": \"seg_read\", \"skip\": %d, \"grid\": %u, \"lane_bytes\": %d, \"ms\": %.3f, \"GBps\": %.1f}\n",
+                           skip, grid, w, ms, (double)nb * 64 * 1400 / (ms * 1e-3) / 1e9);
+                    fflush(stdout);
+                }
+            }
+    }
     // both directions at once: DMA H2D on one stream while a zero-copy write kernel runs
     hipStream_t s2;
     (void)hipStreamCreateWithFlags(&s2, hipStreamNonBlocking);
