@@ -1378,6 +1378,8 @@ int nfec_encode_segment(nfec_codec* c, uint32_t segment_id, const void* data, vo
     if (rc) return rc;
     const hipStream_t st = c->s_stream;
     uint8_t* hp = pc.pin + pc.data0;
+    // (measured: a kernel reading and writing the pinned staging directly, with no copies, is
+    // slower per call -- 140 against 82 us for RS8(64,32): its loads cross PCIe one by one)
     uint8_t* d = pc.dev + pc.data0;
     std::memcpy(hp, data, c->vec);
     for (uint32_t i = 0; i < c->m; ++i) std::memcpy(hp + (size_t)(1 + i) * pc.stride, parity[i], c->vec);

@@ -195,6 +195,10 @@ def fdec_asm(k, m, probe=None, e16=False):
             for i in range(8):
                 L.append(f"v_xor_b32 v{acc_reg(t, i)}, v{w[i]}, v{acc_reg(t, i)}")
         L.append(f"Lskip{c}_%=:")
+        if probe and probe.startswith("sync") and ((c + 1) % int(probe[4:]) == 0 or c + 1 == ncol):
+            # A/B: keep the workgroup's four waves (four blocks) within N columns of each other,
+            # so they stream the same stage-1 code through the instruction cache
+            L.append("s_barrier")
         if c + NSLOT < ncol:
             L += loads(c + NSLOT)
             issued = c + NSLOT
@@ -297,7 +301,7 @@ def clobbers():
 # "dephase" / "dephase2" (first-generation second workgroups start 30 / 17 us late, so the two
 # waves of a SIMD do not ramp their loads in phase): 1.999-2.002 / 1.984-1.987 ms against
 # 1.983-1.986, no gain; generable, not built.
-PROBES = {1: "nos2", 2: "nos1", 3: "noload", 4: "gen"}
+PROBES = {1: "nos2", 2: "nos1", 3: "noload", 4: "gen", 5: "sync4", 6: "sync8", 7: "sync16", 8: "sync80"}
 
 
 def gen_kernel(k, m, probe=None):
@@ -306,7 +310,7 @@ def gen_kernel(k, m, probe=None):
     # e = 16 blocks (every output live) get a copy of stage 2 without the bound checks; m < 16
     # codes never have them
     asm = fdec_asm(k, m, None if probe in ("gen", "dephase", "dephase2") else probe,
-                   e16=(probe in (None, "prio1", "prio2", "dephase", "dephase2") and nr == 16))
+                   e16=((probe in (None, "prio1", "prio2", "dephase", "dephase2") or probe.startswith("sync")) and nr == 16))
     # A/B probe: the first generation's second workgroup per CU (dispatch order 256..511) starts
     # ~half (dephase) / ~a quarter (dephase2) of a block later, so the two waves of a SIMD stop
     # ramping their loads in phase
