@@ -301,7 +301,55 @@ def clobbers():
 # "dephase" / "dephase2" (first-generation second workgroups start 30 / 17 us late, so the two
 # waves of a SIMD do not ramp their loads in phase): 1.999-2.002 / 1.984-1.987 ms against
 # 1.983-1.986, no gain; generable, not built.
-PROBES = {1: "nos2", 2: "nos1", 3: "noload", 4: "gen", 5: "sync4", 6: "sync8", 7: "sync16", 8: "sync80"}
+PROBES = {1: "nos2", 2: "nos1", 3: "noload", 4: "gen", 5: "sync4", 6: "sync8", 7: "sync16", 8: "sync80",
+          9: "persist"}
+# "persist" (A/B): a grid of 1,024 workgroups whose waves loop over the blocks (no wave launch
+# and prologue per block, no tail of partly filled workgroups)
+
+
+def persist_kernel(K, nr, body):
+    """the fused repair as a persistent loop: each wave walks blocks w, w + 4 * gridDim.x, ...;
+    the item offsets are the same for every block (o doubles as the store offsets)"""
+    return f"""__global__ __launch_bounds__(256, 2) void {K}(FdecArgs a)
+{{
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t l4 = (a.ips + 3u) / 4u;
+    if (lane >= l4) return;  // lane-major items (lane_major 2 only in this probe)
+    uint32_t o[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {{
+        const uint32_t item = (uint32_t)q * l4 + lane;
+        o[q] = item < a.ips ? item * 8u : 0x80000000u;
+    }}
+    const uint32_t stride = gridDim.x * 4u;
+    for (uint32_t blk = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6)); blk < a.nblocks;
+         blk += stride) {{
+        const int32_t rows = (int32_t)__builtin_amdgcn_readfirstlane((uint32_t)a.rows[blk]);
+        const uint32_t ps0 = __builtin_amdgcn_readfirstlane(a.psel[2 * (uint64_t)blk]);
+        const uint32_t ps1 = __builtin_amdgcn_readfirstlane(a.psel[2 * (uint64_t)blk + 1]);
+        if (rows <= 0 || rows > 16 || ps1 != 0 || (ps0 >> {nr}) != 0u) continue;
+        const uint32_t e = (uint32_t)rows;
+        const uint32_t tmax = 32u - (uint32_t)__builtin_clz(ps0);
+        const uint64_t em = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane(a.emask[2 * (uint64_t)blk]) |
+                            ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane(a.emask[2 * (uint64_t)blk + 1]) << 32);
+        if (lane == 0) {{
+            a.rows[blk] = 0;
+            a.psel[2 * (uint64_t)blk] = 0;
+        }}
+        const uint8_t* base = a.base + (uint64_t)blk * a.block_stride;
+        const uint8_t* cp = a.coef + (uint64_t)blk * a.coef_block_stride;
+        const uint16_t* sp = a.out_slots + (uint64_t)blk * a.slots_stride;
+        asm volatile(
+            "{body}\\n"
+            :
+            : [base] "s"(base), [em] "s"(em), [cp] "s"(cp), [sp] "s"(sp), [e] "s"(e), [ss] "s"(a.seg_stride),
+              [acc] "s"(a.accumulate), [ps] "s"(ps0), [tmax] "s"(tmax),
+              [o0] "v"(o[0]), [o1] "v"(o[1]), [o2] "v"(o[2]), [o3] "v"(o[3]),
+              [s0] "v"(o[0]), [s1] "v"(o[1]), [s2] "v"(o[2]), [s3] "v"(o[3])
+            : {clobbers()});
+    }}
+}}
+"""
 
 
 def gen_kernel(k, m, probe=None):
@@ -309,8 +357,9 @@ def gen_kernel(k, m, probe=None):
     nr = min(NCOLS_PAR, m)
     # e = 16 blocks (every output live) get a copy of stage 2 without the bound checks; m < 16
     # codes never have them
-    asm = fdec_asm(k, m, None if probe in ("gen", "dephase", "dephase2") else probe,
-                   e16=((probe in (None, "prio1", "prio2", "dephase", "dephase2") or probe.startswith("sync")) and nr == 16))
+    asm = fdec_asm(k, m, None if probe in ("gen", "dephase", "dephase2", "persist") else probe,
+                   e16=((probe in (None, "prio1", "prio2", "dephase", "dephase2", "persist") or probe.startswith("sync"))
+                        and nr == 16))
     # A/B probe: the first generation's second workgroup per CU (dispatch order 256..511) starts
     # ~half (dephase) / ~a quarter (dephase2) of a block later, so the two waves of a SIMD stop
     # ramping their loads in phase
@@ -318,6 +367,8 @@ def gen_kernel(k, m, probe=None):
     dephase = (f"    if (blockIdx.x >= 256u && blockIdx.x < 512u)\n"
                f"        for (int i = 0; i < {nsleep}; ++i) __builtin_amdgcn_s_sleep(127);\n") if nsleep else ""
     body = "\\n\"\n        \"".join(asm)
+    if probe == "persist":
+        return persist_kernel(K, nr, body)
     return f"""__global__ __launch_bounds__(256, 2) void {K}(FdecArgs a)
 {{
     const uint32_t lane = threadIdx.x & 63;
@@ -421,7 +472,8 @@ def main():
     parts.append("    if (!rs8_fused_decode_covers(k, m, a)) return NFEC_ENOTSUP;")
     for v, probe in (PROBES.items() if diag else ()):
         parts.append(f"    if (k == 64 && m == 32 && fdec_variant() == {v}) {{")
-        parts.append(f"        hipLaunchKernelGGL(rs8_fdec_k64_m32_probe_{probe}, dim3((a.nblocks + 3) / 4), dim3(256), 0, s, a);")
+        grid = "std::min((a.nblocks + 3) / 4, 1024u)" if probe == "persist" else "(a.nblocks + 3) / 4"
+        parts.append(f"        hipLaunchKernelGGL(rs8_fdec_k64_m32_probe_{probe}, dim3({grid}), dim3(256), 0, s, a);")
         parts.append("        return hipGetLastError() == hipSuccess ? NFEC_OK : NFEC_EDEVICE;")
         parts.append("    }")
     for k, m in shapes:
