@@ -204,6 +204,10 @@ struct nfec_codec {
     DevBuf<uint16_t> d_lwp, d_lw;  // RS8 closed-form plan constants: log W'(x_j), log W(y_p)
     DevBuf<uint16_t> d_sel16;      // RS16 bit-sliced encode table offsets [k][m][64] (may be absent)
     DevBuf<uint16_t> d_t3off;      // RS16 shared-table encode LDS offsets [k+1][m_pad][48]
+    // RS16 products by the tower-field kernel (gen_gf16_tw.hip) instead of the shared-table one:
+    // snippet offsets [k][ceil(m/11)][48]; the Toeplitz split's three products likewise
+    bool tw = false;
+    DevBuf<uint16_t> d_twoff, d_tmvp_tw;
     // RS16 encode by the Toeplitz split (kernels_tmvp.hip): offsets of the three products, each
     // [k/2+1][m_pad(m/2)][48], then the constants' row masks (c_j [k][16], W [m][16], G0 [m][16])
     bool tmvp = false;
@@ -254,6 +258,8 @@ struct nfec_codec {
         d_lw.release();
         d_sel16.release();
         d_t3off.release();
+        d_twoff.release();
+        d_tmvp_tw.release();
         w_pmap.release();
         w_emask.release();
         w_psel.release();
@@ -296,6 +302,22 @@ bool use_gf16_t3()
 {
     static const bool v = diag_knob("NFEC_GF16_T3", 1) != 0;
     return v;
+}
+
+// RS16 products through the tower field (gen_gf16_tw.hip) instead of the shared LDS tables
+bool use_gf16_tw()
+{
+    static const bool v = [] {
+        const char* e = std::getenv("NFEC_RS16_TW");
+        return e && std::atoi(e) != 0;
+    }();
+    return v;
+}
+
+// one RS16 product (encode, decode stage 1) on the codec's product kernel
+static int launch_rs16_product(const nfec_codec* c, const Gf16T3Args& t, hipStream_t s)
+{
+    return c->tw ? launch_gf16_tw_encode(t, s) : launch_gf16_t3_encode(t, s);
 }
 
 // ---- codec construction ----
@@ -367,7 +389,14 @@ int build_codec(nfec_codec* c)
         }
         // RS16: LDS offsets of the shared-table encode (gen_gf16_t3.hip), 96 bytes per
         // coefficient (C4, k = 4096, m = 256: 104 MB)
-        if (wide && use_gf16_t3()) {
+        if (wide && use_gf16_t3() && use_gf16_tw()) {
+            const uint32_t passes = (c->m + kGf16TwRowsPerPass - 1) / kGf16TwRowsPerPass;
+            std::vector<uint16_t> off((size_t)c->k * passes * 48);
+            gf16_tw_offsets(c->gen, c->k, c->m, off.data());
+            if ((rc = c->d_twoff.reserve(off.size()))) return rc;
+            NFEC_HIP(hipMemcpy(c->d_twoff.p, off.data(), off.size() * 2, hipMemcpyHostToDevice));
+            c->tw = true;
+        } else if (wide && use_gf16_t3()) {
             const uint32_t mp = gf16_t3_rows_padded(c->m);
             std::vector<uint16_t> off((size_t)(c->k + 1) * mp * 48);
             gf16_t3_offsets(c->gen, c->k, c->m, off.data());
@@ -381,22 +410,27 @@ int build_codec(nfec_codec* c)
             const char* ev = std::getenv("NFEC_RS16_TMVP");
             const int mode = ev ? std::atoi(ev) : -1;
             const uint32_t cw = c->m / 2;
-            const bool pays = 3ull * ((cw + kGf16T3RowsPerPass - 1) / kGf16T3RowsPerPass) * (c->k / 2) <
-                              (uint64_t)((c->m + kGf16T3RowsPerPass - 1) / kGf16T3RowsPerPass) * c->k;
+            const uint32_t rpp = c->tw ? kGf16TwRowsPerPass : kGf16T3RowsPerPass;
+            const bool pays = 3ull * ((cw + rpp - 1) / rpp) * (c->k / 2) < (uint64_t)((c->m + rpp - 1) / rpp) * c->k;
             std::vector<uint32_t> prod[3];
             std::vector<uint16_t> cm, wm, gm;
             if (mode != 0 && (mode == 1 || pays) && rs16_tmvp_plan(c->k, c->m, c->gen, prod, cm, wm, gm)) {
                 const uint32_t half = c->k / 2, mp = gf16_t3_rows_padded(cw);
-                const size_t one = (size_t)(half + 1) * mp * 48;
+                const size_t one = c->tw ? (size_t)half * ((cw + kGf16TwRowsPerPass - 1) / kGf16TwRowsPerPass) * 48
+                                         : (size_t)(half + 1) * mp * 48;
                 std::vector<uint16_t> off(3 * one);
-                for (int e = 0; e < 3; ++e) gf16_t3_offsets(prod[e], half, cw, off.data() + e * one);
+                for (int e = 0; e < 3; ++e) {
+                    if (c->tw) gf16_tw_offsets(prod[e], half, cw, off.data() + e * one);
+                    else gf16_t3_offsets(prod[e], half, cw, off.data() + e * one);
+                }
                 std::vector<uint16_t> mat;
                 mat.insert(mat.end(), cm.begin(), cm.end());
                 mat.insert(mat.end(), wm.begin(), wm.end());
                 mat.insert(mat.end(), gm.begin(), gm.end());
-                if ((rc = c->d_tmvp_off.reserve(off.size()))) return rc;
+                DevBuf<uint16_t>& dst = c->tw ? c->d_tmvp_tw : c->d_tmvp_off;
+                if ((rc = dst.reserve(off.size()))) return rc;
                 if ((rc = c->d_tmvp_mat.reserve(mat.size()))) return rc;
-                NFEC_HIP(hipMemcpy(c->d_tmvp_off.p, off.data(), off.size() * 2, hipMemcpyHostToDevice));
+                NFEC_HIP(hipMemcpy(dst.p, off.data(), off.size() * 2, hipMemcpyHostToDevice));
                 NFEC_HIP(hipMemcpy(c->d_tmvp_mat.p, mat.data(), mat.size() * 2, hipMemcpyHostToDevice));
                 NFEC_HIP(hipEventCreateWithFlags(&c->tmvp_done, hipEventDisableTiming));
                 c->tmvp = true;
@@ -542,6 +576,7 @@ int rs16_tmvp_encode(nfec_codec* c, const nfec_block_batch* b, hipStream_t s)
     int rc;
     const uint32_t mp = gf16_t3_rows_padded(cw);
     const size_t one = (size_t)(half + 1) * mp * 48;
+    const size_t one_tw = (size_t)half * ((cw + kGf16TwRowsPerPass - 1) / kGf16TwRowsPerPass) * 48;
     uint32_t shift = 0;
     while ((1u << shift) < cw) ++shift;
     for (uint32_t b0 = 0; b0 < b->nblocks; b0 += sb) {
@@ -569,7 +604,8 @@ int rs16_tmvp_encode(nfec_codec* c, const nfec_block_batch* b, hipStream_t s)
             e[i].m = cw;
             e[i].m_pad = mp;
             e[i].vec_bytes = vec;
-            e[i].offs = c->d_tmvp_off.p + i * one;
+            if (c->tw) e[i].tw = c->d_tmvp_tw.p + i * one_tw;
+            else e[i].offs = c->d_tmvp_off.p + i * one;
             e[i].base = blocks;
             e[i].block_stride = b->block_stride;
             e[i].seg_stride = b->seg_stride;
@@ -604,7 +640,7 @@ int rs16_tmvp_encode(nfec_codec* c, const nfec_block_batch* b, hipStream_t s)
         if ((rc = launch_tmvp_prescale(a, s)))
             return leave(rc == NFEC_ENOTSUP && b0 == 0 ? rc : fail(rc, "tmvp prescale"));
         queued = true;
-        if ((rc = launch_gf16_t3_multi(e, 3, s)))
+        if ((rc = c->tw ? launch_gf16_tw_multi(e, 3, s) : launch_gf16_t3_multi(e, 3, s)))
             return leave(rc == NFEC_ENOTSUP && b0 == 0 ? rc : fail(rc, "tmvp products"));
         if ((rc = launch_tmvp_postscale(a, s))) return leave(fail(rc, "tmvp postscale"));
     }
@@ -668,7 +704,7 @@ int encode_device(nfec_codec* c, const nfec_block_batch* b, hipStream_t s)
             const int rc = rs16_tmvp_encode(c, b, s);
             if (rc != NFEC_ENOTSUP) return rc;
         }
-        if (c->d_t3off.p && !b->num_data) {
+        if ((c->d_t3off.p || c->tw) && !b->num_data) {
             Gf16T3Args t;
             t.base = static_cast<const uint8_t*>(b->blocks);
             t.block_stride = b->block_stride;
@@ -679,8 +715,9 @@ int encode_device(nfec_codec* c, const nfec_block_batch* b, hipStream_t s)
             t.m_pad = gf16_t3_rows_padded(c->m);
             t.vec_bytes = c->vec & ~1u;
             t.offs = c->d_t3off.p;
+            t.tw = c->d_twoff.p;
             t.accumulate = acc;
-            const int rc = launch_gf16_t3_encode(t, s);
+            const int rc = launch_rs16_product(c, t, s);
             if (rc != NFEC_ENOTSUP) return rc;
         }
         if (use_bs16 && c->d_sel16.p) {
@@ -819,6 +856,7 @@ int decode_device(nfec_codec* c, const nfec_block_batch* b, const uint16_t* locs
         t.m_pad = gf16_t3_rows_padded(c->m);
         t.vec_bytes = c->vec & ~1u;
         t.offs = c->d_t3off.p;
+        t.tw = c->d_twoff.p;
         t.accumulate = 1;
         t.out_base = c->w_z.p;
         t.out_block_stride = (uint64_t)dcs * zstride;
@@ -833,9 +871,10 @@ int decode_device(nfec_codec* c, const nfec_block_batch* b, const uint16_t* locs
     };
     // the plan marks blocks for this stage 1 only when the kernel takes the batch's layout
     // (t3_prepare's 2^31 offset bounds); otherwise every block keeps the gather stage
-    bool t3dec = c->kind == NFEC_RS16 && c->d_t3off.p && !b->num_data && !acc && (c->vec % 8) == 0;
+    bool t3dec = c->kind == NFEC_RS16 && (c->d_t3off.p || c->tw) && !b->num_data && !acc && (c->vec % 8) == 0;
     if (t3dec) {
-        t3dec = gf16_t3_covers(t3_stage1(static_cast<uint8_t*>(b->blocks), sb));
+        const Gf16T3Args t = t3_stage1(static_cast<uint8_t*>(b->blocks), sb);
+        t3dec = c->tw ? gf16_tw_covers(t) : gf16_t3_covers(t);
     }
     if (t3dec) {
         if ((rc = c->w_rows1.reserve(sb))) return rc;
@@ -1097,7 +1136,7 @@ int decode_device(nfec_codec* c, const nfec_block_batch* b, const uint16_t* locs
         if (t3dec) {
             // z_t for t below the plan's largest such e; the gather stage then overwrites the z
             // rows of the other blocks
-            rc = launch_gf16_t3_encode(t3_stage1(blocks, nb), s);
+            rc = launch_rs16_product(c, t3_stage1(blocks, nb), s);
             if (rc == NFEC_ENOTSUP) return fail(rc, "t3 decode stage 1: layout not covered");
             if (rc) return rc;
         }

@@ -214,6 +214,8 @@ struct Gf16T3Args {
     // column map: column c is read from slot ((c >> col_shift) * col_chunk + (c & col_mask) +
     // col_base) (identity by default); in_slots bounds the slots read (0: k + m)
     uint32_t col_shift = 31, col_mask = 0xFFFFFFFFu, col_chunk = 0, col_base = 0, in_slots = 0;
+    // tower-field kernel (gen_gf16_tw.hip): [k][ceil(m / 11)][48] snippet offsets (gf16_tw_offsets)
+    const uint16_t* tw = nullptr;
 };
 struct Gf16T3Multi {
     Gf16T3Args e[3];
@@ -247,6 +249,12 @@ int launch_tmvp_postscale(const Rs16TmvpArgs& a, hipStream_t s);
 int launch_gf16_t3_encode(const Gf16T3Args& a, hipStream_t s);  // NFEC_ENOTSUP: shape not covered
 bool gf16_t3_covers(const Gf16T3Args& a);  // launch_gf16_t3_encode would take it
 int launch_gf16_t3_multi(const Gf16T3Args* e, uint32_t n, hipStream_t s);  // n <= 3 independent products
+// the same products through the tower field GF((2^8)^2) (gen_gf16_tw.hip): reads a.tw, not a.offs
+constexpr uint32_t kGf16TwRowsPerPass = 11;
+int launch_gf16_tw_encode(const Gf16T3Args& a, hipStream_t s);  // NFEC_ENOTSUP: shape not covered
+bool gf16_tw_covers(const Gf16T3Args& a);
+int launch_gf16_tw_multi(const Gf16T3Args* e, uint32_t n, hipStream_t s);
+void gf16_tw_offsets(const std::vector<uint32_t>& parity_rows, uint32_t k, uint32_t m, uint16_t* out);
 void gf16_t3_offsets(const std::vector<uint32_t>& parity_rows, uint32_t k, uint32_t m, uint16_t* out);
 int launch_gf16_bs_encode(const Gf16BsEncArgs& a, hipStream_t s);  // NFEC_ENOTSUP: layout not 8-byte aligned
 void gf16_bs_selectors(const std::vector<uint32_t>& parity_rows, uint32_t k, uint32_t m, uint16_t* sel);

@@ -1,0 +1,171 @@
+"""CPU checks of the tower-field RS16 kernel's generator (tools/codegen/gen_gf16_tw.py).
+
+The kernel's arithmetic is straight-line VALU code emitted by the generator: the bit transpose,
+the XOR networks of phi and phi^-1, the four-Russians combinations and the 256 GF(2^8)
+snippets.  These tests run those exact instruction lists on a small interpreter of the few
+VALU opcodes they use (one 32-bit lane; 32 symbols in bit-sliced form) and compare the result
+with GF(2^16) products computed the reference's way (polynomial 0x1100B,
+src/common/normEncoderRS16.cpp).  What they cannot see (the jumps, M0 indexing, loads and
+stores) is covered by the GPU parity tests."""
+import os
+import random
+import re
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "tools", "codegen"))
+import gen_gf16_tw as g  # noqa: E402
+
+M32 = 0xFFFFFFFF
+
+
+class Lane:
+    """one lane of the VALU ops the generator emits; `idx` plays gpr-index mode (SRC0, DST)"""
+
+    def __init__(self):
+        self.v = [0] * 256
+        self.s = {}
+
+    def val(self, tok, idx=0):
+        tok = tok.strip()
+        if tok.startswith("v"):
+            return self.v[int(tok[1:]) + idx]
+        if tok.startswith("s"):
+            return self.s[int(tok[1:])]
+        return int(tok, 0)
+
+    def run(self, ops, idx=0):
+        for op in ops:
+            m = re.match(r"(\S+)\s+(.*)", op)
+            name, rest = m.group(1), m.group(2)
+            if name == "s_mov_b32":
+                d, x = rest.split(",")
+                self.s[int(d.strip()[1:])] = int(x, 0)
+                continue
+            tt = None
+            if "bitop3:" in rest:
+                rest, t = rest.split("bitop3:")
+                tt = int(t, 0)
+            a = [x.strip() for x in rest.split(",")]
+            d = int(a[0][1:]) + idx
+            if name == "v_mov_b32":
+                r = self.val(a[1])
+            elif name == "v_xor_b32":
+                r = self.val(a[1], idx) ^ self.val(a[2])
+            elif name == "v_lshrrev_b32":
+                r = self.val(a[2]) >> int(a[1])
+            elif name == "v_lshlrev_b32":
+                r = (self.val(a[2]) << int(a[1])) & M32
+            elif name == "v_bitop3_b32":
+                x, y, z = self.val(a[1], idx), self.val(a[2]), self.val(a[3])
+                r = 0
+                for bit in range(32):
+                    i = (((x >> bit) & 1) << 2) | (((y >> bit) & 1) << 1) | ((z >> bit) & 1)
+                    r |= ((tt >> i) & 1) << bit
+            else:
+                raise AssertionError(f"interpreter lacks {name}")
+            self.v[d] = r
+
+
+def test_tower_is_a_field_isomorphism():
+    rnd = random.Random(1)
+    # beta is a root of the reference polynomial in the tower field
+    acc, p = 0, 1
+    for i in range(17):
+        if (g.P16 >> i) & 1:
+            acc ^= p
+        p = g.tw_mul(p, g.BETA, g.LAM)
+    assert acc == 0
+    assert g.gf8_trace(g.LAM) == 1   # y^2 + y + lam irreducible over GF(2^8)
+    for _ in range(2000):
+        a, b = rnd.randrange(1 << 16), rnd.randrange(1 << 16)
+        assert g.phi(g.gf16_mul(a, b)) == g.tw_mul(g.phi(a), g.phi(b), g.LAM)
+        assert g.phi(g.phi(a), g.PHI_INV) == a
+
+
+def test_table_entries_give_the_product():
+    rnd = random.Random(2)
+    for _ in range(2000):
+        c, x = rnd.randrange(1 << 16), rnd.randrange(1 << 16)
+        e = [v >> g.SNIP_ALIGN for v in g.table_entries(c)]
+        t = g.phi(x)
+        x0, x1 = t & 255, t >> 8
+        out0 = g.gf8_mul(e[0], x0) ^ g.gf8_mul(e[2], x1)
+        out1 = g.gf8_mul(e[1], x0) ^ g.gf8_mul(e[3], x1)
+        assert out0 | (out1 << 8) == g.phi(g.gf16_mul(c, x))
+
+
+def _load(lane, syms):
+    """32 symbols of one lane as the 8 pieces land in the slot: dword j = symbols 2j, 2j+1"""
+    for j in range(16):
+        lane.v[g.V_SLOT + j] = syms[2 * j] | (syms[2 * j + 1] << 16)
+
+
+def _store(lane):
+    out = []
+    for j in range(16):
+        d = lane.v[g.V_SLOT + j]
+        out += [d & 0xFFFF, d >> 16]
+    return out
+
+
+@pytest.mark.parametrize("k,rows,seed", [(1, 1, 3), (3, 11, 4), (5, 4, 5)])
+def test_column_flow_matches_gf16_products(k, rows, seed):
+    """the kernel's per-column sequence (transpose, phi, combos, row snippets on x0, x1 ->
+    S -> W, combos, row snippets) and its epilogue (phi^-1, transpose), row targets by index"""
+    rnd = random.Random(seed)
+    data = [[rnd.randrange(1 << 16) for _ in range(32)] for _ in range(k)]
+    data[0][:4] = [0, 1, 0xFFFF, 0x8000]
+    G = [[rnd.randrange(1 << 16) for _ in range(k)] for _ in range(rows)]
+    if rows > 1:
+        G[1][0] = 0
+    lane = Lane()
+    lane.run(g.mask_init())
+    snip = {c: g.snippet_body(c) for c in range(256)}
+    for c in range(k):
+        _load(lane, data[c])
+        lane.run(g.transpose16(g.slot(), g.V_TMP))
+        lane.run(g.phi_code())
+        lane.run(g.combos_code())
+        for r in range(rows):
+            e = [v >> g.SNIP_ALIGN for v in g.table_entries(G[r][c])]
+            lane.run(snip[e[0]], idx=16 * r)
+            lane.run(snip[e[1]], idx=16 * r + 8)
+        lane.run([f"v_mov_b32 v{g.V_W + i}, v{g.V_S + i}" for i in range(8)])
+        lane.run(g.combos_code())
+        for r in range(rows):
+            e = [v >> g.SNIP_ALIGN for v in g.table_entries(G[r][c])]
+            lane.run(snip[e[2]], idx=16 * r)
+            lane.run(snip[e[3]], idx=16 * r + 8)
+    for r in range(rows):
+        lane.run(g.phi_inv_code(r))
+        lane.run(g.transpose16(g.slot(), g.V_TMP))
+        got = _store(lane)
+        want = [0] * 32
+        for c in range(k):
+            for s in range(32):
+                want[s] ^= g.gf16_mul(G[r][c], data[c][s])
+        assert got == want, f"row {r}"
+
+
+def test_snippets_fit_their_slots():
+    """each snippet (8 VALU at most + the return) fits its 128-byte slot, so the table offset
+    of coefficient c is c << 7"""
+    for c in range(256):
+        body = g.snippet_body(c)
+        assert len(body) <= 8
+        size = sum(8 if op.startswith("v_bitop3") else 4 for op in body) + 4
+        assert size <= 1 << g.SNIP_ALIGN
+
+
+def test_register_map_is_disjoint():
+    regions = [range(g.V_SLOT, g.V_SLOT + 16), range(g.V_W, g.V_W + 8), range(g.V_S, g.V_S + 8),
+               range(g.V_CA, g.V_CA + 11), range(g.V_CB, g.V_CB + 11), g.V_TMP,
+               range(g.ACC0, g.V_LAST + 1)]
+    seen = set()
+    for r in regions:
+        for v in r:
+            assert v not in seen and 10 <= v <= 255
+            seen.add(v)

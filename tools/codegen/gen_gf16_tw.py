@@ -1,0 +1,639 @@
+#!/usr/bin/env python3
+"""Generate norm_amd/csrc/gen_gf16_tw.hip: RS16 (GF(2^16)) parity products through the tower
+field GF((2^8)^2), multiplications as jumps into a 256-entry GF(2^8) snippet table.
+
+The reference multiplies symbol by symbol through log/exp tables (NormEncoderRS16::Encode,
+src/common/normEncoderRS16.cpp:472-482, addmul1 :261-298).  Any GF(2)-linear isomorphism phi
+from the reference's field (x^16 + x^12 + x^3 + x + 1, src/common/galois.h) onto the tower
+GF(2^8)[y] / (y^2 + y + lam) keeps products: phi(g * x) = phi(g) (x) phi(x).  With
+phi(g) = c0 + c1 y and phi(x) = x0 + x1 y (x0, x1 in the RS8 field 0x11d):
+
+    (g * x)_0 = c0 x0 + (lam c1) x1          (g * x)_1 = c1 x0 + (c0 + c1) x1
+
+four GF(2^8) products by constants.  Bit-sliced (plane b = bit b of 32 symbols), a product
+by a GF(2^8) constant is one v_bitop3 per output plane over the four-Russians combinations of
+the source's planes 0..3 and 4..7 -- the same 8-instruction snippets the RS8 solve jumps into
+(gen_solve_asm.py), 256 of them in 32 KiB of code.  No LDS tables, no per-symbol lookups.
+
+One wave owns one (item group, pass): 64 lanes x 32 symbols (lane L holds 8 pieces of 8 bytes,
+piece i at flat position f0 + 512 i + 8 L, so each load is a 512-byte run) and 11 parity rows
+(16 accumulator planes each, 176 VGPRs).  Per source column:
+  * 8 x buffer_load_dwordx2 (issued one column ahead), a 16 x 16 bit transpose, the XOR
+    network of phi into x0 (8 planes) and x1 (8 planes);
+  * combinations of x0; per row a jump into snippet[c0] (target out0) and snippet[c1]
+    (target out1); then x1's combinations and jumps into snippet[lam c1] and
+    snippet[c0 ^ c1].  The targets are M0-relative (gpr-index mode on SRC0 and DST), the
+    snippet byte offsets (four 16-bit values per row) come from the coefficient table by scalar
+    loads.
+After the last column each row goes back through phi^-1 and the transpose and is stored (XORed
+with the accumulate source when asked).  Workgroup = 4 independent waves (consecutive jobs:
+passes of one item group share their column reads through L2).
+
+Usage: gen_gf16_tw.py OUT.hip [--diag]
+"""
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from gen_rs8_bitsliced import bitmatrix_rows  # noqa: E402
+from gen_rs8_bitsliced import mul as gf8_mul  # noqa: E402  (the RS8 field, 0x11d)
+
+P16 = 0x1100B            # the reference's GF(2^16) polynomial
+ROWS = 11                # parity rows per wave (pass)
+NWAVES = 4               # independent waves per workgroup
+GROUP_BYTES = 4096       # flat bytes per item group: 64 lanes x 8 pieces x 8 bytes
+SNIP_ALIGN = 7           # 128-byte snippet slots
+TBL_HALF = 48            # 16-bit table entries per (column, pass): 11 rows x 4 + 4 padding
+GPR_MODE = 0x9000        # M0[15:12]: index SRC0 and DST
+
+# ---- VGPRs ----
+V_SLOT = 10              # 16: raw column (loads) -> transposed planes; epilogue: output planes
+V_W = 26                 # 8: current source planes (x0, then x1); epilogue: store offsets
+V_S = 34                 # 8: x1 while x0 is applied; epilogue: accumulate-source offsets
+V_CA = 42                # 11: combinations of planes 0..3 of the source
+V_CB = 53                # 11: combinations of planes 4..7
+V_TMP = [64, 65, 66, 67]
+ACC0 = 68                # row r: out0 planes ACC0 + 16 r + (0..7), out1 + 8
+V_LAST = ACC0 + 16 * ROWS - 1   # 243
+# (register pairs of loads and stores must start at even registers; v9 stays unused so the
+# compiler places the nine inputs in v0..v8)
+MULTI = [a for a in range(1, 16) if bin(a).count("1") >= 2]
+
+# ---- SGPRs (clobbered) ----
+S_DESC, S_ODESC, S_ADESC = 36, 40, 44
+S_MASK = 48              # 8: transpose masks (mask, mask << s) for s = 8, 4, 2, 1
+S_SNIP, S_TGT, S_RET, S_TBL = 56, 58, 60, 62
+S_C, S_COL, S_T0, S_T1, S_T2 = 64, 65, 66, 67, 68
+S_OFF = 72               # 24: the column's table entries (s_load_dwordx16 + dwordx8)
+S_LAST = 95
+MASKS = {8: 0x00FF00FF, 4: 0x0F0F0F0F, 2: 0x33333333, 1: 0x55555555}
+
+
+# ---------------------------------------------------------------- field
+def gf16_mul(a, b):
+    r = 0
+    while b:
+        if b & 1:
+            r ^= a
+        b >>= 1
+        a <<= 1
+        if a & 0x10000:
+            a ^= P16
+    return r
+
+
+def gf8_trace(v):
+    t, x = 0, v
+    for _ in range(8):
+        t ^= x
+        x = gf8_mul(x, x)
+    return t
+
+
+def tw_mul(a, b, lam):
+    """tower product: a = a0 + a1 y (a0 low byte), y^2 = y + lam"""
+    a0, a1, b0, b1 = a & 255, a >> 8, b & 255, b >> 8
+    p1 = gf8_mul(a1, b1)
+    lo = gf8_mul(a0, b0) ^ gf8_mul(lam, p1)
+    hi = gf8_mul(a1, b0) ^ gf8_mul(a0, b1) ^ p1
+    return lo | (hi << 8)
+
+
+def _vec_tables():
+    import numpy as np
+    exp = np.zeros(512, dtype=np.int64)
+    log = np.zeros(256, dtype=np.int64)
+    v = 1
+    for i in range(255):
+        exp[i] = v
+        log[v] = i
+        v <<= 1
+        if v & 0x100:
+            v ^= 0x11D
+    exp[255:510] = exp[0:255]
+    return exp, log
+
+
+def _roots(lam):
+    """the 16 roots of P16 in the tower field of lam (vectorised over all elements)"""
+    import numpy as np
+    exp, log = _vec_tables()
+
+    def m8(a, b):
+        r = exp[(log[a] + log[b]) % 255]
+        return np.where((a == 0) | (b == 0), 0, r)
+
+    x = np.arange(1 << 16, dtype=np.int64)
+    x0, x1 = x & 255, x >> 8
+    acc = np.zeros_like(x)
+    p = np.ones_like(x)            # x^i, starting at 1
+    lam_a = np.full_like(x, lam)
+    for i in range(17):
+        if (P16 >> i) & 1:
+            acc ^= p
+        p0, p1 = p & 255, p >> 8
+        q1 = m8(p1, x1)
+        lo = m8(p0, x0) ^ m8(lam_a, q1)
+        hi = m8(p1, x0) ^ m8(p0, x1) ^ q1
+        p = lo | (hi << 8)
+    return [int(v) for v in np.nonzero(acc == 0)[0] if v]
+
+
+def gf2_inverse(cols):
+    """inverse of a 16 x 16 GF(2) matrix given by its columns (ints), as columns"""
+    n = 16
+    rows = [sum(((cols[j] >> i) & 1) << j for j in range(n)) for i in range(n)]
+    aug = [(rows[i], 1 << i) for i in range(n)]
+    for c in range(n):
+        piv = next(r for r in range(c, n) if (aug[r][0] >> c) & 1)
+        aug[c], aug[piv] = aug[piv], aug[c]
+        for r in range(n):
+            if r != c and (aug[r][0] >> c) & 1:
+                aug[r] = (aug[r][0] ^ aug[c][0], aug[r][1] ^ aug[c][1])
+    inv_rows = [aug[i][1] for i in range(n)]
+    return [sum(((inv_rows[i] >> j) & 1) << i for i in range(n)) for j in range(n)]
+
+
+def row_masks(cols):
+    """output bit j of M x = parity(row_j & x)"""
+    return [sum(((cols[i] >> j) & 1) << i for i in range(16)) for j in range(16)]
+
+
+def xor_cost(masks):
+    c = 0
+    for w in (bin(r).count("1") for r in masks):
+        c += 1 if w <= 1 else (w // 2)   # mov / ceil((w - 1) / 2) three-input XORs
+    return c
+
+
+def choose_tower():
+    """the isomorphism (lam, beta) whose phi network is cheapest: phi(x^i) = beta^i"""
+    best = None
+    lams = [v for v in range(1, 256) if gf8_trace(v) == 1]
+    for lam in lams:
+        for beta in _roots(lam):
+            cols, inv = tower_basis(lam, beta)
+            key = (xor_cost(row_masks(cols)), xor_cost(row_masks(inv)), lam, beta)
+            if best is None or key < best[0]:
+                best = (key, lam, beta, cols, inv)
+    return best[1], best[2], best[3], best[4]
+
+
+def tower_basis(lam, beta):
+    """phi's columns (phi(x^i) = beta^i) and those of its inverse"""
+    cols, p = [], 1
+    for _ in range(16):
+        cols.append(p)
+        p = tw_mul(p, beta, lam)
+    return cols, gf2_inverse(cols)
+
+
+# choose_tower()'s pick (about 15 s of search; `gen_gf16_tw.py --search` reruns it):
+# 49 / 53 three-input XORs for phi / phi^-1
+LAM, BETA = 0x6B, 0xCF34
+PHI, PHI_INV = tower_basis(LAM, BETA)
+
+
+def phi(v, cols=None):
+    cols = cols or PHI
+    r = 0
+    for i in range(16):
+        if (v >> i) & 1:
+            r ^= cols[i]
+    return r
+
+
+# ---------------------------------------------------------------- instruction lists
+def mask_init():
+    out = []
+    for s, mi in ((8, 0), (4, 2), (2, 4), (1, 6)):
+        out.append(f"s_mov_b32 s{S_MASK + mi}, 0x{MASKS[s]:08x}")
+        out.append(f"s_mov_b32 s{S_MASK + mi + 1}, 0x{(MASKS[s] << s) & 0xFFFFFFFF:08x}")
+    return out
+
+
+def transpose16(x, temps):
+    """16 x 16 bit transpose of x[0..15] (both 16-bit halves at once), in place: afterwards
+    x[q] holds bit q of the 32 symbols (an involution: the epilogue applies it again)"""
+    out = []
+    ti = 0
+    for s in (8, 4, 2, 1):
+        mi = {8: 0, 4: 2, 2: 4, 1: 6}[s]
+        for d in range(16):
+            if d & s:
+                continue
+            lo, hi = x[d], x[d + s]
+            tu, tv = temps[ti % len(temps)], temps[(ti + 1) % len(temps)]
+            ti += 2
+            out.append(f"v_lshrrev_b32 v{tu}, {s}, v{lo}")
+            out.append(f"v_lshlrev_b32 v{tv}, {s}, v{hi}")
+            out.append(f"v_bitop3_b32 v{hi}, s{S_MASK + mi}, v{tu}, v{hi} bitop3:0xca")
+            out.append(f"v_bitop3_b32 v{lo}, s{S_MASK + mi + 1}, v{tv}, v{lo} bitop3:0xca")
+    return out
+
+
+def xor_network(masks, src, dst):
+    """dst[j] = XOR of src[i] over the set bits i of masks[j] (three-input XOR chains)"""
+    out = []
+    for j, mk in enumerate(masks):
+        ins = [src[i] for i in range(16) if (mk >> i) & 1]
+        d = dst[j]
+        if not ins:
+            out.append(f"v_mov_b32 v{d}, 0")
+            continue
+        if len(ins) == 1:
+            out.append(f"v_mov_b32 v{d}, v{ins[0]}")
+            continue
+        if len(ins) == 2:
+            out.append(f"v_xor_b32 v{d}, v{ins[0]}, v{ins[1]}")
+            ins = []
+        else:
+            out.append(f"v_bitop3_b32 v{d}, v{ins[0]}, v{ins[1]}, v{ins[2]} bitop3:0x96")
+            ins = ins[3:]
+        while ins:
+            if len(ins) == 1:
+                out.append(f"v_xor_b32 v{d}, v{d}, v{ins[0]}")
+                ins = []
+            else:
+                out.append(f"v_bitop3_b32 v{d}, v{d}, v{ins[0]}, v{ins[1]} bitop3:0x96")
+                ins = ins[2:]
+    return out
+
+
+def slot():
+    return [V_SLOT + i for i in range(16)]
+
+
+def w_regs():
+    return [V_W + i for i in range(8)]
+
+
+def s_regs():
+    return [V_S + i for i in range(8)]
+
+
+def phi_code():
+    """transposed planes (slot) -> x0 planes (W) and x1 planes (S)"""
+    return xor_network(row_masks(PHI), slot(), w_regs() + s_regs())
+
+
+def phi_inv_code(r):
+    """row r's accumulators (tower planes) -> polynomial-basis planes in the slot"""
+    src = [ACC0 + 16 * r + i for i in range(16)]
+    return xor_network(row_masks(PHI_INV), src, slot())
+
+
+def operand_maps():
+    """A[a] / B[b]: register of the XOR of source planes {0..3} / {4..7} selected by a / b"""
+    w = w_regs()
+    A = {1 << t: w[t] for t in range(4)}
+    B = {1 << t: w[4 + t] for t in range(4)}
+    for n, a in enumerate(MULTI):
+        A[a] = V_CA + n
+        B[a] = V_CB + n
+    return A, B
+
+
+def combos_code():
+    A, B = operand_maps()
+    out = []
+    for M in (A, B):
+        for a in sorted(MULTI, key=lambda a: bin(a).count("1")):
+            top = a.bit_length() - 1
+            out.append(f"v_xor_b32 v{M[a]}, v{M[a & ~(1 << top)]}, v{M[1 << top]}")
+    return out
+
+
+def snippet_body(c):
+    """acc plane i (register ACC0 + i + M0 index) ^= plane i of c * source (c in GF(2^8))"""
+    A, B = operand_maps()
+    out = []
+    rows = bitmatrix_rows(c) if c else [0] * 8
+    for i in range(8):
+        a, b = rows[i] & 15, rows[i] >> 4
+        d = ACC0 + i
+        if a and b:
+            out.append(f"v_bitop3_b32 v{d}, v{d}, v{A[a]}, v{B[b]} bitop3:0x96")
+        elif a:
+            out.append(f"v_xor_b32 v{d}, v{d}, v{A[a]}")
+        elif b:
+            out.append(f"v_xor_b32 v{d}, v{d}, v{B[b]}")
+    return out
+
+
+def snippets():
+    out = []
+    for c in range(256):
+        out.append(f".p2align {SNIP_ALIGN}")
+        if c == 0:
+            out.append("Lsnip0_%=:")
+        out += snippet_body(c)
+        out.append(f"s_setpc_b64 s[{S_RET}:{S_RET + 1}]")
+    return out
+
+
+def table_entries(g):
+    """the four snippet byte offsets of coefficient g: sweep 1 (source x0) out0 / out1, sweep 2
+    (source x1) out0 / out1"""
+    t = phi(g)
+    c0, c1 = t & 255, t >> 8
+    return [v << SNIP_ALIGN for v in (c0, c1, gf8_mul(LAM, c1), c0 ^ c1)]
+
+
+# ---------------------------------------------------------------- kernel body
+def col_offset():
+    """column index s[S_C] -> byte offset s[S_COL] through the column map
+    ((c >> csh) * cck + (c & cmk) * ss + cbb; identity: csh 31, cck 0, cmk ~0, cbb 0)"""
+    return [f"s_lshr_b32 s{S_T2}, s{S_C}, %[csh]", f"s_mul_i32 s{S_T2}, s{S_T2}, %[cck]",
+            f"s_and_b32 s{S_COL}, s{S_C}, %[cmk]", f"s_mul_i32 s{S_COL}, s{S_COL}, %[ss]",
+            f"s_add_u32 s{S_COL}, s{S_COL}, s{S_T2}", f"s_add_u32 s{S_COL}, s{S_COL}, %[cbb]"]
+
+
+def loads():
+    x = slot()
+    return [f"buffer_load_dwordx2 v[{x[2 * i]}:{x[2 * i + 1]}], %[o{i}], s[{S_DESC}:{S_DESC + 3}], s{S_COL} offen"
+            for i in range(8)]
+
+
+def call(h, target):
+    return [f"s_bfe_u32 s{S_T1}, s{S_OFF + h // 2}, 0x{(16 << 16) | (16 * (h % 2)):x}",
+            f"s_add_u32 s{S_TGT}, s{S_SNIP}, s{S_T1}",
+            f"s_addc_u32 s{S_TGT + 1}, s{S_SNIP + 1}, 0",
+            f"s_mov_b32 m0, 0x{GPR_MODE | target:x}",
+            f"s_swappc_b64 s[{S_RET}:{S_RET + 1}], s[{S_TGT}:{S_TGT + 1}]"]
+
+
+def sweep(n):
+    L = [f"s_mov_b32 s{S_T0}, 0", f"s_set_gpr_idx_on s{S_T0}, gpr_idx(SRC0,DST)"]
+    for r in range(ROWS):
+        if r:
+            L += [f"s_cmp_le_u32 %[nr], {r}", f"s_cbranch_scc1 Lsw{n}_%="]
+        L += call(4 * r + 2 * n, 16 * r)
+        L += call(4 * r + 2 * n + 1, 16 * r + 8)
+    L += [f"Lsw{n}_%=:", "s_set_gpr_idx_off", "s_nop 1"]
+    return L
+
+
+def body():
+    L = [f"s_mov_b64 s[{S_DESC}:{S_DESC + 1}], %[wb]", f"s_mov_b32 s{S_DESC + 2}, 0x80000000",
+         f"s_mov_b32 s{S_DESC + 3}, 0x00020000"]
+    L += mask_init()
+    L += [f"s_getpc_b64 s[{S_SNIP}:{S_SNIP + 1}]",
+          "Lpc_%=:",
+          f"s_add_u32 s{S_SNIP}, s{S_SNIP}, Lsnip0_%=-Lpc_%=",
+          f"s_addc_u32 s{S_SNIP + 1}, s{S_SNIP + 1}, 0",
+          f"s_mov_b64 s[{S_TBL}:{S_TBL + 1}], %[tw]",
+          f"s_mov_b32 s{S_C}, 0"]
+    for v in range(ACC0, V_LAST + 1):
+        L.append(f"v_mov_b32 v{v}, 0")
+    L += col_offset() + loads()
+    L.append("Lcol_%=:")
+    L += [f"s_load_dwordx16 s[{S_OFF}:{S_OFF + 15}], s[{S_TBL}:{S_TBL + 1}], 0x0",
+          f"s_load_dwordx8 s[{S_OFF + 16}:{S_OFF + 23}], s[{S_TBL}:{S_TBL + 1}], 0x40",
+          "s_waitcnt vmcnt(0)"]
+    L += transpose16(slot(), V_TMP)
+    L += phi_code()
+    # next column's loads go into the slot while this one is applied
+    L += [f"s_add_u32 s{S_C}, s{S_C}, 1", f"s_cmp_lt_u32 s{S_C}, %[k]", "s_cbranch_scc0 Lnl_%="]
+    L += col_offset() + loads()
+    L.append("Lnl_%=:")
+    L += combos_code()
+    L.append("s_waitcnt lgkmcnt(0)")
+    L += sweep(0)
+    L += [f"v_mov_b32 v{V_W + i}, v{V_S + i}" for i in range(8)]
+    L += combos_code()
+    L += sweep(1)
+    L += [f"s_add_u32 s{S_TBL}, s{S_TBL}, %[tstep]", f"s_addc_u32 s{S_TBL + 1}, s{S_TBL + 1}, 0",
+          f"s_cmp_lt_u32 s{S_C}, %[k]", "s_cbranch_scc1 Lcol_%="]
+    # ---- epilogue: phi^-1, transpose back, store (XOR the accumulate source first) ----
+    L += [f"s_mov_b64 s[{S_ODESC}:{S_ODESC + 1}], %[ob]", f"s_mov_b32 s{S_ODESC + 2}, 0x80000000",
+          f"s_mov_b32 s{S_ODESC + 3}, 0x00020000",
+          f"s_mov_b64 s[{S_ADESC}:{S_ADESC + 1}], %[ab]", f"s_mov_b32 s{S_ADESC + 2}, 0x80000000",
+          f"s_mov_b32 s{S_ADESC + 3}, 0x00020000"]
+    for i in range(8):
+        L.append(f"ds_read_b32 v{V_W + i}, %[lo] offset:{4 * i}")
+        L.append(f"ds_read_b32 v{V_S + i}, %[lo] offset:{32 + 4 * i}")
+    L.append("s_waitcnt lgkmcnt(0)")
+    x = slot()
+    tmp = [V_CA + i for i in range(16)]
+    for r in range(ROWS):
+        if r:
+            L += [f"s_cmp_le_u32 %[nr], {r}", "s_cbranch_scc1 Lepi_%="]
+        L += phi_inv_code(r)
+        L += transpose16(x, V_TMP)
+        L += [f"s_add_u32 s{S_T1}, %[oslot], {r}", f"s_mul_i32 s{S_T1}, s{S_T1}, %[oss]",
+              "s_cmp_eq_u32 %[acc], 0", f"s_cbranch_scc1 Lna{r}_%=",
+              f"s_add_u32 s{S_T2}, %[aslot], {r}", f"s_mul_i32 s{S_T2}, s{S_T2}, %[ass]"]
+        for i in range(8):
+            L.append(f"buffer_load_dwordx2 v[{tmp[2 * i]}:{tmp[2 * i + 1]}], v{V_S + i}, s[{S_ADESC}:{S_ADESC + 3}], s{S_T2} offen")
+        L.append("s_waitcnt vmcnt(0)")
+        for i in range(16):
+            L.append(f"v_xor_b32 v{x[i]}, v{x[i]}, v{tmp[i]}")
+        L.append(f"Lna{r}_%=:")
+        for i in range(8):
+            L.append(f"buffer_store_dwordx2 v[{x[2 * i]}:{x[2 * i + 1]}], v{V_W + i}, s[{S_ODESC}:{S_ODESC + 3}], s{S_T1} offen")
+    L += ["Lepi_%=:", "s_branch Lend_%="]
+    L += snippets()
+    L.append("Lend_%=:")
+    return L
+
+
+def clobbers():
+    v = [f'"v{i}"' for i in range(V_SLOT, V_LAST + 1)]
+    s = [f'"s{i}"' for i in range(S_DESC, S_LAST + 1)]
+    return ", ".join(v + s + ['"m0"', '"scc"', '"memory"'])
+
+
+def main():
+    if "--search" in sys.argv:
+        lam, beta, _, _ = choose_tower()
+        print(f"LAM, BETA = 0x{lam:02X}, 0x{beta:04X}")
+        return
+    args = [a for a in sys.argv[1:] if a != "--diag"]
+    path = args[0]
+    asm = "\\n\"\n        \"".join(body())
+    ins = ", ".join(f'[o{i}] "v"(o[{i}])' for i in range(8))
+    phi_cols = ", ".join(f"0x{c:04x}" for c in PHI)
+    src = f"""// GENERATED by tools/codegen/gen_gf16_tw.py -- do not edit by hand.
+// RS16 products through the tower field GF((2^8)^2): bit-sliced, GF(2^8) snippet jumps.
+// Isomorphism: lam = 0x{LAM:02x}, beta = 0x{BETA:04x} (phi(x^i) = beta^i).
+#include "nfec_internal.hpp"
+#include "bitslice.hpp"
+
+namespace nfec {{
+static_assert(kGf16TwRowsPerPass == {ROWS}u, "gen_gf16_tw.py and nfec_internal.hpp disagree on the rows per pass");
+namespace {{
+
+__device__ __forceinline__ void tw_body(const Gf16T3Args& a, uint32_t wg)
+{{
+    __shared__ uint32_t lds[{NWAVES} * 64 * 16];
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t job = wg * {NWAVES}u + wave;
+    const uint32_t group = job / a.passes, pass = job - group * a.passes;
+    const uint64_t total = (uint64_t)a.nblocks * a.vec_bytes;   // flat bytes over blocks
+    const uint64_t f0 = (uint64_t)group * {GROUP_BYTES}u;
+    if (f0 >= total) return;
+    // rows actually needed (decode stage 1: the largest erasure count among the blocks it
+    // serves, written by the plan); passes past them leave at once
+    uint32_t rlim = a.m;
+    if (a.rows_lim) rlim = min(rlim, __builtin_amdgcn_readfirstlane(*a.rows_lim));
+    const uint32_t row0 = pass * {ROWS}u;
+    if (row0 >= rlim) return;
+    const uint32_t nr = __builtin_amdgcn_readfirstlane(min(rlim - row0, {ROWS}u));
+    const uint32_t b0 = __builtin_amdgcn_readfirstlane((uint32_t)(f0 / a.vec_bytes));
+    const uint8_t* wb = a.base + (uint64_t)b0 * a.block_stride;
+    uint32_t o[8];
+    uint32_t* po = lds + (wave * 64u + lane) * 16u;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {{
+        const uint64_t f = f0 + (uint64_t)i * 512u + lane * 8u;
+        const uint32_t b = (uint32_t)(f / a.vec_bytes);
+        const uint32_t p = (uint32_t)(f - (uint64_t)b * a.vec_bytes);
+        const bool ok = f < total;
+        o[i] = ok ? (uint32_t)((uint64_t)(b - b0) * a.block_stride) + p : 0x80000000u;
+        po[i] = ok ? (uint32_t)((uint64_t)(b - b0) * a.out_block_stride) + p : 0x80000000u;
+        po[8 + i] = ok ? (uint32_t)((uint64_t)(b - b0) * a.acc_block_stride) + p : 0x80000000u;
+    }}
+    const uint32_t lo = bs::lds_addr(po);
+    const uint16_t* tw = a.tw + (uint64_t)pass * {TBL_HALF}u;
+    const uint32_t tstep = a.passes * {2 * TBL_HALF}u;
+    const uint8_t* ob = a.out_base + (uint64_t)b0 * a.out_block_stride;
+    const uint8_t* ab = a.acc_base + (uint64_t)b0 * a.acc_block_stride;
+    const uint32_t cck = a.col_chunk * a.seg_stride, cbb = a.col_base * a.seg_stride;
+    asm volatile(
+        "{asm}\\n"
+        :
+        : [wb] "s"(wb), [ss] "s"(a.seg_stride), [k] "s"(a.k), [tw] "s"(tw), [tstep] "s"(tstep), [nr] "s"(nr),
+          [csh] "s"(a.col_shift), [cmk] "s"(a.col_mask), [cck] "s"(cck), [cbb] "s"(cbb),
+          [acc] "s"(a.accumulate), [ob] "s"(ob), [ab] "s"(ab), [oslot] "s"(a.out_slot0 + row0),
+          [oss] "s"(a.out_seg_stride), [aslot] "s"(a.acc_slot0 + row0), [ass] "s"(a.acc_seg_stride),
+          [lo] "v"(lo), {ins}
+        : {clobbers()});
+}}
+
+__global__ __launch_bounds__({64 * NWAVES}, 2) void gf16_tw_encode_kernel(Gf16T3Args a)
+{{
+    tw_body(a, bs::wg_index(1));
+}}
+
+// several independent products in one grid (the RS16 Toeplitz split, rs16_tmvp): workgroup
+// ranges [wg_end[i-1], wg_end[i]) run problem i, so their tails share one launch
+__global__ __launch_bounds__({64 * NWAVES}, 2) void gf16_tw_multi_kernel(Gf16T3Multi mm)
+{{
+    const uint32_t wg = bs::wg_index(1);
+    if (wg < mm.wg_end[0]) tw_body(mm.e[0], wg);
+    else if (wg < mm.wg_end[1]) tw_body(mm.e[1], wg - mm.wg_end[0]);
+    else tw_body(mm.e[2], wg - mm.wg_end[1]);
+}}
+
+// checks the shape, fills the default output / accumulate layouts and the pass count
+int tw_prepare(const Gf16T3Args& a, Gf16T3Args& b, uint64_t& wgs)
+{{
+    if ((a.vec_bytes & 7u) || a.vec_bytes == 0 || !a.tw || a.num_data || a.k == 0)
+        return NFEC_ENOTSUP;
+    // every piece offset of a group ({GROUP_BYTES} bytes of flat positions) plus slot offsets within 2^31
+    const uint64_t nbg = {GROUP_BYTES}u / a.vec_bytes + 2u;
+    const uint64_t in_slots = a.in_slots ? a.in_slots : (uint64_t)a.k + a.m;
+    if (nbg * a.block_stride + in_slots * a.seg_stride >= (1ull << 31) ||
+        (a.out_base && nbg * a.out_block_stride + (uint64_t)(a.out_slot0 + a.m) * a.out_seg_stride >= (1ull << 31)) ||
+        (a.acc_base && nbg * a.acc_block_stride + (uint64_t)(a.acc_slot0 + a.m) * a.acc_seg_stride >= (1ull << 31)))
+        return NFEC_ENOTSUP;
+    const uint64_t total = (uint64_t)a.nblocks * a.vec_bytes;
+    b = a;
+    if (!b.out_base) {{  // encode: parity in place, slot k + r; accumulate against it
+        b.out_base = const_cast<uint8_t*>(a.base);
+        b.out_block_stride = a.block_stride;
+        b.out_seg_stride = a.seg_stride;
+        b.out_slot0 = a.k;
+    }}
+    if (!b.acc_base) {{
+        b.acc_base = b.out_base;
+        b.acc_block_stride = b.out_block_stride;
+        b.acc_seg_stride = b.out_seg_stride;
+        b.acc_slot0 = b.out_slot0;
+    }}
+    b.passes = (a.m + {ROWS - 1}u) / {ROWS}u;
+    const uint64_t groups = (total + {GROUP_BYTES - 1}u) / {GROUP_BYTES}u;
+    wgs = (groups * b.passes + {NWAVES - 1}u) / {NWAVES}u;
+    return wgs >= (1ull << 31) ? NFEC_ENOTSUP : NFEC_OK;
+}}
+
+const uint16_t kPhiCol[16] = {{{phi_cols}}};
+
+}}  // namespace
+
+bool gf16_tw_covers(const Gf16T3Args& a)
+{{
+    Gf16T3Args b;
+    uint64_t wgs = 0;
+    return tw_prepare(a, b, wgs) == NFEC_OK;
+}}
+
+int launch_gf16_tw_multi(const Gf16T3Args* e, uint32_t n, hipStream_t s)
+{{
+    if (n == 0 || n > 3) return NFEC_EINVAL;
+    Gf16T3Multi mm;
+    uint64_t end = 0;
+    for (uint32_t i = 0; i < 3; ++i) {{
+        uint64_t w = 0;
+        if (i < n && e[i].nblocks) {{
+            const int rc = tw_prepare(e[i], mm.e[i], w);
+            if (rc) return rc;
+        }}
+        end += w;
+        if (end >= (1ull << 31)) return NFEC_ENOTSUP;
+        mm.wg_end[i] = (uint32_t)end;
+    }}
+    if (end == 0) return NFEC_OK;
+    hipLaunchKernelGGL(gf16_tw_multi_kernel, dim3((uint32_t)end), dim3({64 * NWAVES}), 0, s, mm);
+    const hipError_t err = hipGetLastError();
+    return err == hipSuccess ? NFEC_OK : hip_fail(err, "gf16 tower multi launch");
+}}
+
+int launch_gf16_tw_encode(const Gf16T3Args& a, hipStream_t s)
+{{
+    if (a.nblocks == 0) return NFEC_OK;
+    Gf16T3Args b;
+    uint64_t wgs = 0;
+    const int rc = tw_prepare(a, b, wgs);
+    if (rc) return rc;
+    hipLaunchKernelGGL(gf16_tw_encode_kernel, dim3((uint32_t)wgs), dim3({64 * NWAVES}), 0, s, b);
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? NFEC_OK : hip_fail(e, "gf16 tower encode launch");
+}}
+
+// snippet byte offsets of the tower kernel: coefficient g = parity_rows[r][c] maps to
+// phi(g) = c0 + c1 y; entries [c][pass][4 * (r % {ROWS}) + j] = (c0, c1, lam c1, c0 ^ c1)[j] << {SNIP_ALIGN},
+// rows past m (the last pass's padding) are zero (the empty snippet)
+void gf16_tw_offsets(const std::vector<uint32_t>& parity_rows, uint32_t k, uint32_t m, uint16_t* out)
+{{
+    const Field& f8 = gf8();
+    const uint32_t passes = (m + {ROWS - 1}u) / {ROWS}u;
+    for (uint32_t c = 0; c < k; ++c)
+        for (uint32_t p = 0; p < passes; ++p) {{
+            uint16_t* o = out + ((size_t)c * passes + p) * {TBL_HALF}u;
+            for (uint32_t i = 0; i < {TBL_HALF}u; ++i) o[i] = 0;
+            for (uint32_t r = 0; r < {ROWS}u; ++r) {{
+                const uint32_t row = p * {ROWS}u + r;
+                if (row >= m) break;
+                const uint32_t g = parity_rows[(size_t)row * k + c];
+                uint32_t t = 0;
+                for (int i = 0; i < 16; ++i)
+                    if ((g >> i) & 1u) t ^= kPhiCol[i];
+                const uint32_t c0 = t & 255u, c1 = t >> 8;
+                o[4 * r + 0] = (uint16_t)(c0 << {SNIP_ALIGN});
+                o[4 * r + 1] = (uint16_t)(c1 << {SNIP_ALIGN});
+                o[4 * r + 2] = (uint16_t)(f8.mul(0x{LAM:02x}u, c1) << {SNIP_ALIGN});
+                o[4 * r + 3] = (uint16_t)((c0 ^ c1) << {SNIP_ALIGN});
+            }}
+        }}
+}}
+
+}}  // namespace nfec
+"""
+    open(path, "w").write(src)
+
+
+if __name__ == "__main__":
+    main()
