@@ -68,6 +68,14 @@ S_OFF = 72               # 24: the column's table entries (s_load_dwordx16 + dwo
 S_LAST = 95
 MASKS = {8: 0x00FF00FF, 4: 0x0F0F0F0F, 2: 0x33333333, 1: 0x55555555}
 
+# timing probes (wrong parity on purpose), diagnostic library only (--diag, NFEC_TW_VARIANT=<id>):
+#   "nosweep"  no jumps: loads, transpose, phi and combinations only
+#   "noload"   no column loads (the slot keeps stale data)
+#   "empty"    every jump goes to the empty snippet: the call overhead without its VALU
+VARIANTS = {0: ()}
+DIAG_VARIANTS = {0: (), 1: ("nosweep",), 2: ("noload",), 3: ("empty",)}
+FLAGS = ()
+
 
 # ---------------------------------------------------------------- field
 def gf16_mul(a, b):
@@ -351,26 +359,58 @@ def col_offset():
 
 def loads():
     x = slot()
+    if "noload" in FLAGS:
+        return []
     return [f"buffer_load_dwordx2 v[{x[2 * i]}:{x[2 * i + 1]}], %[o{i}], s[{S_DESC}:{S_DESC + 3}], s{S_COL} offen"
             for i in range(8)]
 
 
 def call(h, target):
-    return [f"s_bfe_u32 s{S_T1}, s{S_OFF + h // 2}, 0x{(16 << 16) | (16 * (h % 2)):x}",
+    if "empty" in FLAGS:
+        first = f"s_mov_b32 s{S_T1}, 0"
+    else:
+        first = f"s_bfe_u32 s{S_T1}, s{S_OFF + h // 2}, 0x{(16 << 16) | (16 * (h % 2)):x}"
+    return [first,
             f"s_add_u32 s{S_TGT}, s{S_SNIP}, s{S_T1}",
             f"s_addc_u32 s{S_TGT + 1}, s{S_SNIP + 1}, 0",
             f"s_mov_b32 m0, 0x{GPR_MODE | target:x}",
             f"s_swappc_b64 s[{S_RET}:{S_RET + 1}], s[{S_TGT}:{S_TGT + 1}]"]
 
 
-def sweep(n):
+def sweep(n, x, full):
+    """the rows' jumps for source n (0: x0, 1: x1); full: the pass has all ROWS rows, so the
+    per-row bound checks are left out"""
+    if "nosweep" in FLAGS:
+        return []
     L = [f"s_mov_b32 s{S_T0}, 0", f"s_set_gpr_idx_on s{S_T0}, gpr_idx(SRC0,DST)"]
     for r in range(ROWS):
-        if r:
-            L += [f"s_cmp_le_u32 %[nr], {r}", f"s_cbranch_scc1 Lsw{n}_%="]
+        if r and not full:
+            L += [f"s_cmp_le_u32 %[nr], {r}", f"s_cbranch_scc1 Lsw{n}{x}_%="]
         L += call(4 * r + 2 * n, 16 * r)
         L += call(4 * r + 2 * n + 1, 16 * r + 8)
-    L += [f"Lsw{n}_%=:", "s_set_gpr_idx_off", "s_nop 1"]
+    L += [f"Lsw{n}{x}_%=:", "s_set_gpr_idx_off", "s_nop 1"]
+    return L
+
+
+def column_loop(x, full):
+    L = [f"Lcol{x}_%=:",
+         f"s_load_dwordx16 s[{S_OFF}:{S_OFF + 15}], s[{S_TBL}:{S_TBL + 1}], 0x0",
+         f"s_load_dwordx8 s[{S_OFF + 16}:{S_OFF + 23}], s[{S_TBL}:{S_TBL + 1}], 0x40",
+         "s_waitcnt vmcnt(0)"]
+    L += transpose16(slot(), V_TMP)
+    L += phi_code()
+    # next column's loads go into the slot while this one is applied
+    L += [f"s_add_u32 s{S_C}, s{S_C}, 1", f"s_cmp_lt_u32 s{S_C}, %[k]", f"s_cbranch_scc0 Lnl{x}_%="]
+    L += col_offset() + loads()
+    L.append(f"Lnl{x}_%=:")
+    L += combos_code()
+    L.append("s_waitcnt lgkmcnt(0)")
+    L += sweep(0, x, full)
+    L += [f"v_mov_b32 v{V_W + i}, v{V_S + i}" for i in range(8)]
+    L += combos_code()
+    L += sweep(1, x, full)
+    L += [f"s_add_u32 s{S_TBL}, s{S_TBL}, %[tstep]", f"s_addc_u32 s{S_TBL + 1}, s{S_TBL + 1}, 0",
+          f"s_cmp_lt_u32 s{S_C}, %[k]", f"s_cbranch_scc1 Lcol{x}_%="]
     return L
 
 
@@ -387,24 +427,11 @@ def body():
     for v in range(ACC0, V_LAST + 1):
         L.append(f"v_mov_b32 v{v}, 0")
     L += col_offset() + loads()
-    L.append("Lcol_%=:")
-    L += [f"s_load_dwordx16 s[{S_OFF}:{S_OFF + 15}], s[{S_TBL}:{S_TBL + 1}], 0x0",
-          f"s_load_dwordx8 s[{S_OFF + 16}:{S_OFF + 23}], s[{S_TBL}:{S_TBL + 1}], 0x40",
-          "s_waitcnt vmcnt(0)"]
-    L += transpose16(slot(), V_TMP)
-    L += phi_code()
-    # next column's loads go into the slot while this one is applied
-    L += [f"s_add_u32 s{S_C}, s{S_C}, 1", f"s_cmp_lt_u32 s{S_C}, %[k]", "s_cbranch_scc0 Lnl_%="]
-    L += col_offset() + loads()
-    L.append("Lnl_%=:")
-    L += combos_code()
-    L.append("s_waitcnt lgkmcnt(0)")
-    L += sweep(0)
-    L += [f"v_mov_b32 v{V_W + i}, v{V_S + i}" for i in range(8)]
-    L += combos_code()
-    L += sweep(1)
-    L += [f"s_add_u32 s{S_TBL}, s{S_TBL}, %[tstep]", f"s_addc_u32 s{S_TBL + 1}, s{S_TBL + 1}, 0",
-          f"s_cmp_lt_u32 s{S_C}, %[k]", "s_cbranch_scc1 Lcol_%="]
+    L += [f"s_cmp_eq_u32 %[nr], {ROWS}", "s_cbranch_scc0 Lcolg_%="]
+    L += column_loop("f", True)
+    L.append("s_branch Lepi0_%=")
+    L += column_loop("g", False)
+    L.append("Lepi0_%=:")
     # ---- epilogue: phi^-1, transpose back, store (XOR the accumulate source first) ----
     L += [f"s_mov_b64 s[{S_ODESC}:{S_ODESC + 1}], %[ob]", f"s_mov_b32 s{S_ODESC + 2}, 0x80000000",
           f"s_mov_b32 s{S_ODESC + 3}, 0x00020000",
@@ -449,14 +476,53 @@ def main():
         lam, beta, _, _ = choose_tower()
         print(f"LAM, BETA = 0x{lam:02X}, 0x{beta:04X}")
         return
+    global FLAGS
+    diag = "--diag" in sys.argv
     args = [a for a in sys.argv[1:] if a != "--diag"]
     path = args[0]
-    asm = "\\n\"\n        \"".join(body())
+    variants = DIAG_VARIANTS if diag else VARIANTS
+    asms = {}
+    for v, f in variants.items():
+        FLAGS = f
+        asms[v] = "\\n\"\n        \"".join(body())
+    FLAGS = ()
     ins = ", ".join(f'[o{i}] "v"(o[{i}])' for i in range(8))
+    blocks = []
+    for v in variants:
+        kw = "if constexpr" if v == 0 else "else if constexpr"
+        blocks.append(f"""    {kw} (V == {v}) {{
+        asm volatile(
+            "{asms[v]}\\n"
+            :
+            : [wb] "s"(wb), [ss] "s"(a.seg_stride), [k] "s"(a.k), [tw] "s"(tw), [tstep] "s"(tstep), [nr] "s"(nr),
+              [csh] "s"(a.col_shift), [cmk] "s"(a.col_mask), [cck] "s"(cck), [cbb] "s"(cbb),
+              [acc] "s"(a.accumulate), [ob] "s"(ob), [ab] "s"(ab), [oslot] "s"(a.out_slot0 + row0),
+              [oss] "s"(a.out_seg_stride), [aslot] "s"(a.acc_slot0 + row0), [ass] "s"(a.acc_seg_stride),
+              [lo] "v"(lo), {ins}
+            : {clobbers()});
+    }}""")
+    asm_blocks = "\n".join(blocks)
+    enc_cases = "\n".join(f"    case {v}: hipLaunchKernelGGL(gf16_tw_encode_kernel<{v}>, dim3((uint32_t)wgs), "
+                           f"dim3({64 * NWAVES}), 0, s, b); break;" for v in variants)
+    multi_cases = "\n".join(f"    case {v}: hipLaunchKernelGGL(gf16_tw_multi_kernel<{v}>, dim3((uint32_t)end), "
+                             f"dim3({64 * NWAVES}), 0, s, mm); break;" for v in variants)
+    if diag:
+        tw_variant = """int tw_variant()
+{
+    static const int v = [] {
+        const char* e = std::getenv("NFEC_TW_VARIANT");
+        const int x = e ? std::atoi(e) : 0;
+        return x >= 0 && x < %d ? x : 0;
+    }();
+    return v;
+}""" % len(variants)
+    else:
+        tw_variant = "constexpr int tw_variant() { return 0; }"
     phi_cols = ", ".join(f"0x{c:04x}" for c in PHI)
     src = f"""// GENERATED by tools/codegen/gen_gf16_tw.py -- do not edit by hand.
 // RS16 products through the tower field GF((2^8)^2): bit-sliced, GF(2^8) snippet jumps.
 // Isomorphism: lam = 0x{LAM:02x}, beta = 0x{BETA:04x} (phi(x^i) = beta^i).
+#include <cstdlib>
 #include "nfec_internal.hpp"
 #include "bitslice.hpp"
 
@@ -464,6 +530,7 @@ namespace nfec {{
 static_assert(kGf16TwRowsPerPass == {ROWS}u, "gen_gf16_tw.py and nfec_internal.hpp disagree on the rows per pass");
 namespace {{
 
+template <int V>
 __device__ __forceinline__ void tw_body(const Gf16T3Args& a, uint32_t wg)
 {{
     __shared__ uint32_t lds[{NWAVES} * 64 * 16];
@@ -501,31 +568,27 @@ __device__ __forceinline__ void tw_body(const Gf16T3Args& a, uint32_t wg)
     const uint8_t* ob = a.out_base + (uint64_t)b0 * a.out_block_stride;
     const uint8_t* ab = a.acc_base + (uint64_t)b0 * a.acc_block_stride;
     const uint32_t cck = a.col_chunk * a.seg_stride, cbb = a.col_base * a.seg_stride;
-    asm volatile(
-        "{asm}\\n"
-        :
-        : [wb] "s"(wb), [ss] "s"(a.seg_stride), [k] "s"(a.k), [tw] "s"(tw), [tstep] "s"(tstep), [nr] "s"(nr),
-          [csh] "s"(a.col_shift), [cmk] "s"(a.col_mask), [cck] "s"(cck), [cbb] "s"(cbb),
-          [acc] "s"(a.accumulate), [ob] "s"(ob), [ab] "s"(ab), [oslot] "s"(a.out_slot0 + row0),
-          [oss] "s"(a.out_seg_stride), [aslot] "s"(a.acc_slot0 + row0), [ass] "s"(a.acc_seg_stride),
-          [lo] "v"(lo), {ins}
-        : {clobbers()});
+{asm_blocks}
 }}
 
+template <int V>
 __global__ __launch_bounds__({64 * NWAVES}, 2) void gf16_tw_encode_kernel(Gf16T3Args a)
 {{
-    tw_body(a, bs::wg_index(1));
+    tw_body<V>(a, bs::wg_index(1));
 }}
 
 // several independent products in one grid (the RS16 Toeplitz split, rs16_tmvp): workgroup
 // ranges [wg_end[i-1], wg_end[i]) run problem i, so their tails share one launch
+template <int V>
 __global__ __launch_bounds__({64 * NWAVES}, 2) void gf16_tw_multi_kernel(Gf16T3Multi mm)
 {{
     const uint32_t wg = bs::wg_index(1);
-    if (wg < mm.wg_end[0]) tw_body(mm.e[0], wg);
-    else if (wg < mm.wg_end[1]) tw_body(mm.e[1], wg - mm.wg_end[0]);
-    else tw_body(mm.e[2], wg - mm.wg_end[1]);
+    if (wg < mm.wg_end[0]) tw_body<V>(mm.e[0], wg);
+    else if (wg < mm.wg_end[1]) tw_body<V>(mm.e[1], wg - mm.wg_end[0]);
+    else tw_body<V>(mm.e[2], wg - mm.wg_end[1]);
 }}
+
+{tw_variant}
 
 // checks the shape, fills the default output / accumulate layouts and the pass count
 int tw_prepare(const Gf16T3Args& a, Gf16T3Args& b, uint64_t& wgs)
@@ -586,7 +649,9 @@ int launch_gf16_tw_multi(const Gf16T3Args* e, uint32_t n, hipStream_t s)
         mm.wg_end[i] = (uint32_t)end;
     }}
     if (end == 0) return NFEC_OK;
-    hipLaunchKernelGGL(gf16_tw_multi_kernel, dim3((uint32_t)end), dim3({64 * NWAVES}), 0, s, mm);
+    switch (tw_variant()) {{
+{multi_cases}
+    }}
     const hipError_t err = hipGetLastError();
     return err == hipSuccess ? NFEC_OK : hip_fail(err, "gf16 tower multi launch");
 }}
@@ -598,7 +663,9 @@ int launch_gf16_tw_encode(const Gf16T3Args& a, hipStream_t s)
     uint64_t wgs = 0;
     const int rc = tw_prepare(a, b, wgs);
     if (rc) return rc;
-    hipLaunchKernelGGL(gf16_tw_encode_kernel, dim3((uint32_t)wgs), dim3({64 * NWAVES}), 0, s, b);
+    switch (tw_variant()) {{
+{enc_cases}
+    }}
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? NFEC_OK : hip_fail(e, "gf16 tower encode launch");
 }}
