@@ -304,14 +304,13 @@ bool use_gf16_t3()
     return v;
 }
 
-// RS16 products through the tower field (gen_gf16_tw.hip) instead of the shared LDS tables
+// RS16 products through the tower field (gen_gf16_tw.hip, the default since round 3) or the
+// shared LDS tables (gen_gf16_t3.hip, NFEC_RS16_TW=0: both are exact, the tests run both)
+// (read per codec construction, so one process can build codecs of both kinds)
 bool use_gf16_tw()
 {
-    static const bool v = [] {
-        const char* e = std::getenv("NFEC_RS16_TW");
-        return e && std::atoi(e) != 0;
-    }();
-    return v;
+    const char* e = std::getenv("NFEC_RS16_TW");
+    return !e || std::atoi(e) != 0;
 }
 
 // one RS16 product (encode, decode stage 1) on the codec's product kernel

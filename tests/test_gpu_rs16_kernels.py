@@ -1,0 +1,70 @@
+"""RS16 products on both GPU kernels against the oracle, bit-exact: the tower-field kernel
+(gen_gf16_tw.hip, the default) and the shared-table kernel (gen_gf16_t3.hip, NFEC_RS16_TW=0).
+The switch is read when a codec is built, so both run in one process.  Covers the one-product
+encode, the Toeplitz split (C4's route) and decode stage 1 (the plan's by-encode blocks).
+Reference: NormEncoderRS16::Encode / NormDecoderRS16::Decode, src/common/normEncoderRS16.cpp:472-482,
+650-755."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+from norm_amd import NFEC_RS16, NormDecoderRS16, NormEncoderRS16  # noqa: E402
+from norm_amd._native import NFEC_FEATURE_RS16_TOEPLITZ  # noqa: E402
+
+KERNELS = ["1", "0"]   # tower, shared tables
+
+
+def _codecs(monkeypatch, tw, k, m, vec, tmvp=None):
+    monkeypatch.setenv("NFEC_RS16_TW", tw)
+    if tmvp is not None:
+        monkeypatch.setenv("NFEC_RS16_TMVP", tmvp)
+    enc, dec = NormEncoderRS16(), NormDecoderRS16()
+    assert enc.Init(k, m, vec) and dec.Init(k, m, vec)
+    return enc, dec
+
+
+@pytest.mark.parametrize("tw", KERNELS)
+@pytest.mark.parametrize("k,m,vec,stride,nb,tmvp", [
+    (100, 20, 1400, 1400, 3, "0"),     # one product, two passes of 11 rows (tower) / one of 44
+    (64, 11, 64, 64, 9, "0"),          # exactly one full tower pass
+    (40, 12, 72, 80, 5, "0"),          # one row past a full pass, padded stride
+    (128, 32, 1408, 1416, 3, "1"),     # Toeplitz split, padded stride
+    (512, 128, 64, 64, 2, "1"),        # Toeplitz split, several passes per product
+])
+def test_rs16_encode_both_kernels(orc, monkeypatch, tw, k, m, vec, stride, nb, tmvp):
+    enc, _ = _codecs(monkeypatch, tw, k, m, vec, tmvp)
+    assert bool(enc.features() & NFEC_FEATURE_RS16_TOEPLITZ) == (tmvp == "1")
+    host = orc.make_blocks(k, m, vec, nb, seg_stride=stride)
+    host[:, k:, :] = 0x5A
+    ref = orc.encode_blocks(NFEC_RS16, k, m, vec, host.copy())
+    dev = torch.from_numpy(host).cuda()
+    enc.encode_blocks(dev)
+    torch.cuda.synchronize()
+    assert np.array_equal(dev.cpu().numpy(), ref)
+
+
+@pytest.mark.parametrize("tw", KERNELS)
+@pytest.mark.parametrize("k,m,vec,nb,es", [(400, 100, 64, 3, 50), (100, 20, 1400, 4, 20), (40, 10, 72, 5, 3)])
+def test_rs16_decode_both_kernels(orc, monkeypatch, tw, k, m, vec, nb, es):
+    """source-only erasures: stage 1 runs on the product kernel for every block"""
+    enc, dec = _codecs(monkeypatch, tw, k, m, vec)
+    host = orc.encode_blocks(NFEC_RS16, k, m, vec, orc.make_blocks(k, m, vec, nb))
+    locs = np.zeros((nb, m), np.uint16)
+    counts = np.zeros(nb, np.uint16)
+    for b in range(nb):
+        e = max(1, es - b)   # different erasure counts per block: rows_lim is the largest
+        src = orc.erasure_pattern(b + 77, k, e)
+        locs[b, :e] = src
+        counts[b] = e
+        host[b, src, :] = 0
+    ref = host.copy()
+    st_ref = orc.decode_blocks(NFEC_RS16, k, m, vec, ref, locs, counts)
+    dev = torch.from_numpy(host).cuda()
+    st = dec.decode_blocks(dev, torch.from_numpy(locs.astype(np.int16)).cuda(),
+                           torch.from_numpy(counts.astype(np.int16)).cuda())
+    torch.cuda.synchronize()
+    assert np.array_equal(st.cpu().numpy(), st_ref)
+    assert np.array_equal(dev.cpu().numpy(), ref)
