@@ -389,8 +389,7 @@ int build_codec(nfec_codec* c)
         // RS16: LDS offsets of the shared-table encode (gen_gf16_t3.hip), 96 bytes per
         // coefficient (C4, k = 4096, m = 256: 104 MB)
         if (wide && use_gf16_t3() && use_gf16_tw()) {
-            const uint32_t passes = (c->m + kGf16TwRowsPerPass - 1) / kGf16TwRowsPerPass;
-            std::vector<uint16_t> off((size_t)c->k * passes * 48);
+            std::vector<uint16_t> off((size_t)c->k * gf16_tw_passes(c->m) * 48);
             gf16_tw_offsets(c->gen, c->k, c->m, off.data());
             if ((rc = c->d_twoff.reserve(off.size()))) return rc;
             NFEC_HIP(hipMemcpy(c->d_twoff.p, off.data(), off.size() * 2, hipMemcpyHostToDevice));
@@ -409,13 +408,14 @@ int build_codec(nfec_codec* c)
             const char* ev = std::getenv("NFEC_RS16_TMVP");
             const int mode = ev ? std::atoi(ev) : -1;
             const uint32_t cw = c->m / 2;
-            const uint32_t rpp = c->tw ? kGf16TwRowsPerPass : kGf16T3RowsPerPass;
-            const bool pays = 3ull * ((cw + rpp - 1) / rpp) * (c->k / 2) < (uint64_t)((c->m + rpp - 1) / rpp) * c->k;
+            const uint32_t rpp = kGf16T3RowsPerPass;
+            const bool pays = c->tw ? 3ull * gf16_tw_passes(cw) * (c->k / 2) < (uint64_t)gf16_tw_passes(c->m) * c->k
+                                    : 3ull * ((cw + rpp - 1) / rpp) * (c->k / 2) < (uint64_t)((c->m + rpp - 1) / rpp) * c->k;
             std::vector<uint32_t> prod[3];
             std::vector<uint16_t> cm, wm, gm;
             if (mode != 0 && (mode == 1 || pays) && rs16_tmvp_plan(c->k, c->m, c->gen, prod, cm, wm, gm)) {
                 const uint32_t half = c->k / 2, mp = gf16_t3_rows_padded(cw);
-                const size_t one = c->tw ? (size_t)half * ((cw + kGf16TwRowsPerPass - 1) / kGf16TwRowsPerPass) * 48
+                const size_t one = c->tw ? (size_t)half * gf16_tw_passes(cw) * 48
                                          : (size_t)(half + 1) * mp * 48;
                 std::vector<uint16_t> off(3 * one);
                 for (int e = 0; e < 3; ++e) {
@@ -575,7 +575,7 @@ int rs16_tmvp_encode(nfec_codec* c, const nfec_block_batch* b, hipStream_t s)
     int rc;
     const uint32_t mp = gf16_t3_rows_padded(cw);
     const size_t one = (size_t)(half + 1) * mp * 48;
-    const size_t one_tw = (size_t)half * ((cw + kGf16TwRowsPerPass - 1) / kGf16TwRowsPerPass) * 48;
+    const size_t one_tw = (size_t)half * gf16_tw_passes(cw) * 48;
     uint32_t shift = 0;
     while ((1u << shift) < cw) ++shift;
     for (uint32_t b0 = 0; b0 < b->nblocks; b0 += sb) {

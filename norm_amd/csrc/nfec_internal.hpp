@@ -214,7 +214,7 @@ struct Gf16T3Args {
     // column map: column c is read from slot ((c >> col_shift) * col_chunk + (c & col_mask) +
     // col_base) (identity by default); in_slots bounds the slots read (0: k + m)
     uint32_t col_shift = 31, col_mask = 0xFFFFFFFFu, col_chunk = 0, col_base = 0, in_slots = 0;
-    // tower-field kernel (gen_gf16_tw.hip): [k][ceil(m / 11)][48] snippet offsets (gf16_tw_offsets)
+    // tower-field kernel (gen_gf16_tw.hip): [k][gf16_tw_passes(m)][48] snippet offsets (gf16_tw_offsets)
     const uint16_t* tw = nullptr;
 };
 struct Gf16T3Multi {
@@ -255,6 +255,7 @@ int launch_gf16_tw_encode(const Gf16T3Args& a, hipStream_t s);  // NFEC_ENOTSUP:
 bool gf16_tw_covers(const Gf16T3Args& a);
 int launch_gf16_tw_multi(const Gf16T3Args* e, uint32_t n, hipStream_t s);
 void gf16_tw_offsets(const std::vector<uint32_t>& parity_rows, uint32_t k, uint32_t m, uint16_t* out);
+uint32_t gf16_tw_passes(uint32_t m);  // passes of the tower kernel's table (a multiple of 4)
 void gf16_t3_offsets(const std::vector<uint32_t>& parity_rows, uint32_t k, uint32_t m, uint16_t* out);
 int launch_gf16_bs_encode(const Gf16BsEncArgs& a, hipStream_t s);  // NFEC_ENOTSUP: layout not 8-byte aligned
 void gf16_bs_selectors(const std::vector<uint32_t>& parity_rows, uint32_t k, uint32_t m, uint16_t* sel);

@@ -169,3 +169,33 @@ def test_register_map_is_disjoint():
         for v in r:
             assert v not in seen and 10 <= v <= 255
             seen.add(v)
+
+
+@pytest.mark.parametrize("m", [1, 4, 11, 12, 44, 45, 50, 100, 128, 200, 256])
+def test_pass_partition(m):
+    """rows spread evenly over whole workgroups of four passes, at most ROWS rows per pass,
+    every row in exactly one pass (the kernel's row0/nr and gf16_tw_offsets use the same split)"""
+    P = g.n_passes(m)
+    assert P % 4 == 0 and P >= 4
+    rows = []
+    for p in range(P):
+        lo, hi = g.pass_rows(m, P, p)
+        assert 0 <= hi - lo <= g.ROWS
+        rows += range(lo, hi)
+    assert rows == list(range(m))
+
+
+def test_entry_registers():
+    """a pass's entries: sweep 0 in the first 12 entry dwords, sweep 1 in the next 12 (so one
+    half loads while the other sweep reads), 16-bit halves j; matches gf16_tw_offsets'
+    2 r + j / 24 + 2 r + j layout"""
+    seen = set()
+    for n in (0, 1):
+        for r in range(g.ROWS):
+            for j in (0, 1):
+                dw, half = g.entry(n, r, j)
+                e = 2 * (dw - g.S_OFF) + half
+                assert e == 24 * n + 2 * r + j
+                assert g.S_OFF + 12 * n <= dw < g.S_OFF + 12 * n + 12
+                seen.add(e)
+    assert len(seen) == 4 * g.ROWS

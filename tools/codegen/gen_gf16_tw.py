@@ -62,9 +62,9 @@ MULTI = [a for a in range(1, 16) if bin(a).count("1") >= 2]
 # ---- SGPRs (clobbered) ----
 S_DESC, S_ODESC, S_ADESC = 36, 40, 44
 S_MASK = 48              # 8: transpose masks (mask, mask << s) for s = 8, 4, 2, 1
-S_SNIP, S_TGT, S_RET, S_TBL = 56, 58, 60, 62
+S_SNIP, S_TGT, S_RET = 56, 58, 60
 S_C, S_COL, S_T0, S_T1, S_T2 = 64, 65, 66, 67, 68
-S_OFF = 72               # 24: the column's table entries (s_load_dwordx16 + dwordx8)
+S_OFF = 72               # 24: the column's table entries (sweep 0: 72..83, sweep 1: 84..95)
 S_LAST = 95
 MASKS = {8: 0x00FF00FF, 4: 0x0F0F0F0F, 2: 0x33333333, 1: 0x55555555}
 
@@ -349,6 +349,59 @@ def table_entries(g):
 
 
 # ---------------------------------------------------------------- kernel body
+def entry(n, r, j):
+    """(dword, half) of the table entry of pass row r, sweep n (source x_n), output j: the
+    entries of sweep 0 fill dwords 0..10 and those of sweep 1 dwords 12..22, so one sweep's
+    entries load while the other sweep runs"""
+    return S_OFF + 12 * n + r, j
+
+
+def call(n, r, j):
+    dw, half = entry(n, r, j)
+    if "empty" in FLAGS:
+        first = f"s_mov_b32 s{S_T1}, 0"
+    else:
+        first = f"s_bfe_u32 s{S_T1}, s{dw}, 0x{(16 << 16) | (16 * half):x}"
+    return [first,
+            f"s_add_u32 s{S_TGT}, s{S_SNIP}, s{S_T1}",
+            f"s_addc_u32 s{S_TGT + 1}, s{S_SNIP + 1}, 0",
+            f"s_mov_b32 m0, 0x{GPR_MODE | (16 * r + 8 * j):x}",
+            f"s_swappc_b64 s[{S_RET}:{S_RET + 1}], s[{S_TGT}:{S_TGT + 1}]"]
+
+
+def sweep(n, x, nrows):
+    """the pass rows' jumps for source x_n; nrows: a fixed row count (no bound checks), or None
+    (rows checked against %[nr])"""
+    if "nosweep" in FLAGS:
+        return []
+    L = [f"s_mov_b32 s{S_T0}, 0", f"s_set_gpr_idx_on s{S_T0}, gpr_idx(SRC0,DST)"]
+    for r in range(nrows or ROWS):
+        if r and nrows is None:
+            L += [f"s_cmp_le_u32 %[nr], {r}", f"s_cbranch_scc1 Lsw{n}{x}_%="]
+        L += call(n, r, 0)
+        L += call(n, r, 1)
+    L += [f"Lsw{n}{x}_%=:", "s_set_gpr_idx_off", "s_nop 1"]
+    return L
+
+
+# ---------------------------------------------------------------- kernel body
+# The four waves of a workgroup run four passes of the same item group (64 lanes x 32 symbols).
+# In step s wave w loads, transposes and maps (phi) column 4 s + w only and writes its 16 tower
+# planes to an LDS exchange slot; after one s_barrier every wave applies columns 4 s .. 4 s + 3
+# to its rows, reading their planes back from LDS.  The per-column transpose and phi network
+# (~180 VALU) run once per workgroup, and each column is read from memory once per workgroup.
+# The LDS planes and the scalar table entries of the next half-column are fetched while the
+# current sweep runs (into S and the other half of the entry registers), so no sweep waits on
+# them.  Exchange: 2 buffers x 4 columns x 8 plane pairs x 64 lanes x 8 bytes = 32 KiB (pair p
+# of a lane at ((buf * 4 + col) * 8 + p) * 512 + lane * 8).
+S_SB, S_BUF, S_WV = 69, 70, 71   # step's first column; exchange buffer byte offset; wave index
+S_TB = 96                        # 2: table base (this pass's entries of column 0)
+S_TBN = 98                       # 2: table address of the column being fetched
+S_LAST4 = 99
+XCH_BUF = 4 * 8 * 64 * 8         # bytes per exchange buffer (4 columns)
+SPECIAL_ROWS = (11, 10, 9, 8)    # pass row counts with their own (unchecked) step loop
+
+
 def col_offset():
     """column index s[S_C] -> byte offset s[S_COL] through the column map
     ((c >> csh) * cck + (c & cmk) * ss + cbb; identity: csh 31, cck 0, cmk ~0, cbb 0)"""
@@ -365,52 +418,78 @@ def loads():
             for i in range(8)]
 
 
-def call(h, target):
-    if "empty" in FLAGS:
-        first = f"s_mov_b32 s{S_T1}, 0"
-    else:
-        first = f"s_bfe_u32 s{S_T1}, s{S_OFF + h // 2}, 0x{(16 << 16) | (16 * (h % 2)):x}"
-    return [first,
-            f"s_add_u32 s{S_TGT}, s{S_SNIP}, s{S_T1}",
-            f"s_addc_u32 s{S_TGT + 1}, s{S_SNIP + 1}, 0",
-            f"s_mov_b32 m0, 0x{GPR_MODE | target:x}",
-            f"s_swappc_b64 s[{S_RET}:{S_RET + 1}], s[{S_TGT}:{S_TGT + 1}]"]
+def xch_addr(j=None, sgpr=None):
+    """v_tmp0 = the lane's exchange address in the current buffer: of column slot j (a
+    constant, returned as the ds offset base) or of the slot held in SGPR s[sgpr]"""
+    if sgpr is None:
+        return [f"v_add_u32 v{V_TMP[0]}, s{S_BUF}, %[xl]"], 4096 * j
+    return [f"s_lshl_b32 s{S_T0}, s{sgpr}, 12", f"s_add_u32 s{S_T0}, s{S_T0}, s{S_BUF}",
+            f"v_add_u32 v{V_TMP[0]}, s{S_T0}, %[xl]"], 0
 
 
-def sweep(n, x, full):
-    """the rows' jumps for source n (0: x0, 1: x1); full: the pass has all ROWS rows, so the
-    per-row bound checks are left out"""
-    if "nosweep" in FLAGS:
-        return []
-    L = [f"s_mov_b32 s{S_T0}, 0", f"s_set_gpr_idx_on s{S_T0}, gpr_idx(SRC0,DST)"]
-    for r in range(ROWS):
-        if r and not full:
-            L += [f"s_cmp_le_u32 %[nr], {r}", f"s_cbranch_scc1 Lsw{n}{x}_%="]
-        L += call(4 * r + 2 * n, 16 * r)
-        L += call(4 * r + 2 * n + 1, 16 * r + 8)
-    L += [f"Lsw{n}{x}_%=:", "s_set_gpr_idx_off", "s_nop 1"]
+def fetch(j, n):
+    """planes of source x_n of column slot j -> S (LDS), table entries of sweep n -> their half"""
+    code, base = xch_addr(j)
+    L = []
+    if n == 0:  # a new column: its table address
+        L += [f"s_add_u32 s{S_T2}, s{S_SB}, {j}", f"s_mul_i32 s{S_T2}, s{S_T2}, %[tstep]",
+              f"s_add_u32 s{S_TBN}, s{S_TB}, s{S_T2}", f"s_addc_u32 s{S_TBN + 1}, s{S_TB + 1}, 0"]
+    L += code
+    for p in range(4):
+        L.append(f"ds_read_b64 v[{V_S + 2 * p}:{V_S + 2 * p + 1}], v{V_TMP[0]} offset:{base + 512 * (4 * n + p)}")
+    o = S_OFF + 12 * n
+    L += [f"s_load_dwordx8 s[{o}:{o + 7}], s[{S_TBN}:{S_TBN + 1}], 0x{48 * n:x}",
+          f"s_load_dwordx4 s[{o + 8}:{o + 11}], s[{S_TBN}:{S_TBN + 1}], 0x{48 * n + 32:x}"]
     return L
 
 
-def column_loop(x, full):
-    L = [f"Lcol{x}_%=:",
-         f"s_load_dwordx16 s[{S_OFF}:{S_OFF + 15}], s[{S_TBL}:{S_TBL + 1}], 0x0",
-         f"s_load_dwordx8 s[{S_OFF + 16}:{S_OFF + 23}], s[{S_TBL}:{S_TBL + 1}], 0x40",
-         "s_waitcnt vmcnt(0)"]
+def apply_col(j, x, nrows):
+    """apply column slot j of the step (entering with x0's planes and sweep-0 entries in flight)"""
+    y = f"{x}{j}"
+    L = []
+    if j:
+        L += [f"s_add_u32 s{S_T2}, s{S_SB}, {j}", f"s_cmp_lt_u32 s{S_T2}, %[k]", f"s_cbranch_scc0 Lend{x}_%="]
+    L.append("s_waitcnt lgkmcnt(0)")
+    L += [f"v_mov_b32 v{V_W + i}, v{V_S + i}" for i in range(8)]
+    L += fetch(j, 1)
+    L += combos_code()
+    L += sweep(0, y, nrows)
+    L.append("s_waitcnt lgkmcnt(0)")
+    L += [f"v_mov_b32 v{V_W + i}, v{V_S + i}" for i in range(8)]
+    if j < 3:
+        L += [f"s_add_u32 s{S_T2}, s{S_SB}, {j + 1}", f"s_cmp_lt_u32 s{S_T2}, %[k]", f"s_cbranch_scc0 Lnf{y}_%="]
+        L += fetch(j + 1, 0)
+        L.append(f"Lnf{y}_%=:")
+    L += combos_code()
+    L += sweep(1, y, nrows)
+    return L
+
+
+def step_loop(x, nrows):
+    """nrows: the pass's row count for a specialised loop, None: checked rows (helper waves with
+    no rows skip the applies)"""
+    L = [f"Lstep{x}_%=:", "s_waitcnt vmcnt(0)",
+         f"s_cmp_lt_u32 s{S_C}, %[k]", f"s_cbranch_scc0 Lnotr{x}_%="]
     L += transpose16(slot(), V_TMP)
     L += phi_code()
-    # next column's loads go into the slot while this one is applied
-    L += [f"s_add_u32 s{S_C}, s{S_C}, 1", f"s_cmp_lt_u32 s{S_C}, %[k]", f"s_cbranch_scc0 Lnl{x}_%="]
+    code, _ = xch_addr(sgpr=S_WV)
+    L += code
+    for p in range(4):
+        L.append(f"ds_write_b64 v{V_TMP[0]}, v[{V_W + 2 * p}:{V_W + 2 * p + 1}] offset:{512 * p}")
+    for p in range(4):
+        L.append(f"ds_write_b64 v{V_TMP[0]}, v[{V_S + 2 * p}:{V_S + 2 * p + 1}] offset:{512 * (4 + p)}")
+    L.append(f"Lnotr{x}_%=:")
+    # the wave's column of the next step goes into the (now free) slot
+    L += [f"s_add_u32 s{S_C}, s{S_C}, 4", f"s_cmp_lt_u32 s{S_C}, %[k]", f"s_cbranch_scc0 Lnl{x}_%="]
     L += col_offset() + loads()
-    L.append(f"Lnl{x}_%=:")
-    L += combos_code()
-    L.append("s_waitcnt lgkmcnt(0)")
-    L += sweep(0, x, full)
-    L += [f"v_mov_b32 v{V_W + i}, v{V_S + i}" for i in range(8)]
-    L += combos_code()
-    L += sweep(1, x, full)
-    L += [f"s_add_u32 s{S_TBL}, s{S_TBL}, %[tstep]", f"s_addc_u32 s{S_TBL + 1}, s{S_TBL + 1}, 0",
-          f"s_cmp_lt_u32 s{S_C}, %[k]", f"s_cbranch_scc1 Lcol{x}_%="]
+    L += [f"Lnl{x}_%=:", "s_waitcnt lgkmcnt(0)", "s_barrier"]
+    if nrows is None:
+        L += ["s_cmp_eq_u32 %[nr], 0", f"s_cbranch_scc1 Lend{x}_%="]
+    L += fetch(0, 0)
+    for j in range(4):
+        L += apply_col(j, x, nrows)
+    L += [f"Lend{x}_%=:", f"s_xor_b32 s{S_BUF}, s{S_BUF}, {XCH_BUF}", f"s_add_u32 s{S_SB}, s{S_SB}, 4",
+          f"s_cmp_lt_u32 s{S_SB}, %[k]", f"s_cbranch_scc1 Lstep{x}_%="]
     return L
 
 
@@ -422,17 +501,30 @@ def body():
           "Lpc_%=:",
           f"s_add_u32 s{S_SNIP}, s{S_SNIP}, Lsnip0_%=-Lpc_%=",
           f"s_addc_u32 s{S_SNIP + 1}, s{S_SNIP + 1}, 0",
-          f"s_mov_b64 s[{S_TBL}:{S_TBL + 1}], %[tw]",
-          f"s_mov_b32 s{S_C}, 0"]
+          f"s_mov_b64 s[{S_TB}:{S_TB + 1}], %[tw]",
+          f"s_mov_b32 s{S_WV}, %[wv]", f"s_mov_b32 s{S_C}, %[wv]",
+          f"s_mov_b32 s{S_SB}, 0", f"s_mov_b32 s{S_BUF}, 0"]
     for v in range(ACC0, V_LAST + 1):
         L.append(f"v_mov_b32 v{v}, 0")
+    L += [f"s_cmp_lt_u32 s{S_C}, %[k]", "s_cbranch_scc0 Lnl0_%="]
     L += col_offset() + loads()
-    L += [f"s_cmp_eq_u32 %[nr], {ROWS}", "s_cbranch_scc0 Lcolg_%="]
-    L += column_loop("f", True)
-    L.append("s_branch Lepi0_%=")
-    L += column_loop("g", False)
-    L.append("Lepi0_%=:")
-    # ---- epilogue: phi^-1, transpose back, store (XOR the accumulate source first) ----
+    L.append("Lnl0_%=:")
+    for nr in SPECIAL_ROWS:
+        L += [f"s_cmp_eq_u32 %[nr], {nr}", f"s_cbranch_scc1 Lstepr{nr}_%="]
+    L.append("s_branch Lstepg_%=")
+    for nr in SPECIAL_ROWS:
+        L += step_loop(f"r{nr}", nr)
+        L.append("s_branch Lepi0_%=")
+    L += step_loop("g", None)
+    L += ["Lepi0_%=:", "s_cmp_eq_u32 %[nr], 0", "s_cbranch_scc1 Lend_%="]
+    L += epilogue()
+    return L
+
+
+def epilogue():
+    """phi^-1, transpose back, store the wave's rows (XOR the accumulate source first); then
+    the snippet table"""
+    L = []
     L += [f"s_mov_b64 s[{S_ODESC}:{S_ODESC + 1}], %[ob]", f"s_mov_b32 s{S_ODESC + 2}, 0x80000000",
           f"s_mov_b32 s{S_ODESC + 3}, 0x00020000",
           f"s_mov_b64 s[{S_ADESC}:{S_ADESC + 1}], %[ab]", f"s_mov_b32 s{S_ADESC + 2}, 0x80000000",
@@ -465,9 +557,20 @@ def body():
     return L
 
 
-def clobbers():
+def pass_rows(m, passes, p):
+    """rows [lo, hi) of pass p when m rows are spread evenly over `passes` passes"""
+    return p * m // passes, (p + 1) * m // passes
+
+
+def n_passes(m):
+    """passes of a product with m rows: the fewest of at most ROWS rows, rounded up to whole
+    workgroups of four"""
+    return (((m + ROWS - 1) // ROWS) + 3) // 4 * 4
+
+
+def clobbers(last_s=None):
     v = [f'"v{i}"' for i in range(V_SLOT, V_LAST + 1)]
-    s = [f'"s{i}"' for i in range(S_DESC, S_LAST + 1)]
+    s = [f'"s{i}"' for i in range(S_DESC, (last_s or S_LAST) + 1)]
     return ", ".join(v + s + ['"m0"', '"scc"', '"memory"'])
 
 
@@ -484,9 +587,14 @@ def main():
     asms = {}
     for v, f in variants.items():
         FLAGS = f
-        asms[v] = "\\n\"\n        \"".join(body())
+        asms[v] = "\\n\"\n            \"".join(body())
     FLAGS = ()
     ins = ", ".join(f'[o{i}] "v"(o[{i}])' for i in range(8))
+    common = """[wb] "s"(wb), [ss] "s"(a.seg_stride), [k] "s"(a.k), [tw] "s"(tw), [tstep] "s"(tstep), [nr] "s"(nr),
+              [csh] "s"(a.col_shift), [cmk] "s"(a.col_mask), [cck] "s"(cck), [cbb] "s"(cbb),
+              [acc] "s"(a.accumulate), [ob] "s"(ob), [ab] "s"(ab), [oslot] "s"(a.out_slot0 + row0),
+              [oss] "s"(a.out_seg_stride), [aslot] "s"(a.acc_slot0 + row0), [ass] "s"(a.acc_seg_stride),
+              [wv] "s"(wave), [lo] "v"(lo), [xl] "v"(xl), """ + ins
     blocks = []
     for v in variants:
         kw = "if constexpr" if v == 0 else "else if constexpr"
@@ -494,18 +602,16 @@ def main():
         asm volatile(
             "{asms[v]}\\n"
             :
-            : [wb] "s"(wb), [ss] "s"(a.seg_stride), [k] "s"(a.k), [tw] "s"(tw), [tstep] "s"(tstep), [nr] "s"(nr),
-              [csh] "s"(a.col_shift), [cmk] "s"(a.col_mask), [cck] "s"(cck), [cbb] "s"(cbb),
-              [acc] "s"(a.accumulate), [ob] "s"(ob), [ab] "s"(ab), [oslot] "s"(a.out_slot0 + row0),
-              [oss] "s"(a.out_seg_stride), [aslot] "s"(a.acc_slot0 + row0), [ass] "s"(a.acc_seg_stride),
-              [lo] "v"(lo), {ins}
-            : {clobbers()});
+            : {common}
+            : {clobbers(S_LAST4)});
     }}""")
     asm_blocks = "\n".join(blocks)
-    enc_cases = "\n".join(f"    case {v}: hipLaunchKernelGGL(gf16_tw_encode_kernel<{v}>, dim3((uint32_t)wgs), "
-                           f"dim3({64 * NWAVES}), 0, s, b); break;" for v in variants)
-    multi_cases = "\n".join(f"    case {v}: hipLaunchKernelGGL(gf16_tw_multi_kernel<{v}>, dim3((uint32_t)end), "
-                             f"dim3({64 * NWAVES}), 0, s, mm); break;" for v in variants)
+
+    def cases(kern, grid, arg):
+        return "\n".join(f"    case {v}: hipLaunchKernelGGL({kern}<{v}>, dim3((uint32_t){grid}), "
+                         f"dim3({64 * NWAVES}), 0, s, {arg}); break;" for v in variants)
+    enc_cases = cases("gf16_tw_encode_kernel", "wgs", "b")
+    multi_cases = cases("gf16_tw_multi_kernel", "end", "mm")
     if diag:
         tw_variant = """int tw_variant()
 {
@@ -533,21 +639,24 @@ namespace {{
 template <int V>
 __device__ __forceinline__ void tw_body(const Gf16T3Args& a, uint32_t wg)
 {{
-    __shared__ uint32_t lds[{NWAVES} * 64 * 16];
+    __shared__ uint32_t lds[{NWAVES} * 64 * 16];       // the lanes' store offsets (epilogue)
+    __shared__ uint64_t xch[2 * {XCH_BUF // 8}];       // column planes exchange (body)
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const uint32_t job = wg * {NWAVES}u + wave;
-    const uint32_t group = job / a.passes, pass = job - group * a.passes;
+    const uint32_t quads = a.passes / 4u;
+    const uint32_t group = wg / quads, quad = wg - group * quads;
     const uint64_t total = (uint64_t)a.nblocks * a.vec_bytes;   // flat bytes over blocks
     const uint64_t f0 = (uint64_t)group * {GROUP_BYTES}u;
-    if (f0 >= total) return;
+    if (f0 >= total) return;  // workgroup-uniform, as the next exit
     // rows actually needed (decode stage 1: the largest erasure count among the blocks it
-    // serves, written by the plan); passes past them leave at once
+    // serves, written by the plan); workgroups past them leave at once, waves past them only
+    // load, transpose and share their columns
     uint32_t rlim = a.m;
     if (a.rows_lim) rlim = min(rlim, __builtin_amdgcn_readfirstlane(*a.rows_lim));
-    const uint32_t row0 = pass * {ROWS}u;
-    if (row0 >= rlim) return;
-    const uint32_t nr = __builtin_amdgcn_readfirstlane(min(rlim - row0, {ROWS}u));
+    if (quad * 4u * a.m / a.passes >= rlim) return;
+    const uint32_t pass = quad * 4u + wave;
+    const uint32_t row0 = pass * a.m / a.passes, row1 = (pass + 1u) * a.m / a.passes;
+    const uint32_t nr = __builtin_amdgcn_readfirstlane(row0 < rlim ? min(row1, rlim) - row0 : 0u);
     const uint32_t b0 = __builtin_amdgcn_readfirstlane((uint32_t)(f0 / a.vec_bytes));
     const uint8_t* wb = a.base + (uint64_t)b0 * a.block_stride;
     uint32_t o[8];
@@ -563,6 +672,7 @@ __device__ __forceinline__ void tw_body(const Gf16T3Args& a, uint32_t wg)
         po[8 + i] = ok ? (uint32_t)((uint64_t)(b - b0) * a.acc_block_stride) + p : 0x80000000u;
     }}
     const uint32_t lo = bs::lds_addr(po);
+    const uint32_t xl = bs::lds_addr(xch) + lane * 8u;
     const uint16_t* tw = a.tw + (uint64_t)pass * {TBL_HALF}u;
     const uint32_t tstep = a.passes * {2 * TBL_HALF}u;
     const uint8_t* ob = a.out_base + (uint64_t)b0 * a.out_block_stride;
@@ -616,9 +726,9 @@ int tw_prepare(const Gf16T3Args& a, Gf16T3Args& b, uint64_t& wgs)
         b.acc_seg_stride = b.out_seg_stride;
         b.acc_slot0 = b.out_slot0;
     }}
-    b.passes = (a.m + {ROWS - 1}u) / {ROWS}u;
+    b.passes = gf16_tw_passes(a.m);
     const uint64_t groups = (total + {GROUP_BYTES - 1}u) / {GROUP_BYTES}u;
-    wgs = (groups * b.passes + {NWAVES - 1}u) / {NWAVES}u;
+    wgs = groups * (b.passes / 4u);
     return wgs >= (1ull << 31) ? NFEC_ENOTSUP : NFEC_OK;
 }}
 
@@ -670,29 +780,36 @@ int launch_gf16_tw_encode(const Gf16T3Args& a, hipStream_t s)
     return e == hipSuccess ? NFEC_OK : hip_fail(e, "gf16 tower encode launch");
 }}
 
+uint32_t gf16_tw_passes(uint32_t m)
+{{
+    return ((m + {ROWS - 1}u) / {ROWS}u + 3u) / 4u * 4u;
+}}
+
 // snippet byte offsets of the tower kernel: coefficient g = parity_rows[r][c] maps to
-// phi(g) = c0 + c1 y; entries [c][pass][4 * (r % {ROWS}) + j] = (c0, c1, lam c1, c0 ^ c1)[j] << {SNIP_ALIGN},
-// rows past m (the last pass's padding) are zero (the empty snippet)
+// phi(g) = c0 + c1 y.  The m rows are spread evenly over gf16_tw_passes(m) passes (pass p:
+// rows [p m / P, (p + 1) m / P), at most {ROWS}); entry block [c][p][48]: sweep 0 (source x0) at
+// 2 r + j = (c0, c1)[j], sweep 1 (source x1) at 24 + 2 r + j = (lam c1, c0 ^ c1)[j], each << {SNIP_ALIGN};
+// unused entries are zero (the empty snippet)
 void gf16_tw_offsets(const std::vector<uint32_t>& parity_rows, uint32_t k, uint32_t m, uint16_t* out)
 {{
     const Field& f8 = gf8();
-    const uint32_t passes = (m + {ROWS - 1}u) / {ROWS}u;
+    const uint32_t passes = gf16_tw_passes(m);
     for (uint32_t c = 0; c < k; ++c)
         for (uint32_t p = 0; p < passes; ++p) {{
             uint16_t* o = out + ((size_t)c * passes + p) * {TBL_HALF}u;
             for (uint32_t i = 0; i < {TBL_HALF}u; ++i) o[i] = 0;
-            for (uint32_t r = 0; r < {ROWS}u; ++r) {{
-                const uint32_t row = p * {ROWS}u + r;
-                if (row >= m) break;
+            const uint32_t r0 = p * m / passes, r1 = (p + 1) * m / passes;
+            for (uint32_t row = r0; row < r1; ++row) {{
+                const uint32_t r = row - r0;
                 const uint32_t g = parity_rows[(size_t)row * k + c];
                 uint32_t t = 0;
                 for (int i = 0; i < 16; ++i)
                     if ((g >> i) & 1u) t ^= kPhiCol[i];
                 const uint32_t c0 = t & 255u, c1 = t >> 8;
-                o[4 * r + 0] = (uint16_t)(c0 << {SNIP_ALIGN});
-                o[4 * r + 1] = (uint16_t)(c1 << {SNIP_ALIGN});
-                o[4 * r + 2] = (uint16_t)(f8.mul(0x{LAM:02x}u, c1) << {SNIP_ALIGN});
-                o[4 * r + 3] = (uint16_t)((c0 ^ c1) << {SNIP_ALIGN});
+                o[2 * r + 0] = (uint16_t)(c0 << {SNIP_ALIGN});
+                o[2 * r + 1] = (uint16_t)(c1 << {SNIP_ALIGN});
+                o[24 + 2 * r + 0] = (uint16_t)(f8.mul(0x{LAM:02x}u, c1) << {SNIP_ALIGN});
+                o[24 + 2 * r + 1] = (uint16_t)((c0 ^ c1) << {SNIP_ALIGN});
             }}
         }}
 }}
