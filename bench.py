@@ -297,8 +297,13 @@ def main():
     value = src_bytes / (elapsed / a.steps) / 2**30
     enc_bytes = (k + m) * vec * nb  # algorithmic HBM bytes of one encode launch (per GPU)
     achieved = enc_bytes / (enc_ms * 1e-3) / 1e9
+    # the repair reads the k - e surviving source and e substitute parity segments and writes the
+    # e repaired ones: (k + e) * vec per block
+    dec_bytes = (k + a.erasures) * vec * nb
+    dec_achieved = dec_bytes / (dec_ms * 1e-3) / 1e9
 
     traffic = None
+    dec_traffic = None
     valu = None
     pmc_path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if os.path.exists(pmc_path):
@@ -306,6 +311,8 @@ def main():
             pmc = json.load(open(pmc_path))
             if pmc.get("blocks") == nb and pmc.get("k") == k and pmc.get("m") == m and pmc.get("vec") == vec:
                 traffic = pmc.get("encode_hbm_bytes_per_launch")
+                if a.erasures == 16:
+                    dec_traffic = pmc.get("decode_hbm_bytes_per_launch")
                 if pmc.get("valu_insts_per_launch"):
                     # the kernel is VALU-bound as much as HBM-bound: its
                     # wave64 VALU instructions (PMC SQ_INSTS_VALU) over the measured launch time
@@ -377,6 +384,17 @@ def main():
                                 "note": "4 GiB device-to-device copy on this GPU by a streaming kernel "
                                         "(nfec_util_stream_copy), read + write bytes; blit_GBps: torch copy_"},
             "valu": valu,
+        },
+        # the other half of the step: the repair (plan + fused repair kernel, one decode call)
+        "roofline_decode": {
+            "bound": "hbm",
+            "achieved": round(dec_achieved, 1),
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": round(dec_achieved / HBM_PEAK_GBS, 4),
+            "traffic": dec_traffic,
+            "kernel": f"nfec::rs8_fdec_k{k}_m{m} + rs_plan2_kernel (one decode call)",
+            "algorithmic_bytes_per_launch": dec_bytes,
         },
         "kernels_ms": {"encode": round(enc_ms, 4), "decode": round(dec_ms, 4)},
         "cpu_baseline": cpu,
