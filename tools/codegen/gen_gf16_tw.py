@@ -356,17 +356,20 @@ def entry(n, r, j):
     return S_OFF + 12 * n + r, j
 
 
-def call(n, r, j):
+def call(n, r, j, carry=True):
+    """jump into the snippet of entry (n, r, j), target accumulators 16 r + 8 j; carry=False
+    (the specialised loops): the table does not straddle a 4 GiB boundary, so the target's
+    high word is set once (s[S_TGT + 1] = s[S_SNIP + 1]) and only the low word is added"""
     dw, half = entry(n, r, j)
     if "empty" in FLAGS:
         first = f"s_mov_b32 s{S_T1}, 0"
     else:
         first = f"s_bfe_u32 s{S_T1}, s{dw}, 0x{(16 << 16) | (16 * half):x}"
-    return [first,
-            f"s_add_u32 s{S_TGT}, s{S_SNIP}, s{S_T1}",
-            f"s_addc_u32 s{S_TGT + 1}, s{S_SNIP + 1}, 0",
-            f"s_mov_b32 m0, 0x{GPR_MODE | (16 * r + 8 * j):x}",
-            f"s_swappc_b64 s[{S_RET}:{S_RET + 1}], s[{S_TGT}:{S_TGT + 1}]"]
+    L = [first, f"s_add_u32 s{S_TGT}, s{S_SNIP}, s{S_T1}"]
+    if carry:
+        L.append(f"s_addc_u32 s{S_TGT + 1}, s{S_SNIP + 1}, 0")
+    return L + [f"s_mov_b32 m0, 0x{GPR_MODE | (16 * r + 8 * j):x}",
+                f"s_swappc_b64 s[{S_RET}:{S_RET + 1}], s[{S_TGT}:{S_TGT + 1}]"]
 
 
 def sweep(n, x, nrows):
@@ -378,8 +381,8 @@ def sweep(n, x, nrows):
     for r in range(nrows or ROWS):
         if r and nrows is None:
             L += [f"s_cmp_le_u32 %[nr], {r}", f"s_cbranch_scc1 Lsw{n}{x}_%="]
-        L += call(n, r, 0)
-        L += call(n, r, 1)
+        L += call(n, r, 0, nrows is None)
+        L += call(n, r, 1, nrows is None)
     L += [f"Lsw{n}{x}_%=:", "s_set_gpr_idx_off", "s_nop 1"]
     return L
 
@@ -508,7 +511,10 @@ def body():
         L.append(f"v_mov_b32 v{v}, 0")
     L += [f"s_cmp_lt_u32 s{S_C}, %[k]", "s_cbranch_scc0 Lnl0_%="]
     L += col_offset() + loads()
-    L.append("Lnl0_%=:")
+    # the specialised loops add only the low word of a snippet address: taken when no entry
+    # (< 32 KiB) can carry into the high word (else the generic loop, which carries)
+    L += ["Lnl0_%=:", f"s_mov_b32 s{S_TGT + 1}, s{S_SNIP + 1}",
+          f"s_add_u32 s{S_T0}, s{S_SNIP}, 0x8000", "s_cbranch_scc1 Lstepg_%="]
     for nr in SPECIAL_ROWS:
         L += [f"s_cmp_eq_u32 %[nr], {nr}", f"s_cbranch_scc1 Lstepr{nr}_%="]
     L.append("s_branch Lstepg_%=")
