@@ -147,4 +147,72 @@ int launch_tmvp_postscale(const Rs16TmvpArgs& a, hipStream_t s)
     return e == hipSuccess ? NFEC_OK : hip_fail(e, "tmvp postscale launch");
 }
 
+namespace {
+
+// RS16 decode stage 2 on the tower kernel (per-block mode, gen_gf16_tw.hip): block b's inverse
+// A^-1 (coef2, column t = z row t, row s = erased output s) becomes the kernel's snippet table
+// [t][pass][48] with the rows spread over the passes as gf16_tw_offsets spreads an encode's
+// parity rows, and the output rows' byte offsets row_off[b][s] = erased slot s * seg_stride.
+// One thread per (block, column, pass); columns and rows at or past the block's e are not read.
+__device__ __forceinline__ uint32_t gf8_mul_11d(uint32_t a, uint32_t b)
+{
+    uint32_t r = 0;
+    for (int i = 0; i < 8; ++i) {
+        if (b & 1u) r ^= a;
+        b >>= 1;
+        a <<= 1;
+        if (a & 0x100u) a ^= 0x11du;
+    }
+    return r;
+}
+
+__global__ void tw_dec_tables_kernel(TwDecTablesArgs a)
+{
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t per_blk = a.M * a.passes;
+    if (i >= (uint64_t)a.nblocks * per_blk) return;
+    const uint32_t b = (uint32_t)(i / per_blk);
+    const uint32_t rem = (uint32_t)(i - (uint64_t)b * per_blk);
+    const uint32_t t = rem / a.passes, p = rem - t * a.passes;
+    const int32_t e = a.rows[b];
+    if (p == 0) {  // the output row offsets (and 12 padding entries the pass loads may touch)
+        uint32_t* ro = a.row_off + (uint64_t)b * (a.M + 12u);
+        ro[t] = (int32_t)t < e ? (uint32_t)a.out_slots[(uint64_t)b * a.slots_stride + t] * a.seg_stride : 0u;
+        if (t < 12u) ro[a.M + t] = 0u;
+    }
+    if (e <= 0 || (int32_t)t >= e) return;
+    uint16_t o[48];
+#pragma unroll
+    for (int j = 0; j < 48; ++j) o[j] = 0;
+    const uint32_t r0 = p * a.M / a.passes, r1 = min((p + 1u) * a.M / a.passes, (uint32_t)e);
+    const uint16_t* col = a.coef2 + ((uint64_t)b * a.dcs + t) * a.dcs;
+    for (uint32_t row = r0; row < r1; ++row) {
+        const uint32_t g = col[row], r = row - r0;
+        uint32_t tt = 0;
+#pragma unroll
+        for (int k = 0; k < 16; ++k)
+            if ((g >> k) & 1u) tt ^= a.phi[k];
+        const uint32_t c0 = tt & 255u, c1 = tt >> 8;
+        o[2 * r] = (uint16_t)(c0 << 7);
+        o[2 * r + 1] = (uint16_t)(c1 << 7);
+        o[24 + 2 * r] = (uint16_t)(gf8_mul_11d(a.lam, c1) << 7);
+        o[24 + 2 * r + 1] = (uint16_t)((c0 ^ c1) << 7);
+    }
+    uint4* dst = reinterpret_cast<uint4*>(a.tw + (((uint64_t)b * a.M + t) * a.passes + p) * 48u);
+    const uint4* src = reinterpret_cast<const uint4*>(o);
+#pragma unroll
+    for (int j = 0; j < 6; ++j) dst[j] = src[j];
+}
+
+}  // namespace
+
+int launch_tw_dec_tables(const TwDecTablesArgs& a, hipStream_t s)
+{
+    const uint64_t n = (uint64_t)a.nblocks * a.M * a.passes;
+    if (n == 0) return NFEC_OK;
+    hipLaunchKernelGGL(tw_dec_tables_kernel, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, s, a);
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? NFEC_OK : hip_fail(e, "tw decode tables launch");
+}
+
 }  // namespace nfec

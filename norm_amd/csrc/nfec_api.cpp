@@ -205,7 +205,7 @@ struct nfec_codec {
     DevBuf<uint16_t> d_sel16;      // RS16 bit-sliced encode table offsets [k][m][64] (may be absent)
     DevBuf<uint16_t> d_t3off;      // RS16 shared-table encode LDS offsets [k+1][m_pad][48]
     // RS16 products by the tower-field kernel (gen_gf16_tw.hip) instead of the shared-table one:
-    // snippet offsets [k][ceil(m/11)][48]; the Toeplitz split's three products likewise
+    // snippet offsets [k][gf16_tw_passes(m)][48]; the Toeplitz split's three products likewise
     bool tw = false;
     DevBuf<uint16_t> d_twoff, d_tmvp_tw;
     // RS16 encode by the Toeplitz split (kernels_tmvp.hip): offsets of the three products, each
@@ -223,6 +223,8 @@ struct nfec_codec {
     DevBuf<uint16_t> w_islots, w_oslots, w_cols;
     DevBuf<uint8_t> w_coef1, w_coef2, w_z, w_work, w_pmap;
     DevBuf<uint32_t> w_emask, w_psel, w_gate;
+    DevBuf<uint16_t> w_tw2;        // RS16 decode stage 2 on the tower kernel: per-block tables
+    DevBuf<uint32_t> w_rowoff;     // ... and output row offsets (TwDecTablesArgs)
     uint32_t gate_gen = 0;         // per-pass generation written into w_gate (RsPlan2Args)
     // per-call staging (nfec_encode_segment / nfec_decode_vectors, guarded by mu): one device
     // buffer and one pinned mirror of the same layout, and a stream of the codec's own, so a
@@ -271,6 +273,8 @@ struct nfec_codec {
         w_islots.release();
         w_oslots.release();
         w_cols.release();
+        w_tw2.release();
+        w_rowoff.release();
     }
 };
 
@@ -879,6 +883,15 @@ int decode_device(nfec_codec* c, const nfec_block_batch* b, const uint16_t* locs
         if ((rc = c->w_rows1.reserve(sb))) return rc;
         if ((rc = c->w_rmax.reserve(1))) return rc;
     }
+    // RS16 stage 2 (d_E = A^-1 z) on the tower kernel in per-block mode, with the batches stage
+    // 1 takes by encode (overwrite, unshortened); tables of M = min(k, m) rows per block
+    const uint32_t M2 = std::min(c->k, c->m);
+    const uint32_t P2 = gf16_tw_passes(M2);
+    const bool tw2 = t3dec && c->tw && diag_knob("NFEC_RS16_TW2", 1) != 0;
+    if (tw2) {
+        if ((rc = c->w_tw2.reserve((size_t)sb * M2 * P2 * 48))) return rc;
+        if ((rc = c->w_rowoff.reserve((size_t)sb * (M2 + 12)))) return rc;
+    }
     const bool fast = c->kind == NFEC_RS8 && !b->num_data && c->m <= 32 && c->k <= 64 && !force_generic() &&
                       has_bitsliced(c->k, c->m) && bs::offsets_fit(b->block_stride, b->seg_stride);
     if (fast) {
@@ -1205,6 +1218,43 @@ int decode_device(nfec_codec* c, const nfec_block_batch* b, const uint16_t* locs
             a.nblocks = nb;
             a.vec_bytes = vb;
             if ((rc = launch_gf16_matmul(a, s))) return rc;
+            if (tw2) {
+                TwDecTablesArgs d;
+                d.coef2 = reinterpret_cast<const uint16_t*>(c->w_coef2.p);
+                d.dcs = dcs;
+                d.rows = c->w_rows.p;
+                d.out_slots = c->w_oslots.p;
+                d.slots_stride = c->k;
+                d.seg_stride = b->seg_stride;
+                d.nblocks = nb;
+                d.M = M2;
+                d.passes = P2;
+                d.tw = c->w_tw2.p;
+                d.row_off = c->w_rowoff.p;
+                gf16_tw_field(d.phi, &d.lam);
+                if ((rc = launch_tw_dec_tables(d, s))) return rc;
+                Gf16T3Args t;
+                t.base = c->w_z.p;
+                t.block_stride = (uint64_t)dcs * zstride;
+                t.seg_stride = zstride;
+                t.nblocks = nb;
+                t.k = M2;
+                t.m = M2;
+                t.vec_bytes = vb;
+                t.tw = c->w_tw2.p;
+                t.tw_block_stride = (uint64_t)M2 * P2 * 48;
+                t.blk_rows = c->w_rows.p;
+                t.row_off = c->w_rowoff.p;
+                t.row_off_stride = M2 + 12;
+                t.out_base = blocks;
+                t.out_block_stride = b->block_stride;
+                t.out_seg_stride = b->seg_stride;
+                rc = launch_gf16_tw_encode(t, s);
+                if (rc != NFEC_ENOTSUP) {
+                    if (rc) return rc;
+                    continue;
+                }
+            }
             Gf16MatmulArgs a2 = a;
             a2.in_base = c->w_z.p;
             a2.in_block_stride = (uint64_t)dcs * zstride;

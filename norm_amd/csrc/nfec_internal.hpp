@@ -216,6 +216,14 @@ struct Gf16T3Args {
     uint32_t col_shift = 31, col_mask = 0xFFFFFFFFu, col_chunk = 0, col_base = 0, in_slots = 0;
     // tower-field kernel (gen_gf16_tw.hip): [k][gf16_tw_passes(m)][48] snippet offsets (gf16_tw_offsets)
     const uint16_t* tw = nullptr;
+    // per-block mode (RS16 decode stage 2 on the tower kernel): item groups stay inside one
+    // block; block b has its own table (tw + b * tw_block_stride), e = blk_rows[b] rows and
+    // columns, and its rows' output byte offsets row_off[b * row_off_stride + r] (from out_base
+    // + b * out_block_stride); no accumulate source
+    const int32_t* blk_rows = nullptr;
+    uint64_t tw_block_stride = 0;
+    const uint32_t* row_off = nullptr;
+    uint32_t row_off_stride = 0;
 };
 struct Gf16T3Multi {
     Gf16T3Args e[3];
@@ -256,6 +264,23 @@ bool gf16_tw_covers(const Gf16T3Args& a);
 int launch_gf16_tw_multi(const Gf16T3Args* e, uint32_t n, hipStream_t s);
 void gf16_tw_offsets(const std::vector<uint32_t>& parity_rows, uint32_t k, uint32_t m, uint16_t* out);
 uint32_t gf16_tw_passes(uint32_t m);  // passes of the tower kernel's table (a multiple of 4)
+void gf16_tw_field(uint16_t phi_cols[16], uint32_t* lam);  // the tower isomorphism's constants
+// RS16 decode stage 2 on the tower kernel: per-block snippet tables and output row offsets from
+// the plan's e x e inverses (kernels_tmvp.hip)
+struct TwDecTablesArgs {
+    const uint16_t* coef2 = nullptr;  // [b][dcs][dcs] inverse, column-major ([t][s])
+    uint32_t dcs = 0;
+    const int32_t* rows = nullptr;    // e per block
+    const uint16_t* out_slots = nullptr;  // [b][slots_stride] erased source slots
+    uint32_t slots_stride = 0;
+    uint32_t seg_stride = 0;          // output segment stride (bytes)
+    uint32_t nblocks = 0, M = 0, passes = 0;  // M rows / columns at most (min(k, m))
+    uint16_t* tw = nullptr;           // [b][M][passes][48]
+    uint32_t* row_off = nullptr;      // [b][M + 12]
+    uint16_t phi[16] = {};
+    uint32_t lam = 0;
+};
+int launch_tw_dec_tables(const TwDecTablesArgs& a, hipStream_t s);
 void gf16_t3_offsets(const std::vector<uint32_t>& parity_rows, uint32_t k, uint32_t m, uint16_t* out);
 int launch_gf16_bs_encode(const Gf16BsEncArgs& a, hipStream_t s);  // NFEC_ENOTSUP: layout not 8-byte aligned
 void gf16_bs_selectors(const std::vector<uint32_t>& parity_rows, uint32_t k, uint32_t m, uint16_t* sel);

@@ -538,7 +538,14 @@ def epilogue():
     for i in range(8):
         L.append(f"ds_read_b32 v{V_W + i}, %[lo] offset:{4 * i}")
         L.append(f"ds_read_b32 v{V_S + i}, %[lo] offset:{32 + 4 * i}")
-    L.append("s_waitcnt lgkmcnt(0)")
+    # the rows' output byte offsets (the table entries' registers are free now): per-block mode
+    # from the row table, else (oslot + r) * oss
+    L += ["s_cmp_eq_u64 %[rp], 0", "s_cbranch_scc1 Lflat_%=",
+          f"s_load_dwordx8 s[{S_OFF}:{S_OFF + 7}], %[rp], 0x0",
+          f"s_load_dwordx4 s[{S_OFF + 8}:{S_OFF + 11}], %[rp], 0x20", "s_branch Lrows_%=", "Lflat_%=:"]
+    for r in range(ROWS):
+        L += [f"s_add_u32 s{S_OFF + r}, %[oslot], {r}", f"s_mul_i32 s{S_OFF + r}, s{S_OFF + r}, %[oss]"]
+    L += ["Lrows_%=:", "s_waitcnt lgkmcnt(0)"]
     x = slot()
     tmp = [V_CA + i for i in range(16)]
     for r in range(ROWS):
@@ -546,7 +553,7 @@ def epilogue():
             L += [f"s_cmp_le_u32 %[nr], {r}", "s_cbranch_scc1 Lepi_%="]
         L += phi_inv_code(r)
         L += transpose16(x, V_TMP)
-        L += [f"s_add_u32 s{S_T1}, %[oslot], {r}", f"s_mul_i32 s{S_T1}, s{S_T1}, %[oss]",
+        L += [f"s_mov_b32 s{S_T1}, s{S_OFF + r}",
               "s_cmp_eq_u32 %[acc], 0", f"s_cbranch_scc1 Lna{r}_%=",
               f"s_add_u32 s{S_T2}, %[aslot], {r}", f"s_mul_i32 s{S_T2}, s{S_T2}, %[ass]"]
         for i in range(8):
@@ -596,11 +603,11 @@ def main():
         asms[v] = "\\n\"\n            \"".join(body())
     FLAGS = ()
     ins = ", ".join(f'[o{i}] "v"(o[{i}])' for i in range(8))
-    common = """[wb] "s"(wb), [ss] "s"(a.seg_stride), [k] "s"(a.k), [tw] "s"(tw), [tstep] "s"(tstep), [nr] "s"(nr),
+    common = """[wb] "s"(wb), [ss] "s"(a.seg_stride), [k] "s"(kk), [tw] "s"(tw), [tstep] "s"(tstep), [nr] "s"(nr),
               [csh] "s"(a.col_shift), [cmk] "s"(a.col_mask), [cck] "s"(cck), [cbb] "s"(cbb),
               [acc] "s"(a.accumulate), [ob] "s"(ob), [ab] "s"(ab), [oslot] "s"(a.out_slot0 + row0),
               [oss] "s"(a.out_seg_stride), [aslot] "s"(a.acc_slot0 + row0), [ass] "s"(a.acc_seg_stride),
-              [wv] "s"(wave), [lo] "v"(lo), [xl] "v"(xl), """ + ins
+              [wv] "s"(wave), [rp] "s"(rp), [lo] "v"(lo), [xl] "v"(xl), """ + ins
     blocks = []
     for v in variants:
         kw = "if constexpr" if v == 0 else "else if constexpr"
@@ -651,27 +658,38 @@ __device__ __forceinline__ void tw_body(const Gf16T3Args& a, uint32_t wg)
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t quads = a.passes / 4u;
     const uint32_t group = wg / quads, quad = wg - group * quads;
-    const uint64_t total = (uint64_t)a.nblocks * a.vec_bytes;   // flat bytes over blocks
-    const uint64_t f0 = (uint64_t)group * {GROUP_BYTES}u;
-    if (f0 >= total) return;  // workgroup-uniform, as the next exit
+    // flat mode: item groups run over the batch's bytes across blocks (one coefficient table);
+    // per-block mode (blk_rows): each group lies in one block, which has its own table, row
+    // count e (also its column count) and output row offsets
+    const bool pb = a.blk_rows != nullptr;
+    const uint32_t chunks = (a.vec_bytes + {GROUP_BYTES - 1}u) / {GROUP_BYTES}u;
+    const uint32_t pblk = pb ? group / chunks : 0u;
+    const uint64_t total = pb ? (uint64_t)a.vec_bytes : (uint64_t)a.nblocks * a.vec_bytes;
+    const uint64_t f0 = pb ? (uint64_t)(group - pblk * chunks) * {GROUP_BYTES}u : (uint64_t)group * {GROUP_BYTES}u;
+    if ((pb && pblk >= a.nblocks) || f0 >= total) return;  // workgroup-uniform, as the next exits
     // rows actually needed (decode stage 1: the largest erasure count among the blocks it
-    // serves, written by the plan); workgroups past them leave at once, waves past them only
-    // load, transpose and share their columns
-    uint32_t rlim = a.m;
+    // serves, written by the plan; per-block mode: the block's e); workgroups past them leave
+    // at once, waves past them only load, transpose and share their columns
+    uint32_t rlim = a.m, kk = a.k;
     if (a.rows_lim) rlim = min(rlim, __builtin_amdgcn_readfirstlane(*a.rows_lim));
+    if (pb) {{
+        const int32_t e = (int32_t)__builtin_amdgcn_readfirstlane((uint32_t)a.blk_rows[pblk]);
+        rlim = e > 0 ? min(rlim, (uint32_t)e) : 0u;
+        kk = min(kk, rlim);
+    }}
     if (quad * 4u * a.m / a.passes >= rlim) return;
     const uint32_t pass = quad * 4u + wave;
     const uint32_t row0 = pass * a.m / a.passes, row1 = (pass + 1u) * a.m / a.passes;
     const uint32_t nr = __builtin_amdgcn_readfirstlane(row0 < rlim ? min(row1, rlim) - row0 : 0u);
-    const uint32_t b0 = __builtin_amdgcn_readfirstlane((uint32_t)(f0 / a.vec_bytes));
+    const uint32_t b0 = pb ? pblk : __builtin_amdgcn_readfirstlane((uint32_t)(f0 / a.vec_bytes));
     const uint8_t* wb = a.base + (uint64_t)b0 * a.block_stride;
     uint32_t o[8];
     uint32_t* po = lds + (wave * 64u + lane) * 16u;
 #pragma unroll
     for (int i = 0; i < 8; ++i) {{
         const uint64_t f = f0 + (uint64_t)i * 512u + lane * 8u;
-        const uint32_t b = (uint32_t)(f / a.vec_bytes);
-        const uint32_t p = (uint32_t)(f - (uint64_t)b * a.vec_bytes);
+        const uint32_t b = pb ? b0 : (uint32_t)(f / a.vec_bytes);
+        const uint32_t p = (uint32_t)(f - (uint64_t)(pb ? 0u : b) * a.vec_bytes);
         const bool ok = f < total;
         o[i] = ok ? (uint32_t)((uint64_t)(b - b0) * a.block_stride) + p : 0x80000000u;
         po[i] = ok ? (uint32_t)((uint64_t)(b - b0) * a.out_block_stride) + p : 0x80000000u;
@@ -679,7 +697,9 @@ __device__ __forceinline__ void tw_body(const Gf16T3Args& a, uint32_t wg)
     }}
     const uint32_t lo = bs::lds_addr(po);
     const uint32_t xl = bs::lds_addr(xch) + lane * 8u;
-    const uint16_t* tw = a.tw + (uint64_t)pass * {TBL_HALF}u;
+    const uint16_t* tw = a.tw + (uint64_t)b0 * (pb ? a.tw_block_stride : 0u) + (uint64_t)pass * {TBL_HALF}u;
+    // per-block mode: byte offsets of the pass's output rows (row_off[b][row0 ..]); flat: null
+    const uint32_t* rp = pb ? a.row_off + (uint64_t)b0 * a.row_off_stride + row0 : nullptr;
     const uint32_t tstep = a.passes * {2 * TBL_HALF}u;
     const uint8_t* ob = a.out_base + (uint64_t)b0 * a.out_block_stride;
     const uint8_t* ab = a.acc_base + (uint64_t)b0 * a.acc_block_stride;
@@ -733,7 +753,10 @@ int tw_prepare(const Gf16T3Args& a, Gf16T3Args& b, uint64_t& wgs)
         b.acc_slot0 = b.out_slot0;
     }}
     b.passes = gf16_tw_passes(a.m);
-    const uint64_t groups = (total + {GROUP_BYTES - 1}u) / {GROUP_BYTES}u;
+    // per-block mode: one table and one set of row offsets per block, no accumulate source
+    if (a.blk_rows && (!a.row_off || !a.tw_block_stride || a.accumulate)) return NFEC_ENOTSUP;
+    const uint64_t groups = a.blk_rows ? (uint64_t)a.nblocks * ((a.vec_bytes + {GROUP_BYTES - 1}u) / {GROUP_BYTES}u)
+                                       : (total + {GROUP_BYTES - 1}u) / {GROUP_BYTES}u;
     wgs = groups * (b.passes / 4u);
     return wgs >= (1ull << 31) ? NFEC_ENOTSUP : NFEC_OK;
 }}
@@ -784,6 +807,12 @@ int launch_gf16_tw_encode(const Gf16T3Args& a, hipStream_t s)
     }}
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? NFEC_OK : hip_fail(e, "gf16 tower encode launch");
+}}
+
+void gf16_tw_field(uint16_t phi_cols[16], uint32_t* lam)
+{{
+    for (int i = 0; i < 16; ++i) phi_cols[i] = kPhiCol[i];
+    *lam = 0x{LAM:02x}u;
 }}
 
 uint32_t gf16_tw_passes(uint32_t m)

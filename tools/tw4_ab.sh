@@ -4,7 +4,7 @@
 #   bash tools/tw4_ab.sh   -> gpurun_out/tw4_*.{log,json}
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
-timeout -k 10 400 python3 -u -m pytest tests/test_gpu_rs16_kernels.py tests/test_gpu_tmvp.py tests/test_c4_c5.py -m gpu -x -q \
+timeout -k 10 400 python3 -u -m pytest tests/test_gpu_rs16_kernels.py tests/test_gpu_tmvp.py tests/test_c4_c5.py tests/test_gpu_parity.py -m gpu -x -q \
     --timeout 120 --timeout-method thread -p no:cacheprovider > gpurun_out/tw4_pytest.log 2>&1 || { tail -30 gpurun_out/tw4_pytest.log; exit 1; }
 tail -2 gpurun_out/tw4_pytest.log
 timeout -k 10 200 python3 tools/bench_extra.py --workload rs16 --steps 3 > gpurun_out/tw4_rs16.json 2>&1 || exit 1
