@@ -704,18 +704,20 @@ __global__ __launch_bounds__(64 * kPlan2Waves) void rs_plan2_kernel(RsPlan2Args 
     wave_lds_sync();
     uint8_t* coef = a.coef2 + (uint64_t)b * cs * cs;
     if (fused) {
-        // by parity row: 16 x 16 bytes, row sP[t] holds z_t's coefficients, unused rows zero (the
-        // fused kernel applies rows 0..max used row; a zero coefficient's snippet is empty)
+        // by parity row: 16 rows of 16 u16 (cs = 32 bytes), row sP[t] holds z_t's coefficients
+        // as the fused kernel's snippet byte offsets (c << 7), unused rows zero (the fused kernel
+        // applies rows 0..max used row; a zero coefficient's snippet is empty)
+        uint16_t* coef16 = reinterpret_cast<uint16_t*>(coef);
         for (uint32_t idx = lane; idx < 16 * 16; idx += 64) {
             const uint32_t row = idx >> 4, s = idx & 15;
             const uint32_t t = (uint32_t)__popcll(pused & ((1ull << row) - 1ull));  // rank of row
-            uint8_t v = 0;
+            uint32_t v = 0;
             if (((pused >> row) & 1ull) && s < e) {
                 int32_t l = lA[s] + lB[t] - (int32_t)lg[xs[s] ^ yt[t]];
                 if (l < 0) l += 255;
                 v = ex[l];
             }
-            coef[(uint64_t)row * cs + s] = v;
+            coef16[(uint64_t)row * (cs / 2) + s] = (uint16_t)(v << 7);
         }
     } else {
         for (uint32_t idx = lane; idx < e * e; idx += 64) {

@@ -214,7 +214,10 @@ def fdec_asm(k, m, probe=None, e16=False):
 
     def stage2(x, full):
         """x: label suffix; full: the block has e = 16 (then every output is live and the used
-        parity rows are 0..15), so the per-output and per-row bound checks are left out"""
+        parity rows are 0..15), so the per-output and per-row bound checks are left out, and the
+        snippet addresses add only their low word (the wave checked that no offset carries).
+        The plan writes each coefficient as its snippet's byte offset (u16, c << 7); row t holds
+        16 of them (32 bytes), half h loads its 8 (16 bytes at 32 t + 16 h)."""
         S = []
         for h in range(2):
             if h == 1 and not full:
@@ -229,7 +232,7 @@ def fdec_asm(k, m, probe=None, e16=False):
                 S.append("s_waitcnt lgkmcnt(0)")
                 # next coefficient row (after row 15: row 0 again, for the second half)
                 nt = (t + 1) % 16
-                S.append(f"s_load_dwordx4 s[{cbuf[nt % 2]}:{cbuf[nt % 2] + 3}], %[cp], 0x{32 * nt:x}")
+                S.append(f"s_load_dwordx4 s[{cbuf[nt % 2]}:{cbuf[nt % 2] + 3}], %[cp], 0x{32 * nt + 16 * h:x}")
                 for i in range(8):
                     S.append(f"v_mov_b32 v{win[i]}, v{acc_reg(t, i)}")
                 S.extend(all_tables(win)[0])
@@ -238,11 +241,11 @@ def fdec_asm(k, m, probe=None, e16=False):
                     s = 8 * h + sl
                     if not full:
                         S.extend([f"s_cmp_le_u32 %[e], {s}", f"s_cbranch_scc1 Lsend{h}_{t}{x}_%="])
-                    S.extend([f"s_bfe_u32 s{S_T}, s{cur + s // 4}, 0x{(8 << 16) | (8 * (s % 4)):x}",
-                              f"s_lshl_b32 s{S_T}, s{S_T}, {SNIP_ALIGN}",
-                              f"s_add_u32 s{S_TAB + 2}, s{S_TAB}, s{S_T}",
-                              f"s_addc_u32 s{S_TAB + 3}, s{S_TAB + 1}, 0",
-                              f"s_mov_b32 m0, 0x{GPR_MODE | (16 * sl):x}",
+                    S.extend([f"s_bfe_u32 s{S_T}, s{cur + sl // 2}, 0x{(16 << 16) | (16 * (sl % 2)):x}",
+                              f"s_add_u32 s{S_TAB + 2}, s{S_TAB}, s{S_T}"])
+                    if not full:
+                        S.append(f"s_addc_u32 s{S_TAB + 3}, s{S_TAB + 1}, 0")
+                    S.extend([f"s_mov_b32 m0, 0x{GPR_MODE | (16 * sl):x}",
                               f"s_swappc_b64 s[{S_RET}:{S_RET + 1}], s[{S_TAB + 2}:{S_TAB + 3}]"])
                 S.extend([f"Lsend{h}_{t}{x}_%=:", "s_set_gpr_idx_off"])
             S.append(f"Lrows{h}{x}_%=:")
@@ -250,7 +253,7 @@ def fdec_asm(k, m, probe=None, e16=False):
             S.append("s_waitcnt lgkmcnt(0)")
             if h == 0:
                 # the next half starts at row 0, which must sit in buffer 0
-                S.append(f"s_load_dwordx4 s[{S_COEF1}:{S_COEF1 + 3}], %[cp], 0x0")
+                S.append(f"s_load_dwordx4 s[{S_COEF1}:{S_COEF1 + 3}], %[cp], 0x10")
             for sl in range(8):
                 s = 8 * h + sl
                 if not full:
@@ -275,7 +278,11 @@ def fdec_asm(k, m, probe=None, e16=False):
         return S
 
     if e16:
-        L += ["s_cmp_eq_u32 %[e], 16", "s_cbranch_scc0 Lgen_%="]
+        # the e = 16 copy adds only the low word of a snippet address: taken when no offset
+        # (< 32 KiB) can carry into the high word
+        L += ["s_cmp_eq_u32 %[e], 16", "s_cbranch_scc0 Lgen_%=",
+              f"s_mov_b32 s{S_TAB + 3}, s{S_TAB + 1}", f"s_add_u32 s{S_T}, s{S_TAB}, 0x8000",
+              "s_cbranch_scc1 Lgen_%="]
         L += stage2("f", True)
         L += ["s_branch Ldone_%=", "Lgen_%=:"]
     L += stage2("", False)
