@@ -181,27 +181,27 @@ __global__ void tw_dec_tables_kernel(TwDecTablesArgs a)
         if (t < 12u) ro[a.M + t] = 0u;
     }
     if (e <= 0 || (int32_t)t >= e) return;
-    uint16_t o[48];
-#pragma unroll
-    for (int j = 0; j < 48; ++j) o[j] = 0;
     const uint32_t r0 = p * a.M / a.passes, r1 = min((p + 1u) * a.M / a.passes, (uint32_t)e);
     const uint16_t* col = a.coef2 + ((uint64_t)b * a.dcs + t) * a.dcs;
-    for (uint32_t row = r0; row < r1; ++row) {
-        const uint32_t g = col[row], r = row - r0;
-        uint32_t tt = 0;
+    // entry dwords: [r] = (c0, c1) of sweep 0, [12 + r] = (lam c1, c0 ^ c1) of sweep 1
+    uint32_t* dst = reinterpret_cast<uint32_t*>(a.tw + (((uint64_t)b * a.M + t) * a.passes + p) * 48u);
 #pragma unroll
-        for (int k = 0; k < 16; ++k)
-            if ((g >> k) & 1u) tt ^= a.phi[k];
-        const uint32_t c0 = tt & 255u, c1 = tt >> 8;
-        o[2 * r] = (uint16_t)(c0 << 7);
-        o[2 * r + 1] = (uint16_t)(c1 << 7);
-        o[24 + 2 * r] = (uint16_t)(gf8_mul_11d(a.lam, c1) << 7);
-        o[24 + 2 * r + 1] = (uint16_t)((c0 ^ c1) << 7);
+    for (uint32_t r = 0; r < 12; ++r) {
+        const uint32_t row = r0 + r;
+        uint32_t w0 = 0, w1 = 0;
+        if (row < r1) {
+            const uint32_t g = col[row];
+            uint32_t tt = 0;
+#pragma unroll
+            for (int k = 0; k < 16; ++k)
+                if ((g >> k) & 1u) tt ^= a.phi[k];
+            const uint32_t c0 = tt & 255u, c1 = tt >> 8;
+            w0 = (c0 << 7) | (c1 << 23);
+            w1 = (gf8_mul_11d(a.lam, c1) << 7) | ((c0 ^ c1) << 23);
+        }
+        dst[r] = w0;
+        dst[12 + r] = w1;
     }
-    uint4* dst = reinterpret_cast<uint4*>(a.tw + (((uint64_t)b * a.M + t) * a.passes + p) * 48u);
-    const uint4* src = reinterpret_cast<const uint4*>(o);
-#pragma unroll
-    for (int j = 0; j < 6; ++j) dst[j] = src[j];
 }
 
 }  // namespace
