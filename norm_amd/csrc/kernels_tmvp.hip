@@ -151,9 +151,10 @@ namespace {
 
 // RS16 decode stage 2 on the tower kernel (per-block mode, gen_gf16_tw.hip): block b's inverse
 // A^-1 (coef2, column t = z row t, row s = erased output s) becomes the kernel's snippet table
-// [t][pass][48] with the rows spread over the passes as gf16_tw_offsets spreads an encode's
-// parity rows, and the output rows' byte offsets row_off[b][s] = erased slot s * seg_stride.
-// One thread per (block, column, pass); columns and rows at or past the block's e are not read.
+// [t][sweep][s][2] as gf16_tw_offsets lays out an encode's generator (the kernel spreads the
+// block's e rows over its passes itself), and the output rows' byte offsets row_off[b][s] =
+// erased slot s * seg_stride.  One thread per (block, column, row); columns and rows at or past
+// the block's e are never read.
 __device__ __forceinline__ uint32_t gf8_mul_11d(uint32_t a, uint32_t b)
 {
     uint32_t r = 0;
@@ -169,46 +170,34 @@ __device__ __forceinline__ uint32_t gf8_mul_11d(uint32_t a, uint32_t b)
 __global__ void tw_dec_tables_kernel(TwDecTablesArgs a)
 {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const uint32_t per_blk = a.M * a.passes;
+    const uint32_t per_blk = a.M * a.M;
     if (i >= (uint64_t)a.nblocks * per_blk) return;
     const uint32_t b = (uint32_t)(i / per_blk);
     const uint32_t rem = (uint32_t)(i - (uint64_t)b * per_blk);
-    const uint32_t t = rem / a.passes, p = rem - t * a.passes;
+    const uint32_t t = rem / a.M, row = rem - t * a.M;
     const int32_t e = a.rows[b];
-    if (p == 0) {  // the output row offsets (and 12 padding entries the pass loads may touch)
+    if (t == 0) {  // the output row offsets (and 12 padding entries a pass's loads may touch)
         uint32_t* ro = a.row_off + (uint64_t)b * (a.M + 12u);
-        ro[t] = (int32_t)t < e ? (uint32_t)a.out_slots[(uint64_t)b * a.slots_stride + t] * a.seg_stride : 0u;
-        if (t < 12u) ro[a.M + t] = 0u;
+        ro[row] = (int32_t)row < e ? (uint32_t)a.out_slots[(uint64_t)b * a.slots_stride + row] * a.seg_stride : 0u;
+        if (row < 12u) ro[a.M + row] = 0u;
     }
-    if (e <= 0 || (int32_t)t >= e) return;
-    const uint32_t r0 = p * a.M / a.passes, r1 = min((p + 1u) * a.M / a.passes, (uint32_t)e);
-    const uint16_t* col = a.coef2 + ((uint64_t)b * a.dcs + t) * a.dcs;
-    // entry dwords: [r] = (c0, c1) of sweep 0, [12 + r] = (lam c1, c0 ^ c1) of sweep 1
-    uint32_t* dst = reinterpret_cast<uint32_t*>(a.tw + (((uint64_t)b * a.M + t) * a.passes + p) * 48u);
+    if ((int32_t)t >= e || (int32_t)row >= e) return;
+    const uint32_t g = a.coef2[((uint64_t)b * a.dcs + t) * a.dcs + row];
+    uint32_t tt = 0;
 #pragma unroll
-    for (uint32_t r = 0; r < 12; ++r) {
-        const uint32_t row = r0 + r;
-        uint32_t w0 = 0, w1 = 0;
-        if (row < r1) {
-            const uint32_t g = col[row];
-            uint32_t tt = 0;
-#pragma unroll
-            for (int k = 0; k < 16; ++k)
-                if ((g >> k) & 1u) tt ^= a.phi[k];
-            const uint32_t c0 = tt & 255u, c1 = tt >> 8;
-            w0 = (c0 << 7) | (c1 << 23);
-            w1 = (gf8_mul_11d(a.lam, c1) << 7) | ((c0 ^ c1) << 23);
-        }
-        dst[r] = w0;
-        dst[12 + r] = w1;
-    }
+    for (int k = 0; k < 16; ++k)
+        if ((g >> k) & 1u) tt ^= a.phi[k];
+    const uint32_t c0 = tt & 255u, c1 = tt >> 8;
+    uint32_t* col = reinterpret_cast<uint32_t*>(a.tw + (uint64_t)b * a.tw_block_stride + (uint64_t)t * 4u * a.M);
+    col[row] = (c0 << 7) | (c1 << 23);
+    col[a.M + row] = (gf8_mul_11d(a.lam, c1) << 7) | ((c0 ^ c1) << 23);
 }
 
 }  // namespace
 
 int launch_tw_dec_tables(const TwDecTablesArgs& a, hipStream_t s)
 {
-    const uint64_t n = (uint64_t)a.nblocks * a.M * a.passes;
+    const uint64_t n = (uint64_t)a.nblocks * a.M * a.M;
     if (n == 0) return NFEC_OK;
     hipLaunchKernelGGL(tw_dec_tables_kernel, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, s, a);
     const hipError_t e = hipGetLastError();

@@ -393,7 +393,7 @@ int build_codec(nfec_codec* c)
         // RS16: LDS offsets of the shared-table encode (gen_gf16_t3.hip), 96 bytes per
         // coefficient (C4, k = 4096, m = 256: 104 MB)
         if (wide && use_gf16_t3() && use_gf16_tw()) {
-            std::vector<uint16_t> off((size_t)c->k * gf16_tw_passes(c->m) * 48);
+            std::vector<uint16_t> off(gf16_tw_table_elems(c->k, c->m));
             gf16_tw_offsets(c->gen, c->k, c->m, off.data());
             if ((rc = c->d_twoff.reserve(off.size()))) return rc;
             NFEC_HIP(hipMemcpy(c->d_twoff.p, off.data(), off.size() * 2, hipMemcpyHostToDevice));
@@ -419,7 +419,7 @@ int build_codec(nfec_codec* c)
             std::vector<uint16_t> cm, wm, gm;
             if (mode != 0 && (mode == 1 || pays) && rs16_tmvp_plan(c->k, c->m, c->gen, prod, cm, wm, gm)) {
                 const uint32_t half = c->k / 2, mp = gf16_t3_rows_padded(cw);
-                const size_t one = c->tw ? (size_t)half * gf16_tw_passes(cw) * 48
+                const size_t one = c->tw ? gf16_tw_table_elems(half, cw)
                                          : (size_t)(half + 1) * mp * 48;
                 std::vector<uint16_t> off(3 * one);
                 for (int e = 0; e < 3; ++e) {
@@ -579,7 +579,7 @@ int rs16_tmvp_encode(nfec_codec* c, const nfec_block_batch* b, hipStream_t s)
     int rc;
     const uint32_t mp = gf16_t3_rows_padded(cw);
     const size_t one = (size_t)(half + 1) * mp * 48;
-    const size_t one_tw = (size_t)half * gf16_tw_passes(cw) * 48;
+    const size_t one_tw = gf16_tw_table_elems(half, cw);
     uint32_t shift = 0;
     while ((1u << shift) < cw) ++shift;
     for (uint32_t b0 = 0; b0 < b->nblocks; b0 += sb) {
@@ -886,10 +886,10 @@ int decode_device(nfec_codec* c, const nfec_block_batch* b, const uint16_t* locs
     // RS16 stage 2 (d_E = A^-1 z) on the tower kernel in per-block mode, with the batches stage
     // 1 takes by encode (overwrite, unshortened); tables of M = min(k, m) rows per block
     const uint32_t M2 = std::min(c->k, c->m);
-    const uint32_t P2 = gf16_tw_passes(M2);
+    const size_t tw2_elems = gf16_tw_table_elems(M2, M2);
     const bool tw2 = t3dec && c->tw && diag_knob("NFEC_RS16_TW2", 1) != 0;
     if (tw2) {
-        if ((rc = c->w_tw2.reserve((size_t)sb * M2 * P2 * 48))) return rc;
+        if ((rc = c->w_tw2.reserve((size_t)sb * tw2_elems))) return rc;
         if ((rc = c->w_rowoff.reserve((size_t)sb * (M2 + 12)))) return rc;
     }
     const bool fast = c->kind == NFEC_RS8 && !b->num_data && c->m <= 32 && c->k <= 64 && !force_generic() &&
@@ -1228,8 +1228,8 @@ int decode_device(nfec_codec* c, const nfec_block_batch* b, const uint16_t* locs
                 d.seg_stride = b->seg_stride;
                 d.nblocks = nb;
                 d.M = M2;
-                d.passes = P2;
                 d.tw = c->w_tw2.p;
+                d.tw_block_stride = tw2_elems;
                 d.row_off = c->w_rowoff.p;
                 gf16_tw_field(d.phi, &d.lam);
                 if ((rc = launch_tw_dec_tables(d, s))) return rc;
@@ -1242,7 +1242,7 @@ int decode_device(nfec_codec* c, const nfec_block_batch* b, const uint16_t* locs
                 t.m = M2;
                 t.vec_bytes = vb;
                 t.tw = c->w_tw2.p;
-                t.tw_block_stride = (uint64_t)M2 * P2 * 48;
+                t.tw_block_stride = tw2_elems;
                 t.blk_rows = c->w_rows.p;
                 t.row_off = c->w_rowoff.p;
                 t.row_off_stride = M2 + 12;

@@ -214,8 +214,7 @@ struct Gf16T3Args {
     // column map: column c is read from slot ((c >> col_shift) * col_chunk + (c & col_mask) +
     // col_base) (identity by default); in_slots bounds the slots read (0: k + m)
     uint32_t col_shift = 31, col_mask = 0xFFFFFFFFu, col_chunk = 0, col_base = 0, in_slots = 0;
-    // tower-field kernel (gen_gf16_tw.hip): [k][gf16_tw_passes(m)][48] snippet offsets (gf16_tw_offsets)
-    const uint16_t* tw = nullptr;
+    const uint16_t* tw = nullptr;   // [k][2][m][2] snippet offsets (gf16_tw_offsets)
     // per-block mode (RS16 decode stage 2 on the tower kernel): item groups stay inside one
     // block; block b has its own table (tw + b * tw_block_stride), e = blk_rows[b] rows and
     // columns, and its rows' output byte offsets row_off[b * row_off_stride + r] (from out_base
@@ -263,7 +262,8 @@ int launch_gf16_tw_encode(const Gf16T3Args& a, hipStream_t s);  // NFEC_ENOTSUP:
 bool gf16_tw_covers(const Gf16T3Args& a);
 int launch_gf16_tw_multi(const Gf16T3Args* e, uint32_t n, hipStream_t s);
 void gf16_tw_offsets(const std::vector<uint32_t>& parity_rows, uint32_t k, uint32_t m, uint16_t* out);
-uint32_t gf16_tw_passes(uint32_t m);  // passes of the tower kernel's table (a multiple of 4)
+uint32_t gf16_tw_passes(uint32_t m);  // passes of the tower kernel for m rows (a multiple of 4)
+size_t gf16_tw_table_elems(uint32_t k, uint32_t m);  // u16 elements of a k-column, m-row table
 void gf16_tw_field(uint16_t phi_cols[16], uint32_t* lam);  // the tower isomorphism's constants
 // RS16 decode stage 2 on the tower kernel: per-block snippet tables and output row offsets from
 // the plan's e x e inverses (kernels_tmvp.hip)
@@ -274,8 +274,9 @@ struct TwDecTablesArgs {
     const uint16_t* out_slots = nullptr;  // [b][slots_stride] erased source slots
     uint32_t slots_stride = 0;
     uint32_t seg_stride = 0;          // output segment stride (bytes)
-    uint32_t nblocks = 0, M = 0, passes = 0;  // M rows / columns at most (min(k, m))
-    uint16_t* tw = nullptr;           // [b][M][passes][48]
+    uint32_t nblocks = 0, M = 0;      // M rows / columns at most (min(k, m))
+    uint64_t tw_block_stride = 0;     // u16 elements per block table
+    uint16_t* tw = nullptr;           // [b][gf16_tw_table_elems(M, M)]: [t][sweep][row][2]
     uint32_t* row_off = nullptr;      // [b][M + 12]
     uint16_t phi[16] = {};
     uint32_t lam = 0;

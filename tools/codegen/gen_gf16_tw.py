@@ -441,8 +441,10 @@ def fetch(j, n):
     for p in range(4):
         L.append(f"ds_read_b64 v[{V_S + 2 * p}:{V_S + 2 * p + 1}], v{V_TMP[0]} offset:{base + 512 * (4 * n + p)}")
     o = S_OFF + 12 * n
-    L += [f"s_load_dwordx8 s[{o}:{o + 7}], s[{S_TBN}:{S_TBN + 1}], 0x{48 * n:x}",
-          f"s_load_dwordx4 s[{o + 8}:{o + 11}], s[{S_TBN}:{S_TBN + 1}], 0x{48 * n + 32:x}"]
+    if n == 1:  # the column's sweep-1 entries follow its m sweep-0 rows
+        L += [f"s_add_u32 s{S_TBN}, s{S_TBN}, %[t1off]", f"s_addc_u32 s{S_TBN + 1}, s{S_TBN + 1}, 0"]
+    L += [f"s_load_dwordx8 s[{o}:{o + 7}], s[{S_TBN}:{S_TBN + 1}], 0x0",
+          f"s_load_dwordx4 s[{o + 8}:{o + 11}], s[{S_TBN}:{S_TBN + 1}], 0x20"]
     return L
 
 
@@ -603,7 +605,7 @@ def main():
         asms[v] = "\\n\"\n            \"".join(body())
     FLAGS = ()
     ins = ", ".join(f'[o{i}] "v"(o[{i}])' for i in range(8))
-    common = """[wb] "s"(wb), [ss] "s"(a.seg_stride), [k] "s"(kk), [tw] "s"(tw), [tstep] "s"(tstep), [nr] "s"(nr),
+    common = """[wb] "s"(wb), [ss] "s"(a.seg_stride), [k] "s"(kk), [tw] "s"(tw), [tstep] "s"(tstep), [t1off] "s"(t1off), [nr] "s"(nr),
               [csh] "s"(a.col_shift), [cmk] "s"(a.col_mask), [cck] "s"(cck), [cbb] "s"(cbb),
               [acc] "s"(a.accumulate), [ob] "s"(ob), [ab] "s"(ab), [oslot] "s"(a.out_slot0 + row0),
               [oss] "s"(a.out_seg_stride), [aslot] "s"(a.acc_slot0 + row0), [ass] "s"(a.acc_seg_stride),
@@ -649,6 +651,11 @@ namespace nfec {{
 static_assert(kGf16TwRowsPerPass == {ROWS}u, "gen_gf16_tw.py and nfec_internal.hpp disagree on the rows per pass");
 namespace {{
 
+__device__ __forceinline__ uint32_t gf16_tw_passes_dev(uint32_t m)
+{{
+    return ((m + {ROWS - 1}u) / {ROWS}u + 3u) / 4u * 4u;
+}}
+
 template <int V>
 __device__ __forceinline__ void tw_body(const Gf16T3Args& a, uint32_t wg)
 {{
@@ -677,10 +684,13 @@ __device__ __forceinline__ void tw_body(const Gf16T3Args& a, uint32_t wg)
         rlim = e > 0 ? min(rlim, (uint32_t)e) : 0u;
         kk = min(kk, rlim);
     }}
-    if (quad * 4u * a.m / a.passes >= rlim) return;
+    // the rows in play spread evenly over whole workgroups of four passes (the table holds any
+    // row range); the launch sized the grid for a.m rows, so later workgroups may leave
+    const uint32_t npass = gf16_tw_passes_dev(rlim);
+    if (rlim == 0u || quad * 4u >= npass) return;
     const uint32_t pass = quad * 4u + wave;
-    const uint32_t row0 = pass * a.m / a.passes, row1 = (pass + 1u) * a.m / a.passes;
-    const uint32_t nr = __builtin_amdgcn_readfirstlane(row0 < rlim ? min(row1, rlim) - row0 : 0u);
+    const uint32_t row0 = pass * rlim / npass, row1 = (pass + 1u) * rlim / npass;
+    const uint32_t nr = __builtin_amdgcn_readfirstlane(row1 - row0);
     const uint32_t b0 = pb ? pblk : __builtin_amdgcn_readfirstlane((uint32_t)(f0 / a.vec_bytes));
     const uint8_t* wb = a.base + (uint64_t)b0 * a.block_stride;
     uint32_t o[8];
@@ -697,10 +707,11 @@ __device__ __forceinline__ void tw_body(const Gf16T3Args& a, uint32_t wg)
     }}
     const uint32_t lo = bs::lds_addr(po);
     const uint32_t xl = bs::lds_addr(xch) + lane * 8u;
-    const uint16_t* tw = a.tw + (uint64_t)b0 * (pb ? a.tw_block_stride : 0u) + (uint64_t)pass * {TBL_HALF}u;
+    // table [column][sweep][row][2 entries]: this pass's rows start 2 * row0 elements in
+    const uint16_t* tw = a.tw + (uint64_t)b0 * (pb ? a.tw_block_stride : 0u) + 2u * row0;
     // per-block mode: byte offsets of the pass's output rows (row_off[b][row0 ..]); flat: null
     const uint32_t* rp = pb ? a.row_off + (uint64_t)b0 * a.row_off_stride + row0 : nullptr;
-    const uint32_t tstep = a.passes * {2 * TBL_HALF}u;
+    const uint32_t tstep = 8u * a.m, t1off = 4u * a.m;   // bytes per column; sweep 1's offset
     const uint8_t* ob = a.out_base + (uint64_t)b0 * a.out_block_stride;
     const uint8_t* ab = a.acc_base + (uint64_t)b0 * a.acc_block_stride;
     const uint32_t cck = a.col_chunk * a.seg_stride, cbb = a.col_base * a.seg_stride;
@@ -820,32 +831,31 @@ uint32_t gf16_tw_passes(uint32_t m)
     return ((m + {ROWS - 1}u) / {ROWS}u + 3u) / 4u * 4u;
 }}
 
+size_t gf16_tw_table_elems(uint32_t k, uint32_t m)
+{{
+    return (size_t)k * 4u * m + 32u;   // + the overread of a pass's 12-row entry loads
+}}
+
 // snippet byte offsets of the tower kernel: coefficient g = parity_rows[r][c] maps to
-// phi(g) = c0 + c1 y.  The m rows are spread evenly over gf16_tw_passes(m) passes (pass p:
-// rows [p m / P, (p + 1) m / P), at most {ROWS}); entry block [c][p][48]: sweep 0 (source x0) at
-// 2 r + j = (c0, c1)[j], sweep 1 (source x1) at 24 + 2 r + j = (lam c1, c0 ^ c1)[j], each << {SNIP_ALIGN};
-// unused entries are zero (the empty snippet)
+// phi(g) = c0 + c1 y.  Table [c][sweep][row][2]: sweep 0 (source x0) = (c0, c1), sweep 1
+// (source x1) = (lam c1, c0 ^ c1), each the snippet's byte offset c << {SNIP_ALIGN}.  Rows are
+// contiguous, so the kernel can spread any number of rows over its passes at run time.
 void gf16_tw_offsets(const std::vector<uint32_t>& parity_rows, uint32_t k, uint32_t m, uint16_t* out)
 {{
     const Field& f8 = gf8();
-    const uint32_t passes = gf16_tw_passes(m);
+    for (size_t i = 0; i < gf16_tw_table_elems(k, m); ++i) out[i] = 0;
     for (uint32_t c = 0; c < k; ++c)
-        for (uint32_t p = 0; p < passes; ++p) {{
-            uint16_t* o = out + ((size_t)c * passes + p) * {TBL_HALF}u;
-            for (uint32_t i = 0; i < {TBL_HALF}u; ++i) o[i] = 0;
-            const uint32_t r0 = p * m / passes, r1 = (p + 1) * m / passes;
-            for (uint32_t row = r0; row < r1; ++row) {{
-                const uint32_t r = row - r0;
-                const uint32_t g = parity_rows[(size_t)row * k + c];
-                uint32_t t = 0;
-                for (int i = 0; i < 16; ++i)
-                    if ((g >> i) & 1u) t ^= kPhiCol[i];
-                const uint32_t c0 = t & 255u, c1 = t >> 8;
-                o[2 * r + 0] = (uint16_t)(c0 << {SNIP_ALIGN});
-                o[2 * r + 1] = (uint16_t)(c1 << {SNIP_ALIGN});
-                o[24 + 2 * r + 0] = (uint16_t)(f8.mul(0x{LAM:02x}u, c1) << {SNIP_ALIGN});
-                o[24 + 2 * r + 1] = (uint16_t)((c0 ^ c1) << {SNIP_ALIGN});
-            }}
+        for (uint32_t row = 0; row < m; ++row) {{
+            const uint32_t g = parity_rows[(size_t)row * k + c];
+            uint32_t t = 0;
+            for (int i = 0; i < 16; ++i)
+                if ((g >> i) & 1u) t ^= kPhiCol[i];
+            const uint32_t c0 = t & 255u, c1 = t >> 8;
+            uint16_t* o = out + (size_t)c * 4u * m + 2u * row;
+            o[0] = (uint16_t)(c0 << {SNIP_ALIGN});
+            o[1] = (uint16_t)(c1 << {SNIP_ALIGN});
+            o[2u * m] = (uint16_t)(f8.mul(0x{LAM:02x}u, c1) << {SNIP_ALIGN});
+            o[2u * m + 1] = (uint16_t)((c0 ^ c1) << {SNIP_ALIGN});
         }}
 }}
 
