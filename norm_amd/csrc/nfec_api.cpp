@@ -825,10 +825,14 @@ int decode_device(nfec_codec* c, const nfec_block_batch* b, const uint16_t* locs
     // matrices and the z rows are sized by that, not by m (m >> k codes, e.g. npc's auto mode)
     const uint32_t dcs = c->kind == NFEC_MDP ? c->cs : round_up(std::max(1u, std::min(c->k, c->m)), kRowPad);
     const bool big_plan = c->kind != NFEC_MDP && std::min(c->k, c->m) > 64;
+    // (+ RS16 on the tower kernel: stage 2's per-block snippet tables and row offsets)
     const uint64_t ws_per_block = c->kind == NFEC_MDP
                                       ? (uint64_t)n * c->cs
                                       : (uint64_t)dcs * zstride + ((uint64_t)c->k + dcs) * dcs * c->sym +
-                                            (big_plan ? rs_plan_work_bytes(dcs, c->sym) : 0);
+                                            (big_plan ? rs_plan_work_bytes(dcs, c->sym) : 0) +
+                                            (c->tw ? 2ull * gf16_tw_table_elems(std::min(c->k, c->m), std::min(c->k, c->m)) +
+                                                         4ull * (std::min(c->k, c->m) + 12)
+                                                   : 0);
     const uint32_t sb = std::min(b->nblocks, sub_batch(ws_per_block + 4ull * n + 64));
     int rc;
     if ((rc = c->w_rows.reserve(sb))) return rc;
