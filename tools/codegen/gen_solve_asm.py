@@ -173,7 +173,11 @@ def solve_asm():
         L += [f"s_mov_b32 s{S_T}, 0",
               f"s_set_gpr_idx_on s{S_T}, gpr_idx(SRC0,DST)"]
         for s in range(16):
-            L += [f"s_cmp_le_u32 %[e], {s}", f"s_cbranch_scc1 Lsend{t}_%="]
+            # one bound check per four outputs: mdp_plan_kernel zero-fills the coefficient rows
+            # past e (to cs), so the calls of the outputs s >= e left in a group jump into the
+            # empty snippet, and their accumulators are never stored
+            if s % 4 == 0:
+                L += [f"s_cmp_le_u32 %[e], {s}", f"s_cbranch_scc1 Lsend{t}_%="]
             L += [f"s_bfe_u32 s{S_T}, s{cur + s // 4}, 0x{(8 << 16) | (8 * (s % 4)):x}",
                   f"s_lshl_b32 s{S_T}, s{S_T}, {SNIP_ALIGN}",
                   f"s_add_u32 s{S_TAB + 2}, s{S_TAB}, s{S_T}",
@@ -281,7 +285,11 @@ def mdp_solve_asm():
         L += [f"s_mov_b32 s{S_T}, 0",
               f"s_set_gpr_idx_on s{S_T}, gpr_idx(SRC0,DST)"]
         for s in range(16):
-            L += [f"s_cmp_le_u32 %[e], {s}", f"s_cbranch_scc1 Lsend{t}_%="]
+            # one bound check per four outputs: mdp_plan_kernel zero-fills the coefficient rows
+            # past e (to cs), so the calls of the outputs s >= e left in a group jump into the
+            # empty snippet, and their accumulators are never stored
+            if s % 4 == 0:
+                L += [f"s_cmp_le_u32 %[e], {s}", f"s_cbranch_scc1 Lsend{t}_%="]
             L += [f"s_bfe_u32 s{S_T}, s{cur + s // 4}, 0x{(8 << 16) | (8 * (s % 4)):x}",
                   f"s_lshl_b32 s{S_T}, s{S_T}, {SNIP_ALIGN}",
                   f"s_add_u32 s{S_TAB + 2}, s{S_TAB}, s{S_T}",
