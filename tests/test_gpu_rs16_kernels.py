@@ -68,3 +68,32 @@ def test_rs16_decode_both_kernels(orc, monkeypatch, tw, k, m, vec, nb, es):
     torch.cuda.synchronize()
     assert np.array_equal(st.cpu().numpy(), st_ref)
     assert np.array_equal(dev.cpu().numpy(), ref)
+
+
+@pytest.mark.parametrize("k,m,vec,counts", [
+    (40, 10, 72, [0, 1, 10, 3, 10, 0, 7]),      # e from 0 to M = min(k, m) in one batch
+    (30, 12, 4104, [12, 1, 5]),                 # segments past one 4 KiB item group (two per block)
+    (12, 30, 64, [12, 0, 11, 6]),               # k < m: M = k
+])
+def test_rs16_decode_per_block_rows(orc, monkeypatch, k, m, vec, counts):
+    """decode stage 2 on the tower kernel in per-block mode: each block's own e (rows and
+    columns), blocks with nothing to repair, several item groups per block"""
+    nb = len(counts)
+    enc, dec = _codecs(monkeypatch, "1", k, m, vec)
+    host = orc.encode_blocks(NFEC_RS16, k, m, vec, orc.make_blocks(k, m, vec, nb))
+    locs = np.zeros((nb, m), np.uint16)
+    cnt = np.zeros(nb, np.uint16)
+    for b, e in enumerate(counts):
+        if e:
+            src = orc.erasure_pattern(b + 5, k, e)
+            locs[b, :e] = src
+            host[b, src, :] = 0
+        cnt[b] = e
+    ref = host.copy()
+    st_ref = orc.decode_blocks(NFEC_RS16, k, m, vec, ref, locs, cnt)
+    dev = torch.from_numpy(host).cuda()
+    st = dec.decode_blocks(dev, torch.from_numpy(locs.astype(np.int16)).cuda(),
+                           torch.from_numpy(cnt.astype(np.int16)).cuda())
+    torch.cuda.synchronize()
+    assert np.array_equal(st.cpu().numpy(), st_ref)
+    assert np.array_equal(dev.cpu().numpy(), ref)
