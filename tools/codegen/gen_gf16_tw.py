@@ -330,7 +330,9 @@ def snippet_body(c):
 
 
 def snippets():
-    out = []
+    # 64 KiB-aligned table start: a snippet address is then the table address's high half
+    # packed with the 16-bit entry (s_pack_*_b32_b16), with no add (the specialised loops)
+    out = [".p2align 16"]
     for c in range(256):
         out.append(f".p2align {SNIP_ALIGN}")
         if c == 0:
@@ -356,18 +358,23 @@ def entry(n, r, j):
     return S_OFF + 12 * n + r, j
 
 
-def call(n, r, j, carry=True):
-    """jump into the snippet of entry (n, r, j), target accumulators 16 r + 8 j; carry=False
-    (the specialised loops): the table does not straddle a 4 GiB boundary, so the target's
-    high word is set once (s[S_TGT + 1] = s[S_SNIP + 1]) and only the low word is added"""
+def call(n, r, j, generic=True):
+    """jump into the snippet of entry (n, r, j), target accumulators 16 r + 8 j.  generic=False
+    (the specialised loops, taken when the table sits at a 64 KiB boundary): the target's high
+    word is set once (s[S_TGT + 1] = s[S_SNIP + 1]) and its low word is the table address's
+    high half packed with the entry; generic: extract the entry, add with carry"""
     dw, half = entry(n, r, j)
     if "empty" in FLAGS:
-        first = f"s_mov_b32 s{S_T1}, 0"
+        L = [f"s_mov_b32 s{S_T1}, 0", f"s_add_u32 s{S_TGT}, s{S_SNIP}, s{S_T1}"]
+        if generic:
+            L.append(f"s_addc_u32 s{S_TGT + 1}, s{S_SNIP + 1}, 0")
+    elif generic:
+        L = [f"s_bfe_u32 s{S_T1}, s{dw}, 0x{(16 << 16) | (16 * half):x}",
+             f"s_add_u32 s{S_TGT}, s{S_SNIP}, s{S_T1}",
+             f"s_addc_u32 s{S_TGT + 1}, s{S_SNIP + 1}, 0"]
     else:
-        first = f"s_bfe_u32 s{S_T1}, s{dw}, 0x{(16 << 16) | (16 * half):x}"
-    L = [first, f"s_add_u32 s{S_TGT}, s{S_SNIP}, s{S_T1}"]
-    if carry:
-        L.append(f"s_addc_u32 s{S_TGT + 1}, s{S_SNIP + 1}, 0")
+        op = "s_pack_lh_b32_b16" if half == 0 else "s_pack_hh_b32_b16"
+        L = [f"{op} s{S_TGT}, s{dw}, s{S_SNIP}"]
     return L + [f"s_mov_b32 m0, 0x{GPR_MODE | (16 * r + 8 * j):x}",
                 f"s_swappc_b64 s[{S_RET}:{S_RET + 1}], s[{S_TGT}:{S_TGT + 1}]"]
 
@@ -402,7 +409,7 @@ S_TB = 96                        # 2: table base (this pass's entries of column 
 S_TBN = 98                       # 2: table address of the column being fetched
 S_LAST4 = 99
 XCH_BUF = 4 * 8 * 64 * 8         # bytes per exchange buffer (4 columns)
-SPECIAL_ROWS = (11, 10, 9, 8)    # pass row counts with their own (unchecked) step loop
+SPECIAL_ROWS = (11, 10, 9, 8, 7, 6)   # pass row counts with their own (unchecked) step loop
 
 
 def col_offset():
@@ -513,10 +520,10 @@ def body():
         L.append(f"v_mov_b32 v{v}, 0")
     L += [f"s_cmp_lt_u32 s{S_C}, %[k]", "s_cbranch_scc0 Lnl0_%="]
     L += col_offset() + loads()
-    # the specialised loops add only the low word of a snippet address: taken when no entry
-    # (< 32 KiB) can carry into the high word (else the generic loop, which carries)
+    # the specialised loops pack a snippet address from the table address's high half and the
+    # entry: taken when the table starts at a 64 KiB boundary in memory (else the generic loop)
     L += ["Lnl0_%=:", f"s_mov_b32 s{S_TGT + 1}, s{S_SNIP + 1}",
-          f"s_add_u32 s{S_T0}, s{S_SNIP}, 0x8000", "s_cbranch_scc1 Lstepg_%="]
+          f"s_and_b32 s{S_T0}, s{S_SNIP}, 0xffff", f"s_cmp_lg_u32 s{S_T0}, 0", "s_cbranch_scc1 Lstepg_%="]
     for nr in SPECIAL_ROWS:
         L += [f"s_cmp_eq_u32 %[nr], {nr}", f"s_cbranch_scc1 Lstepr{nr}_%="]
     L.append("s_branch Lstepg_%=")
