@@ -93,7 +93,9 @@ def all_tables(w):
 
 def snippets(regs):
     A, B = regs
-    out = []
+    # 64 KiB-aligned table start: in the e = 16 solve a snippet address's low word is the table
+    # address's high half packed with the u16 offset (s_pack_*_b32_b16), no extract, no add
+    out = [".p2align 16"]
     for c in range(256):
         out.append(f".p2align {SNIP_ALIGN}")
         if c == 0:
@@ -241,10 +243,13 @@ def fdec_asm(k, m, probe=None, e16=False):
                     s = 8 * h + sl
                     if not full:
                         S.extend([f"s_cmp_le_u32 %[e], {s}", f"s_cbranch_scc1 Lsend{h}_{t}{x}_%="])
-                    S.extend([f"s_bfe_u32 s{S_T}, s{cur + sl // 2}, 0x{(16 << 16) | (16 * (sl % 2)):x}",
-                              f"s_add_u32 s{S_TAB + 2}, s{S_TAB}, s{S_T}"])
-                    if not full:
-                        S.append(f"s_addc_u32 s{S_TAB + 3}, s{S_TAB + 1}, 0")
+                    if full:
+                        op = "s_pack_lh_b32_b16" if sl % 2 == 0 else "s_pack_hh_b32_b16"
+                        S.append(f"{op} s{S_TAB + 2}, s{cur + sl // 2}, s{S_TAB}")
+                    else:
+                        S.extend([f"s_bfe_u32 s{S_T}, s{cur + sl // 2}, 0x{(16 << 16) | (16 * (sl % 2)):x}",
+                                  f"s_add_u32 s{S_TAB + 2}, s{S_TAB}, s{S_T}",
+                                  f"s_addc_u32 s{S_TAB + 3}, s{S_TAB + 1}, 0"])
                     S.extend([f"s_mov_b32 m0, 0x{GPR_MODE | (16 * sl):x}",
                               f"s_swappc_b64 s[{S_RET}:{S_RET + 1}], s[{S_TAB + 2}:{S_TAB + 3}]"])
                 S.extend([f"Lsend{h}_{t}{x}_%=:", "s_set_gpr_idx_off"])
@@ -278,11 +283,11 @@ def fdec_asm(k, m, probe=None, e16=False):
         return S
 
     if e16:
-        # the e = 16 copy adds only the low word of a snippet address: taken when no offset
-        # (< 32 KiB) can carry into the high word
+        # the e = 16 copy packs a snippet address from the table address's high half and the
+        # offset: taken when the table starts at a 64 KiB boundary in memory
         L += ["s_cmp_eq_u32 %[e], 16", "s_cbranch_scc0 Lgen_%=",
-              f"s_mov_b32 s{S_TAB + 3}, s{S_TAB + 1}", f"s_add_u32 s{S_T}, s{S_TAB}, 0x8000",
-              "s_cbranch_scc1 Lgen_%="]
+              f"s_mov_b32 s{S_TAB + 3}, s{S_TAB + 1}", f"s_and_b32 s{S_T}, s{S_TAB}, 0xffff",
+              f"s_cmp_lg_u32 s{S_T}, 0", "s_cbranch_scc1 Lgen_%="]
         L += stage2("f", True)
         L += ["s_branch Ldone_%=", "Lgen_%=:"]
     L += stage2("", False)
