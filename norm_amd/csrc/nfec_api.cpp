@@ -1499,6 +1499,20 @@ int nfec_encode_segment(nfec_codec* c, uint32_t segment_id, const void* data, vo
             out_first = c->m + 1;
         }
         if ((rc = launch_gf8_matmul(a, false, st))) return rc;
+    } else if (c->tw && (c->vec % 8) == 0) {
+        // the tower kernel over one column: the generator column segment_id is its own block
+        // of the codec's table; parity slots 1..m, accumulated (normEncoderRS16.cpp:472-482)
+        Gf16T3Args t;
+        t.base = d;
+        t.block_stride = (uint64_t)(c->m + 1) * pc.stride;
+        t.seg_stride = pc.stride;
+        t.nblocks = 1;
+        t.k = 1;
+        t.m = c->m;
+        t.vec_bytes = c->vec;
+        t.tw = c->d_twoff.p + (size_t)segment_id * 4u * c->m;
+        t.accumulate = 1;
+        if ((rc = launch_gf16_tw_encode(t, st))) return rc;
     } else {
         Gf16MatmulArgs a;
         a.in_base = d;
@@ -1554,13 +1568,31 @@ int nfec_decode_vectors(nfec_codec* c, void* const* vectors, uint32_t num_data, 
     NFEC_HIP(hipMemcpyAsync(pc.dev + 8, pc.pin + 8, pc.data0 - 8 + (size_t)nslots * pc.stride, hipMemcpyHostToDevice, st));
     uint16_t* dl = reinterpret_cast<uint16_t*>(pc.dev + 8);
     int32_t* dstatus = reinterpret_cast<int32_t*>(pc.dev);
+    // The reference XORs the repair into the erased buffers (accumulate).  NORM hands them in
+    // zero-filled (normObject.cpp:1579), and then overwriting is the same; a full block
+    // (numData = k) with zero erased buffers therefore takes the batch fast paths (fused RS8
+    // repair, RS16 stages on the tower kernel), anything else the general ones.
+    bool zero_erased = true;
+    for (uint32_t i = 0; i < erasure_count && zero_erased; ++i) {
+        const uint32_t s = erasure_locs[i];
+        if (s >= num_data || !vectors[s]) continue;
+        const uint8_t* v = static_cast<const uint8_t*>(vectors[s]);
+        uint64_t acc = 0, w;
+        size_t j = 0;
+        for (; j + 8 <= c->vec; j += 8) {
+            std::memcpy(&w, v + j, 8);
+            acc |= w;
+        }
+        for (; j < c->vec; ++j) acc |= v[j];
+        zero_erased = acc == 0;
+    }
     nfec_block_batch b{};
     b.blocks = pc.dev + pc.data0;
     b.block_stride = (uint64_t)(c->k + c->m) * pc.stride;
     b.seg_stride = pc.stride;
     b.nblocks = 1;
-    b.num_data = dl + c->m + 1;
-    b.flags = c->kind == NFEC_MDP ? 0 : NFEC_ACCUMULATE;
+    b.num_data = num_data == c->k ? nullptr : dl + c->m + 1;
+    b.flags = (c->kind == NFEC_MDP || zero_erased) ? 0 : NFEC_ACCUMULATE;
     if ((rc = decode_device(c, &b, dl, c->m, dl + c->m, dstatus, st, true))) return rc;
     // status and the source slots in one copy (the meta bytes between them ride along)
     NFEC_HIP(hipMemcpyAsync(pc.pin, pc.dev, pc.data0 + (size_t)num_data * pc.stride, hipMemcpyDeviceToHost, st));

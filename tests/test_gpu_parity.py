@@ -297,6 +297,42 @@ def test_per_call_reference_surface(orc, kind):
         assert bytes(vlist[s]) == ref[s].tobytes()
 
 
+@pytest.mark.parametrize("kind", [NFEC_RS8, NFEC_RS16])
+@pytest.mark.parametrize("vec,nd,junk", [(64, 20, False), (64, 20, True), (66, 20, False), (64, 13, False),
+                                          (1408, 20, True)])
+def test_per_call_paths(orc, kind, vec, nd, junk):
+    """The per-call Encode/Decode take the batch fast paths for a full block with zero-filled
+    erased buffers (tower kernel / fused repair, overwrite) and the general ones otherwise:
+    a shortened block (numData < k), non-zero erased buffers (the reference XORs the repair
+    into them, normEncoderRS8.cpp:728-755), an odd-multiple vector size (vec % 8 != 0)."""
+    k, m = 20, 6
+    enc, dec = _codecs(kind, k, m, vec)
+    blk = orc.make_blocks(k, m, vec, 1, num_data=np.array([nd], np.uint16))[0]
+    ref = orc.encode_blocks(kind, k, m, vec, blk[None].copy(), np.array([nd], np.uint16))[0]
+    parity = [bytearray(vec) for _ in range(m)]
+    for s in range(nd):
+        enc.Encode(s, blk[s, :vec].tobytes(), parity)
+    assert all(bytes(parity[i]) == ref[nd + i, :vec].tobytes() for i in range(m))
+    vecs = [bytearray(ref[s, :vec].tobytes()) for s in range(nd + m)]
+    erased = [0, 3, nd - 1, nd + 1]
+    rng = np.random.default_rng(7)
+    noise = {}
+    for s in erased:
+        noise[s] = rng.integers(0, 256, vec, dtype=np.uint8).tobytes() if junk else bytes(vec)
+        vecs[s] = bytearray(noise[s])
+    assert dec.Decode(vecs, nd, len(erased), erased) == len(erased)
+    nbytes = vec if kind == NFEC_RS8 else vec // 2 * 2
+    for s in range(nd):
+        want = bytearray(ref[s, :vec].tobytes())
+        if s in noise:  # accumulate: repair XOR what the buffer held (odd RS16 last byte: untouched)
+            n = np.frombuffer(noise[s], np.uint8)
+            w = np.frombuffer(bytes(want), np.uint8).copy()
+            w[:nbytes] ^= n[:nbytes]
+            w[nbytes:] = n[nbytes:]
+            want = bytearray(w.tobytes())
+        assert bytes(vecs[s]) == bytes(want), s
+
+
 def test_host_batch_paths_match_device(orc):
     k, m, vec, nb = 64, 32, 1400, 40
     enc, dec = _codecs(NFEC_RS8, k, m, vec)
