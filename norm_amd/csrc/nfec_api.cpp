@@ -891,7 +891,9 @@ int decode_device(nfec_codec* c, const nfec_block_batch* b, const uint16_t* locs
     // 1 takes by encode (overwrite, unshortened); tables of M = min(k, m) rows per block
     const uint32_t M2 = std::min(c->k, c->m);
     const size_t tw2_elems = gf16_tw_table_elems(M2, M2);
-    const bool tw2 = t3dec && c->tw && diag_knob("NFEC_RS16_TW2", 1) != 0;
+    // (the per-block row offsets are 32-bit buffer offsets of erased source slots: slot * stride)
+    const bool tw2 = t3dec && c->tw && diag_knob("NFEC_RS16_TW2", 1) != 0 &&
+                     (uint64_t)c->k * b->seg_stride + c->vec < (1ull << 31);
     if (tw2) {
         if ((rc = c->w_tw2.reserve((size_t)sb * tw2_elems))) return rc;
         if ((rc = c->w_rowoff.reserve((size_t)sb * (M2 + 12)))) return rc;
