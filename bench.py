@@ -85,9 +85,9 @@ def parse():
     p.add_argument("--host-steps", type=int, default=2,
                    help="also time K steps with blocks in pinned host memory (PCIe-inclusive, reported "
                         "under 'host_resident'; never the headline value; 0: skip)")
-    p.add_argument("--host-blocks", type=int, default=16384,
+    p.add_argument("--host-blocks", type=int, default=0,
                    help="blocks per GPU in the pinned host batch of --host-steps (the first ones of the "
-                        "device batch; the rate is link-bound, so a quarter of the batch measures it)")
+                        "device batch; 0: all of them, the headline workload)")
     return p.parse_args()
 
 
