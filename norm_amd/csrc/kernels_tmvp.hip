@@ -153,8 +153,8 @@ namespace {
 // A^-1 (coef2, column t = z row t, row s = erased output s) becomes the kernel's snippet table
 // [t][sweep][s][2] as gf16_tw_offsets lays out an encode's generator (the kernel spreads the
 // block's e rows over its passes itself), and the output rows' byte offsets row_off[b][s] =
-// erased slot s * seg_stride.  One thread per (block, column, row); columns and rows at or past
-// the block's e are never read.
+// erased slot s * seg_stride.  One workgroup per block; columns and rows at or past the block's
+// e are never read.
 __device__ __forceinline__ uint32_t gf8_mul_11d(uint32_t a, uint32_t b)
 {
     uint32_t r = 0;
@@ -167,39 +167,36 @@ __device__ __forceinline__ uint32_t gf8_mul_11d(uint32_t a, uint32_t b)
     return r;
 }
 
-__global__ void tw_dec_tables_kernel(TwDecTablesArgs a)
+__global__ __launch_bounds__(256) void tw_dec_tables_kernel(TwDecTablesArgs a)
 {
-    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const uint32_t per_blk = a.M * a.M;
-    if (i >= (uint64_t)a.nblocks * per_blk) return;
-    const uint32_t b = (uint32_t)(i / per_blk);
-    const uint32_t rem = (uint32_t)(i - (uint64_t)b * per_blk);
-    const uint32_t t = rem / a.M, row = rem - t * a.M;
+    // one workgroup per block: the e x e entries and the M + 12 row offsets
+    const uint32_t b = blockIdx.x;
     const int32_t e = a.rows[b];
-    if (t == 0) {  // the output row offsets (and 12 padding entries a pass's loads may touch)
-        uint32_t* ro = a.row_off + (uint64_t)b * (a.M + 12u);
-        ro[row] = (int32_t)row < e ? (uint32_t)a.out_slots[(uint64_t)b * a.slots_stride + row] * a.seg_stride : 0u;
-        if (row < 12u) ro[a.M + row] = 0u;
-    }
-    if ((int32_t)t >= e || (int32_t)row >= e) return;
-    const uint32_t g = a.coef2[((uint64_t)b * a.dcs + t) * a.dcs + row];
-    uint32_t tt = 0;
+    uint32_t* ro = a.row_off + (uint64_t)b * (a.M + 12u);
+    for (uint32_t r = threadIdx.x; r < a.M + 12u; r += blockDim.x)
+        ro[r] = (int32_t)r < e ? (uint32_t)a.out_slots[(uint64_t)b * a.slots_stride + r] * a.seg_stride : 0u;
+    if (e <= 0) return;
+    const uint32_t ue = (uint32_t)e;
+    for (uint32_t idx = threadIdx.x; idx < ue * ue; idx += blockDim.x) {
+        const uint32_t t = idx / ue, row = idx - t * ue;
+        const uint32_t g = a.coef2[((uint64_t)b * a.dcs + t) * a.dcs + row];
+        uint32_t tt = 0;
 #pragma unroll
-    for (int k = 0; k < 16; ++k)
-        if ((g >> k) & 1u) tt ^= a.phi[k];
-    const uint32_t c0 = tt & 255u, c1 = tt >> 8;
-    uint32_t* col = reinterpret_cast<uint32_t*>(a.tw + (uint64_t)b * a.tw_block_stride + (uint64_t)t * 4u * a.M);
-    col[row] = (c0 << 7) | (c1 << 23);
-    col[a.M + row] = (gf8_mul_11d(a.lam, c1) << 7) | ((c0 ^ c1) << 23);
+        for (int k = 0; k < 16; ++k)
+            if ((g >> k) & 1u) tt ^= a.phi[k];
+        const uint32_t c0 = tt & 255u, c1 = tt >> 8;
+        uint32_t* col = reinterpret_cast<uint32_t*>(a.tw + (uint64_t)b * a.tw_block_stride + (uint64_t)t * 4u * a.M);
+        col[row] = (c0 << 7) | (c1 << 23);
+        col[a.M + row] = (gf8_mul_11d(a.lam, c1) << 7) | ((c0 ^ c1) << 23);
+    }
 }
 
 }  // namespace
 
 int launch_tw_dec_tables(const TwDecTablesArgs& a, hipStream_t s)
 {
-    const uint64_t n = (uint64_t)a.nblocks * a.M * a.M;
-    if (n == 0) return NFEC_OK;
-    hipLaunchKernelGGL(tw_dec_tables_kernel, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, s, a);
+    if (a.nblocks == 0 || a.M == 0) return NFEC_OK;
+    hipLaunchKernelGGL(tw_dec_tables_kernel, dim3(a.nblocks), dim3(256), 0, s, a);
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? NFEC_OK : hip_fail(e, "tw decode tables launch");
 }
