@@ -70,13 +70,14 @@ struct DevBuf {
 constexpr uint32_t kRowPad = 32;       // coefficient rows padded (kernel row chunk multiple)
 // decode blocks per planning pass: bounds the workspace (stage-1 rows z, plan matrices).
 // Larger passes measured faster (fewer, fuller launches: 16k -> 64k blocks took
-// decode from 2.92 to 2.77 ms per 64k blocks), so a pass is as large as 4 GiB of z allows.
+// decode from 2.92 to 2.77 ms per 64k blocks), so a pass is as large as 8 GiB of workspace
+// allows (3 % of an MI355X's 288 GB).
 // NFEC_SUBBATCH overrides (A/B runs, diagnostic library).
 static uint32_t sub_batch(uint64_t ws_bytes_per_block)
 {
     static const long env = diag_knob("NFEC_SUBBATCH", 0, 0, 1L << 20);
     if (env > 0) return (uint32_t)std::max(256L, std::min(env, 1L << 20));
-    const uint64_t cap = (4ull << 30) / std::max<uint64_t>(ws_bytes_per_block, 1);
+    const uint64_t cap = (8ull << 30) / std::max<uint64_t>(ws_bytes_per_block, 1);
     return (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(65536, cap));
 }
 
@@ -833,7 +834,10 @@ int decode_device(nfec_codec* c, const nfec_block_batch* b, const uint16_t* locs
                                             (c->tw ? 2ull * gf16_tw_table_elems(std::min(c->k, c->m), std::min(c->k, c->m)) +
                                                          4ull * (std::min(c->k, c->m) + 12)
                                                    : 0);
-    const uint32_t sb = std::min(b->nblocks, sub_batch(ws_per_block + 4ull * n + 64));
+    // passes of equal size, so no launch runs a small tail batch
+    const uint32_t cap = std::min(b->nblocks, sub_batch(ws_per_block + 4ull * n + 64));
+    const uint32_t npass = (b->nblocks + cap - 1) / std::max(cap, 1u);
+    const uint32_t sb = std::max(1u, (b->nblocks + npass - 1) / std::max(npass, 1u));
     int rc;
     if ((rc = c->w_rows.reserve(sb))) return rc;
     if ((rc = c->w_cols.reserve(sb))) return rc;
