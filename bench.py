@@ -87,7 +87,7 @@ def parse():
                         "under 'host_resident'; never the headline value; 0: skip)")
     p.add_argument("--host-blocks", type=int, default=0,
                    help="blocks per GPU in the pinned host batch of --host-steps (the first ones of the "
-                        "device batch; 0: all of them, the headline workload)")
+                        "device batch; 0: all of them at N = 1, a quarter per rank at N > 1)")
     return p.parse_args()
 
 
@@ -240,7 +240,10 @@ def main():
     if a.host_steps > 0:
         import numpy as np
 
-        hb = min(nb, a.host_blocks) if a.host_blocks > 0 else nb
+        # default: the whole batch on one GPU; a quarter per rank when several ranks pin host
+        # memory at once (8 ranks x 8.8 GB of page-locked buffers is more than a node may grant)
+        default_hb = nb if world == 1 else max(1, nb // 4)
+        hb = min(nb, a.host_blocks) if a.host_blocks > 0 else default_hb
         hblocks = torch.empty((hb,) + tuple(blocks.shape[1:]), dtype=torch.uint8, pin_memory=True)
         hblocks.copy_(blocks[:hb])
         hnp = hblocks.numpy()
