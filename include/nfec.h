@@ -7,7 +7,7 @@
  * compute path behind this header (a missing/failed GPU yields NFEC_EDEVICE).
  *
  * Reference interfaces each entry replaces (paths in USNavalResearchLaboratory/norm):
- *   nfec_codec_create     NormEncoderRS8::Init   src/common/normEncoderRS8.cpp:400-462
+ *   nfec_codec_create(_ex) NormEncoderRS8::Init  src/common/normEncoderRS8.cpp:400-462
  *                         NormDecoderRS8::Init   src/common/normEncoderRS8.cpp:542-649
  *                         NormEncoderRS16::Init  src/common/normEncoderRS16.cpp:399-461
  *                         NormEncoderMDP::Init   src/common/normEncoderMDP.cpp:56-84
@@ -97,6 +97,10 @@ typedef struct nfec_block_batch {
 
 /* ---- version / device ---- */
 int nfec_abi_version(void);
+/* SHA-256 (hex) of the sources this library was built from: the files of norm_amd/csrc, then the
+ * .h files of include and include/norm_fec, each list sorted by path, contents concatenated
+ * (norm_amd/Makefile). */
+const char* nfec_build_id(void);
 /* number of visible gfx950 devices (0 when none) */
 int nfec_device_count(void);
 /* human-readable message for the last error on this thread */
@@ -111,6 +115,36 @@ int nfec_build_generator(int kind, uint32_t num_data, uint32_t num_parity, void*
 /* ---- codec lifecycle ---- */
 int nfec_codec_create(int device, int kind, uint32_t num_data, uint32_t num_parity,
                       uint32_t vector_size, nfec_codec** out);
+
+/* Codec options (nfec_codec_config.flags): correct alternatives of the RS16 kernels, chosen per
+ * codec (the tests run both; the defaults are the faster ones). */
+enum {
+    NFEC_OPT_RS16_SHARED_TABLES = 1u << 0, /* RS16 products on the shared-LDS-table kernel
+                                              instead of the tower-field one */
+    NFEC_OPT_RS16_TOEPLITZ_OFF = 1u << 1,  /* RS16 encode never uses the Toeplitz split */
+    NFEC_OPT_RS16_TOEPLITZ_ON = 1u << 2    /* ... uses it whenever the shape allows it, not
+                                              only where it needs fewer passes */
+};
+
+/* One codec over one or several GPUs of a node.  With several devices the codec holds the
+ * generator on each (one full codec per device; a device may be listed twice, which gives two
+ * independent pipelines on it) and stripes every host batch (nfec_*_host, nfec_*_host_vectors
+ * and their async forms) over them in contiguous block ranges [i*B/N, (i+1)*B/N), one host
+ * thread and one staging pipeline per device, no exchange between the ranges: the in-process
+ * form of SURVEY 8e's block striping for single-process callers such as one NORM session
+ * (normSession.cpp:834-889) or npc (normPrecode.cpp:588-880).  A device batch (nfec_encode /
+ * nfec_decode) runs on the first listed device that holds it (NFEC_EINVAL when none does);
+ * per-call work (nfec_encode_segment / nfec_decode_vectors) on the first device. */
+typedef struct nfec_codec_config {
+    int32_t kind;             /* NFEC_RS8 / NFEC_RS16 / NFEC_MDP */
+    uint32_t num_data, num_parity, vector_size;
+    const int32_t* devices;   /* HIP device ordinals (NULL with num_devices 0: device 0) */
+    uint32_t num_devices;     /* 0 or 1: one device; at most 64 */
+    uint32_t flags;           /* NFEC_OPT_* */
+} nfec_codec_config;
+int nfec_codec_create_ex(const nfec_codec_config* config, nfec_codec** out);
+/* Number of devices of a codec; their ordinals go to devices[0 .. min(n, cap)) when non-NULL. */
+int nfec_codec_num_devices(const nfec_codec* codec, int32_t* devices, uint32_t cap);
 void nfec_codec_destroy(nfec_codec* codec);
 int nfec_codec_get_info(const nfec_codec* codec, nfec_codec_info* out);
 /* Encode paths the codec chose at creation (bit mask, < 0 on error):

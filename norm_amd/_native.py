@@ -19,6 +19,7 @@ NFEC_RS8, NFEC_RS16, NFEC_MDP = 1, 2, 3
 NFEC_OK, NFEC_EINVAL, NFEC_ENOMEM, NFEC_EDEVICE, NFEC_ERANGE, NFEC_ENOTSUP = 0, -1, -2, -3, -4, -5
 NFEC_ACCUMULATE = 1
 NFEC_FEATURE_RS16_TOEPLITZ = 1
+NFEC_OPT_RS16_SHARED_TABLES, NFEC_OPT_RS16_TOEPLITZ_OFF, NFEC_OPT_RS16_TOEPLITZ_ON = 1, 2, 4
 
 
 class NfecError(RuntimeError):
@@ -47,6 +48,18 @@ class CodecInfo(ctypes.Structure):
         ("num_parity", ctypes.c_uint32),
         ("vector_size", ctypes.c_uint32),
         ("symbol_bytes", ctypes.c_uint32),
+    ]
+
+
+class CodecConfig(ctypes.Structure):
+    _fields_ = [
+        ("kind", ctypes.c_int32),
+        ("num_data", ctypes.c_uint32),
+        ("num_parity", ctypes.c_uint32),
+        ("vector_size", ctypes.c_uint32),
+        ("devices", ctypes.POINTER(ctypes.c_int32)),
+        ("num_devices", ctypes.c_uint32),
+        ("flags", ctypes.c_uint32),
     ]
 
 
@@ -101,10 +114,13 @@ _U64 = ctypes.c_uint64
 _I = ctypes.c_int
 _SIGS = {
     "nfec_abi_version": (_I, []),
+    "nfec_build_id": (ctypes.c_char_p, []),
     "nfec_device_count": (_I, []),
     "nfec_last_error": (ctypes.c_char_p, []),
     "nfec_build_generator": (_I, [_I, _U32, _U32, _P, ctypes.c_size_t]),
     "nfec_codec_create": (_I, [_I, _I, _U32, _U32, _U32, ctypes.POINTER(_P)]),
+    "nfec_codec_create_ex": (_I, [ctypes.POINTER(CodecConfig), ctypes.POINTER(_P)]),
+    "nfec_codec_num_devices": (_I, [_P, ctypes.POINTER(ctypes.c_int32), _U32]),
     "nfec_codec_destroy": (None, [_P]),
     "nfec_codec_get_info": (_I, [_P, ctypes.POINTER(CodecInfo)]),
     "nfec_codec_features": (_I, [_P]),
@@ -172,6 +188,22 @@ def check(rc, what):
     if rc < 0:
         raise NfecError(rc, what)
     return rc
+
+
+def source_build_id(root=None):
+    """SHA-256 of the library's sources in this tree, computed as norm_amd/Makefile computes
+    nfec_build_id(): csrc/* then include/*.h and include/norm_fec/*.h, each sorted by path."""
+    import glob
+    import hashlib
+
+    root = root or os.path.dirname(_HERE)
+    csrc = sorted(p for p in glob.glob(os.path.join(root, "norm_amd", "csrc", "*")) if os.path.isfile(p))
+    inc = sorted(glob.glob(os.path.join(root, "include", "*.h")) + glob.glob(os.path.join(root, "include", "norm_fec", "*.h")))
+    h = hashlib.sha256()
+    for path in csrc + inc:
+        with open(path, "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()
 
 
 def declared_symbols():

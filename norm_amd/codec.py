@@ -103,17 +103,28 @@ def _batch_struct(blocks, num_data, accumulate):
 
 
 class _Codec:
+    """device: the GPU; devices: several GPUs (or one GPU listed several times) for one codec that
+    stripes host batches over them (nfec_codec_create_ex); options: NFEC_OPT_* flags."""
     KIND = None
 
-    def __init__(self, device=0):
+    def __init__(self, device=0, devices=None, options=0):
         self.device = device
+        self.devices = list(devices) if devices else [device]
+        self.options = options
         self._h = ctypes.c_void_p()
         self.ndata = self.npar = self.vector_size = 0
 
     # -- reference surface --
     def Init(self, numData, numParity, vectorSize):
         self.Destroy()
-        rc = N.lib().nfec_codec_create(self.device, self.KIND, numData, numParity, vectorSize, ctypes.byref(self._h))
+        cfg = N.CodecConfig()
+        cfg.kind = self.KIND
+        cfg.num_data, cfg.num_parity, cfg.vector_size = numData, numParity, vectorSize
+        devs = (ctypes.c_int32 * len(self.devices))(*self.devices)
+        cfg.devices = ctypes.cast(devs, ctypes.POINTER(ctypes.c_int32))
+        cfg.num_devices = len(self.devices)
+        cfg.flags = self.options
+        rc = N.lib().nfec_codec_create_ex(ctypes.byref(cfg), ctypes.byref(self._h))
         if rc == N.NFEC_ERANGE:
             return False  # reference: PLOG(PL_FATAL) + return false (normEncoderRS8.cpp:405-409)
         N.check(rc, "nfec_codec_create")
@@ -139,6 +150,14 @@ class _Codec:
 
     def GetVectorSize(self):
         return self.vector_size
+
+    def num_devices(self):
+        """The device ordinals the codec runs on (nfec_codec_num_devices)."""
+        self._need()
+        n = N.check(N.lib().nfec_codec_num_devices(self._h, None, 0), "nfec_codec_num_devices")
+        out = (ctypes.c_int32 * n)()
+        N.lib().nfec_codec_num_devices(self._h, out, n)
+        return list(out)
 
     def generator(self):
         import numpy as np

@@ -115,12 +115,16 @@ constexpr uint32_t kMoveMaxSlots = 65536;
 __device__ void slot_move_block(const SlotMoveArgs& a, uint32_t b, uint32_t* erased, uint32_t& sh_end,
                                 uint32_t& sh_bad, uint32_t& sh_es)
 {
-    const uint32_t nd = a.num_data ? a.num_data[b] : a.k;
+    const uint32_t nd_in = a.num_data ? a.num_data[b] : a.k;
+    // an out-of-range numData marks the block bad and the slot range stays the block's own
+    // k + m slots: the moves never reach past a block (nor the erased bitmap past its size)
+    const bool nd_bad = nd_in == 0 || nd_in > a.k;
+    const uint32_t nd = nd_bad ? a.k : nd_in;
     const uint32_t nvec = nd + a.m;
     const uint32_t words = (nvec + 31) / 32;
     for (uint32_t w = threadIdx.x; w < words; w += blockDim.x) erased[w] = 0;
     if (threadIdx.x == 0) {
-        sh_bad = (nd == 0 || nd > a.k || a.counts[b] > a.lstride) ? 1u : 0u;
+        sh_bad = (nd_bad || a.counts[b] > a.lstride) ? 1u : 0u;
         sh_es = 0;
     }
     __syncthreads();

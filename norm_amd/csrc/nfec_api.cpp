@@ -72,12 +72,13 @@ constexpr uint32_t kRowPad = 32;       // coefficient rows padded (kernel row ch
 // Larger passes measured faster (fewer, fuller launches: 16k -> 64k blocks took
 // decode from 2.92 to 2.77 ms per 64k blocks), so a pass is as large as 8 GiB of workspace
 // allows (3 % of an MI355X's 288 GB).
-// NFEC_SUBBATCH overrides (A/B runs, diagnostic library).
-static uint32_t sub_batch(uint64_t ws_bytes_per_block)
+// budget_bytes caps it further (decode_device: half of the device memory free plus what the
+// codec already holds).  NFEC_SUBBATCH overrides (A/B runs, diagnostic library).
+static uint32_t sub_batch(uint64_t ws_bytes_per_block, uint64_t budget_bytes = 8ull << 30)
 {
     static const long env = diag_knob("NFEC_SUBBATCH", 0, 0, 1L << 20);
     if (env > 0) return (uint32_t)std::max(256L, std::min(env, 1L << 20));
-    const uint64_t cap = (8ull << 30) / std::max<uint64_t>(ws_bytes_per_block, 1);
+    const uint64_t cap = std::min<uint64_t>(8ull << 30, budget_bytes) / std::max<uint64_t>(ws_bytes_per_block, 1);
     return (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(65536, cap));
 }
 
@@ -191,7 +192,13 @@ struct AsyncQueue {
 struct nfec_codec {
     int kind = 0;
     int device = 0;
+    uint32_t opts = 0;  // NFEC_OPT_* (nfec_codec_create_ex)
     uint32_t k = 0, m = 0, vec = 0, sym = 1;
+    // a codec over several devices (nfec_codec_create_ex): one full single-device codec per
+    // listed device.  Host batches are striped over them in contiguous block ranges; device
+    // batches run on the stripe of the batch's device; per-call work on stripe 0.  The outer
+    // codec keeps the shape and the generator but no device state.
+    std::vector<std::unique_ptr<nfec_codec>> stripes;
     uint32_t cs = 0;  // padded parity-row count
     std::vector<uint32_t> gen;  // m x k parity rows (RS) / LFSR map for a full block (MDP)
 
@@ -310,12 +317,12 @@ bool use_gf16_t3()
 }
 
 // RS16 products through the tower field (gen_gf16_tw.hip, the default since round 3) or the
-// shared LDS tables (gen_gf16_t3.hip, NFEC_RS16_TW=0: both are exact, the tests run both)
-// (read per codec construction, so one process can build codecs of both kinds)
-bool use_gf16_tw()
+// shared LDS tables (gen_gf16_t3.hip, NFEC_OPT_RS16_SHARED_TABLES: both are exact, the tests run
+// both); chosen per codec, so one process can hold codecs of both kinds.  NFEC_RS16_TW=0/1
+// overrides (diagnostic library).
+bool use_gf16_tw(const nfec_codec* c)
 {
-    const char* e = std::getenv("NFEC_RS16_TW");
-    return !e || std::atoi(e) != 0;
+    return diag_knob("NFEC_RS16_TW", (c->opts & NFEC_OPT_RS16_SHARED_TABLES) ? 0 : 1) != 0;
 }
 
 // one RS16 product (encode, decode stage 1) on the codec's product kernel
@@ -393,7 +400,7 @@ int build_codec(nfec_codec* c)
         }
         // RS16: LDS offsets of the shared-table encode (gen_gf16_t3.hip), 96 bytes per
         // coefficient (C4, k = 4096, m = 256: 104 MB)
-        if (wide && use_gf16_t3() && use_gf16_tw()) {
+        if (wide && use_gf16_t3() && use_gf16_tw(c)) {
             std::vector<uint16_t> off(gf16_tw_table_elems(c->k, c->m));
             gf16_tw_offsets(c->gen, c->k, c->m, off.data());
             if ((rc = c->d_twoff.reserve(off.size()))) return rc;
@@ -408,10 +415,14 @@ int build_codec(nfec_codec* c)
         }
         // RS16: the Toeplitz split of the generator, three (m/2)-row products over k/2 columns
         // instead of one m-row product over k (kernels_tmvp.hip), where its passes are fewer:
-        // NFEC_RS16_TMVP=0 never, =1 whenever the shape allows it (tests), unset when it pays
+        // NFEC_OPT_RS16_TOEPLITZ_OFF never, NFEC_OPT_RS16_TOEPLITZ_ON whenever the shape allows
+        // it (tests), neither when it pays (NFEC_RS16_TMVP=0/1/-1 overrides, diagnostic library)
         if (wide && use_gf16_t3() && (c->vec % 8) == 0) {
-            const char* ev = std::getenv("NFEC_RS16_TMVP");
-            const int mode = ev ? std::atoi(ev) : -1;
+            const int mode = (int)diag_knob("NFEC_RS16_TMVP",
+                                            (c->opts & NFEC_OPT_RS16_TOEPLITZ_OFF)  ? 0
+                                            : (c->opts & NFEC_OPT_RS16_TOEPLITZ_ON) ? 1
+                                                                                    : -1,
+                                            -1, 1);
             const uint32_t cw = c->m / 2;
             const uint32_t rpp = kGf16T3RowsPerPass;
             const bool pays = c->tw ? 3ull * gf16_tw_passes(cw) * (c->k / 2) < (uint64_t)gf16_tw_passes(c->m) * c->k
@@ -835,7 +846,19 @@ int decode_device(nfec_codec* c, const nfec_block_batch* b, const uint16_t* locs
                                                          4ull * (std::min(c->k, c->m) + 12)
                                                    : 0);
     // passes of equal size, so no launch runs a small tail batch
-    const uint32_t cap = std::min(b->nblocks, sub_batch(ws_per_block + 4ull * n + 64));
+    // passes as large as 8 GiB of workspace allows; when that would grow the workspace past what
+    // the codec holds, also within half of the device memory free now (plus what it holds), so
+    // a smaller GPU or several codecs per device get smaller passes instead of NFEC_ENOMEM
+    const uint64_t per_block = ws_per_block + 4ull * n + 64;
+    uint32_t cap = std::min(b->nblocks, sub_batch(per_block));
+    const uint64_t held = c->w_z.n + c->w_coef1.n + c->w_coef2.n + c->w_work.n + 2ull * c->w_tw2.n;
+    if ((uint64_t)cap * per_block > held) {
+        size_t free_b = 0, total_b = 0;
+        if (hipMemGetInfo(&free_b, &total_b) == hipSuccess)
+            cap = std::min(cap, sub_batch(per_block, ((uint64_t)free_b + held) / 2));
+        else
+            (void)hipGetLastError();
+    }
     const uint32_t npass = (b->nblocks + cap - 1) / std::max(cap, 1u);
     const uint32_t sb = std::max(1u, (b->nblocks + npass - 1) / std::max(npass, 1u));
     int rc;
@@ -1313,14 +1336,13 @@ int nfec_device_count(void)
     return good;
 }
 
-int nfec_codec_create(int device, int kind, uint32_t num_data, uint32_t num_parity, uint32_t vector_size,
-                      nfec_codec** out)
+}  // extern "C"
+
+namespace {
+
+int create_one(int device, int kind, uint32_t num_data, uint32_t num_parity, uint32_t vector_size, uint32_t opts,
+               nfec_codec** out)
 {
-    if (!out) return fail(NFEC_EINVAL, "null output pointer");
-    *out = nullptr;
-    if (kind != NFEC_RS8 && kind != NFEC_RS16 && kind != NFEC_MDP) return fail(NFEC_EINVAL, "unknown codec kind");
-    if (num_data == 0 || num_parity == 0) return fail(NFEC_EINVAL, "numData and numParity must be > 0");
-    if (vector_size == 0 || vector_size > 65535) return fail(NFEC_EINVAL, "vectorSize must be in [1, 65535]");
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev) {
         (void)hipGetLastError();
@@ -1334,6 +1356,7 @@ int nfec_codec_create(int device, int kind, uint32_t num_data, uint32_t num_pari
     std::unique_ptr<nfec_codec> c(new nfec_codec);
     c->kind = kind;
     c->device = device;
+    c->opts = opts;
     c->k = num_data;
     c->m = num_parity;
     c->vec = vector_size;
@@ -1342,6 +1365,89 @@ int nfec_codec_create(int device, int kind, uint32_t num_data, uint32_t num_pari
     if (rc) return rc;
     *out = c.release();
     return NFEC_OK;
+}
+
+// the codec that runs per-call work and answers shape queries
+const nfec_codec* primary(const nfec_codec* c) { return c->stripes.empty() ? c : c->stripes[0].get(); }
+nfec_codec* primary(nfec_codec* c) { return c->stripes.empty() ? c : c->stripes[0].get(); }
+
+// the stripe whose device holds a device batch (a single-device codec: itself)
+nfec_codec* stripe_for(nfec_codec* c, const void* dev_ptr)
+{
+    if (c->stripes.empty()) return c;
+    hipPointerAttribute_t at;
+    if (hipPointerGetAttributes(&at, dev_ptr) != hipSuccess) {
+        (void)hipGetLastError();
+        return nullptr;
+    }
+    for (auto& st : c->stripes)
+        if (st->device == at.device) return st.get();
+    return nullptr;
+}
+
+}  // namespace
+
+extern "C" {
+
+int nfec_codec_create(int device, int kind, uint32_t num_data, uint32_t num_parity, uint32_t vector_size,
+                      nfec_codec** out)
+{
+    nfec_codec_config cfg{};
+    cfg.kind = kind;
+    cfg.num_data = num_data;
+    cfg.num_parity = num_parity;
+    cfg.vector_size = vector_size;
+    const int32_t dev = device;
+    cfg.devices = &dev;
+    cfg.num_devices = 1;
+    return nfec_codec_create_ex(&cfg, out);
+}
+
+int nfec_codec_create_ex(const nfec_codec_config* cfg, nfec_codec** out)
+{
+    if (!out || !cfg) return fail(NFEC_EINVAL, "null argument");
+    *out = nullptr;
+    const int kind = cfg->kind;
+    if (kind != NFEC_RS8 && kind != NFEC_RS16 && kind != NFEC_MDP) return fail(NFEC_EINVAL, "unknown codec kind");
+    if (cfg->num_data == 0 || cfg->num_parity == 0) return fail(NFEC_EINVAL, "numData and numParity must be > 0");
+    if (cfg->vector_size == 0 || cfg->vector_size > 65535) return fail(NFEC_EINVAL, "vectorSize must be in [1, 65535]");
+    if (cfg->flags & ~(uint32_t)(NFEC_OPT_RS16_SHARED_TABLES | NFEC_OPT_RS16_TOEPLITZ_OFF | NFEC_OPT_RS16_TOEPLITZ_ON))
+        return fail(NFEC_EINVAL, "unknown option flag");
+    if ((cfg->flags & NFEC_OPT_RS16_TOEPLITZ_OFF) && (cfg->flags & NFEC_OPT_RS16_TOEPLITZ_ON))
+        return fail(NFEC_EINVAL, "Toeplitz split both on and off");
+    const uint32_t nd = cfg->num_devices ? cfg->num_devices : 1;
+    if (nd > 64) return fail(NFEC_EINVAL, "more than 64 devices");
+    if (cfg->num_devices > 0 && !cfg->devices) return fail(NFEC_EINVAL, "null device list");
+    auto dev_at = [&](uint32_t i) { return cfg->devices ? (int)cfg->devices[i] : 0; };
+    if (nd == 1) return create_one(dev_at(0), kind, cfg->num_data, cfg->num_parity, cfg->vector_size, cfg->flags, out);
+    std::unique_ptr<nfec_codec> c(new nfec_codec);
+    for (uint32_t i = 0; i < nd; ++i) {
+        nfec_codec* one = nullptr;
+        const int rc = create_one(dev_at(i), kind, cfg->num_data, cfg->num_parity, cfg->vector_size, cfg->flags, &one);
+        if (rc) return rc;  // the stripes built so far go with c
+        c->stripes.emplace_back(one);
+    }
+    const nfec_codec* s0 = c->stripes[0].get();
+    c->kind = kind;
+    c->device = s0->device;
+    c->opts = cfg->flags;
+    c->k = s0->k;
+    c->m = s0->m;
+    c->vec = s0->vec;
+    c->sym = s0->sym;
+    c->cs = s0->cs;
+    c->gen = s0->gen;
+    c->async.device = s0->device;
+    *out = c.release();
+    return NFEC_OK;
+}
+
+int nfec_codec_num_devices(const nfec_codec* c, int32_t* devices, uint32_t cap)
+{
+    if (!c) return fail(NFEC_EINVAL, "null argument");
+    const uint32_t n = c->stripes.empty() ? 1u : (uint32_t)c->stripes.size();
+    for (uint32_t i = 0; i < n && devices && i < cap; ++i) devices[i] = c->stripes.empty() ? c->device : c->stripes[i]->device;
+    return (int)n;
 }
 
 void nfec_codec_destroy(nfec_codec* codec) { delete codec; }
@@ -1386,7 +1492,7 @@ int nfec_codec_get_info(const nfec_codec* c, nfec_codec_info* out)
 int nfec_codec_features(const nfec_codec* c)
 {
     if (!c) return fail(NFEC_EINVAL, "null argument");
-    return c->tmvp ? NFEC_FEATURE_RS16_TOEPLITZ : 0;
+    return primary(c)->tmvp ? NFEC_FEATURE_RS16_TOEPLITZ : 0;
 }
 
 int nfec_codec_get_generator(const nfec_codec* c, void* host_out, size_t bytes)
@@ -1405,6 +1511,7 @@ int nfec_encode(nfec_codec* codec, const nfec_block_batch* batch, void* stream)
 {
     int rc = check_batch(codec, batch);
     if (rc || batch->nblocks == 0) return rc;
+    if (!(codec = stripe_for(codec, batch->blocks))) return fail(NFEC_EINVAL, "batch is not on a device of the codec");
     DeviceGuard g(codec->device);
     return encode_device(codec, batch, static_cast<hipStream_t>(stream));
 }
@@ -1415,6 +1522,7 @@ int nfec_decode(nfec_codec* codec, const nfec_block_batch* batch, const uint16_t
     int rc = check_batch(codec, batch);
     if (rc || batch->nblocks == 0) return rc;
     if (erasure_stride == 0) return fail(NFEC_EINVAL, "erasure_stride must be > 0");
+    if (!(codec = stripe_for(codec, batch->blocks))) return fail(NFEC_EINVAL, "batch is not on a device of the codec");
     DeviceGuard g(codec->device);
     return decode_device(codec, batch, erasure_locs, erasure_stride, erasure_counts, status,
                          static_cast<hipStream_t>(stream));
@@ -1464,6 +1572,7 @@ int per_call_stage(nfec_codec* c, uint32_t nslots, PerCall& pc)
 int nfec_encode_segment(nfec_codec* c, uint32_t segment_id, const void* data, void* const* parity)
 {
     if (!c || !data || !parity) return fail(NFEC_EINVAL, "null argument");
+    c = primary(c);
     if (segment_id >= c->k) return fail(NFEC_EINVAL, "segmentId >= numData");
     for (uint32_t i = 0; i < c->m; ++i)
         if (!parity[i]) return fail(NFEC_EINVAL, "null parity vector");
@@ -1505,9 +1614,10 @@ int nfec_encode_segment(nfec_codec* c, uint32_t segment_id, const void* data, vo
             out_first = c->m + 1;
         }
         if ((rc = launch_gf8_matmul(a, false, st))) return rc;
-    } else if (c->tw && (c->vec % 8) == 0) {
+    } else {
         // the tower kernel over one column: the generator column segment_id is its own block
-        // of the codec's table; parity slots 1..m, accumulated (normEncoderRS16.cpp:472-482)
+        // of the codec's table; parity slots 1..m, accumulated (normEncoderRS16.cpp:472-482).
+        // A layout it does not take (its 2^31 offset bounds) goes to the exp-table kernel.
         Gf16T3Args t;
         t.base = d;
         t.block_stride = (uint64_t)(c->m + 1) * pc.stride;
@@ -1516,26 +1626,28 @@ int nfec_encode_segment(nfec_codec* c, uint32_t segment_id, const void* data, vo
         t.k = 1;
         t.m = c->m;
         t.vec_bytes = c->vec;
-        t.tw = c->d_twoff.p + (size_t)segment_id * 4u * c->m;
+        t.tw = c->tw ? c->d_twoff.p + (size_t)segment_id * 4u * c->m : nullptr;
         t.accumulate = 1;
-        if ((rc = launch_gf16_tw_encode(t, st))) return rc;
-    } else {
-        Gf16MatmulArgs a;
-        a.in_base = d;
-        a.in_seg_stride = pc.stride;
-        a.cols_const = 1;
-        a.out_base = d;
-        a.out_seg_stride = pc.stride;
-        a.out_slot_mode = OUT_SLOT_AFTER_INPUT;
-        a.rows_const = c->m;
-        a.coef = reinterpret_cast<const uint16_t*>(c->d_coef.p) + (size_t)segment_id * c->cs;
-        a.coef_col_stride = c->cs;
-        a.exp_tab = reinterpret_cast<const uint16_t*>(c->d_exp.p);
-        a.log_tab = c->d_log.p;
-        a.nblocks = 1;
-        a.vec_bytes = c->vec & ~1u;
-        a.accumulate = 1;
-        if ((rc = launch_gf16_matmul(a, st))) return rc;
+        rc = c->tw && (c->vec % 8) == 0 && gf16_tw_covers(t) ? launch_gf16_tw_encode(t, st) : NFEC_ENOTSUP;
+        if (rc != NFEC_ENOTSUP && rc) return rc;
+        if (rc == NFEC_ENOTSUP) {
+            Gf16MatmulArgs a;
+            a.in_base = d;
+            a.in_seg_stride = pc.stride;
+            a.cols_const = 1;
+            a.out_base = d;
+            a.out_seg_stride = pc.stride;
+            a.out_slot_mode = OUT_SLOT_AFTER_INPUT;
+            a.rows_const = c->m;
+            a.coef = reinterpret_cast<const uint16_t*>(c->d_coef.p) + (size_t)segment_id * c->cs;
+            a.coef_col_stride = c->cs;
+            a.exp_tab = reinterpret_cast<const uint16_t*>(c->d_exp.p);
+            a.log_tab = c->d_log.p;
+            a.nblocks = 1;
+            a.vec_bytes = c->vec & ~1u;
+            a.accumulate = 1;
+            if ((rc = launch_gf16_matmul(a, st))) return rc;
+        }
     }
     const size_t off = (size_t)out_first * pc.stride;
     NFEC_HIP(hipMemcpyAsync(hp + off, d + off, (size_t)c->m * pc.stride, hipMemcpyDeviceToHost, st));
@@ -1549,6 +1661,7 @@ int nfec_decode_vectors(nfec_codec* c, void* const* vectors, uint32_t num_data, 
                         const uint32_t* erasure_locs)
 {
     if (!c || !vectors || (erasure_count && !erasure_locs)) return fail(NFEC_EINVAL, "null argument");
+    c = primary(c);
     if (num_data == 0 || num_data > c->k) return fail(NFEC_EINVAL, "numData out of range");
     if (erasure_count > c->m) return 0;
     DeviceGuard g(c->device);
@@ -1921,11 +2034,49 @@ static int host_decode_zc(nfec_codec* c, const nfec_block_batch* hb, HostSlot& s
     return ae == hipSuccess ? NFEC_OK : hip_fail(ae, "host decode status");
 }
 
+// A host batch on a codec over several devices: contiguous block ranges [i*B/N, (i+1)*B/N), one
+// per stripe, each through that stripe's own pipeline on a host thread of its own (SURVEY 8e:
+// no exchange between the ranges).  fn(stripe, first block, blocks) runs one range.  The
+// first failing range's status and message are returned on the calling thread.
+extern "C++" template <typename F>
+static int run_striped(nfec_codec* c, uint32_t nblocks, F fn)
+{
+    const uint32_t ns = (uint32_t)std::min<size_t>(c->stripes.size(), std::max(nblocks, 1u));
+    std::vector<int> rcs(ns, NFEC_OK);
+    std::vector<std::string> errs(ns);
+    auto one = [&](uint32_t i) {
+        const uint32_t lo = (uint32_t)((uint64_t)nblocks * i / ns), hi = (uint32_t)((uint64_t)nblocks * (i + 1) / ns);
+        rcs[i] = hi > lo ? fn(c->stripes[i].get(), lo, hi - lo) : NFEC_OK;
+        if (rcs[i] < 0) errs[i] = last_error_cstr();
+    };
+    std::vector<std::thread> th;
+    for (uint32_t i = 1; i < ns; ++i) th.emplace_back(one, i);
+    one(0);
+    for (auto& t : th) t.join();
+    for (uint32_t i = 0; i < ns; ++i)
+        if (rcs[i] < 0) return fail(rcs[i], errs[i]);
+    return NFEC_OK;
+}
+
 static int run_host_batch(nfec_codec* c, const nfec_block_batch* hb, const uint16_t* locs, uint32_t lstride,
                           const uint16_t* counts, int32_t* status, bool decode)
 {
     int rc = check_batch(c, hb);
     if (rc || hb->nblocks == 0) return rc;
+    if (!c->stripes.empty())
+        return run_striped(c, hb->nblocks, [&](nfec_codec* sc, uint32_t b0, uint32_t nb) {
+            nfec_block_batch sub = *hb;
+            sub.blocks = static_cast<uint8_t*>(hb->blocks) + (uint64_t)b0 * hb->block_stride;
+            sub.nblocks = nb;
+            sub.num_data = hb->num_data ? hb->num_data + b0 : nullptr;
+            return run_host_batch(sc, &sub, locs ? locs + (uint64_t)b0 * lstride : nullptr, lstride,
+                                  counts ? counts + b0 : nullptr, status ? status + b0 : nullptr, decode);
+        });
+    // numData is on the host here: reject what no block of k + m slots can hold before any
+    // transfer is sized from it (as run_host_vectors does)
+    if (hb->num_data)
+        for (uint32_t b = 0; b < hb->nblocks; ++b)
+            if (hb->num_data[b] == 0 || hb->num_data[b] > c->k) return fail(NFEC_EINVAL, "num_data out of range");
     DeviceGuard g(c->device);
     std::lock_guard<std::mutex> stage_lock(c->stage_mu);
     const uint64_t hbs = hb->block_stride;
@@ -2036,7 +2187,9 @@ static int run_host_batch(nfec_codec* c, const nfec_block_batch* hb, const uint1
         const uint64_t ul = decode ? decode_up_len(b0, j.nb, dl) : up_len;
         j.dl = dl;
         hipError_t ae;
-        if (zc) {
+        // (a pageable caller's chunk goes through the slot's pinned staging, which the zero-copy
+        // kernels need device-mapped; where it is not, the window DMA below takes the chunk)
+        if (zc && (pinned || s.pin_dev)) {
             if ((rc = host_decode_zc(c, hb, s, b0, j.nb, chunk, locs, lstride, counts, pinned ? hbase_dev : nullptr,
                                      ul)))
                 return bail(rc);
@@ -2143,6 +2296,12 @@ static int run_host_vectors(nfec_codec* c, void* const* vecs, uint32_t nblocks, 
     if (!c || (nblocks && !vecs)) return fail(NFEC_EINVAL, "null codec or vector list");
     if (decode && (!locs || !counts || lstride == 0)) return fail(NFEC_EINVAL, "bad erasure arrays");
     if (nblocks == 0) return NFEC_OK;
+    if (!c->stripes.empty())
+        return run_striped(c, nblocks, [&](nfec_codec* sc, uint32_t b0, uint32_t nb) {
+            return run_host_vectors(sc, vecs + (uint64_t)b0 * (c->k + c->m), nb, num_data ? num_data + b0 : nullptr,
+                                    locs ? locs + (uint64_t)b0 * lstride : nullptr, lstride,
+                                    counts ? counts + b0 : nullptr, status ? status + b0 : nullptr, flags, decode);
+        });
     const uint32_t n = c->k + c->m;
     const uint64_t ss = round_up(c->vec, 8u);
     const uint64_t dbs = (uint64_t)n * ss;

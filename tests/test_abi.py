@@ -18,6 +18,14 @@ def test_library_loads_and_exports_header_symbols():
     assert L.nfec_abi_version() == 1
 
 
+def test_library_built_from_this_tree():
+    """The prebuilt libnfec.so (it travels to the GPU box, git keeps sources only) embeds the
+    SHA-256 of the sources it was built from; it must be this tree's."""
+    built = N.lib().nfec_build_id().decode()
+    assert len(built) == 64
+    assert built == N.source_build_id(), "libnfec.so is stale: rebuild with make -C norm_amd"
+
+
 def test_drop_in_classes_exported():
     import subprocess
 
@@ -82,3 +90,22 @@ def test_generator_limits():
     assert L.nfec_build_generator(N.NFEC_MDP, 250, 6, buf.ctypes.data, buf.nbytes) == N.NFEC_ERANGE
     assert L.nfec_build_generator(N.NFEC_RS8, 200, 55, buf.ctypes.data, buf.nbytes) == N.NFEC_OK
     assert L.nfec_build_generator(N.NFEC_RS8, 64, 32, buf.ctypes.data, 10) == N.NFEC_EINVAL
+
+
+def test_codec_config_validation_without_gpu():
+    """nfec_codec_create_ex checks its arguments before it needs a device"""
+    cfg = N.CodecConfig()
+    cfg.kind, cfg.num_data, cfg.num_parity, cfg.vector_size = N.NFEC_RS16, 400, 100, 1400
+    h = ctypes.c_void_p()
+    cfg.flags = 1 << 7
+    assert N.lib().nfec_codec_create_ex(ctypes.byref(cfg), ctypes.byref(h)) == N.NFEC_EINVAL
+    cfg.flags = N.NFEC_OPT_RS16_TOEPLITZ_OFF | N.NFEC_OPT_RS16_TOEPLITZ_ON
+    assert N.lib().nfec_codec_create_ex(ctypes.byref(cfg), ctypes.byref(h)) == N.NFEC_EINVAL
+    cfg.flags = 0
+    cfg.num_devices = 2  # a device count with no list
+    assert N.lib().nfec_codec_create_ex(ctypes.byref(cfg), ctypes.byref(h)) == N.NFEC_EINVAL
+    if N.lib().nfec_device_count() == 0:
+        devs = (ctypes.c_int32 * 2)(0, 0)
+        cfg.devices = ctypes.cast(devs, ctypes.POINTER(ctypes.c_int32))
+        assert N.lib().nfec_codec_create_ex(ctypes.byref(cfg), ctypes.byref(h)) == N.NFEC_EDEVICE
+    assert not h

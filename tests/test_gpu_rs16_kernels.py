@@ -1,6 +1,6 @@
 """RS16 products on both GPU kernels against the oracle, bit-exact: the tower-field kernel
-(gen_gf16_tw.hip, the default) and the shared-table kernel (gen_gf16_t3.hip, NFEC_RS16_TW=0).
-The switch is read when a codec is built, so both run in one process.  Covers the one-product
+(gen_gf16_tw.hip, the default) and the shared-table kernel (gen_gf16_t3.hip,
+NFEC_OPT_RS16_SHARED_TABLES).  The option is per codec, so both run in one process.  Covers the one-product
 encode, the Toeplitz split (C4's route) and decode stage 1 (the plan's by-encode blocks).
 Reference: NormEncoderRS16::Encode / NormDecoderRS16::Decode, src/common/normEncoderRS16.cpp:472-482,
 650-755."""
@@ -12,16 +12,16 @@ pytestmark = pytest.mark.gpu
 torch = pytest.importorskip("torch")
 
 from norm_amd import NFEC_RS16, NormDecoderRS16, NormEncoderRS16  # noqa: E402
-from norm_amd._native import NFEC_FEATURE_RS16_TOEPLITZ  # noqa: E402
+from norm_amd._native import (NFEC_FEATURE_RS16_TOEPLITZ, NFEC_OPT_RS16_SHARED_TABLES,  # noqa: E402
+                              NFEC_OPT_RS16_TOEPLITZ_OFF, NFEC_OPT_RS16_TOEPLITZ_ON)
 
 KERNELS = ["1", "0"]   # tower, shared tables
 
 
 def _codecs(monkeypatch, tw, k, m, vec, tmvp=None):
-    monkeypatch.setenv("NFEC_RS16_TW", tw)
-    if tmvp is not None:
-        monkeypatch.setenv("NFEC_RS16_TMVP", tmvp)
-    enc, dec = NormEncoderRS16(), NormDecoderRS16()
+    opts = (0 if tw == "1" else NFEC_OPT_RS16_SHARED_TABLES) | \
+        {None: 0, "0": NFEC_OPT_RS16_TOEPLITZ_OFF, "1": NFEC_OPT_RS16_TOEPLITZ_ON}[tmvp]
+    enc, dec = NormEncoderRS16(options=opts), NormDecoderRS16(options=opts)
     assert enc.Init(k, m, vec) and dec.Init(k, m, vec)
     return enc, dec
 

@@ -1,7 +1,7 @@
 """RS16 encode by the Toeplitz split (kernels_tmvp.hip + gen_gf16_t3.hip multi launch) against
-the oracle on the GPU, bit-exact.  NFEC_RS16_TMVP=1 forces the split for shapes where it is
-allowed but not chosen by default; (256, 64) and C4 take it by default."""
-import os
+the oracle on the GPU, bit-exact.  NFEC_OPT_RS16_TOEPLITZ_ON forces the split for shapes where
+it is allowed but not chosen by default (NFEC_OPT_RS16_TOEPLITZ_OFF: never); (256, 64) and C4
+take it by default."""
 
 import numpy as np
 import pytest
@@ -11,21 +11,13 @@ pytestmark = pytest.mark.gpu
 torch = pytest.importorskip("torch")
 
 from norm_amd import NFEC_RS16, NormDecoderRS16, NormEncoderRS16  # noqa: E402
-from norm_amd._native import NFEC_FEATURE_RS16_TOEPLITZ  # noqa: E402
+from norm_amd._native import (NFEC_FEATURE_RS16_TOEPLITZ, NFEC_OPT_RS16_TOEPLITZ_OFF,  # noqa: E402
+                              NFEC_OPT_RS16_TOEPLITZ_ON)
 
 
 def _encoder(k, m, vec, force):
-    old = os.environ.get("NFEC_RS16_TMVP")
-    if force is not None:
-        os.environ["NFEC_RS16_TMVP"] = force
-    try:
-        enc = NormEncoderRS16()
-        assert enc.Init(k, m, vec)
-    finally:
-        if old is None:
-            os.environ.pop("NFEC_RS16_TMVP", None)
-        else:
-            os.environ["NFEC_RS16_TMVP"] = old
+    enc = NormEncoderRS16(options={None: 0, "0": NFEC_OPT_RS16_TOEPLITZ_OFF, "1": NFEC_OPT_RS16_TOEPLITZ_ON}[force])
+    assert enc.Init(k, m, vec)
     return enc
 
 

@@ -139,3 +139,25 @@ def test_plan_launch():
         os.environ.pop("WORLD_SIZE", None)
         if old["WORLD_SIZE"] is not None:
             os.environ["WORLD_SIZE"] = old["WORLD_SIZE"]
+
+
+def test_bench_c5_dry_run_pinned_budget():
+    """tools/bench_c5.py --gpus N --dry-run: N ranks on gloo, contiguous disjoint shares covering
+    the stream, and a page-locked budget per rank (4 GB at N > 1) instead of the 26.8 GB share."""
+    import json
+    import subprocess
+    import sys
+
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "bench_c5.py"), "--gpus", "2", "--dry-run"],
+                       capture_output=True, text=True, timeout=300, env=env, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-2000:]
+    out = [json.loads(ln) for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(out) == 1 and out[0]["n_gpus"] == 2
+    ranks, pinned = out[0]["ranks"], out[0]["pinned"]
+    assert [x["first"] for x in ranks] == [0, 131072]
+    assert all(sum(x["blocks"].values()) == 131072 for x in ranks)
+    assert all(0 < b <= 4_000_000_000 for b in pinned["per_rank_bytes"])
+    assert pinned["total_bytes"] == sum(pinned["per_rank_bytes"]) < pinned["share_bytes_total"]
+    for x in ranks:
+        assert all(0 < x["pinned_blocks"][n] <= x["blocks"][n] for n in x["blocks"])

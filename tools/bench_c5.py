@@ -16,6 +16,13 @@ codec's pinned-staging pipeline (nfec_encode_host / nfec_decode_host).
 Reported as one JSON line in bench.py's schema: value = host-resident GiB/s (source bytes
 through encode + decode, all ranks / max-over-ranks time), plus the device-resident GiB/s of the
 same mix with the blocks already in HBM.
+
+Page-locked memory: a rank's whole share is 26.8 GB (114,726 RS8 x 96 x 1400 + 16,346 RS16 x
+500 x 1400), 215 GB over 8 ranks.  At N = 1 the whole share is pinned; at N > 1 the host-resident
+timing runs on the first blocks of each sub-stream within --pinned-gb per rank (default 4 GB,
+32 GB over 8 ranks), the device-resident timing on the whole share.  The line reports the pinned
+bytes per rank and in total.  --dry-run rehearses the launch, the per-rank plan and the pinned
+budget on the CPU (gloo, no GPU, no FEC work).
 """
 import argparse
 import json
@@ -52,6 +59,11 @@ def main():
     p.add_argument("--steps", type=int, default=2)
     p.add_argument("--warmup", type=int, default=1)
     p.add_argument("--serial", action="store_true", help="run the RS8 and RS16 sub-streams one after the other")
+    p.add_argument("--pinned-gb", type=float, default=0.0,
+                   help="page-locked bytes per rank for the host-resident timing (0: the whole share at N = 1, "
+                        "4 GB at N > 1)")
+    p.add_argument("--dry-run", action="store_true",
+                   help="CPU rehearsal: launch, per-rank plan and pinned budget (gloo; no GPU, no FEC work)")
     a = p.parse_args()
     from norm_amd.dist import launch_local_ranks, plan_launch
 
@@ -64,6 +76,8 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if a.dry_run:
+        return dry_run(a, world, rank)
     torch.cuda.set_device(local)
     dist = None
     if world > 1:
@@ -73,15 +87,8 @@ def main():
     dev = torch.device("cuda", local)
     import norm_amd as na
 
-    from norm_amd.dist import shard
-
-    per = a.blocks or ((1 << 20) if a.strong else (1 << 20) // 8)
-    first, nmine = shard(per, world, rank, a.strong)
-    total = per if a.strong else per * world
-    lo, hi = first, first + nmine
-    ids = np.arange(lo, hi, dtype=np.uint64)
-    is16 = (splitmix64(np.uint64(SEED) ^ ids) % np.uint64(8)) == 0
-    counts = {"RS8": int((~is16).sum()), "RS16": int(is16.sum())}
+    pl = plan(a, world, rank)
+    total, lo, counts, pinned = pl["total"], pl["first"], pl["blocks"], pl["pinned_blocks"]
 
     jobs = []
     for name, (k, m, vec, er), n, enc_c, dec_c in (("RS8", RS8, counts["RS8"], na.NormEncoderRS8, na.NormDecoderRS8),
@@ -90,19 +97,17 @@ def main():
             continue
         enc, dec = enc_c(device=local), dec_c(device=local)
         assert enc.Init(k, m, vec) and dec.Init(k, m, vec)
-        host = torch.empty((n, k + m, vec), dtype=torch.uint8, pin_memory=True)
-        # synthetic source generated on the GPU in chunks, then moved to pinned host memory
-        chunk = max(1, (2 << 30) // ((k + m) * vec))
-        for b0 in range(0, n, chunk):
-            nb = min(chunk, n - b0)
-            d = torch.zeros((nb, k + m, vec), dtype=torch.uint8, device=dev)
-            na.fill_blocks(d, k, vec, SEED ^ (0x16 if name == "RS16" else 0x8), first_block=lo + b0)
-            host[b0:b0 + nb].copy_(d)
-            del d
+        # synthetic source generated in HBM (the whole share: the device-resident timing); the
+        # first `hn` blocks are also copied to pinned host memory (the host-resident timing)
+        d = torch.zeros((n, k + m, vec), dtype=torch.uint8, device=dev)
+        na.fill_blocks(d, k, vec, SEED ^ (0x16 if name == "RS16" else 0x8), first_block=lo)
+        hn = pinned[name]
+        host = torch.empty((hn, k + m, vec), dtype=torch.uint8, pin_memory=True)
+        host.copy_(d[:hn])
         locs, cnts = na.make_erasures(n, k, er, SEED, m, first_block=lo)
-        jobs.append(dict(name=name, k=k, m=m, vec=vec, er=er, n=n, enc=enc, dec=dec, host=host,
-                         hnp=host.numpy(), locs=locs.cpu().numpy().view(np.uint16), cnts=cnts.cpu().numpy().view(np.uint16),
-                         dlocs=locs, dcnts=cnts))
+        jobs.append(dict(name=name, k=k, m=m, vec=vec, er=er, n=n, hn=hn, enc=enc, dec=dec, host=host, dev=d,
+                         hnp=host.numpy(), locs=locs[:hn].cpu().numpy().view(np.uint16),
+                         cnts=cnts[:hn].cpu().numpy().view(np.uint16), dlocs=locs, dcnts=cnts))
     torch.cuda.synchronize()
 
     def host_job(j):
@@ -149,7 +154,7 @@ def main():
     # light round-trip check on a sample: erase, repair through the host path, compare
     sample_ok = True
     for j in jobs:
-        n = min(64, j["n"])
+        n = min(64, j["hn"])
         keep = j["hnp"][:n].copy()
         rx = keep.copy()
         for b in range(n):
@@ -161,8 +166,8 @@ def main():
     # device-resident rate of the same mix (blocks in HBM)
     dev_jobs = []
     for j in jobs:
-        d = j["host"].to(dev)
-        dev_jobs.append((j, d, torch.empty(j["n"], dtype=torch.int32, device=dev)))
+        del j["host"], j["hnp"]  # the pinned copies are done with
+        dev_jobs.append((j, j["dev"], torch.empty(j["n"], dtype=torch.int32, device=dev)))
     stream = torch.cuda.current_stream(dev)
 
     def dev_step():
@@ -180,21 +185,29 @@ def main():
     barrier()
     dev_s = max_time((time.perf_counter() - t0) / a.steps)
 
-    src_rank = sum(j["k"] * j["vec"] * j["n"] for j in jobs)
-    src_all = torch.tensor([float(src_rank)], dtype=torch.float64, device=dev)
-    if dist is not None:
-        dist.all_reduce(src_all)
-    src_all = float(src_all.item())
+    def sum_ranks(v):
+        t = torch.tensor([float(v)], dtype=torch.float64, device=dev)
+        if dist is not None:
+            dist.all_reduce(t)
+        return float(t.item())
+
+    src_all = sum_ranks(sum(j["k"] * j["vec"] * j["n"] for j in jobs))        # device-resident step
+    src_host = sum_ranks(sum(j["k"] * j["vec"] * j["hn"] for j in jobs))      # host-resident step
+    pinned_all = sum_ranks(pl["pinned_bytes"])
     if rank == 0:
         print(json.dumps({
             "metric": "FEC encode+erasure-decode GiB/s (host-resident, pinned H2D/D2H), C5 mixed RS8/RS16 stream",
-            "value": round(src_all / host_s / 2**30, 2), "unit": "GiB/s", "n_gpus": world,
+            "value": round(src_host / host_s / 2**30, 2), "unit": "GiB/s", "n_gpus": world,
             "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(host_s * 1e3, 1),
             "higher_is_better": True, "scaling": "strong" if a.strong else "weak", "vs_baseline": None,
             "dtype": "u8", "data": "synthetic (splitmix64 source segments, reference generators)",
             "config": {"workload": "C5 mixed RS8(64,32)/RS16(400,100) stream, vec=1400, pinned host segments",
                        "blocks_total": total, "rank0_blocks": counts,
                        "parallelism": f"block-striped x{world} (no collective)"},
+            "pinned": {"rank0_blocks": pinned, "rank0_bytes": pl["pinned_bytes"], "total_bytes": int(pinned_all),
+                       "budget_bytes_per_rank": pl["budget_bytes"],
+                       "note": "host-resident timing on these first blocks of each sub-stream (page-locked); "
+                               "device-resident timing on every block of the share"},
             "device_resident": {"value": round(src_all / dev_s / 2**30, 2), "unit": "GiB/s",
                                 "ms_per_step": round(dev_s * 1e3, 2)},
             "status_ok": host_ok, "sample_round_trip_ok": sample_ok,
@@ -203,6 +216,55 @@ def main():
                     "GiB/s counts source bytes, all ranks / max-over-ranks time",
         }), flush=True)
     if dist is not None:
+        dist.destroy_process_group()
+
+
+def plan(a, world, rank):
+    """This rank's share of the stream (contiguous block range, split into its RS8 and RS16
+    sub-streams) and how much of it is pinned for the host-resident timing."""
+    import numpy as np
+
+    from norm_amd.dist import shard
+
+    per = a.blocks or ((1 << 20) if a.strong else (1 << 20) // 8)
+    first, nmine = shard(per, world, rank, a.strong)
+    ids = np.arange(first, first + nmine, dtype=np.uint64)
+    is16 = (splitmix64(np.uint64(SEED) ^ ids) % np.uint64(8)) == 0
+    blocks = {"RS8": int((~is16).sum()), "RS16": int(is16.sum())}
+    bpb = {"RS8": (RS8[0] + RS8[1]) * RS8[2], "RS16": (RS16[0] + RS16[1]) * RS16[2]}
+    share = sum(blocks[n] * bpb[n] for n in blocks)
+    budget = int(a.pinned_gb * 1e9) if a.pinned_gb > 0 else (share if world == 1 else int(4e9))
+    frac = min(1.0, budget / max(share, 1))
+    pinned = {n: (blocks[n] if frac >= 1.0 else min(blocks[n], max(1, int(blocks[n] * frac)))) if blocks[n] else 0
+              for n in blocks}
+    return {"total": per if a.strong else per * world, "first": first, "blocks": blocks, "pinned_blocks": pinned,
+            "pinned_bytes": sum(pinned[n] * bpb[n] for n in pinned), "share_bytes": share, "budget_bytes": budget}
+
+
+def dry_run(a, world, rank):
+    """The launch, the per-rank plans and the pinned budget on the CPU (gloo), one JSON line."""
+    import torch
+    import torch.distributed as dist
+
+    if world > 1:
+        dist.init_process_group("gloo")
+    mine = plan(a, world, rank)
+    plans = [mine]
+    if world > 1:
+        plans = [None] * world
+        dist.all_gather_object(plans, mine)
+    if rank == 0:
+        print(json.dumps({
+            "metric": "FEC encode+erasure-decode GiB/s (host-resident, pinned H2D/D2H), C5 mixed RS8/RS16 stream",
+            "value": None, "n_gpus": len(plans), "dry_run": True, "world_size": world,
+            "config": {"blocks_total": plans[0]["total"], "parallelism": f"block-striped x{world} (no collective)"},
+            "pinned": {"per_rank_bytes": [p["pinned_bytes"] for p in plans],
+                       "total_bytes": sum(p["pinned_bytes"] for p in plans),
+                       "share_bytes_total": sum(p["share_bytes"] for p in plans),
+                       "budget_bytes_per_rank": mine["budget_bytes"]},
+            "ranks": [{"first": p["first"], "blocks": p["blocks"], "pinned_blocks": p["pinned_blocks"]} for p in plans],
+        }), flush=True)
+    if world > 1:
         dist.destroy_process_group()
 
 

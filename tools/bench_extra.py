@@ -6,6 +6,9 @@ c4    RS16 k=4096 m=256 vec=1400 encode (BASELINE C4), default 4096 blocks in HB
 rs16  RS16 k=400 m=100 vec=1400 encode + 50-erasure decode (the C5 RS16 block type)
 mdp   MDP k=64 m=32 vec=1400 encode + 16-erasure decode
 rs8   RS8 with --k/--m/--erasures (other shapes than the headline)
+rs8sweep  RS8 encode + decode over NORM-plausible shapes, one line per shape, with the time per
+      source byte relative to (64, 32): (64,32), (16,4), (32,16), (64,16) shortened (numData
+      drawn per block from [32, 64]), (128,32), (200,55), (64,8), (8,2) -- the generic-shape cliff
 
 Inputs are synthetic (splitmix64 segments generated on the GPU); GiB/s counts source bytes
 (k * vec per block) per pass, like the headline metric.
@@ -36,6 +39,9 @@ def main():
     a = p.parse_args()
     import torch
     import norm_amd as na
+
+    if a.workload == "rs8sweep":
+        return rs8_sweep(a)
 
     shapes = {  # kind, k, m, blocks, erasures (0: encode only)
         "c4": (na.NFEC_RS16, 4096, 256, 4096, 0),
@@ -144,6 +150,84 @@ def main():
             "verified": bool(torch.equal(blocks[:, :k], keep[:, :k])) and bool((status == er).all()),
         })
     print(json.dumps(out), flush=True)
+
+
+SWEEP = [  # k, m, shortened, source erasures
+    (64, 32, False, 16), (16, 4, False, 4), (32, 16, False, 16), (64, 16, True, 8), (128, 32, False, 16),
+    (200, 55, False, 16), (64, 8, False, 8), (8, 2, False, 2),
+]
+
+
+def rs8_sweep(a):
+    """encode + source-erasure repair per shape; ns per source byte against the (64, 32) line"""
+    import numpy as np
+    import torch
+    import norm_amd as na
+
+    torch.cuda.set_device(0)
+    stream = torch.cuda.current_stream()
+    vec = a.vec
+    base = None
+
+    def timed(fn, n):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for _ in range(n):
+            fn()
+        e1.record(stream)
+        e1.synchronize()
+        return e0.elapsed_time(e1) / n
+
+    for k, m, short, er in SWEEP:
+        # about 5.9 GB of source per shape (the headline's 65,536 x 64 x 1400), at most 1M blocks
+        nb = a.blocks or min(1 << 20, (65536 * 64) // k)
+        enc, dec = na.NormEncoderRS8(), na.NormDecoderRS8()
+        assert enc.Init(k, m, vec) and dec.Init(k, m, vec)
+        blocks = torch.zeros((nb, k + m, vec), dtype=torch.uint8, device="cuda")
+        rng = np.random.default_rng(k * 1000 + m)
+        nd = None
+        if short:
+            ndh = rng.integers(k // 2, k + 1, nb).astype(np.uint16)
+            nd = torch.from_numpy(ndh.view(np.int16)).cuda()
+            na.fill_blocks(blocks, k, vec, 0x4E4F524D, per_block_num_data=nd)
+            hl = np.zeros((nb, m), np.int16)
+            for b in range(nb):
+                hl[b, :er] = np.sort(rng.choice(int(ndh[b]), er, replace=False))
+            locs = torch.from_numpy(hl).cuda()
+            counts = torch.full((nb,), er, dtype=torch.int16, device="cuda")
+            src = float(ndh.astype(np.float64).sum()) * vec
+        else:
+            na.fill_blocks(blocks, k, vec, 0x4E4F524D)
+            locs, counts = na.make_erasures(nb, k, er, 0x4E4F524D, m)
+            src = float(k) * vec * nb
+        status = torch.empty(nb, dtype=torch.int32, device="cuda")
+        enc.encode_blocks(blocks, num_data=nd, stream=stream)
+        dec.decode_blocks(blocks, locs, counts, num_data=nd, status=status, stream=stream)
+        torch.cuda.synchronize()
+        enc_ms = timed(lambda: enc.encode_blocks(blocks, num_data=nd, stream=stream), a.steps)
+        dec_ms = timed(lambda: dec.decode_blocks(blocks, locs, counts, num_data=nd, status=status, stream=stream),
+                       a.steps)
+        # one clean round trip: encode, erase, repair, compare
+        enc.encode_blocks(blocks, num_data=nd, stream=stream)
+        keep = blocks.clone()
+        na.zero_erasures(blocks, locs, counts, vec, stream=stream)
+        dec.decode_blocks(blocks, locs, counts, num_data=nd, status=status, stream=stream)
+        torch.cuda.synchronize()
+        ok = bool(torch.equal(blocks, keep)) and bool((status == er).all())
+        enc_ns, dec_ns = enc_ms * 1e6 / src, dec_ms * 1e6 / src
+        if base is None:
+            base = (enc_ns, dec_ns)
+        print(json.dumps({
+            "workload": "rs8sweep", "k": k, "m": m, "shortened": short, "vec": vec, "blocks": nb, "erasures": er,
+            "source_GB": round(src / 1e9, 3),
+            "encode_ms": round(enc_ms, 3), "decode_ms": round(dec_ms, 3),
+            "encode_ns_per_source_byte": round(enc_ns, 5), "decode_ns_per_source_byte": round(dec_ns, 5),
+            "encode_vs_64_32": round(enc_ns / base[0], 3), "decode_vs_64_32": round(dec_ns / base[1], 3),
+            "encode_hbm_GBps": round((src / vec) * (k + m) / k * vec / (enc_ms * 1e-3) / 1e9, 1),
+            "verified": ok,
+        }), flush=True)
+        del blocks, keep, status, locs, counts
+        torch.cuda.empty_cache()
 
 
 if __name__ == "__main__":
