@@ -134,6 +134,18 @@ void mdp_encode_matrix(const std::vector<uint8_t>& g, uint32_t m, uint32_t nd, u
     }
 }
 
+// coefficient table of the runtime-coefficient kernel (gen_rs8_rt.hip): entry (c, r) is the
+// byte offset of coefficient rows[r][c]'s snippet (value << 7), columns rs8_rt_col_stride(m)
+// bytes apart, 16 bytes of padding for the kernel's 8-row entry loads
+std::vector<uint16_t> rs8_rt_table(const std::vector<uint32_t>& rows, uint32_t k, uint32_t m)
+{
+    const uint32_t cs = rs8_rt_col_stride(m) / 2;
+    std::vector<uint16_t> t((size_t)k * cs + 8, 0);
+    for (uint32_t c = 0; c < k; ++c)
+        for (uint32_t r = 0; r < m; ++r) t[(size_t)c * cs + r] = (uint16_t)((rows[(size_t)r * k + c] & 0xffu) << 7);
+    return t;
+}
+
 void vperm_table(uint32_t c, uint32_t out[8])
 {
     const Field& f = gf8();

@@ -210,6 +210,10 @@ struct nfec_codec {
     DevBuf<uint16_t> d_log;      // field log table (q+1)
     DevBuf<uint8_t> d_mdp_step;  // MDP single LFSR step matrix, column-major [m+1][cs]
     DevBuf<uint16_t> d_lwp, d_lw;  // RS8 closed-form plan constants: log W'(x_j), log W(y_p)
+    // RS8 / MDP products with runtime coefficients (gen_rs8_rt.hip): the generator as snippet
+    // offsets [k][m] (RS8), or one [k][m] table per block length nd = 1..k (MDP, shortened)
+    DevBuf<uint16_t> d_rt;
+    uint64_t rt_block_bytes = 0;   // MDP: bytes per numData table
     DevBuf<uint16_t> d_sel16;      // RS16 bit-sliced encode table offsets [k][m][64] (may be absent)
     DevBuf<uint16_t> d_t3off;      // RS16 shared-table encode LDS offsets [k+1][m_pad][48]
     // RS16 products by the tower-field kernel (gen_gf16_tw.hip) instead of the shared-table one:
@@ -266,6 +270,7 @@ struct nfec_codec {
         d_log.release();
         d_lwp.release();
         d_lw.release();
+        d_rt.release();
         d_sel16.release();
         d_t3off.release();
         d_twoff.release();
@@ -356,6 +361,19 @@ int build_codec(nfec_codec* c)
         }
         int rc = upload(c->d_coef, coef.data(), coef.size());
         if (rc) return rc;
+        {
+            // the same block maps as runtime-coefficient tables, one per nd (shortened encodes)
+            const uint32_t cs = rs8_rt_col_stride(c->m) / 2;
+            c->rt_block_bytes = (uint64_t)c->k * cs * 2;
+            std::vector<uint16_t> t((size_t)c->k * c->k * cs + 8, 0);
+            for (uint32_t nd = 1; nd <= c->k; ++nd)
+                for (uint32_t col = 0; col < nd; ++col)
+                    for (uint32_t r = 0; r < c->m; ++r)
+                        t[((size_t)(nd - 1) * c->k + col) * cs + r] =
+                            (uint16_t)(coef[((size_t)(nd - 1) * c->k + col) * c->cs + r] << 7);
+            if ((rc = c->d_rt.reserve(t.size()))) return rc;
+            NFEC_HIP(hipMemcpy(c->d_rt.p, t.data(), t.size() * 2, hipMemcpyHostToDevice));
+        }
         // one in-order Encode step: inputs [d, P0..P(m-1)] -> new P (normEncoderMDP.cpp:178-211)
         std::vector<uint8_t> step((size_t)(c->m + 1) * c->cs, 0);
         for (uint32_t i = 0; i < c->m; ++i) {
@@ -387,6 +405,11 @@ int build_codec(nfec_codec* c)
         if (rc) return rc;
         rc = upload(c->d_gen, genb.data(), genb.size());
         if (rc) return rc;
+        if (!wide) {
+            const std::vector<uint16_t> t = rs8_rt_table(c->gen, c->k, c->m);
+            if ((rc = c->d_rt.reserve(t.size()))) return rc;
+            NFEC_HIP(hipMemcpy(c->d_rt.p, t.data(), t.size() * 2, hipMemcpyHostToDevice));
+        }
         // RS16: table offsets of the bit-sliced encode, 128 bytes per coefficient.  Every wave
         // re-reads its rows' offsets per column, so the kernel only wins while the table stays
         // cache-resident: (400, 100) is 5.3 MB and 11 % faster than the exp-table kernel,
@@ -662,6 +685,42 @@ int rs16_tmvp_encode(nfec_codec* c, const nfec_block_batch* b, hipStream_t s)
     return leave(NFEC_OK);
 }
 
+// RS8 / MDP encode on the runtime-coefficient kernel (gen_rs8_rt.hip); NFEC_ENOTSUP for layouts
+// it does not take (segment tails: vec % 8 != 0, offsets past 2^31)
+int launch_rt_encode(nfec_codec* c, const nfec_block_batch* b, hipStream_t s)
+{
+    static const bool use_rt = diag_knob("NFEC_RT", 1) != 0;  // 0: the v_perm kernel (A/B)
+    if (!use_rt || !c->d_rt.p || (c->vec & 7u)) return NFEC_ENOTSUP;
+    const bool mdp = c->kind == NFEC_MDP;
+    Rs8RtArgs a;
+    a.in_base = static_cast<const uint8_t*>(b->blocks);
+    a.in_block_stride = b->block_stride;
+    a.in_seg_stride = b->seg_stride;
+    a.out_base = static_cast<uint8_t*>(b->blocks);
+    a.out_block_stride = b->block_stride;
+    a.out_seg_stride = b->seg_stride;
+    a.nblocks = b->nblocks;
+    a.vec_bytes = c->vec;
+    a.k = c->k;
+    a.m = c->m;
+    a.tab = c->d_rt.p;
+    a.tab_col_stride = rs8_rt_col_stride(c->m);
+    a.accumulate = (b->flags & NFEC_ACCUMULATE) ? 1u : 0u;
+    if (b->num_data) {
+        a.per_block = 1;
+        a.num_data = b->num_data;
+        a.out_after_data = 1;
+        if (mdp) {
+            a.tab_block_stride = c->rt_block_bytes;
+            a.tab_by_count = 1;
+        }
+    } else {
+        a.out_slot0 = c->k;
+        if (mdp) a.tab = c->d_rt.p + (uint64_t)(c->k - 1) * (c->rt_block_bytes / 2);
+    }
+    return launch_rs8_rt(a, s);
+}
+
 int encode_device(nfec_codec* c, const nfec_block_batch* b, hipStream_t s)
 {
     const bool acc = b->flags & NFEC_ACCUMULATE;
@@ -692,6 +751,12 @@ int encode_device(nfec_codec* c, const nfec_block_batch* b, hipStream_t s)
 #endif
         const int rc = launch_rs8_bitsliced_encode(c->k, c->m, e, s);
         if (rc != NFEC_ENOTSUP) return rc == NFEC_OK ? NFEC_OK : fail(rc, "bit-sliced encode launch failed");
+    }
+    if (c->kind == NFEC_RS8 && !force_generic()) {
+        // any other shape, and shortened batches (per-block mode: the block's numData columns,
+        // parity at slot numData + r): bit-sliced with runtime coefficients
+        const int rc = launch_rt_encode(c, b, s);
+        if (rc != NFEC_ENOTSUP) return rc;
     }
     if (c->kind == NFEC_RS8) {
         Gf8MatmulArgs a;
@@ -798,6 +863,11 @@ int encode_device(nfec_codec* c, const nfec_block_batch* b, hipStream_t s)
         const int rc = launch_mdp_asm_encode(c->k, c->m, e, s);
         if (rc != NFEC_ENOTSUP) return rc == NFEC_OK ? NFEC_OK : fail(rc, "MDP assembly encode launch failed");
 #endif
+    }
+    if (!force_generic()) {
+        // other shapes and shortened blocks (the block map of each block length as a table)
+        const int rc = launch_rt_encode(c, b, s);
+        if (rc != NFEC_ENOTSUP) return rc;
     }
     Gf8MatmulArgs a;
     a.in_base = static_cast<const uint8_t*>(b->blocks);

@@ -286,6 +286,49 @@ void gf16_t3_offsets(const std::vector<uint32_t>& parity_rows, uint32_t k, uint3
 int launch_gf16_bs_encode(const Gf16BsEncArgs& a, hipStream_t s);  // NFEC_ENOTSUP: layout not 8-byte aligned
 void gf16_bs_selectors(const std::vector<uint32_t>& parity_rows, uint32_t k, uint32_t m, uint16_t* sel);
 
+// GF(2^8) block-matrix products with runtime coefficients (gen_rs8_rt.hip): bit-sliced, each
+// coefficient a jump into a 256-entry snippet table.  out[b][oslot(r)] (^)= sum_c coef[c][r] *
+// in[b][islot(c)] for r < rows(b), c < cols(b).  The table holds snippet byte offsets (u16,
+// c << 7): entry (c, r) at tab + [block or count] * tab_block_stride + c * tab_col_stride + 2 r
+// (bytes), padded by 16 bytes past the last entry.
+//   flat mode (per_block = 0): item groups run across the blocks; cols = k, rows = m, islot =
+//     in_slot0 + c, oslot = out_slot0 + r (unshortened encode)
+//   per-block mode: item groups inside one block; cols = blk_cols[b] (else num_data[b], else k),
+//     rows = blk_rows[b] (<= 0: skip; else m); islot = in_slots[b][c] or in_slot0 + c; oslot =
+//     out_slots[b][r] or out_slot0 (+ num_data[b] with out_after_data) + r; table per block
+//     (tab_block_stride) or per numData (tab_by_count: block nd - 1, MDP) or shared (stride 0)
+struct Rs8RtArgs {
+    const uint8_t* in_base = nullptr;
+    uint64_t in_block_stride = 0;
+    uint32_t in_seg_stride = 0;
+    uint8_t* out_base = nullptr;
+    uint64_t out_block_stride = 0;
+    uint32_t out_seg_stride = 0;
+    uint32_t nblocks = 0;
+    uint32_t vec_bytes = 0;              // multiple of 8
+    uint32_t k = 0, m = 0;               // columns / rows (per-block mode: the largest)
+    uint32_t per_block = 0;
+    const uint16_t* num_data = nullptr;
+    const uint16_t* blk_cols = nullptr;
+    const int32_t* blk_rows = nullptr;
+    const uint16_t* in_slots = nullptr;
+    uint32_t in_slots_stride = 0, in_slot0 = 0;
+    const uint16_t* out_slots = nullptr;
+    uint32_t out_slots_stride = 0, out_slot0 = 0, out_after_data = 0;
+    const uint16_t* tab = nullptr;
+    uint64_t tab_block_stride = 0;       // bytes
+    uint32_t tab_col_stride = 0;         // bytes, multiple of 4
+    uint32_t tab_by_count = 0;
+    uint32_t accumulate = 0;             // XOR into the output slots
+    uint32_t pass_sets = 0;              // set by the launcher
+};
+constexpr uint32_t kRs8RtRows = 8;       // parity rows per pass (gen_rs8_rt.py asserts it)
+int launch_rs8_rt(const Rs8RtArgs& a, hipStream_t s);  // NFEC_ENOTSUP: layout not covered
+// snippet-offset table of an m x k generator (row-major parity rows): [c][r] u16, column stride
+// round_up(2m, 4) bytes, 16 bytes of padding
+std::vector<uint16_t> rs8_rt_table(const std::vector<uint32_t>& rows, uint32_t k, uint32_t m);
+inline uint32_t rs8_rt_col_stride(uint32_t m) { return (2u * m + 3u) & ~3u; }
+
 // RS decode planning (per block): pick parities, invert the e x e system, emit the
 // stage-1 (gather) and stage-2 (inverse) matrices and slot lists.
 struct RsPlanArgs {
