@@ -11,7 +11,7 @@ import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 # product kernels; gen_rs8_asm.py (the round-1 2-role encode) feeds the diagnostic library only
-GENERATORS = ["rs8_bitsliced", "rs8_q4", "fdec_asm", "solve_asm", "gf16_t3", "gf16_tw"]
+GENERATORS = ["rs8_bitsliced", "rs8_q4", "fdec_asm", "solve_asm", "gf16_t3", "gf16_tw", "rs8_rt"]
 
 
 @pytest.mark.parametrize("name", GENERATORS)
