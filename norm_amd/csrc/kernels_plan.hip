@@ -145,7 +145,10 @@ __global__ __launch_bounds__(kWave) void rs_plan_kernel(RsPlanArgs a)
                 if (s_idx >= 0) v = (E)((uint32_t)s_idx == t);
                 else v = gp[(uint64_t)(listP[t] - nd) * k + c];
             }
-            coef1[(uint64_t)c * cs + t] = v;
+            if (sizeof(E) == 1 && a.snip)
+                reinterpret_cast<uint16_t*>(a.coef1)[(uint64_t)b * k * cs + (uint64_t)c * cs + t] = (uint16_t)((uint32_t)v << 7);
+            else
+                coef1[(uint64_t)c * cs + t] = v;
         }
     }
 
@@ -234,7 +237,10 @@ __global__ __launch_bounds__(kWave) void rs_plan_kernel(RsPlanArgs a)
         const uint32_t t = idx / cs, s = idx % cs;  // column t (input z_t), row s (output)
         E v = 0;
         if (t < e && s < e) v = work[s * w2 + e + t];
-        coef2[idx] = v;
+        if (sizeof(E) == 1 && a.snip)
+            reinterpret_cast<uint16_t*>(a.coef2)[(uint64_t)b * cs * cs + idx] = (uint16_t)((uint32_t)v << 7);
+        else
+            coef2[idx] = v;
     }
     uint16_t* oslots = a.out_slots2 + (uint64_t)b * k;
     for (uint32_t s = lane; s < e; s += kWave) oslots[s] = listE[s];

@@ -938,11 +938,16 @@ int decode_device(nfec_codec* c, const nfec_block_batch* b, const uint16_t* locs
     // + 128: the bit-sliced solves' scalar loads read up to 128 slots past a block's list
     if ((rc = c->w_islots.reserve((size_t)sb * n + 128))) return rc;
     if ((rc = c->w_oslots.reserve((size_t)sb * n + 128))) return rc;
+    // RS8 repair of the blocks the fused / fixed-shape kernels do not take: both stages on the
+    // runtime-coefficient kernel, the plan writing snippet offsets (u16) instead of bytes
+    static const bool use_rt = diag_knob("NFEC_RT", 1) != 0;
+    const bool rt_dec = use_rt && c->kind == NFEC_RS8 && (c->vec % 8) == 0 && c->d_rt.p && !force_generic();
+    const uint32_t esz = rt_dec ? 2u : c->sym;  // bytes per plan coefficient
     if (c->kind == NFEC_MDP) {
         if ((rc = c->w_coef1.reserve((size_t)sb * n * dcs))) return rc;
     } else {
-        if ((rc = c->w_coef1.reserve((size_t)sb * c->k * dcs * c->sym))) return rc;
-        if ((rc = c->w_coef2.reserve((size_t)sb * dcs * dcs * c->sym))) return rc;
+        if ((rc = c->w_coef1.reserve((size_t)sb * c->k * dcs * esz + 16))) return rc;
+        if ((rc = c->w_coef2.reserve((size_t)sb * dcs * dcs * esz + 16))) return rc;
         if ((rc = c->w_z.reserve((size_t)sb * dcs * zstride))) return rc;
         if (big_plan && (rc = c->w_work.reserve((size_t)sb * rs_plan_work_bytes(dcs, c->sym)))) return rc;
     }
@@ -1247,7 +1252,52 @@ int decode_device(nfec_codec* c, const nfec_block_batch* b, const uint16_t* locs
             p.zero_seg_stride = b->seg_stride;
             p.zero_vec = c->vec & ~1u;
         }
+        // stage 1: z_t = sum over the block's nd columns (slots in_slots1: the surviving
+        // source and, for an erased one, its substitute parity) of the gathered generator
+        Rs8RtArgs r1;
+        r1.in_base = blocks;
+        r1.in_block_stride = b->block_stride;
+        r1.in_seg_stride = b->seg_stride;
+        r1.out_base = c->w_z.p;
+        r1.out_block_stride = (uint64_t)dcs * zstride;
+        r1.out_seg_stride = zstride;
+        r1.nblocks = nb;
+        r1.vec_bytes = c->vec;
+        r1.k = c->k;
+        r1.m = std::min(c->k, c->m);
+        r1.per_block = 1;
+        r1.num_data = nd;
+        r1.blk_rows = c->w_rows.p;
+        r1.in_slots = c->w_islots.p;
+        r1.in_slots_stride = c->k;
+        r1.tab = reinterpret_cast<const uint16_t*>(c->w_coef1.p);
+        r1.tab_block_stride = (uint64_t)c->k * dcs * 2;
+        r1.tab_col_stride = dcs * 2;
+        r1.slot_bound = c->k + c->m;
+        // stage 2: d_E = A^-1 z into the erased source slots
+        Rs8RtArgs r2 = r1;
+        r2.in_base = c->w_z.p;
+        r2.in_block_stride = (uint64_t)dcs * zstride;
+        r2.in_seg_stride = zstride;
+        r2.in_slots = nullptr;
+        r2.num_data = nullptr;
+        r2.blk_cols = c->w_cols.p;
+        r2.out_base = blocks;
+        r2.out_block_stride = b->block_stride;
+        r2.out_seg_stride = b->seg_stride;
+        r2.out_slots = c->w_oslots.p;
+        r2.out_slots_stride = c->k;
+        r2.tab = reinterpret_cast<const uint16_t*>(c->w_coef2.p);
+        r2.tab_block_stride = (uint64_t)dcs * dcs * 2;
+        r2.accumulate = acc;
+        r2.slot_bound = c->k;
+        p.snip = rt_dec && !fast && rs8_rt_covers(r1) && rs8_rt_covers(r2) ? 1u : 0u;
         if ((rc = launch_rs_plan(p, s))) return rc;
+        if (p.snip) {
+            if ((rc = launch_rs8_rt(r1, s)) || (rc = launch_rs8_rt(r2, s)))
+                return fail(rc == NFEC_ENOTSUP ? NFEC_EDEVICE : rc, "runtime-coefficient repair launch failed");
+            continue;
+        }
         if (t3dec) {
             // z_t for t below the plan's largest such e; the gather stage then overwrites the z
             // rows of the other blocks

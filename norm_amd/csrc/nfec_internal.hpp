@@ -320,10 +320,12 @@ struct Rs8RtArgs {
     uint32_t tab_col_stride = 0;         // bytes, multiple of 4
     uint32_t tab_by_count = 0;
     uint32_t accumulate = 0;             // XOR into the output slots
+    uint32_t slot_bound = 0;             // slot lists hold slots below this (0: 65536)
     uint32_t pass_sets = 0;              // set by the launcher
 };
 constexpr uint32_t kRs8RtRows = 8;       // parity rows per pass (gen_rs8_rt.py asserts it)
 int launch_rs8_rt(const Rs8RtArgs& a, hipStream_t s);  // NFEC_ENOTSUP: layout not covered
+bool rs8_rt_covers(const Rs8RtArgs& a);                // launch_rs8_rt would take it
 // snippet-offset table of an m x k generator (row-major parity rows): [c][r] u16, column stride
 // round_up(2m, 4) bytes, 16 bytes of padding
 std::vector<uint16_t> rs8_rt_table(const std::vector<uint32_t>& rows, uint32_t k, uint32_t m);
@@ -367,6 +369,9 @@ struct RsPlanArgs {
     // A^-1 from the Cauchy form of the Lagrange generator instead of Gauss-Jordan
     const uint16_t* lwp = nullptr;      // [k] log W'(x_j)
     const uint16_t* lw = nullptr;       // [m] log W(y_p)
+    // RS8: coef1 and coef2 as u16 snippet offsets (value << 7) for the runtime-coefficient
+    // kernel (gen_rs8_rt.hip) instead of bytes; same indexing, twice the bytes
+    uint32_t snip = 0;
 };
 constexpr uint32_t kPlanCfMaxE = 256;
 // per-block scratch of launch_rs_plan for decode row stride cs (elements of sym bytes)

@@ -117,3 +117,70 @@ def test_rt_round_trip_sweep_shapes(orc):
         sample = keep[:3].cpu().numpy()
         ref = orc.encode_blocks(NFEC_RS8, k, m, 1400, sample.copy())
         assert np.array_equal(sample, ref), (k, m)
+
+
+DEC = [
+    # k, m, vec, nblocks, source erasures, parity erasures, shortened
+    (16, 4, 1400, 31, 3, 1, False),
+    (32, 16, 1408, 17, 10, 6, False),
+    (128, 32, 1400, 9, 20, 5, False),
+    (200, 55, 136, 7, 40, 10, True),
+    (64, 32, 1400, 40, 16, 0, True),      # the headline shape, shortened: generic path
+    (3, 100, 64, 9, 3, 50, False),        # m > k
+    (127, 128, 72, 3, 100, 27, False),    # e = 100: four waves, several pass sets per stage
+    (64, 20, 4096, 5, 12, 3, False),      # two item groups per segment
+    (10, 7, 8, 200, 7, 0, False),         # e = m, one piece per segment
+]
+
+
+@pytest.mark.parametrize("k,m,vec,nb,es,ep,short", DEC)
+def test_rt_decode_matches_oracle(orc, k, m, vec, nb, es, ep, short):
+    rng = np.random.default_rng(k * 7 + m)
+    nd = rng.integers(max(1, es), k + 1, nb).astype(np.uint16) if short else np.full(nb, k, np.uint16)
+    host = orc.make_blocks(k, m, vec, nb, num_data=nd if short else None)
+    clean = orc.encode_blocks(NFEC_RS8, k, m, vec, host, nd if short else None)
+    locs = np.zeros((nb, m), np.uint16)
+    counts = np.zeros(nb, np.uint16)
+    rx = clean.copy()
+    for b in range(nb):
+        n = int(nd[b])
+        e = np.sort(np.concatenate([rng.choice(n, min(es, n), replace=False),
+                                    n + rng.choice(m, ep, replace=False)]))[:m]
+        counts[b] = len(e)
+        locs[b, :len(e)] = e
+        for s in e:
+            rx[b, s] = 0
+    ref = rx.copy()
+    st_ref = orc.decode_blocks(NFEC_RS8, k, m, vec, ref, locs, counts, nd if short else None)
+    dec = NormDecoderRS8()
+    assert dec.Init(k, m, vec)
+    dev = torch.from_numpy(rx).cuda()
+    st = dec.decode_blocks(dev, torch.from_numpy(locs.view(np.int16)).cuda(),
+                           torch.from_numpy(counts.view(np.int16)).cuda(),
+                           num_data=torch.from_numpy(nd.view(np.int16)).cuda() if short else None)
+    torch.cuda.synchronize()
+    assert np.array_equal(st.cpu().numpy(), st_ref)
+    assert np.array_equal(dev.cpu().numpy(), ref)
+
+
+def test_rt_decode_accumulates(orc):
+    """erased buffers that are not zero: the repair XORs into them, as the reference's addmul does"""
+    k, m, vec, nb = 32, 16, 1400, 6
+    clean = orc.encode_blocks(NFEC_RS8, k, m, vec, orc.make_blocks(k, m, vec, nb))
+    rng = np.random.default_rng(2)
+    locs = np.zeros((nb, m), np.uint16)
+    counts = np.full(nb, 9, np.uint16)
+    rx = clean.copy()
+    for b in range(nb):
+        e = np.sort(rng.choice(k, 9, replace=False))
+        locs[b, :9] = e
+        rx[b, e] = rng.integers(0, 256, (9, vec), dtype=np.uint8)
+    ref = rx.copy()
+    st_ref = orc.decode_blocks(NFEC_RS8, k, m, vec, ref, locs, counts)
+    dec = NormDecoderRS8()
+    assert dec.Init(k, m, vec)
+    dev = torch.from_numpy(rx).cuda()
+    st = dec.decode_blocks(dev, torch.from_numpy(locs.view(np.int16)).cuda(),
+                           torch.from_numpy(counts.view(np.int16)).cuda(), accumulate=True)
+    torch.cuda.synchronize()
+    assert np.array_equal(st.cpu().numpy(), st_ref) and np.array_equal(dev.cpu().numpy(), ref)

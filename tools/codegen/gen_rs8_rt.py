@@ -520,21 +520,26 @@ __global__ __launch_bounds__(256, 4) void rs8_rt_kernel(Rs8RtArgs a)
 
 }}  // namespace
 
+bool rs8_rt_covers(const Rs8RtArgs& a)
+{{
+    if ((a.vec_bytes & 7u) || a.vec_bytes == 0 || !a.tab || a.k == 0 || (a.tab_col_stride & 3u) ||
+        (a.per_block && (a.tab_block_stride & 3u)))
+        return false;
+    // every offset a wave forms stays below 2^31 (a flat item group spans at most
+    // 2048 / vec + 2 blocks), as do the slot offsets
+    const uint64_t nbg = a.per_block ? 1u : kGroupBytes / a.vec_bytes + 2u;
+    const uint64_t bound = a.slot_bound ? a.slot_bound : 65536u;
+    const uint64_t in_slots = a.in_slots ? bound : (uint64_t)a.in_slot0 + a.k;
+    const uint64_t out_slots = a.out_slots ? bound : (uint64_t)a.out_slot0 + (a.out_after_data ? a.k : 0u) + a.m;
+    return nbg * a.in_block_stride + in_slots * a.in_seg_stride + a.vec_bytes < (1ull << 31) &&
+           nbg * a.out_block_stride + out_slots * a.out_seg_stride + a.vec_bytes < (1ull << 31);
+}}
+
 int launch_rs8_rt(const Rs8RtArgs& in, hipStream_t s)
 {{
     if (in.nblocks == 0 || in.m == 0) return NFEC_OK;
-    if ((in.vec_bytes & 7u) || in.vec_bytes == 0 || !in.tab || in.k == 0 || (in.tab_col_stride & 3u) ||
-        (in.per_block && in.tab_block_stride & 3u))
-        return NFEC_ENOTSUP;
+    if (!rs8_rt_covers(in)) return NFEC_ENOTSUP;
     Rs8RtArgs a = in;
-    // every offset a wave forms stays below 2^31 (its item group spans at most 2 blocks in flat
-    // mode), as do the slot offsets
-    const uint64_t nbg = a.per_block ? 1u : kGroupBytes / a.vec_bytes + 2u;
-    const uint64_t in_slots = a.in_slots ? 65536u : (uint64_t)a.in_slot0 + a.k;
-    const uint64_t out_slots = a.out_slots ? 65536u : (uint64_t)a.out_slot0 + (a.out_after_data ? a.k : 0u) + a.m;
-    if (nbg * a.in_block_stride + in_slots * a.in_seg_stride + a.vec_bytes >= (1ull << 31) ||
-        nbg * a.out_block_stride + out_slots * a.out_seg_stride + a.vec_bytes >= (1ull << 31))
-        return NFEC_ENOTSUP;
     const uint32_t G = a.m <= {R}u ? 1u : a.m <= {2 * R}u ? 2u : 4u;
     a.pass_sets = (a.m + G * {R}u - 1u) / (G * {R}u);
     const uint64_t groups = a.per_block ? (uint64_t)a.nblocks * ((a.vec_bytes + kGroupBytes - 1u) / kGroupBytes)
