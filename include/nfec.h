@@ -3,8 +3,10 @@
  *
  * Drop-in boundary for NORM's FEC plugin layer (reference include/normEncoder.h:38-54):
  * plain pointers, sizes and integer status codes; no C++ or torch types cross it.
- * Every compute entry point runs hand-written gfx950 HIP kernels; there is no CPU
- * compute path behind this header (a missing/failed GPU yields NFEC_EDEVICE).
+ * Every compute entry point runs hand-written gfx950 HIP kernels (a missing/failed GPU yields
+ * NFEC_EDEVICE; nothing falls back to the CPU), except the two entry points named *_host in
+ * "host CPU per-segment path" below, which are the host path by definition: one Encode call of
+ * NORM's incremental sender is a few microseconds of work, less than a GPU round trip.
  *
  * Reference interfaces each entry replaces (paths in USNavalResearchLaboratory/norm):
  *   nfec_codec_create(_ex) NormEncoderRS8::Init  src/common/normEncoderRS8.cpp:400-462
@@ -233,6 +235,22 @@ int nfec_encode_segment(nfec_codec* codec, uint32_t segment_id, const void* data
 /* NormDecoder::Decode: returns erasure_count on success, 0 when undecodable, <0 on error. */
 int nfec_decode_vectors(nfec_codec* codec, void* const* vector_list, uint32_t num_data,
                         uint32_t erasure_count, const uint32_t* erasure_locs);
+/* ---- host CPU per-segment path (NORM's incremental sender) ----
+ * NormObject::NextSenderMsg calls Encode once per source segment and reads the parity without
+ * a call that ends the block (normObject.cpp:2038-2052), so each call must finish on return:
+ * m products of one segment, microseconds of CPU work against ~80 us for a GPU round trip
+ * (INTEGRATION.md section 1).  These run on the calling CPU thread: GF(2^8) products by GFNI
+ * affine transforms, AVX2 nibble tables or a scalar product table, whichever the CPU has. */
+enum { NFEC_HOST_GF_SCALAR = 0, NFEC_HOST_GF_AVX2 = 1, NFEC_HOST_GF_GFNI = 2 };
+/* dst[0..bytes) ^= c * src[0..bytes) in the RS8 field (0x11d).  isa: an NFEC_HOST_GF_* form, or
+ * < 0 for the best this CPU has.  Returns the form used, NFEC_ENOTSUP when the CPU lacks it. */
+int nfec_gf8_addmul_host(void* dst, const void* src, uint8_t c, size_t bytes, int isa);
+/* NormEncoderRS8::Encode (normEncoderRS8.cpp:473-483) on the host: parity_vectors[i] ^=
+ * G[k+i][segment_id] * data over vector_size bytes.  RS8 codecs only (NFEC_ENOTSUP otherwise).
+ * Reads only the codec's generator: concurrent calls on one codec are safe. */
+int nfec_encode_segment_host(nfec_codec* codec, uint32_t segment_id, const void* data,
+                             void* const* parity_vectors);
+
 /* sizeof() of the drop-in class NormEncoder<kind> (decoder = 0) or NormDecoder<kind>
  * (decoder = 1) as the library was compiled (include/norm_fec/normEncoder*.h), 0 for an
  * unknown kind: a NORM build can check that its translation units see the same layout. */

@@ -16,6 +16,11 @@ class NfecCodecBase
     // GPU used by codecs created afterwards in this process (one process per GPU)
     static void SetDevice(int device) { default_device = device; }
     static int GetDevice() { return default_device; }
+    // Where RS8 Encode runs, the incremental sender's per-segment call (normObject.cpp:2038-2052):
+    // on the host CPU (default; nfec_encode_segment_host, a few us per 1.4 KB segment) or as a
+    // GPU round trip (nfec_encode_segment, ~80 us).  Decode and the batch calls use the GPU.
+    static void SetSegmentEncodeOnHost(bool on) { segment_on_host = on; }
+    static bool GetSegmentEncodeOnHost() { return segment_on_host; }
     nfec_codec* Handle() const { return codec; }
     // Batched device-resident calls (see nfec_encode / nfec_decode): the throughput path for
     // block-at-once call sites such as NormObject::CalculateBlockParity (normObject.cpp:2203-2229).
@@ -33,6 +38,7 @@ class NfecCodecBase
     unsigned int npar;         // No. of parity packets (n-k)
     unsigned int vector_size;  // Size of biggest vector to encode
     static int default_device;
+    static bool segment_on_host;
 };
 
 #endif  // NFEC_CODEC_BASE_H

@@ -20,6 +20,7 @@ NFEC_OK, NFEC_EINVAL, NFEC_ENOMEM, NFEC_EDEVICE, NFEC_ERANGE, NFEC_ENOTSUP = 0, 
 NFEC_ACCUMULATE = 1
 NFEC_FEATURE_RS16_TOEPLITZ = 1
 NFEC_OPT_RS16_SHARED_TABLES, NFEC_OPT_RS16_TOEPLITZ_OFF, NFEC_OPT_RS16_TOEPLITZ_ON = 1, 2, 4
+NFEC_HOST_GF_SCALAR, NFEC_HOST_GF_AVX2, NFEC_HOST_GF_GFNI = 0, 1, 2
 
 
 class NfecError(RuntimeError):
@@ -136,6 +137,8 @@ _SIGS = {
     "nfec_request_test": (_I, [_P]),
     "nfec_request_wait": (_I, [_P]),
     "nfec_encode_segment": (_I, [_P, _U32, _P, _P]),
+    "nfec_encode_segment_host": (_I, [_P, _U32, _P, _P]),
+    "nfec_gf8_addmul_host": (_I, [_P, _P, _U8, ctypes.c_size_t, _I]),
     "nfec_decode_vectors": (_I, [_P, _P, _U32, _U32, _P]),
     "nfec_dropin_sizeof": (ctypes.c_size_t, [_I, _I]),
     "nfec_util_fill": (_I, [ctypes.POINTER(BlockBatch), _U32, _U32, _U64, _U64, _P]),

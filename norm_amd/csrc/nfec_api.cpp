@@ -1777,6 +1777,20 @@ int nfec_encode_segment(nfec_codec* c, uint32_t segment_id, const void* data, vo
     return NFEC_OK;
 }
 
+int nfec_encode_segment_host(nfec_codec* c, uint32_t segment_id, const void* data, void* const* parity)
+{
+    if (!c || !data || !parity) return fail(NFEC_EINVAL, "null argument");
+    if (c->kind != NFEC_RS8) return fail(NFEC_ENOTSUP, "the host per-segment path is RS8 only");
+    if (segment_id >= c->k) return fail(NFEC_EINVAL, "segmentId >= numData");
+    for (uint32_t i = 0; i < c->m; ++i)
+        if (!parity[i]) return fail(NFEC_EINVAL, "null parity vector");
+    const uint8_t* d = static_cast<const uint8_t*>(data);
+    const int isa = host_gf8_isa();
+    for (uint32_t i = 0; i < c->m; ++i)
+        host_gf8_addmul(static_cast<uint8_t*>(parity[i]), d, c->gen[(size_t)i * c->k + segment_id], c->vec, isa);
+    return NFEC_OK;
+}
+
 int nfec_decode_vectors(nfec_codec* c, void* const* vectors, uint32_t num_data, uint32_t erasure_count,
                         const uint32_t* erasure_locs)
 {

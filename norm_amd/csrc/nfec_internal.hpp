@@ -72,6 +72,10 @@ inline uint32_t rs_point(const Field& f, uint32_t row) { return row == 0 ? 0u : 
 void mdp_generator_poly(uint32_t m, std::vector<uint8_t>& g);
 void mdp_encode_matrix(const std::vector<uint8_t>& g, uint32_t m, uint32_t nd, uint8_t* out);
 
+// host_gf8.cpp: dst ^= c * src over n bytes on the host CPU (isa: NFEC_HOST_GF_*, < 0 best)
+void host_gf8_addmul(uint8_t* dst, const uint8_t* src, uint32_t c, size_t n, int isa);
+int host_gf8_isa();
+
 // v_perm product tables for one GF(2^8) constant c: 8 dwords (32 bytes)
 //   t0 = c*{0,1,2,3}   t1 = c*{4,5,6,7}       (low 3 bits)
 //   t2 = c*{0,8,16,24} t3 = c*{32,40,48,56}   (middle 3 bits)

@@ -13,6 +13,7 @@ NormEncoder::~NormEncoder() {}
 NormDecoder::~NormDecoder() {}
 
 int NfecCodecBase::default_device = 0;
+bool NfecCodecBase::segment_on_host = true;
 
 bool NfecCodecBase::InitCodec(int kind, unsigned int numData, unsigned int numParity, UINT16 vectorSize)
 {
@@ -62,7 +63,9 @@ int NfecCodecBase::DecodeBlocks(const nfec_block_batch* batch, const uint16_t* e
     void NAME::Encode(unsigned int segmentId, const char* dataVector, char** parityVectorList)   \
     {                                                                                            \
         if (!codec) return;                                                                      \
-        int rc = nfec_encode_segment(codec, segmentId, dataVector, (void* const*)parityVectorList); \
+        int rc = (KIND == NFEC_RS8 && segment_on_host)                                           \
+                     ? nfec_encode_segment_host(codec, segmentId, dataVector, (void* const*)parityVectorList) \
+                     : nfec_encode_segment(codec, segmentId, dataVector, (void* const*)parityVectorList); \
         if (rc != NFEC_OK) std::fprintf(stderr, "nfec: Encode failed: %s\n", nfec_last_error()); \
     }
 

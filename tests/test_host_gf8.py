@@ -1,0 +1,99 @@
+"""The host per-segment path (nfec_gf8_addmul_host, the body of nfec_encode_segment_host and of the
+drop-in NormEncoderRS8::Encode): dst ^= c * src in the RS8 field, every form this CPU has (GFNI,
+AVX2, scalar) against the oracle's product table -- the table the reference builds with
+init_mul_table (src/common/normEncoderRS8.cpp:140-149), pinned to galois.cpp's field
+(tests/test_oracle.py).  CPU only: no GPU is involved."""
+import ctypes
+
+import numpy as np
+import pytest
+
+from norm_amd import _native as N
+
+FORMS = [N.NFEC_HOST_GF_SCALAR, N.NFEC_HOST_GF_AVX2, N.NFEC_HOST_GF_GFNI]
+
+
+def _best():
+    src = np.zeros(1, np.uint8)
+    dst = np.zeros(1, np.uint8)
+    return N.lib().nfec_gf8_addmul_host(dst.ctypes.data, src.ctypes.data, 1, 1, -1)
+
+
+def _call(dst, src, c, n, form):
+    return N.lib().nfec_gf8_addmul_host(dst.ctypes.data, src.ctypes.data, c, n, form)
+
+
+@pytest.mark.parametrize("form", FORMS)
+def test_every_coefficient_matches_oracle(orc, form):
+    if form > _best():
+        pytest.skip("this CPU lacks the instructions of that form")
+    mul = orc.gf8_mul_table()
+    rng = np.random.default_rng(form)
+    src = np.arange(256, dtype=np.uint8).repeat(2)   # every byte value, 512 bytes
+    for c in range(256):
+        dst = rng.integers(0, 256, src.size, dtype=np.uint8)
+        want = dst ^ mul[c][src]
+        assert _call(dst, src, c, src.size, form) == form
+        assert np.array_equal(dst, want), c
+
+
+@pytest.mark.parametrize("form", FORMS)
+@pytest.mark.parametrize("n", [0, 1, 31, 32, 33, 63, 1400, 1401, 1408])
+def test_lengths_and_guard_bytes(orc, form, n):
+    """unaligned buffers, tails: exactly n bytes change (the reference processes vector_size bytes)"""
+    if form > _best():
+        pytest.skip("this CPU lacks the instructions of that form")
+    mul = orc.gf8_mul_table()
+    rng = np.random.default_rng(n)
+    src_buf = rng.integers(0, 256, n + 40, dtype=np.uint8)
+    dst_buf = rng.integers(0, 256, n + 40, dtype=np.uint8)
+    src, dst = src_buf[3:3 + n], dst_buf[5:5 + n]   # odd alignments
+    before = dst_buf.copy()
+    c = 0x8e
+    _call(dst, src, c, n, form)
+    want = before.copy()
+    want[5:5 + n] ^= mul[c][src]
+    assert np.array_equal(dst_buf, want)
+
+
+def test_zero_coefficient_and_bad_form():
+    src = np.full(64, 7, np.uint8)
+    dst = np.arange(64, dtype=np.uint8)
+    assert _call(dst, src, 0, 64, -1) >= 0
+    assert np.array_equal(dst, np.arange(64, dtype=np.uint8))
+    assert _call(dst, src, 3, 64, 7) == N.NFEC_EINVAL
+    assert N.lib().nfec_gf8_addmul_host(None, None, 3, 0, -1) >= 0
+    assert N.lib().nfec_gf8_addmul_host(ctypes.c_void_p(0), src.ctypes.data, 3, 8, -1) == N.NFEC_EINVAL
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("k,m,vec", [(64, 16, 1408), (64, 32, 1400), (200, 55, 1401), (1, 1, 8)])
+def test_encode_segment_host_matches_gpu_and_oracle(orc, k, m, vec):
+    """nfec_encode_segment_host (the drop-in RS8 Encode's default) and nfec_encode_segment (the
+    GPU round trip) give the oracle's per-segment parity, accumulated over a whole block"""
+    import norm_amd as na
+
+    enc = na.NormEncoderRS8()
+    assert enc.Init(k, m, vec)
+    host = orc.make_blocks(k, m, vec, 1)
+    ref = orc.encode_blocks(N.NFEC_RS8, k, m, vec, host.copy())
+    for fn in ("nfec_encode_segment_host", "nfec_encode_segment"):
+        par = [np.zeros(vec, np.uint8) for _ in range(m)]
+        arr = (ctypes.c_void_p * m)(*[p.ctypes.data for p in par])
+        for s in range(k):
+            d = np.ascontiguousarray(host[0, s, :vec])
+            assert getattr(N.lib(), fn)(enc._h, s, d.ctypes.data, arr) == 0
+        for p in range(m):
+            assert np.array_equal(par[p], ref[0, k + p, :vec]), (fn, p)
+
+
+@pytest.mark.gpu
+def test_encode_segment_host_is_rs8_only():
+    import norm_amd as na
+
+    enc = na.NormEncoderRS16()
+    assert enc.Init(10, 4, 64)
+    par = [np.zeros(64, np.uint8) for _ in range(4)]
+    arr = (ctypes.c_void_p * 4)(*[p.ctypes.data for p in par])
+    d = np.zeros(64, np.uint8)
+    assert N.lib().nfec_encode_segment_host(enc._h, 0, d.ctypes.data, arr) == N.NFEC_ENOTSUP

@@ -67,9 +67,22 @@ int main(int argc, char** argv)
     double t0 = now_us();
     for (unsigned i = 0; i < iters; ++i) enc->Encode(i % k, list[i % k], list.data() + k);
     const double enc_us = (now_us() - t0) / iters;
+    // RS8 Encode runs on the host CPU by default (nfec_encode_segment_host); the GPU round trip
+    // (nfec_encode_segment) beside it
+    double enc_gpu_us = -1;
+    if (!rs16 && !mdp) {
+        NfecCodecBase::SetSegmentEncodeOnHost(false);
+        for (unsigned i = 0; i < 8; ++i) enc->Encode(i % k, list[i % k], list.data() + k);
+        t0 = now_us();
+        for (unsigned i = 0; i < iters; ++i) enc->Encode(i % k, list[i % k], list.data() + k);
+        enc_gpu_us = (now_us() - t0) / iters;
+        NfecCodecBase::SetSegmentEncodeOnHost(true);
+    }
     // a clean encode of the block for the decode below
     for (unsigned p = k; p < n; ++p) std::memset(list[p], 0, vec);
     for (unsigned i = 0; i < k; ++i) enc->Encode(i, list[i], list.data() + k);
+    std::vector<std::vector<char>> parity_dropin(m);
+    for (unsigned p = 0; p < m; ++p) parity_dropin[p] = seg[k + p];
 
     // ---- one-block Decode with ne source erasures ----
     std::vector<unsigned> locs;
@@ -107,6 +120,8 @@ int main(int argc, char** argv)
             if (rs16) orc_rs16_encode(g16.data(), k, m, vec, i, ul[i], ul + k);
             else orc_rs8_encode(g8.data(), k, m, vec, i, ul[i], ul + k);
         }
+        // the drop-in's parity equals the oracle's
+        for (unsigned p = 0; p < m; ++p) bad += std::memcmp(parity_dropin[p].data(), list[k + p], vec) != 0;
         orc_dec_us = 0;
         for (unsigned it = 0; it < iters; ++it) {
             for (unsigned i = 0; i < ne; ++i) std::memset(list[locs[i]], 0, vec);
@@ -118,9 +133,12 @@ int main(int argc, char** argv)
         orc_dec_us /= iters;
     }
     std::printf("{\"kind\": \"%s\", \"k\": %u, \"m\": %u, \"vec\": %u, \"erasures\": %u, \"iters\": %u, "
-                "\"encode_us_per_call\": %.2f, \"decode_us_per_call\": %.2f, \"decode_status\": %d, \"bad\": %d, "
+                "\"encode_us_per_call\": %.2f, \"encode_gpu_us_per_call\": %.2f, \"encode_path\": \"%s\", "
+                "\"decode_us_per_call\": %.2f, \"decode_status\": %d, \"bad\": %d, "
                 "\"oracle_encode_us_per_call\": %.2f, \"oracle_decode_us_per_call\": %.2f}\n",
-                kind, k, m, vec, ne, iters, enc_us, dec_us, st, bad, orc_enc_us, orc_dec_us);
+                kind, k, m, vec, ne, iters, enc_us, enc_gpu_us,
+                (!rs16 && !mdp) ? "host (nfec_encode_segment_host)" : "gpu (nfec_encode_segment)", dec_us, st, bad,
+                orc_enc_us, orc_dec_us);
     delete enc;
     delete dec;
     return bad ? 1 : 0;
