@@ -145,10 +145,7 @@ __global__ __launch_bounds__(kWave) void rs_plan_kernel(RsPlanArgs a)
                 if (s_idx >= 0) v = (E)((uint32_t)s_idx == t);
                 else v = gp[(uint64_t)(listP[t] - nd) * k + c];
             }
-            if (sizeof(E) == 1 && a.snip)
-                reinterpret_cast<uint16_t*>(a.coef1)[(uint64_t)b * k * cs + (uint64_t)c * cs + t] = (uint16_t)((uint32_t)v << 7);
-            else
-                coef1[(uint64_t)c * cs + t] = v;
+            coef1[(uint64_t)c * cs + t] = v;
         }
     }
 
@@ -237,10 +234,7 @@ __global__ __launch_bounds__(kWave) void rs_plan_kernel(RsPlanArgs a)
         const uint32_t t = idx / cs, s = idx % cs;  // column t (input z_t), row s (output)
         E v = 0;
         if (t < e && s < e) v = work[s * w2 + e + t];
-        if (sizeof(E) == 1 && a.snip)
-            reinterpret_cast<uint16_t*>(a.coef2)[(uint64_t)b * cs * cs + idx] = (uint16_t)((uint32_t)v << 7);
-        else
-            coef2[idx] = v;
+        coef2[idx] = v;
     }
     uint16_t* oslots = a.out_slots2 + (uint64_t)b * k;
     for (uint32_t s = lane; s < e; s += kWave) oslots[s] = listE[s];
@@ -736,7 +730,147 @@ __global__ __launch_bounds__(64 * kPlan2Waves) void rs_plan2_kernel(RsPlan2Args 
     if (lane < e) a.out_slots2[(uint64_t)b * k + lane] = sE[lane];
 }
 
+// RS8 plan for the runtime-coefficient repair (gen_rs8_rt.hip), any (k, m) with k + m <= 255 and
+// shortened blocks: the outputs of rs_plan_kernel<uint8_t> (status, rows, the stage-1 gather
+// matrix over the block's numData columns with its slot list, the erased slots) with A^-1 in
+// the closed (Cauchy) form of rs_plan2_kernel, both matrices written as the kernel's snippet
+// offsets (u16, value << 7) in compact tables: coef1 [b][c < numData][t < e], coef2
+// [b][t < e][s < e], column stride cst u16.  Entries past e are never read.  One wave per
+// block, four blocks per workgroup sharing the field tables.
+__global__ __launch_bounds__(64 * kPlan2Waves) void rs8_plan_rt_kernel(RsPlanArgs a, uint32_t cst)
+{
+    constexpr uint32_t kE = 128;  // e <= min(k, m) <= 127 (k + m <= 255)
+    __shared__ uint8_t ex[512];
+    __shared__ uint16_t lg[256];
+    __shared__ uint8_t xs_w[kPlan2Waves][kE], yt_w[kPlan2Waves][kE];
+    __shared__ uint16_t sP_w[kPlan2Waves][kE], sE_w[kPlan2Waves][kE];
+    __shared__ int32_t lA_w[kPlan2Waves][kE], lB_w[kPlan2Waves][kE];
+    __shared__ uint8_t ers_w[kPlan2Waves][256];
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t w = uni(threadIdx.x >> 6);
+    uint8_t* xs = xs_w[w];
+    uint8_t* yt = yt_w[w];
+    uint16_t* sP = sP_w[w];
+    uint16_t* sE = sE_w[w];
+    int32_t* lA = lA_w[w];
+    int32_t* lB = lB_w[w];
+    uint8_t* ers = ers_w[w];
+    const uint32_t b = blockIdx.x * kPlan2Waves + w;
+    const bool live = b < a.nblocks;
+    const uint32_t k = a.k, m = a.m;
+    const uint32_t nd = live ? (a.num_data ? uni(a.num_data[b]) : k) : 1u;
+    const uint32_t ec = live ? uni(a.erasure_counts[b]) : 0u;
+    const uint16_t* locs = a.erasure_locs + (uint64_t)b * a.erasure_stride;
+    const uint8_t* gex = reinterpret_cast<const uint8_t*>(a.exp_tab);
+    for (uint32_t i = threadIdx.x; i < 510; i += 64 * kPlan2Waves) ex[i] = gex[i];
+    for (uint32_t i = threadIdx.x; i < 256; i += 64 * kPlan2Waves) lg[i] = a.log_tab[i];
+    for (uint32_t i = lane; i < 256; i += 64) ers[i] = 0;
+    __syncthreads();  // the only workgroup barrier: tables staged
+    if (!live) return;
+    // validate (sorted, in range) and count the source erasures (a prefix of the sorted list)
+    bool ok = nd >= 1 && nd <= k && ec <= m && ec <= a.erasure_stride;
+    uint32_t es = 0;
+    if (ok) {
+        bool bad = false;
+        uint32_t nsrc = 0;
+        for (uint32_t i = lane; i < ec; i += 64) {
+            const uint32_t l = locs[i];
+            if (l >= nd + m || (i > 0 && l <= locs[i - 1])) bad = true;
+            nsrc += l < nd;
+        }
+        for (int off = 32; off > 0; off >>= 1) nsrc += __shfl_xor(nsrc, off);
+        ok = !__any(bad);
+        es = uni(nsrc);
+    }
+    wave_lds_sync();
+    if (ok)
+        for (uint32_t i = lane; i < ec; i += 64) ers[locs[i]] = 1;
+    wave_lds_sync();
+    // the first es surviving parities in ascending slot order (reference scan :660-718)
+    uint32_t np = 0;
+    if (ok && es > 0) {
+        for (uint32_t base = 0; base < m && np < es; base += 64) {
+            const uint32_t p = base + lane;
+            const bool alive = p < m && !ers[nd + p];
+            const uint64_t bal = __ballot(alive);
+            const uint32_t r = np + (uint32_t)__popcll(bal & ((1ull << lane) - 1ull));
+            if (alive && r < es) {
+                sP[r] = (uint16_t)p;
+                yt[r] = ex[(k - 1 + p) % 255u];  // parity row p: generator row k + p, point alpha^(k+p-1)
+            }
+            np += (uint32_t)__popcll(bal);
+        }
+        if (np < es) ok = false;  // not enough parity
+    }
+    const uint32_t e = ok ? es : 0;
+    if (lane == 0) {
+        if (a.status) a.status[b] = ok ? (int32_t)ec : 0;
+        a.rows[b] = (int32_t)e;
+        a.cols2[b] = (uint16_t)e;
+    }
+    if (e == 0) return;
+    for (uint32_t i = lane; i < e; i += 64) {
+        const uint32_t s = locs[i];
+        sE[i] = (uint16_t)s;
+        xs[i] = s == 0 ? 0 : ex[(s - 1) % 255u];
+    }
+    wave_lds_sync();
+    // stage 1: the gather matrix over the block's columns; an erased column reads its
+    // substitute parity with a unit coefficient on its own row
+    uint16_t* c1 = reinterpret_cast<uint16_t*>(a.coef1) + (uint64_t)b * k * cst;
+    uint16_t* isl = a.in_slots1 + (uint64_t)b * k;
+    const uint8_t* gp = reinterpret_cast<const uint8_t*>(a.gen_parity);
+    for (uint32_t c = lane; c < nd; c += 64) {
+        uint32_t lo = 0, hi = e;  // is c erased? (sE sorted)
+        while (lo < hi) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (sE[mid] < c) lo = mid + 1;
+            else hi = mid;
+        }
+        const bool er = lo < e && sE[lo] == c;
+        isl[c] = er ? (uint16_t)(nd + sP[lo]) : (uint16_t)c;
+        for (uint32_t t = 0; t < e; ++t)
+            c1[(uint64_t)c * cst + t] = er ? (uint16_t)((lo == t) << 7) : (uint16_t)((uint32_t)gp[(uint64_t)sP[t] * k + c] << 7);
+    }
+    // stage 2: A^-1[s][t] = exp(lA[s] + lB[t] - log(x_s ^ y_t)) (rs_plan2_kernel's algebra)
+    for (uint32_t i = lane; i < e; i += 64) {
+        const uint32_t x = xs[i], y = yt[i];
+        int32_t acc = (int32_t)a.lwp[sE[i]], bcc = -(int32_t)a.lw[sP[i]];
+        for (uint32_t t = 0; t < e; ++t) {
+            acc += (int32_t)lg[x ^ yt[t]] - (int32_t)lg[x ^ xs[t]];
+            bcc += (int32_t)lg[y ^ xs[t]] - (int32_t)lg[y ^ yt[t]];
+        }
+        acc += (int32_t)lg[0];  // the t == i terms subtracted lg[x ^ x] = lg[0]
+        bcc += (int32_t)lg[0];
+        acc %= 255;
+        bcc %= 255;
+        lA[i] = acc < 0 ? acc + 255 : acc;
+        lB[i] = bcc < 0 ? bcc + 255 : bcc;
+    }
+    wave_lds_sync();
+    uint16_t* c2 = reinterpret_cast<uint16_t*>(a.coef2) + (uint64_t)b * min(k, m) * cst;
+    for (uint32_t idx = lane; idx < e * e; idx += 64) {
+        const uint32_t t = idx / e, s = idx - t * e;
+        int32_t l = lA[s] + lB[t] - (int32_t)lg[xs[s] ^ yt[t]];
+        if (l < 0) l += 255;
+        c2[(uint64_t)t * cst + s] = (uint16_t)((uint32_t)ex[l] << 7);
+    }
+    for (uint32_t i = lane; i < e; i += 64) a.out_slots2[(uint64_t)b * k + i] = sE[i];
+}
+
 }  // namespace
+
+int launch_rs8_plan_rt(const RsPlanArgs& a, uint32_t cst, hipStream_t s)
+{
+    if (a.nblocks == 0) return NFEC_OK;
+    if (a.bits != 8 || a.k + a.m > 255 || !a.lwp || !a.lw || (cst & 1u) || cst < std::min(a.k, a.m))
+        return NFEC_ENOTSUP;
+    hipLaunchKernelGGL(rs8_plan_rt_kernel, dim3((a.nblocks + kPlan2Waves - 1) / kPlan2Waves), dim3(64 * kPlan2Waves),
+                       0, s, a, cst);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return hip_fail(e, "rs8_plan_rt launch");
+    return NFEC_OK;
+}
 
 int launch_rs_plan2(const RsPlan2Args& a, hipStream_t s)
 {

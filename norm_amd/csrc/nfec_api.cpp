@@ -939,15 +939,18 @@ int decode_device(nfec_codec* c, const nfec_block_batch* b, const uint16_t* locs
     if ((rc = c->w_islots.reserve((size_t)sb * n + 128))) return rc;
     if ((rc = c->w_oslots.reserve((size_t)sb * n + 128))) return rc;
     // RS8 repair of the blocks the fused / fixed-shape kernels do not take: both stages on the
-    // runtime-coefficient kernel, the plan writing snippet offsets (u16) instead of bytes
+    // runtime-coefficient kernel, after a closed-form plan that writes its snippet tables
     static const bool use_rt = diag_knob("NFEC_RT", 1) != 0;
     const bool rt_dec = use_rt && c->kind == NFEC_RS8 && (c->vec % 8) == 0 && c->d_rt.p && !force_generic();
-    const uint32_t esz = rt_dec ? 2u : c->sym;  // bytes per plan coefficient
+    // (compact tables: columns of cst = min(k, m) rounded up to even entries, not dcs)
+    const uint32_t E = std::min(c->k, c->m), cst = (E + 1u) & ~1u;
     if (c->kind == NFEC_MDP) {
         if ((rc = c->w_coef1.reserve((size_t)sb * n * dcs))) return rc;
     } else {
-        if ((rc = c->w_coef1.reserve((size_t)sb * c->k * dcs * esz + 16))) return rc;
-        if ((rc = c->w_coef2.reserve((size_t)sb * dcs * dcs * esz + 16))) return rc;
+        if ((rc = c->w_coef1.reserve(std::max((size_t)sb * c->k * dcs * c->sym, (size_t)sb * c->k * cst * 2) + 16)))
+            return rc;
+        if ((rc = c->w_coef2.reserve(std::max((size_t)sb * dcs * dcs * c->sym, (size_t)sb * E * cst * 2) + 16)))
+            return rc;
         if ((rc = c->w_z.reserve((size_t)sb * dcs * zstride))) return rc;
         if (big_plan && (rc = c->w_work.reserve((size_t)sb * rs_plan_work_bytes(dcs, c->sym)))) return rc;
     }
@@ -1271,8 +1274,8 @@ int decode_device(nfec_codec* c, const nfec_block_batch* b, const uint16_t* locs
         r1.in_slots = c->w_islots.p;
         r1.in_slots_stride = c->k;
         r1.tab = reinterpret_cast<const uint16_t*>(c->w_coef1.p);
-        r1.tab_block_stride = (uint64_t)c->k * dcs * 2;
-        r1.tab_col_stride = dcs * 2;
+        r1.tab_block_stride = (uint64_t)c->k * cst * 2;
+        r1.tab_col_stride = cst * 2;
         r1.slot_bound = c->k + c->m;
         // stage 2: d_E = A^-1 z into the erased source slots
         Rs8RtArgs r2 = r1;
@@ -1288,16 +1291,18 @@ int decode_device(nfec_codec* c, const nfec_block_batch* b, const uint16_t* locs
         r2.out_slots = c->w_oslots.p;
         r2.out_slots_stride = c->k;
         r2.tab = reinterpret_cast<const uint16_t*>(c->w_coef2.p);
-        r2.tab_block_stride = (uint64_t)dcs * dcs * 2;
+        r2.tab_block_stride = (uint64_t)E * cst * 2;
         r2.accumulate = acc;
         r2.slot_bound = c->k;
-        p.snip = rt_dec && !fast && rs8_rt_covers(r1) && rs8_rt_covers(r2) ? 1u : 0u;
-        if ((rc = launch_rs_plan(p, s))) return rc;
-        if (p.snip) {
+        if (rt_dec && c->d_lwp.p && rs8_rt_covers(r1) && rs8_rt_covers(r2)) {
+            p.lwp = c->d_lwp.p;
+            p.lw = c->d_lw.p;
+            if ((rc = launch_rs8_plan_rt(p, cst, s))) return rc;
             if ((rc = launch_rs8_rt(r1, s)) || (rc = launch_rs8_rt(r2, s)))
                 return fail(rc == NFEC_ENOTSUP ? NFEC_EDEVICE : rc, "runtime-coefficient repair launch failed");
             continue;
         }
+        if ((rc = launch_rs_plan(p, s))) return rc;
         if (t3dec) {
             // z_t for t below the plan's largest such e; the gather stage then overwrites the z
             // rows of the other blocks

@@ -373,9 +373,6 @@ struct RsPlanArgs {
     // A^-1 from the Cauchy form of the Lagrange generator instead of Gauss-Jordan
     const uint16_t* lwp = nullptr;      // [k] log W'(x_j)
     const uint16_t* lw = nullptr;       // [m] log W(y_p)
-    // RS8: coef1 and coef2 as u16 snippet offsets (value << 7) for the runtime-coefficient
-    // kernel (gen_rs8_rt.hip) instead of bytes; same indexing, twice the bytes
-    uint32_t snip = 0;
 };
 constexpr uint32_t kPlanCfMaxE = 256;
 // per-block scratch of launch_rs_plan for decode row stride cs (elements of sym bytes)
@@ -384,6 +381,10 @@ inline uint64_t rs_plan_work_bytes(uint32_t cs, uint32_t sym)
     return ((uint64_t)cs * 2 * cs * sym + (uint64_t)cs * (4 + sym) + 7) & ~7ull;
 }
 int launch_rs_plan(const RsPlanArgs& a, hipStream_t s);
+// RS8 closed-form plan for the runtime-coefficient repair: rs_plan's outputs with coef1 as
+// [b][k][cst] and coef2 as [b][min(k, m)][cst] snippet-offset tables (u16, cst even and >=
+// min(k, m)); needs lwp / lw.  Entries past a block's e are not written.
+int launch_rs8_plan_rt(const RsPlanArgs& a, uint32_t cst, hipStream_t s);
 
 // RS decode planning, closed form (RS8, m <= 64): the systematic generator is the Lagrange
 // basis of the points x_j = point(j) evaluated at y_p = point(k+p), so the e x e system
