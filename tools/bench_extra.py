@@ -106,36 +106,8 @@ def main():
         "encode_ms": round(enc_ms, 3),
         "encode_GiBps": round(k * vec * nb / (enc_ms * 1e-3) / 2**30, 2),
     }
-    if kind == na.NFEC_RS16 and os.environ.get("NFEC_GF16_T3", "1") != "0" and vec % 8 == 0:
-        # op roofline of the shared-table RS16 encode (gen_gf16_t3.hip), counted from its code:
-        # per (item group of 64 lanes x 64 symbols, source column) every live parity row issues
-        # 16 planes x 3 ds_read_b64 (512 B each) and 7 VALU per plane, and per pass of up to RP
-        # rows the builder issues 506 VALU and 125 ds_write_b64 (RP = 44: 11 row waves x 4 rows;
-        # row waves past the last row leave).  With the Toeplitz split (features bit 0) the
-        # products are three of m/2 rows over k/2 columns instead of one of m rows over k.
-        groups = -(-nb * vec // 8192)
-        RP = 44
-        split = bool(enc.features() & na.NFEC_FEATURE_RS16_TOEPLITZ)
-        nprod, ncols, rows = (3, k // 2, m // 2) if split else (1, k, m)
-        passes = -(-rows // RP)
-        rows4 = -(-rows // 4) * 4
-        units = groups * ncols * nprod
-        lds_bytes = units * rows4 * 16 * 3 * 512
-        valu = units * (rows4 * 16 * 7 + passes * 506)
-        t = enc_ms * 1e-3
-        out["op_roofline"] = {
-            "kernel": "gf16_t3_multi_kernel (Toeplitz split: 3 products of m/2 rows over k/2 columns)"
-                      if split else "gf16_t3_encode_kernel",
-            "gf16_macs_per_s": float("%.4g" % (k * m * (vec // 2) * nb / t)),
-            "macs_note": "k*m*symbols of the generator product per second (the split computes 3/4 of them)"
-                         if split else "k*m*symbols per second",
-            "lds": {"achieved": float("%.4g" % (lds_bytes / t)), "peak": 256 * 256 * 2.4e9, "unit": "B/s",
-                    "frac": round(lds_bytes / t / (256 * 256 * 2.4e9), 4),
-                    "note": "table reads only (ds_read_b64, counted at 256 B/clk/CU), over the whole encode time"},
-            "valu": {"achieved": float("%.4g" % (valu * 64 / t)), "peak": 7.86e13, "unit": "lane-ops/s",
-                     "frac": round(valu * 64 / t / 7.86e13, 4), "insts_per_launch": valu},
-            "lds_insts_per_launch": units * rows4 * 16 * 3 + groups * nprod * passes * ncols * 125,
-        }
+    if kind == na.NFEC_RS16 and vec % 8 == 0:
+        out["op_roofline"] = rs16_op_roofline(enc, k, m, nb, vec, enc_ms)
     if er:
         dec_ms = timed(lambda: dec.decode_blocks(blocks, locs, counts, status=status, stream=stream), a.steps)
         keep = blocks.clone()
@@ -150,6 +122,57 @@ def main():
             "verified": bool(torch.equal(blocks[:, :k], keep[:, :k])) and bool((status == er).all()),
         })
     print(json.dumps(out), flush=True)
+
+
+VALU_PEAK = 7.86e13   # 256 CU x 4 SIMD x 32 lanes x 2.4 GHz (a wave64 VALU instruction: 2 cycles)
+
+
+def rs16_op_roofline(enc, k, m, nb, vec, enc_ms):
+    """Op roofline of the RS16 products from the tower kernel's own PMC counters (committed
+    under profiles/, tools/pmc_r03.sh on this workload): per launch SQ_INSTS_VALU / SALU / BRANCH
+    / LDS and the kernel's cycles (GRBM_GUI_ACTIVE / 8 XCDs).  Issue fractions: VALU x 2 cycles
+    over 1,024 SIMDs, SALU and branches one per cycle per CU (256), against those cycles."""
+    import glob
+    import norm_amd as na
+
+    split = bool(enc.features() & na.NFEC_FEATURE_RS16_TOEPLITZ)
+    name = "gf16_tw_multi_kernel" if split else "gf16_tw_encode_kernel"
+    out = {"kernel": name + (" (Toeplitz split: 3 tower-field products of m/2 rows over k/2 columns)"
+                             if split else " (tower-field products, snippet calls)"),
+           "gf16_macs_per_s": float("%.4g" % (k * m * (vec // 2) * nb / (enc_ms * 1e-3))),
+           "macs_note": "k*m*symbols of the generator product per second"
+                        + (" (the split computes 3/4 of them)" if split else "")}
+    src = None
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "r0*", "pmc_tw_*summary.json")), reverse=True):
+        d = json.load(open(path))
+        meta = d.get("_workload", {})
+        if meta.get("k") == k and meta.get("m") == m and meta.get("blocks") == nb and meta.get("vec") == vec:
+            src = (path, d)
+            break
+    if src is None:
+        out["pmc"] = None
+        out["note"] = "no committed tower-kernel PMC summary for this shape (tools/pmc_r03.sh, PMC_SCRIPT=tools/bench_extra.py)"
+        return out
+    path, d = src
+    kern = [v for kk, v in d.items() if kk != "_workload" and name in kk]
+    if not kern:
+        out["pmc"] = None
+        return out
+    c = kern[0]
+    cycles = c["GRBM_GUI_ACTIVE"] / 8.0
+    out.update({
+        "pmc": os.path.relpath(path, ROOT),
+        "cycles_per_launch": round(cycles),
+        "insts_per_launch": {n: round(c[f"SQ_INSTS_{n.upper()}"]) for n in ("valu", "salu", "branch", "lds", "smem")
+                             if f"SQ_INSTS_{n.upper()}" in c},
+        "valu_issue_frac": round(c["SQ_INSTS_VALU"] * 2 / (1024 * cycles), 4),
+        "salu_issue_frac": round(c["SQ_INSTS_SALU"] / (256 * cycles), 4),
+        "branch_issue_frac": round(c.get("SQ_INSTS_BRANCH", 0) / (256 * cycles), 4),
+        "valu_lane_ops_frac_of_peak": round(c["SQ_INSTS_VALU"] * 64 / (enc_ms * 1e-3) / VALU_PEAK, 4),
+        "note": "counters per launch of the product kernel; issue fractions against its own cycles "
+                "(VALU 2 cycles per wave64 instruction per SIMD, SALU / branch 1 per cycle per CU)",
+    })
+    return out
 
 
 SWEEP = [  # k, m, shortened, source erasures
