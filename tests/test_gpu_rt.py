@@ -184,3 +184,28 @@ def test_rt_decode_accumulates(orc):
                            torch.from_numpy(counts.view(np.int16)).cuda(), accumulate=True)
     torch.cuda.synchronize()
     assert np.array_equal(st.cpu().numpy(), st_ref) and np.array_equal(dev.cpu().numpy(), ref)
+
+
+def test_rt_decode_blocks_without_erasures(orc):
+    """blocks with nothing to repair (e = 0) beside ones with erasures: the plan writes no slot
+    list or table for them, so the repair must not read any (tests/test_gpu_random.py seed 24)"""
+    k, m, vec, nb = 77, 134, 1408, 40
+    clean = orc.encode_blocks(NFEC_RS8, k, m, vec, orc.make_blocks(k, m, vec, nb))
+    rng = np.random.default_rng(24)
+    locs = np.zeros((nb, m), np.uint16)
+    counts = np.zeros(nb, np.uint16)
+    rx = clean.copy()
+    for b in range(0, nb, 2):
+        e = np.sort(rng.choice(k, 1 + b % 70, replace=False))
+        locs[b, :len(e)] = e
+        counts[b] = len(e)
+        rx[b, e] = 0
+    ref = rx.copy()
+    st_ref = orc.decode_blocks(NFEC_RS8, k, m, vec, ref, locs, counts)
+    dec = NormDecoderRS8()
+    assert dec.Init(k, m, vec)
+    dev = torch.from_numpy(rx).cuda()
+    st = dec.decode_blocks(dev, torch.from_numpy(locs.view(np.int16)).cuda(),
+                           torch.from_numpy(counts.view(np.int16)).cuda())
+    torch.cuda.synchronize()
+    assert np.array_equal(st.cpu().numpy(), st_ref) and np.array_equal(dev.cpu().numpy(), ref)

@@ -459,7 +459,9 @@ __device__ __forceinline__ void rt_body(const Rs8RtArgs& a, uint32_t wg)
             const int32_t e = (int32_t)__builtin_amdgcn_readfirstlane((uint32_t)a.blk_rows[blk]);
             rows = e > 0 ? min((uint32_t)e, a.m) : 0u;
         }}
-        if (kk == 0u || kk > a.k || nd == 0u || nd > a.k) rows = 0u, kk = 0u;  // (the plan rejected it)
+        // a block with nothing to compute reads nothing: a plan writes no slot list or table for
+        // a block it rejected or that has no erasure (e = 0), so they must not be read
+        if (rows == 0u || kk == 0u || kk > a.k || nd == 0u || nd > a.k) rows = 0u, kk = 0u;
     }}
     if (!live) rows = 0u, kk = 0u;
     // the workgroup's step count: every wave runs the same number of barriers (G > 1)
