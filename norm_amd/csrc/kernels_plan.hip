@@ -816,21 +816,21 @@ __global__ __launch_bounds__(64 * kPlan2Waves) void rs8_plan_rt_kernel(RsPlanArg
     }
     wave_lds_sync();
     // stage 1: the gather matrix over the block's columns; an erased column reads its
-    // substitute parity with a unit coefficient on its own row
+    // substitute parity with a unit coefficient on its own row.  ers[c] becomes the erased
+    // column's rank s + 1 (0: present), so the entries can be written row-fastest (contiguous)
+    for (uint32_t i = lane; i < e; i += 64) ers[sE[i]] = (uint8_t)(i + 1);
+    wave_lds_sync();
     uint16_t* c1 = reinterpret_cast<uint16_t*>(a.coef1) + (uint64_t)b * k * cst;
     uint16_t* isl = a.in_slots1 + (uint64_t)b * k;
     const uint8_t* gp = reinterpret_cast<const uint8_t*>(a.gen_parity);
     for (uint32_t c = lane; c < nd; c += 64) {
-        uint32_t lo = 0, hi = e;  // is c erased? (sE sorted)
-        while (lo < hi) {
-            const uint32_t mid = (lo + hi) >> 1;
-            if (sE[mid] < c) lo = mid + 1;
-            else hi = mid;
-        }
-        const bool er = lo < e && sE[lo] == c;
-        isl[c] = er ? (uint16_t)(nd + sP[lo]) : (uint16_t)c;
-        for (uint32_t t = 0; t < e; ++t)
-            c1[(uint64_t)c * cst + t] = er ? (uint16_t)((lo == t) << 7) : (uint16_t)((uint32_t)gp[(uint64_t)sP[t] * k + c] << 7);
+        const uint32_t r = ers[c];
+        isl[c] = r ? (uint16_t)(nd + sP[r - 1]) : (uint16_t)c;
+    }
+    for (uint32_t idx = lane; idx < nd * e; idx += 64) {
+        const uint32_t c = idx / e, t = idx - c * e;
+        const uint32_t r = ers[c];
+        c1[(uint64_t)c * cst + t] = r ? (uint16_t)((r - 1 == t) << 7) : (uint16_t)((uint32_t)gp[(uint64_t)sP[t] * k + c] << 7);
     }
     // stage 2: A^-1[s][t] = exp(lA[s] + lB[t] - log(x_s ^ y_t)) (rs_plan2_kernel's algebra)
     for (uint32_t i = lane; i < e; i += 64) {

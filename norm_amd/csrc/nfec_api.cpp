@@ -74,12 +74,12 @@ constexpr uint32_t kRowPad = 32;       // coefficient rows padded (kernel row ch
 // allows (3 % of an MI355X's 288 GB).
 // budget_bytes caps it further (decode_device: half of the device memory free plus what the
 // codec already holds).  NFEC_SUBBATCH overrides (A/B runs, diagnostic library).
-static uint32_t sub_batch(uint64_t ws_bytes_per_block, uint64_t budget_bytes = 8ull << 30)
+static uint32_t sub_batch(uint64_t ws_bytes_per_block, uint64_t budget_bytes = 8ull << 30, uint32_t max_blocks = 65536)
 {
     static const long env = diag_knob("NFEC_SUBBATCH", 0, 0, 1L << 20);
     if (env > 0) return (uint32_t)std::max(256L, std::min(env, 1L << 20));
     const uint64_t cap = std::min<uint64_t>(8ull << 30, budget_bytes) / std::max<uint64_t>(ws_bytes_per_block, 1);
-    return (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(65536, cap));
+    return (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(max_blocks, cap));
 }
 
 uint32_t round_up(uint32_t v, uint32_t a) { return (v + a - 1) / a * a; }
@@ -907,25 +907,37 @@ int decode_device(nfec_codec* c, const nfec_block_batch* b, const uint16_t* locs
     // matrices and the z rows are sized by that, not by m (m >> k codes, e.g. npc's auto mode)
     const uint32_t dcs = c->kind == NFEC_MDP ? c->cs : round_up(std::max(1u, std::min(c->k, c->m)), kRowPad);
     const bool big_plan = c->kind != NFEC_MDP && std::min(c->k, c->m) > 64;
+    // RS8 blocks the fused / fixed-shape kernels do not take: both repair stages on the
+    // runtime-coefficient kernel after a closed-form plan that writes its snippet tables, in
+    // compact per-block tables (columns of cst = min(k, m) rounded up to even entries) and z
+    // rows (E = min(k, m) per block)
+    const bool fast = c->kind == NFEC_RS8 && !b->num_data && c->m <= 32 && c->k <= 64 && !force_generic() &&
+                      has_bitsliced(c->k, c->m) && bs::offsets_fit(b->block_stride, b->seg_stride);
+    static const bool use_rt = diag_knob("NFEC_RT", 1) != 0;
+    const bool rt_dec = use_rt && !fast && c->kind == NFEC_RS8 && (c->vec % 8) == 0 && c->d_rt.p && c->d_lwp.p &&
+                        !force_generic() &&
+                        b->block_stride + (uint64_t)(c->k + c->m) * b->seg_stride + c->vec < (1ull << 31);
+    const uint32_t E = std::min(c->k, c->m), cst = (E + 1u) & ~1u;
     // (+ RS16 on the tower kernel: stage 2's per-block snippet tables and row offsets)
-    const uint64_t ws_per_block = c->kind == NFEC_MDP
-                                      ? (uint64_t)n * c->cs
-                                      : (uint64_t)dcs * zstride + ((uint64_t)c->k + dcs) * dcs * c->sym +
-                                            (big_plan ? rs_plan_work_bytes(dcs, c->sym) : 0) +
-                                            (c->tw ? 2ull * gf16_tw_table_elems(std::min(c->k, c->m), std::min(c->k, c->m)) +
-                                                         4ull * (std::min(c->k, c->m) + 12)
-                                                   : 0);
+    const uint64_t ws_per_block = c->kind == NFEC_MDP ? (uint64_t)n * c->cs
+                                  : rt_dec            ? (uint64_t)E * zstride + ((uint64_t)c->k + E) * cst * 2
+                                                      : (uint64_t)dcs * zstride + ((uint64_t)c->k + dcs) * dcs * c->sym +
+                                                 (big_plan ? rs_plan_work_bytes(dcs, c->sym) : 0) +
+                                                 (c->tw ? 2ull * gf16_tw_table_elems(E, E) + 4ull * (E + 12) : 0);
+    // the runtime-coefficient repair takes passes of up to 1M blocks (its launches stay well
+    // below the grid limits): small codes, many blocks, no per-pass launch and plan overhead
+    const uint32_t max_pass = rt_dec ? (1u << 20) : 65536u;
     // passes of equal size, so no launch runs a small tail batch
     // passes as large as 8 GiB of workspace allows; when that would grow the workspace past what
     // the codec holds, also within half of the device memory free now (plus what it holds), so
     // a smaller GPU or several codecs per device get smaller passes instead of NFEC_ENOMEM
     const uint64_t per_block = ws_per_block + 4ull * n + 64;
-    uint32_t cap = std::min(b->nblocks, sub_batch(per_block));
+    uint32_t cap = std::min(b->nblocks, sub_batch(per_block, 8ull << 30, max_pass));
     const uint64_t held = c->w_z.n + c->w_coef1.n + c->w_coef2.n + c->w_work.n + 2ull * c->w_tw2.n;
     if ((uint64_t)cap * per_block > held) {
         size_t free_b = 0, total_b = 0;
         if (hipMemGetInfo(&free_b, &total_b) == hipSuccess)
-            cap = std::min(cap, sub_batch(per_block, ((uint64_t)free_b + held) / 2));
+            cap = std::min(cap, sub_batch(per_block, ((uint64_t)free_b + held) / 2, max_pass));
         else
             (void)hipGetLastError();
     }
@@ -938,19 +950,15 @@ int decode_device(nfec_codec* c, const nfec_block_batch* b, const uint16_t* locs
     // + 128: the bit-sliced solves' scalar loads read up to 128 slots past a block's list
     if ((rc = c->w_islots.reserve((size_t)sb * n + 128))) return rc;
     if ((rc = c->w_oslots.reserve((size_t)sb * n + 128))) return rc;
-    // RS8 repair of the blocks the fused / fixed-shape kernels do not take: both stages on the
-    // runtime-coefficient kernel, after a closed-form plan that writes its snippet tables
-    static const bool use_rt = diag_knob("NFEC_RT", 1) != 0;
-    const bool rt_dec = use_rt && c->kind == NFEC_RS8 && (c->vec % 8) == 0 && c->d_rt.p && !force_generic();
-    // (compact tables: columns of cst = min(k, m) rounded up to even entries, not dcs)
-    const uint32_t E = std::min(c->k, c->m), cst = (E + 1u) & ~1u;
     if (c->kind == NFEC_MDP) {
         if ((rc = c->w_coef1.reserve((size_t)sb * n * dcs))) return rc;
+    } else if (rt_dec) {
+        if ((rc = c->w_coef1.reserve((size_t)sb * c->k * cst * 2 + 16))) return rc;
+        if ((rc = c->w_coef2.reserve((size_t)sb * E * cst * 2 + 16))) return rc;
+        if ((rc = c->w_z.reserve((size_t)sb * E * zstride))) return rc;
     } else {
-        if ((rc = c->w_coef1.reserve(std::max((size_t)sb * c->k * dcs * c->sym, (size_t)sb * c->k * cst * 2) + 16)))
-            return rc;
-        if ((rc = c->w_coef2.reserve(std::max((size_t)sb * dcs * dcs * c->sym, (size_t)sb * E * cst * 2) + 16)))
-            return rc;
+        if ((rc = c->w_coef1.reserve((size_t)sb * c->k * dcs * c->sym))) return rc;
+        if ((rc = c->w_coef2.reserve((size_t)sb * dcs * dcs * c->sym))) return rc;
         if ((rc = c->w_z.reserve((size_t)sb * dcs * zstride))) return rc;
         if (big_plan && (rc = c->w_work.reserve((size_t)sb * rs_plan_work_bytes(dcs, c->sym)))) return rc;
     }
@@ -1003,8 +1011,6 @@ int decode_device(nfec_codec* c, const nfec_block_batch* b, const uint16_t* locs
         if ((rc = c->w_tw2.reserve((size_t)sb * tw2_elems))) return rc;
         if ((rc = c->w_rowoff.reserve((size_t)sb * (M2 + 12)))) return rc;
     }
-    const bool fast = c->kind == NFEC_RS8 && !b->num_data && c->m <= 32 && c->k <= 64 && !force_generic() &&
-                      has_bitsliced(c->k, c->m) && bs::offsets_fit(b->block_stride, b->seg_stride);
     if (fast) {
         if ((rc = c->w_emask.reserve((size_t)sb * 2))) return rc;
         if ((rc = c->w_psel.reserve((size_t)sb * 2))) return rc;
@@ -1262,7 +1268,7 @@ int decode_device(nfec_codec* c, const nfec_block_batch* b, const uint16_t* locs
         r1.in_block_stride = b->block_stride;
         r1.in_seg_stride = b->seg_stride;
         r1.out_base = c->w_z.p;
-        r1.out_block_stride = (uint64_t)dcs * zstride;
+        r1.out_block_stride = (uint64_t)E * zstride;
         r1.out_seg_stride = zstride;
         r1.nblocks = nb;
         r1.vec_bytes = c->vec;
@@ -1280,7 +1286,7 @@ int decode_device(nfec_codec* c, const nfec_block_batch* b, const uint16_t* locs
         // stage 2: d_E = A^-1 z into the erased source slots
         Rs8RtArgs r2 = r1;
         r2.in_base = c->w_z.p;
-        r2.in_block_stride = (uint64_t)dcs * zstride;
+        r2.in_block_stride = (uint64_t)E * zstride;
         r2.in_seg_stride = zstride;
         r2.in_slots = nullptr;
         r2.num_data = nullptr;
@@ -1294,7 +1300,9 @@ int decode_device(nfec_codec* c, const nfec_block_batch* b, const uint16_t* locs
         r2.tab_block_stride = (uint64_t)E * cst * 2;
         r2.accumulate = acc;
         r2.slot_bound = c->k;
-        if (rt_dec && c->d_lwp.p && rs8_rt_covers(r1) && rs8_rt_covers(r2)) {
+        if (rt_dec) {
+            if (!rs8_rt_covers(r1) || !rs8_rt_covers(r2))
+                return fail(NFEC_ENOTSUP, "runtime-coefficient repair: batch layout past its 2^31 offsets");
             p.lwp = c->d_lwp.p;
             p.lw = c->d_lw.p;
             if ((rc = launch_rs8_plan_rt(p, cst, s))) return rc;

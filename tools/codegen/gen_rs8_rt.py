@@ -423,12 +423,15 @@ namespace {{
 
 constexpr uint32_t kGroupBytes = 2048;   // 64 lanes x 4 pieces x 8 bytes
 
-// rows [row0, row1) of pass p of P (even boundaries: a pass's entries start 4-byte aligned)
-__device__ __forceinline__ void pass_rows(uint32_t rows, uint32_t P, uint32_t p, uint32_t& row0, uint32_t& row1)
+// rows [row0, row1) of pass p: the fewest passes of at most {R} rows, P = ceil(rows / {R}), rows
+// spread evenly over them (even boundaries: a pass's entries start 4-byte aligned); passes p >= P
+// have none (their waves only load and share columns, or leave)
+__device__ __forceinline__ void pass_rows(uint32_t rows, uint32_t p, uint32_t& row0, uint32_t& row1)
 {{
+    const uint32_t P = max(1u, (rows + {R - 1}u) / {R}u);
     const uint32_t h = (rows + 1u) / 2u;
-    row0 = min(rows, 2u * (p * h / P));
-    row1 = min(rows, 2u * ((p + 1u) * h / P));
+    row0 = p < P ? min(rows, 2u * (p * h / P)) : rows;
+    row1 = p < P ? min(rows, 2u * ((p + 1u) * h / P)) : rows;
 }}
 
 template <int G>
@@ -477,12 +480,14 @@ __device__ __forceinline__ void rt_body(const Rs8RtArgs& a, uint32_t wg)
         }}
     }}
     uint32_t row0 = 0, row1 = 0;
-    pass_rows(rows, G * sets, set * G + pw, row0, row1);
+    pass_rows(rows, set * G + pw, row0, row1);
     const uint32_t nr = __builtin_amdgcn_readfirstlane(row1 - row0);
     if constexpr (G == 1) {{
         if (nr == 0u) return;
     }} else {{
-        if (kl == 0u) return;  // workgroup-uniform
+        // workgroup-uniform: no columns anywhere in the workgroup, or (one item group per
+        // workgroup) a pass set past the block's rows
+        if (kl == 0u || (NG == 1 && set * G * {R}u >= rows)) return;
     }}
     const uint32_t b0 = pb ? blk : __builtin_amdgcn_readfirstlane((uint32_t)(min(f0, total - 1) / a.vec_bytes));
     const uint8_t* wb = a.in_base + (uint64_t)b0 * a.in_block_stride;
