@@ -181,11 +181,25 @@ def sweep(nr, x, ebuf):
 
 def col_offset(col_sgpr):
     """column index s[col_sgpr] -> its slot's byte offset s[S_COL]: slot = islot0 + c, or the
-    per-block slot list isl[c] (u16) when isl != 0"""
+    per-block slot list isl[c] (u16) when isl != 0 (one scalar load, waited for)"""
+    return slot_prefetch(col_sgpr) + ["s_waitcnt lgkmcnt(0)"] + col_offset_slw(col_sgpr)
+
+
+def slot_prefetch(col_sgpr, add=0):
+    """issue the scalar load of the slot-list dword holding column s[col_sgpr] + add into
+    s[S_SLW] (nothing in identity mode); a later lgkmcnt(0) wait makes it usable"""
+    L = [f"s_cmp_eq_u64 %[isl], 0", f"s_cbranch_scc1 Lpf_%=_{{uid}}",
+         f"s_add_u32 s{S_T2}, s{col_sgpr}, %[iph]"]
+    if add:
+        L.append(f"s_add_u32 s{S_T2}, s{S_T2}, {add}")
+    L += [f"s_lshr_b32 s{S_T2}, s{S_T2}, 1", f"s_lshl_b32 s{S_T2}, s{S_T2}, 2",
+          f"s_load_dword s{S_SLW}, %[isl], s{S_T2}", f"Lpf_%=_{{uid}}:"]
+    return L
+
+
+def col_offset_slw(col_sgpr):
+    """s[S_COL] = byte offset of column s[col_sgpr], its slot read from the prefetched s[S_SLW]"""
     return [f"s_cmp_eq_u64 %[isl], 0", f"s_cbranch_scc1 Lid_%=_{{uid}}",
-            f"s_add_u32 s{S_T2}, s{col_sgpr}, %[iph]",
-            f"s_lshr_b32 s{S_T2}, s{S_T2}, 1", f"s_lshl_b32 s{S_T2}, s{S_T2}, 2",
-            f"s_load_dword s{S_SLW}, %[isl], s{S_T2}", "s_waitcnt lgkmcnt(0)",
             f"s_add_u32 s{S_T2}, s{col_sgpr}, %[iph]", f"s_and_b32 s{S_T2}, s{S_T2}, 1",
             f"s_lshl_b32 s{S_T2}, s{S_T2}, 4",
             f"s_lshr_b32 s{S_COL}, s{S_SLW}, s{S_T2}", f"s_and_b32 s{S_COL}, s{S_COL}, 0xffff",
@@ -240,9 +254,10 @@ def step_loop_shared(G, x, nr):
         L.append(f"ds_write_b64 v{TMP[0]}, v[{SLOT[2 * p]}:{SLOT[2 * p + 1]}] offset:{512 * p}")
     L.append(f"Lnotr{x}_%=:")
     # the slot's data went to LDS: wait before the next column's loads overwrite it
+    # (the wait also covers the slot-list dword of the next column, prefetched a step ago)
     L += ["s_waitcnt lgkmcnt(0)",
           f"s_add_u32 s{S_C}, s{S_C}, {G}", f"s_cmp_lt_u32 s{S_C}, %[k]", f"s_cbranch_scc0 Lnl{x}_%="]
-    L += uniq(col_offset(S_C)) + loads(SLOT)
+    L += uniq(col_offset_slw(S_C)) + loads(SLOT) + uniq(slot_prefetch(S_C, G))
     L += [f"Lnl{x}_%=:", "s_barrier"]
     if nr != 0:
         # fetch column 0 of the step: planes -> S, entries -> buffer 0 (a wave whose item
@@ -284,8 +299,8 @@ def step_loop_single(x, nr):
         # (into the other slot) and entries go out
         L += ["s_waitcnt lgkmcnt(0)",
               f"s_add_u32 s{S_C}, s{S_SB}, 1", f"s_cmp_lt_u32 s{S_C}, %[k]", f"s_cbranch_scc0 Lnl{y}_%="]
-        L += uniq(col_offset(S_C)) + loads(nxt)
-        L += table_fetch(S_C, S_OFF[(half + 1) % 2])
+        L += uniq(col_offset_slw(S_C)) + loads(nxt)
+        L += table_fetch(S_C, S_OFF[(half + 1) % 2]) + uniq(slot_prefetch(S_C, 1))
         L += ["s_waitcnt vmcnt(4)", f"s_branch Lgo{y}_%=",
               f"Lnl{y}_%=:", "s_waitcnt vmcnt(0)", f"Lgo{y}_%=:"]
         L += transpose(cur, temps_pool())
@@ -311,13 +326,13 @@ def body(G):
         for i in range(8):
             L.append(f"v_mov_b32 v{acc_reg(r, i)}, 0")
     if G == 1:
-        # column 0 and its entries
+        # column 0 and its entries; column 1's slot-list dword
         L += [f"s_mov_b32 s{S_C}, 0", f"s_cmp_lt_u32 s{S_C}, %[k]", "s_cbranch_scc0 Lnl0_%="]
         L += uniq(col_offset(S_C)) + loads(SLOT)
-        L += table_fetch(S_C, S_OFF[0])
+        L += table_fetch(S_C, S_OFF[0]) + uniq(slot_prefetch(S_C, 1))
     else:
         L += [f"s_mov_b32 s{S_C}, %[wv]", f"s_cmp_lt_u32 s{S_C}, %[k]", "s_cbranch_scc0 Lnl0_%="]
-        L += uniq(col_offset(S_C)) + loads(SLOT)
+        L += uniq(col_offset(S_C)) + loads(SLOT) + uniq(slot_prefetch(S_C, G))
     L += ["Lnl0_%=:", f"s_mov_b32 s{S_TGT + 1}, s{S_SNIP + 1}"]
     # helpers (G >= 2, no rows) only load and share
     if G > 1:
@@ -467,6 +482,8 @@ __device__ __forceinline__ void rt_body(const Rs8RtArgs& a, uint32_t wg)
         if (rows == 0u || kk == 0u || kk > a.k || nd == 0u || nd > a.k) rows = 0u, kk = 0u;
     }}
     if (!live) rows = 0u, kk = 0u;
+    // an item group whose rows all lie before this pass set has nothing to do here
+    if (set * G * {R}u >= rows) rows = 0u, kk = 0u;
     // the workgroup's step count: every wave runs the same number of barriers (G > 1)
     uint32_t kl = kk;
     if constexpr (G > 1) {{
@@ -485,9 +502,7 @@ __device__ __forceinline__ void rt_body(const Rs8RtArgs& a, uint32_t wg)
     if constexpr (G == 1) {{
         if (nr == 0u) return;
     }} else {{
-        // workgroup-uniform: no columns anywhere in the workgroup, or (one item group per
-        // workgroup) a pass set past the block's rows
-        if (kl == 0u || (NG == 1 && set * G * {R}u >= rows)) return;
+        if (kl == 0u) return;  // workgroup-uniform: no group of the workgroup has work in this set
     }}
     const uint32_t b0 = pb ? blk : __builtin_amdgcn_readfirstlane((uint32_t)(min(f0, total - 1) / a.vec_bytes));
     const uint8_t* wb = a.in_base + (uint64_t)b0 * a.in_block_stride;
@@ -547,7 +562,9 @@ int launch_rs8_rt(const Rs8RtArgs& in, hipStream_t s)
     if (in.nblocks == 0 || in.m == 0) return NFEC_OK;
     if (!rs8_rt_covers(in)) return NFEC_ENOTSUP;
     Rs8RtArgs a = in;
-    const uint32_t G = a.m <= {R}u ? 1u : a.m <= {2 * R}u ? 2u : 4u;
+    // waves per item group: by the row count in flat mode; per-block mode (rows vary per block,
+    // a repair's e is usually well below m) two waves of {R} rows, more pass sets for more rows
+    const uint32_t G = a.m <= {R}u ? 1u : (a.m <= {2 * R}u || a.per_block) ? 2u : 4u;
     a.pass_sets = (a.m + G * {R}u - 1u) / (G * {R}u);
     const uint64_t groups = a.per_block ? (uint64_t)a.nblocks * ((a.vec_bytes + kGroupBytes - 1u) / kGroupBytes)
                                         : ((uint64_t)a.nblocks * a.vec_bytes + kGroupBytes - 1u) / kGroupBytes;
