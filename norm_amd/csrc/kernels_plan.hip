@@ -731,12 +731,21 @@ __global__ __launch_bounds__(64 * kPlan2Waves) void rs_plan2_kernel(RsPlan2Args 
 }
 
 // RS8 plan for the runtime-coefficient repair (gen_rs8_rt.hip), any (k, m) with k + m <= 255 and
-// shortened blocks: the outputs of rs_plan_kernel<uint8_t> (status, rows, the stage-1 gather
-// matrix over the block's numData columns with its slot list, the erased slots) with A^-1 in
-// the closed (Cauchy) form of rs_plan2_kernel, both matrices written as the kernel's snippet
-// offsets (u16, value << 7) in compact tables: coef1 [b][c < numData][t < e], coef2
-// [b][t < e][s < e], column stride cst u16.  Entries past e are never read.  One wave per
-// block, four blocks per workgroup sharing the field tables.
+// shortened blocks, in ONE pass over the block: the erased source d_E is a linear map of the
+// block's numData received columns (the surviving source and, in place of each erased one, its
+// substitute parity), d_E = A^-1 (P_S + G_{S,R} d_R), so the plan writes the whole e x numData
+// matrix of that map and the repair is an encode-like product, numData columns in, e rows out.
+// The generator's parity rows are a scaled Cauchy matrix, G[p][j] = a_p b_j / (y_p + x_j)
+// (the points and scalings behind rs_plan2_kernel's closed-form A^-1), so both parts are closed
+// forms:
+//   erased column j = E_r (reads parity S_r):  W[s][j] = A^-1[s][r] = exp(lA[s] + lB[r] - log(x_s + y_r))
+//   received column j:   W[s][j] = (A^-1 G_{S,j})[s] = exp(lA[s] + lC[j] - log(x_s + x_j)),
+//   lC[j] = log b_j + sum_s' log(x_j + x_s') - sum_t log(x_j + y_t)
+// (the partial-fraction solution of a Cauchy system with one more column; lwp = -log b).  Per
+// block: status and rows (e) as rs_plan_kernel<uint8_t>, the column slot list, the erased slots,
+// and the matrix as the kernel's snippet offsets (u16, value << 7) in a compact table coef1
+// [b][j < numData][s < e], column stride cst u16.  One wave per block, four blocks per
+// workgroup sharing the field tables.
 __global__ __launch_bounds__(64 * kPlan2Waves) void rs8_plan_rt_kernel(RsPlanArgs a, uint32_t cst)
 {
     constexpr uint32_t kE = 128;  // e <= min(k, m) <= 127 (k + m <= 255)
@@ -745,7 +754,7 @@ __global__ __launch_bounds__(64 * kPlan2Waves) void rs8_plan_rt_kernel(RsPlanArg
     __shared__ uint8_t xs_w[kPlan2Waves][kE], yt_w[kPlan2Waves][kE];
     __shared__ uint16_t sP_w[kPlan2Waves][kE], sE_w[kPlan2Waves][kE];
     __shared__ int32_t lA_w[kPlan2Waves][kE], lB_w[kPlan2Waves][kE];
-    __shared__ uint8_t ers_w[kPlan2Waves][256];
+    __shared__ uint8_t ers_w[kPlan2Waves][256], lC_w[kPlan2Waves][256];
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t w = uni(threadIdx.x >> 6);
     uint8_t* xs = xs_w[w];
@@ -755,6 +764,7 @@ __global__ __launch_bounds__(64 * kPlan2Waves) void rs8_plan_rt_kernel(RsPlanArg
     int32_t* lA = lA_w[w];
     int32_t* lB = lB_w[w];
     uint8_t* ers = ers_w[w];
+    uint8_t* lC = lC_w[w];
     const uint32_t b = blockIdx.x * kPlan2Waves + w;
     const bool live = b < a.nblocks;
     const uint32_t k = a.k, m = a.m;
@@ -815,24 +825,16 @@ __global__ __launch_bounds__(64 * kPlan2Waves) void rs8_plan_rt_kernel(RsPlanArg
         xs[i] = s == 0 ? 0 : ex[(s - 1) % 255u];
     }
     wave_lds_sync();
-    // stage 1: the gather matrix over the block's columns; an erased column reads its
-    // substitute parity with a unit coefficient on its own row.  ers[c] becomes the erased
-    // column's rank s + 1 (0: present), so the entries can be written row-fastest (contiguous)
+    // ers[j] becomes the erased column's rank r + 1 (0: received), the column slot list reads
+    // the substitute parity S_r for it
     for (uint32_t i = lane; i < e; i += 64) ers[sE[i]] = (uint8_t)(i + 1);
     wave_lds_sync();
-    uint16_t* c1 = reinterpret_cast<uint16_t*>(a.coef1) + (uint64_t)b * k * cst;
     uint16_t* isl = a.in_slots1 + (uint64_t)b * k;
-    const uint8_t* gp = reinterpret_cast<const uint8_t*>(a.gen_parity);
-    for (uint32_t c = lane; c < nd; c += 64) {
-        const uint32_t r = ers[c];
-        isl[c] = r ? (uint16_t)(nd + sP[r - 1]) : (uint16_t)c;
+    for (uint32_t j = lane; j < nd; j += 64) {
+        const uint32_t r = ers[j];
+        isl[j] = r ? (uint16_t)(nd + sP[r - 1]) : (uint16_t)j;
     }
-    for (uint32_t idx = lane; idx < nd * e; idx += 64) {
-        const uint32_t c = idx / e, t = idx - c * e;
-        const uint32_t r = ers[c];
-        c1[(uint64_t)c * cst + t] = r ? (uint16_t)((r - 1 == t) << 7) : (uint16_t)((uint32_t)gp[(uint64_t)sP[t] * k + c] << 7);
-    }
-    // stage 2: A^-1[s][t] = exp(lA[s] + lB[t] - log(x_s ^ y_t)) (rs_plan2_kernel's algebra)
+    // lA, lB: A^-1[s][t] = exp(lA[s] + lB[t] - log(x_s ^ y_t)) (rs_plan2_kernel's algebra)
     for (uint32_t i = lane; i < e; i += 64) {
         const uint32_t x = xs[i], y = yt[i];
         int32_t acc = (int32_t)a.lwp[sE[i]], bcc = -(int32_t)a.lw[sP[i]];
@@ -847,13 +849,28 @@ __global__ __launch_bounds__(64 * kPlan2Waves) void rs8_plan_rt_kernel(RsPlanArg
         lA[i] = acc < 0 ? acc + 255 : acc;
         lB[i] = bcc < 0 ? bcc + 255 : bcc;
     }
+    // lC for the received columns (x_j differs from every erased and parity point)
+    for (uint32_t j = lane; j < nd; j += 64) {
+        if (ers[j]) continue;
+        const uint32_t x = j == 0 ? 0u : ex[(j - 1) % 255u];
+        int32_t acc = -(int32_t)a.lwp[j];
+        for (uint32_t t = 0; t < e; ++t) acc += (int32_t)lg[x ^ xs[t]] - (int32_t)lg[x ^ yt[t]];
+        acc %= 255;
+        lC[j] = (uint8_t)(acc < 0 ? acc + 255 : acc);
+    }
     wave_lds_sync();
-    uint16_t* c2 = reinterpret_cast<uint16_t*>(a.coef2) + (uint64_t)b * min(k, m) * cst;
-    for (uint32_t idx = lane; idx < e * e; idx += 64) {
-        const uint32_t t = idx / e, s = idx - t * e;
-        int32_t l = lA[s] + lB[t] - (int32_t)lg[xs[s] ^ yt[t]];
+    // the matrix, row-fastest (contiguous writes)
+    uint16_t* c1 = reinterpret_cast<uint16_t*>(a.coef1) + (uint64_t)b * k * cst;
+    for (uint32_t idx = lane; idx < nd * e; idx += 64) {
+        const uint32_t j = idx / e, s = idx - j * e;
+        const uint32_t r = ers[j];
+        int32_t l;
+        if (r)
+            l = lA[s] + lB[r - 1] - (int32_t)lg[xs[s] ^ yt[r - 1]];
+        else
+            l = lA[s] + (int32_t)lC[j] - (int32_t)lg[xs[s] ^ (j == 0 ? 0u : ex[(j - 1) % 255u])];
         if (l < 0) l += 255;
-        c2[(uint64_t)t * cst + s] = (uint16_t)((uint32_t)ex[l] << 7);
+        c1[(uint64_t)j * cst + s] = (uint16_t)((uint32_t)ex[l] << 7);
     }
     for (uint32_t i = lane; i < e; i += 64) a.out_slots2[(uint64_t)b * k + i] = sE[i];
 }

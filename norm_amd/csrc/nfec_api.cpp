@@ -907,10 +907,10 @@ int decode_device(nfec_codec* c, const nfec_block_batch* b, const uint16_t* locs
     // matrices and the z rows are sized by that, not by m (m >> k codes, e.g. npc's auto mode)
     const uint32_t dcs = c->kind == NFEC_MDP ? c->cs : round_up(std::max(1u, std::min(c->k, c->m)), kRowPad);
     const bool big_plan = c->kind != NFEC_MDP && std::min(c->k, c->m) > 64;
-    // RS8 blocks the fused / fixed-shape kernels do not take: both repair stages on the
-    // runtime-coefficient kernel after a closed-form plan that writes its snippet tables, in
-    // compact per-block tables (columns of cst = min(k, m) rounded up to even entries) and z
-    // rows (E = min(k, m) per block)
+    // RS8 blocks the fused / fixed-shape kernels do not take: a closed-form plan writes each
+    // block's whole repair map (e x numData, rs8_plan_rt_kernel) as a compact snippet table
+    // (columns of cst = min(k, m) rounded up to even entries) and ONE pass of the
+    // runtime-coefficient kernel computes the erased source from the received columns
     const bool fast = c->kind == NFEC_RS8 && !b->num_data && c->m <= 32 && c->k <= 64 && !force_generic() &&
                       has_bitsliced(c->k, c->m) && bs::offsets_fit(b->block_stride, b->seg_stride);
     static const bool use_rt = diag_knob("NFEC_RT", 1) != 0;
@@ -920,7 +920,7 @@ int decode_device(nfec_codec* c, const nfec_block_batch* b, const uint16_t* locs
     const uint32_t E = std::min(c->k, c->m), cst = (E + 1u) & ~1u;
     // (+ RS16 on the tower kernel: stage 2's per-block snippet tables and row offsets)
     const uint64_t ws_per_block = c->kind == NFEC_MDP ? (uint64_t)n * c->cs
-                                  : rt_dec            ? (uint64_t)E * zstride + ((uint64_t)c->k + E) * cst * 2
+                                  : rt_dec            ? (uint64_t)c->k * cst * 2
                                                       : (uint64_t)dcs * zstride + ((uint64_t)c->k + dcs) * dcs * c->sym +
                                                  (big_plan ? rs_plan_work_bytes(dcs, c->sym) : 0) +
                                                  (c->tw ? 2ull * gf16_tw_table_elems(E, E) + 4ull * (E + 12) : 0);
@@ -954,8 +954,6 @@ int decode_device(nfec_codec* c, const nfec_block_batch* b, const uint16_t* locs
         if ((rc = c->w_coef1.reserve((size_t)sb * n * dcs))) return rc;
     } else if (rt_dec) {
         if ((rc = c->w_coef1.reserve((size_t)sb * c->k * cst * 2 + 16))) return rc;
-        if ((rc = c->w_coef2.reserve((size_t)sb * E * cst * 2 + 16))) return rc;
-        if ((rc = c->w_z.reserve((size_t)sb * E * zstride))) return rc;
     } else {
         if ((rc = c->w_coef1.reserve((size_t)sb * c->k * dcs * c->sym))) return rc;
         if ((rc = c->w_coef2.reserve((size_t)sb * dcs * dcs * c->sym))) return rc;
@@ -1261,52 +1259,38 @@ int decode_device(nfec_codec* c, const nfec_block_batch* b, const uint16_t* locs
             p.zero_seg_stride = b->seg_stride;
             p.zero_vec = c->vec & ~1u;
         }
-        // stage 1: z_t = sum over the block's nd columns (slots in_slots1: the surviving
-        // source and, for an erased one, its substitute parity) of the gathered generator
-        Rs8RtArgs r1;
-        r1.in_base = blocks;
-        r1.in_block_stride = b->block_stride;
-        r1.in_seg_stride = b->seg_stride;
-        r1.out_base = c->w_z.p;
-        r1.out_block_stride = (uint64_t)E * zstride;
-        r1.out_seg_stride = zstride;
-        r1.nblocks = nb;
-        r1.vec_bytes = c->vec;
-        r1.k = c->k;
-        r1.m = std::min(c->k, c->m);
-        r1.per_block = 1;
-        r1.num_data = nd;
-        r1.blk_rows = c->w_rows.p;
-        r1.in_slots = c->w_islots.p;
-        r1.in_slots_stride = c->k;
-        r1.tab = reinterpret_cast<const uint16_t*>(c->w_coef1.p);
-        r1.tab_block_stride = (uint64_t)c->k * cst * 2;
-        r1.tab_col_stride = cst * 2;
-        r1.slot_bound = c->k + c->m;
-        // stage 2: d_E = A^-1 z into the erased source slots
-        Rs8RtArgs r2 = r1;
-        r2.in_base = c->w_z.p;
-        r2.in_block_stride = (uint64_t)E * zstride;
-        r2.in_seg_stride = zstride;
-        r2.in_slots = nullptr;
-        r2.num_data = nullptr;
-        r2.blk_cols = c->w_cols.p;
-        r2.out_base = blocks;
-        r2.out_block_stride = b->block_stride;
-        r2.out_seg_stride = b->seg_stride;
-        r2.out_slots = c->w_oslots.p;
-        r2.out_slots_stride = c->k;
-        r2.tab = reinterpret_cast<const uint16_t*>(c->w_coef2.p);
-        r2.tab_block_stride = (uint64_t)E * cst * 2;
-        r2.accumulate = acc;
-        r2.slot_bound = c->k;
         if (rt_dec) {
-            if (!rs8_rt_covers(r1) || !rs8_rt_covers(r2))
+            // d_E (erased source slots out_slots2) = W x the block's nd received columns (slots
+            // in_slots1: the surviving source and, for an erased one, its substitute parity)
+            Rs8RtArgs r;
+            r.in_base = blocks;
+            r.in_block_stride = b->block_stride;
+            r.in_seg_stride = b->seg_stride;
+            r.out_base = blocks;
+            r.out_block_stride = b->block_stride;
+            r.out_seg_stride = b->seg_stride;
+            r.nblocks = nb;
+            r.vec_bytes = c->vec;
+            r.k = c->k;
+            r.m = E;
+            r.per_block = 1;
+            r.num_data = nd;
+            r.blk_rows = c->w_rows.p;
+            r.in_slots = c->w_islots.p;
+            r.in_slots_stride = c->k;
+            r.out_slots = c->w_oslots.p;
+            r.out_slots_stride = c->k;
+            r.tab = reinterpret_cast<const uint16_t*>(c->w_coef1.p);
+            r.tab_block_stride = (uint64_t)c->k * cst * 2;
+            r.tab_col_stride = cst * 2;
+            r.accumulate = acc;
+            r.slot_bound = c->k + c->m;
+            if (!rs8_rt_covers(r))
                 return fail(NFEC_ENOTSUP, "runtime-coefficient repair: batch layout past its 2^31 offsets");
             p.lwp = c->d_lwp.p;
             p.lw = c->d_lw.p;
             if ((rc = launch_rs8_plan_rt(p, cst, s))) return rc;
-            if ((rc = launch_rs8_rt(r1, s)) || (rc = launch_rs8_rt(r2, s)))
+            if ((rc = launch_rs8_rt(r, s)))
                 return fail(rc == NFEC_ENOTSUP ? NFEC_EDEVICE : rc, "runtime-coefficient repair launch failed");
             continue;
         }

@@ -562,9 +562,9 @@ int launch_rs8_rt(const Rs8RtArgs& in, hipStream_t s)
     if (in.nblocks == 0 || in.m == 0) return NFEC_OK;
     if (!rs8_rt_covers(in)) return NFEC_ENOTSUP;
     Rs8RtArgs a = in;
-    // waves per item group: by the row count in flat mode; per-block mode (rows vary per block,
-    // a repair's e is usually well below m) two waves of {R} rows, more pass sets for more rows
-    const uint32_t G = a.m <= {R}u ? 1u : (a.m <= {2 * R}u || a.per_block) ? 2u : 4u;
+    // waves per item group by the row capacity: with fewer rows than 8 G (per-block rows below
+    // m) the spare waves only load and transpose columns for the others
+    const uint32_t G = a.m <= {R}u ? 1u : a.m <= {2 * R}u ? 2u : 4u;
     a.pass_sets = (a.m + G * {R}u - 1u) / (G * {R}u);
     const uint64_t groups = a.per_block ? (uint64_t)a.nblocks * ((a.vec_bytes + kGroupBytes - 1u) / kGroupBytes)
                                         : ((uint64_t)a.nblocks * a.vec_bytes + kGroupBytes - 1u) / kGroupBytes;
