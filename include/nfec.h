@@ -364,6 +364,16 @@ int nfec_npc_encode_file(int device, const char* in_path, const char* out_path,
 int nfec_npc_decode_file(int device, const char* in_path, const char* out_path,
                          const nfec_npc_params* params, uint64_t* out_bytes, char* name_out,
                          size_t name_cap);
+/* The same file passes over several GPUs (devices[0..num_devices), may repeat a device):
+ * device i takes the i-th contiguous range of FEC blocks, with its own codec, staging and host
+ * thread; host copy threads (NFEC_NPC_THREADS) are shared among them.  Output bytes are
+ * identical to the one-device call.  NFEC_EINVAL for an empty list or a device index out of
+ * range.  The one-device functions above are these with a list of one. */
+int nfec_npc_encode_file_multi(const int32_t* devices, int32_t num_devices, const char* in_path,
+                               const char* out_path, const nfec_npc_params* params);
+int nfec_npc_decode_file_multi(const int32_t* devices, int32_t num_devices, const char* in_path,
+                               const char* out_path, const nfec_npc_params* params,
+                               uint64_t* out_bytes, char* name_out, size_t name_cap);
 /* CRC-32 (npc's ComputeCRC32, :1303-1313) of the first len bytes of slots [0, slots) of every
  * block of a device batch -> crc[b*slots + s] (device), asynchronously on stream. */
 int nfec_crc32_slots(const nfec_block_batch* batch, uint32_t slots, uint32_t len, uint32_t* crc,

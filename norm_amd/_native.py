@@ -159,6 +159,9 @@ _SIGS = {
     "nfec_npc_encode_file": (_I, [_I, ctypes.c_char_p, ctypes.c_char_p, ctypes.POINTER(NpcParams)]),
     "nfec_npc_decode_file": (_I, [_I, ctypes.c_char_p, ctypes.c_char_p, ctypes.POINTER(NpcParams),
                                   ctypes.POINTER(_U64), ctypes.c_char_p, ctypes.c_size_t]),
+    "nfec_npc_encode_file_multi": (_I, [_P, _I, ctypes.c_char_p, ctypes.c_char_p, ctypes.POINTER(NpcParams)]),
+    "nfec_npc_decode_file_multi": (_I, [_P, _I, ctypes.c_char_p, ctypes.c_char_p, ctypes.POINTER(NpcParams),
+                                        ctypes.POINTER(_U64), ctypes.c_char_p, ctypes.c_size_t]),
     "nfec_crc32_slots": (_I, [ctypes.POINTER(BlockBatch), _U32, _U32, _P, _P]),
 }
 

@@ -911,7 +911,9 @@ int decode_device(nfec_codec* c, const nfec_block_batch* b, const uint16_t* locs
     // block's whole repair map (e x numData, rs8_plan_rt_kernel) as a compact snippet table
     // (columns of cst = min(k, m) rounded up to even entries) and ONE pass of the
     // runtime-coefficient kernel computes the erased source from the received columns
-    const bool fast = c->kind == NFEC_RS8 && !b->num_data && c->m <= 32 && c->k <= 64 && !force_generic() &&
+    // (NFEC_RT_DEC=1: the one-pass runtime-coefficient repair for those shapes too, for A/B)
+    static const bool rt_first = diag_knob("NFEC_RT_DEC", 0) != 0;
+    const bool fast = !rt_first && c->kind == NFEC_RS8 && !b->num_data && c->m <= 32 && c->k <= 64 && !force_generic() &&
                       has_bitsliced(c->k, c->m) && bs::offsets_fit(b->block_stride, b->seg_stride);
     static const bool use_rt = diag_knob("NFEC_RT", 1) != 0;
     const bool rt_dec = use_rt && !fast && c->kind == NFEC_RS8 && (c->vec % 8) == 0 && c->d_rt.p && c->d_lwp.p &&

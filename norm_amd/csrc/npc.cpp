@@ -29,11 +29,14 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
+#include <condition_variable>
 #include <cstdio>
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <string>
 #include <thread>
 #include <vector>
@@ -158,16 +161,22 @@ int resolve(const nfec_npc_params* p, uint64_t file_size, int encode, uint32_t* 
 }
 
 struct Threads {
-    // run f(lo, hi) over [0, n) split across host threads
-    template <typename F>
-    static void run(uint64_t n, F f)
+    // host copy threads of a file pass (NFEC_NPC_THREADS, default min(16, cores)), shared
+    // evenly by its device workers
+    static unsigned total()
     {
         static const unsigned nt = [] {
             const char* e = std::getenv("NFEC_NPC_THREADS");
             const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
             return e ? std::max(1, std::atoi(e)) : std::min(16u, hw);
         }();
-        const unsigned t = (unsigned)std::min<uint64_t>(nt, std::max<uint64_t>(1, n / 4));
+        return nt;
+    }
+    // run f(lo, hi) over [0, n) split across up to nt host threads
+    template <typename F>
+    static void run(uint64_t n, unsigned nt, F f)
+    {
+        const unsigned t = (unsigned)std::min<uint64_t>(std::max(1u, nt), std::max<uint64_t>(1, n / 4));
         if (t <= 1) {
             f(0, n);
             return;
@@ -324,6 +333,43 @@ std::string base_name(const char* path)
     return s ? s + 1 : path;
 }
 
+int check_devices(const int32_t* devices, int32_t n)
+{
+    if (!devices || n < 1) return fail(NFEC_EINVAL, "npc: empty device list");
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess) {
+        (void)hipGetLastError();
+        return fail(NFEC_EDEVICE, "npc: no HIP device");
+    }
+    for (int32_t i = 0; i < n; ++i)
+        if (devices[i] < 0 || devices[i] >= count) return fail(NFEC_EINVAL, "npc: device index out of range");
+    return NFEC_OK;
+}
+
+// the file pass over ndev devices: device i takes the contiguous block range
+// [nblocks * i / ndev, nblocks * (i + 1) / ndev) through its own staging pipeline and codec, on
+// its own host thread (one device: the calling thread, whose current device is restored).
+// Returns the first failing worker's code in device-list order.
+template <typename F>
+int run_devices(const int32_t* devices, uint32_t ndev, uint64_t nblocks, F worker)
+{
+    if (ndev == 1) {
+        int prev = -1;
+        (void)hipGetDevice(&prev);
+        const int rc = worker(0u, devices[0], (uint64_t)0, nblocks);
+        if (prev >= 0) (void)hipSetDevice(prev);
+        return rc;
+    }
+    std::vector<int> rcs(ndev, NFEC_OK);
+    std::vector<std::thread> th;
+    for (uint32_t i = 0; i < ndev; ++i)
+        th.emplace_back([&, i] { rcs[i] = worker(i, devices[i], nblocks * i / ndev, nblocks * (i + 1) / ndev); });
+    for (auto& t : th) t.join();
+    for (int rc : rcs)
+        if (rc) return rc;
+    return NFEC_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -408,11 +454,19 @@ int nfec_npc_positions(const nfec_npc_layout* l, uint64_t first, uint64_t count,
 
 int nfec_npc_encode_file(int device, const char* in_path, const char* out_path, const nfec_npc_params* p)
 {
+    const int32_t dev = device;
+    return nfec_npc_encode_file_multi(&dev, 1, in_path, out_path, p);
+}
+
+int nfec_npc_encode_file_multi(const int32_t* devices, int32_t num_devices, const char* in_path, const char* out_path,
+                               const nfec_npc_params* p)
+{
     if (!in_path || !out_path || !p) return fail(NFEC_EINVAL, "null argument");
+    int rc = check_devices(devices, num_devices);
+    if (rc) return rc;
     Phases ph;
     MappedFile in;
-    int rc = in.open_read(in_path);
-    if (rc) return rc;
+    if ((rc = in.open_read(in_path))) return rc;
     ph.mark(4);
     nfec_npc_layout l;
     if ((rc = nfec_npc_layout_for(p, in.size, 1, &l))) return rc;
@@ -431,119 +485,130 @@ int nfec_npc_encode_file(int device, const char* in_path, const char* out_path, 
     const std::string name = base_name(in_path);
     std::memcpy(meta.data() + 8, name.data(), std::min<size_t>(name.size(), ss - 12));
 
-    int prev_dev = -1;
-    (void)hipGetDevice(&prev_dev);
-    const uint32_t cb = chunk_blocks(bstride, l.num_blocks);
-    Stage S;
-    rc = S.init(device, l, stride, cb);
     MappedFile out;
-    if (!rc) rc = out.open_write(out_path, l.num_segments * ss);
-    if (rc) {
-        if (prev_dev >= 0) (void)hipSetDevice(prev_dev);
-        return rc;
-    }
+    if ((rc = out.open_write(out_path, l.num_segments * ss))) return rc;
     const bool zero_parity = l.kind == NFEC_RS16 && (ds & 1);  // RS16 leaves an odd last byte alone
+    const uint32_t ndev = (uint32_t)std::min<uint64_t>((uint64_t)num_devices, l.num_blocks);
+    const unsigned tpw = std::max(1u, Threads::total() / ndev);
+    const uint32_t cb = chunk_blocks(bstride, (l.num_blocks + ndev - 1) / ndev);
 
-    auto fill = [&](int slot, uint64_t b0, uint32_t nb) {
-        uint8_t* H = S.hblk[slot];
-        Threads::run(nb, [&](uint64_t lo, uint64_t hi) {
-            for (uint64_t bi = lo; bi < hi; ++bi) {
-                const uint64_t b = b0 + bi;
-                const uint32_t nd = (b + 1 == l.num_blocks) ? l.last_block_data : k;
-                uint8_t* blk = H + bi * bstride;
-                if (nd < k) std::memset(blk, 0, (size_t)k * stride);
-                for (uint32_t i = 0; i < nd; ++i) {
-                    const uint64_t j = b * k + i;  // input segment
-                    uint8_t* dst = blk + (uint64_t)((b * m + i) % k) * stride;
-                    if (j == 0) {
-                        std::memcpy(dst, meta.data(), ds);
-                    } else {
-                        const uint32_t len = (j + 1 == l.input_segments) ? l.last_segment_bytes : ds;
-                        std::memcpy(dst, in.p + (j - 1) * ds, len);
-                        if (len < ds) std::memset(dst + len, 0, ds - len);
+    // one device's share: fill (host) -> H2D, encode, CRCs, D2H -> scatter (host), two staging
+    // slots so the host copies of one chunk overlap the GPU work of the next
+    auto worker = [&](uint32_t wi, int dev, uint64_t blo, uint64_t bhi) -> int {
+        Phases* P = wi == 0 ? &ph : nullptr;
+        Stage S;
+        int rc = S.init(dev, l, stride, cb);
+        if (rc) return rc;
+        auto fill = [&](int slot, uint64_t b0, uint32_t nb) {
+            uint8_t* H = S.hblk[slot];
+            Threads::run(nb, tpw, [&](uint64_t lo, uint64_t hi) {
+                for (uint64_t bi = lo; bi < hi; ++bi) {
+                    const uint64_t b = b0 + bi;
+                    const uint32_t nd = (b + 1 == l.num_blocks) ? l.last_block_data : k;
+                    uint8_t* blk = H + bi * bstride;
+                    if (nd < k) std::memset(blk, 0, (size_t)k * stride);
+                    for (uint32_t i = 0; i < nd; ++i) {
+                        const uint64_t j = b * k + i;  // input segment
+                        uint8_t* dst = blk + (uint64_t)((b * m + i) % k) * stride;
+                        if (j == 0) {
+                            std::memcpy(dst, meta.data(), ds);
+                        } else {
+                            const uint32_t len = (j + 1 == l.input_segments) ? l.last_segment_bytes : ds;
+                            std::memcpy(dst, in.p + (j - 1) * ds, len);
+                            if (len < ds) std::memset(dst + len, 0, ds - len);
+                        }
                     }
                 }
-            }
-        });
-    };
-    auto launch = [&](int slot, uint32_t nb) -> int {
-        uint8_t* H = S.hblk[slot];
-        NFEC_HIP(hipMemcpy2DAsync(S.dblk, bstride, H, bstride, (size_t)k * stride, nb, hipMemcpyHostToDevice, S.st));
-        if (zero_parity)
-            NFEC_HIP(hipMemset2DAsync(S.dblk + (size_t)k * stride, bstride, 0, (size_t)m * stride, nb, S.st));
-        nfec_block_batch bb{};
-        bb.blocks = S.dblk;
-        bb.block_stride = bstride;
-        bb.seg_stride = stride;
-        bb.nblocks = nb;
-        int r = nfec_encode(S.codec, &bb, S.st);
-        if (r) return r;
-        CrcArgs c;
-        c.base = S.dblk;
-        c.block_stride = bstride;
-        c.seg_stride = stride;
-        c.nblocks = nb;
-        c.slots = n;
-        c.len = ds;
-        c.crc = S.dcrc;
-        if ((r = launch_crc32_slots(c, S.st))) return r;
-        NFEC_HIP(hipMemcpy2DAsync(H + (size_t)k * stride, bstride, S.dblk + (size_t)k * stride, bstride,
-                                  (size_t)m * stride, nb, hipMemcpyDeviceToHost, S.st));
-        NFEC_HIP(hipMemcpyAsync(S.hcrc[slot], S.dcrc, (size_t)nb * n * 4, hipMemcpyDeviceToHost, S.st));
-        NFEC_HIP(hipEventRecord(S.done[slot], S.st));
-        return NFEC_OK;
-    };
-    auto scatter = [&](int slot, uint64_t b0, uint32_t nb) -> int {
-        NFEC_HIP(hipEventSynchronize(S.done[slot]));
-        const uint8_t* H = S.hblk[slot];
-        const uint32_t* crc = S.hcrc[slot];
-        Threads::run(nb, [&](uint64_t lo, uint64_t hi) {
-            for (uint64_t bi = lo; bi < hi; ++bi) {
-                const uint64_t b = b0 + bi;
-                const uint32_t nd = (b + 1 == l.num_blocks) ? l.last_block_data : k;
-                for (uint32_t t = 0; t < nd + m; ++t) {
-                    const uint32_t s = t < nd ? (uint32_t)((b * m + t) % k) : k + (t - nd);
-                    uint8_t* dst = out.p + pos[b * n + t] * ss;
-                    std::memcpy(dst, H + bi * bstride + (uint64_t)s * stride, ds);
-                    put_be32(dst + ds, crc[bi * n + s]);
+            });
+        };
+        auto launch = [&](int slot, uint32_t nb) -> int {
+            uint8_t* H = S.hblk[slot];
+            NFEC_HIP(hipMemcpy2DAsync(S.dblk, bstride, H, bstride, (size_t)k * stride, nb, hipMemcpyHostToDevice, S.st));
+            if (zero_parity)
+                NFEC_HIP(hipMemset2DAsync(S.dblk + (size_t)k * stride, bstride, 0, (size_t)m * stride, nb, S.st));
+            nfec_block_batch bb{};
+            bb.blocks = S.dblk;
+            bb.block_stride = bstride;
+            bb.seg_stride = stride;
+            bb.nblocks = nb;
+            int r = nfec_encode(S.codec, &bb, S.st);
+            if (r) return r;
+            CrcArgs c;
+            c.base = S.dblk;
+            c.block_stride = bstride;
+            c.seg_stride = stride;
+            c.nblocks = nb;
+            c.slots = n;
+            c.len = ds;
+            c.crc = S.dcrc;
+            if ((r = launch_crc32_slots(c, S.st))) return r;
+            NFEC_HIP(hipMemcpy2DAsync(H + (size_t)k * stride, bstride, S.dblk + (size_t)k * stride, bstride,
+                                      (size_t)m * stride, nb, hipMemcpyDeviceToHost, S.st));
+            NFEC_HIP(hipMemcpyAsync(S.hcrc[slot], S.dcrc, (size_t)nb * n * 4, hipMemcpyDeviceToHost, S.st));
+            NFEC_HIP(hipEventRecord(S.done[slot], S.st));
+            return NFEC_OK;
+        };
+        auto scatter = [&](int slot, uint64_t b0, uint32_t nb) -> int {
+            NFEC_HIP(hipEventSynchronize(S.done[slot]));
+            const uint8_t* H = S.hblk[slot];
+            const uint32_t* crc = S.hcrc[slot];
+            Threads::run(nb, tpw, [&](uint64_t lo, uint64_t hi) {
+                for (uint64_t bi = lo; bi < hi; ++bi) {
+                    const uint64_t b = b0 + bi;
+                    const uint32_t nd = (b + 1 == l.num_blocks) ? l.last_block_data : k;
+                    for (uint32_t t = 0; t < nd + m; ++t) {
+                        const uint32_t s = t < nd ? (uint32_t)((b * m + t) % k) : k + (t - nd);
+                        uint8_t* dst = out.p + pos[b * n + t] * ss;
+                        std::memcpy(dst, H + bi * bstride + (uint64_t)s * stride, ds);
+                        put_be32(dst + ds, crc[bi * n + s]);
+                    }
                 }
-            }
-        });
-        return NFEC_OK;
+            });
+            return NFEC_OK;
+        };
+        int slot = 0;
+        uint64_t pb0 = 0;
+        uint32_t pnb = 0;
+        if (P) P->mark(0);
+        for (uint64_t b0 = blo; b0 < bhi && !rc; b0 += cb) {
+            const uint32_t nb = (uint32_t)std::min<uint64_t>(cb, bhi - b0);
+            fill(slot, b0, nb);
+            if (P) P->mark(1);
+            // the staging slot being filled was last read by the scatter two chunks ago (host)
+            if ((rc = launch(slot, nb))) break;
+            if (P) P->mark(2);
+            if (pnb) rc = scatter(slot ^ 1, pb0, pnb);
+            if (P) P->mark(3);
+            pb0 = b0;
+            pnb = nb;
+            slot ^= 1;
+        }
+        if (!rc && pnb) rc = scatter(slot ^ 1, pb0, pnb);
+        if (P) P->mark(3);
+        return rc;
     };
-
-    int slot = 0;
-    uint64_t pb0 = 0;
-    uint32_t pnb = 0;
-    ph.mark(0);
-    for (uint64_t b0 = 0; b0 < l.num_blocks && !rc; b0 += cb) {
-        const uint32_t nb = (uint32_t)std::min<uint64_t>(cb, l.num_blocks - b0);
-        fill(slot, b0, nb);
-        ph.mark(1);
-        // the staging slot being filled was last read by the scatter two chunks ago (host)
-        if ((rc = launch(slot, nb))) break;
-        ph.mark(2);
-        if (pnb) rc = scatter(slot ^ 1, pb0, pnb);
-        ph.mark(3);
-        pb0 = b0;
-        pnb = nb;
-        slot ^= 1;
-    }
-    if (!rc && pnb) rc = scatter(slot ^ 1, pb0, pnb);
-    ph.mark(3);
+    rc = run_devices(devices, ndev, l.num_blocks, worker);
     ph.report("encode");
-    if (prev_dev >= 0) (void)hipSetDevice(prev_dev);
     return rc;
 }
 
 int nfec_npc_decode_file(int device, const char* in_path, const char* out_path, const nfec_npc_params* p,
                          uint64_t* out_bytes, char* name_out, size_t name_cap)
 {
+    const int32_t dev = device;
+    return nfec_npc_decode_file_multi(&dev, 1, in_path, out_path, p, out_bytes, name_out, name_cap);
+}
+
+int nfec_npc_decode_file_multi(const int32_t* devices, int32_t num_devices, const char* in_path,
+                               const char* out_path, const nfec_npc_params* p, uint64_t* out_bytes,
+                               char* name_out, size_t name_cap)
+{
     if (!in_path || !p) return fail(NFEC_EINVAL, "null argument");
+    int rc = check_devices(devices, num_devices);
+    if (rc) return rc;
     Phases ph;
     MappedFile in;
-    int rc = in.open_read(in_path);
-    if (rc) return rc;
+    if ((rc = in.open_read(in_path))) return rc;
     ph.mark(4);
     nfec_npc_layout l;
     if ((rc = nfec_npc_layout_for(p, in.size, 0, &l))) return rc;
@@ -553,158 +618,173 @@ int nfec_npc_decode_file(int device, const char* in_path, const char* out_path, 
     std::vector<uint64_t> pos(l.num_segments);
     if ((rc = nfec_npc_positions(&l, 0, l.num_segments, pos.data()))) return rc;
     ph.mark(5);
+    const uint32_t ndev = (uint32_t)std::min<uint64_t>((uint64_t)num_devices, l.num_blocks);
+    const unsigned tpw = std::max(1u, Threads::total() / ndev);
+    const uint32_t cb = chunk_blocks(bstride, (l.num_blocks + ndev - 1) / ndev);
 
-    int prev_dev = -1;
-    (void)hipGetDevice(&prev_dev);
-    const uint32_t cb = chunk_blocks(bstride, l.num_blocks);
-    Stage S;
-    if ((rc = S.init(device, l, stride, cb))) {
-        if (prev_dev >= 0) (void)hipSetDevice(prev_dev);
-        return rc;
-    }
-
+    // The output's size and name are in the meta segment (block 0's first source segment), known
+    // once block 0 is repaired: worker 0 opens the file then, the others wait for it before
+    // their first write.  Block b's source lands at a fixed offset: every block before the last
+    // holds k segments of ds bytes, and block 0's first is the meta segment.
     MappedFile outm;
-    uint64_t out_size = 0, written = 0;
+    uint64_t out_size = 0;
+    std::mutex omu;
+    std::condition_variable ocv;
+    int ostate = 0;  // 0 pending, 1 open, -1 worker 0 failed first
+    std::atomic<uint64_t> written{0};
+    auto out_offset = [&](uint64_t b) -> uint64_t { return b == 0 ? 0 : (b * k - 1) * ds; };
+    auto seg_len = [&](uint64_t b, uint32_t i, uint32_t nd) -> uint32_t {
+        if (b + 1 == l.num_blocks && i + 1 == nd) {
+            const uint32_t len = (uint32_t)(out_size % ds);
+            return len ? len : ds;
+        }
+        return ds;
+    };
+    auto set_state = [&](int st) {
+        std::lock_guard<std::mutex> g(omu);
+        if (ostate == 0) ostate = st;
+        ocv.notify_all();
+    };
 
-    auto gather = [&](int slot, uint64_t b0, uint32_t nb) {
-        uint8_t* H = S.hblk[slot];
-        for (uint32_t bi = 0; bi < nb; ++bi)
-            S.hnd[slot][bi] = (uint16_t)((b0 + bi + 1 == l.num_blocks) ? l.last_block_data : k);
-        Threads::run(nb, [&](uint64_t lo, uint64_t hi) {
-            for (uint64_t bi = lo; bi < hi; ++bi) {
-                const uint64_t b = b0 + bi;
-                const uint32_t nd = S.hnd[slot][bi];
-                for (uint32_t t = 0; t < nd + m; ++t)
-                    std::memcpy(H + bi * bstride + (uint64_t)t * stride, in.p + pos[b * n + t] * ss, ss);
-            }
-        });
-    };
-    auto launch = [&](int slot, uint32_t nb) -> int {
-        uint8_t* H = S.hblk[slot];
-        NFEC_HIP(hipMemcpyAsync(S.dblk, H, (size_t)nb * bstride, hipMemcpyHostToDevice, S.st));
-        NFEC_HIP(hipMemcpyAsync(S.dnd, S.hnd[slot], (size_t)nb * 2, hipMemcpyHostToDevice, S.st));
-        CrcArgs c;
-        c.base = S.dblk;
-        c.block_stride = bstride;
-        c.seg_stride = stride;
-        c.nblocks = nb;
-        c.slots = n;
-        c.len = ds;
-        c.bad = S.dbad;
-        int r;
-        if ((r = launch_crc32_slots(c, S.st))) return r;
-        ErasureListArgs e;
-        e.bad = S.dbad;
-        e.slots = n;
-        e.num_data = S.dnd;
-        e.k = k;
-        e.m = m;
-        e.nblocks = nb;
-        e.locs = S.dlocs;
-        e.stride = m;
-        e.counts = S.dcounts;
-        if ((r = launch_erasure_list(e, S.st))) return r;
-        NFEC_HIP(hipMemcpyAsync(S.hcounts[slot], S.dcounts, (size_t)nb * 2, hipMemcpyDeviceToHost, S.st));
-        NFEC_HIP(hipStreamSynchronize(S.st));
-        for (uint32_t bi = 0; bi < nb; ++bi)
-            if (S.hcounts[slot][bi] > m) return fail(NFEC_ERANGE, "npc: decoding encountered block with too many errors");
-        // erased vectors are zeroed before Decode (normPrecode.cpp:1049, :1087)
-        if ((r = launch_zero_slots(S.dblk, bstride, stride, nb, S.dlocs, m, S.dcounts, ds, S.st))) return r;
-        nfec_block_batch bb{};
-        bb.blocks = S.dblk;
-        bb.block_stride = bstride;
-        bb.seg_stride = stride;
-        bb.nblocks = nb;
-        bb.num_data = S.dnd;
-        if ((r = nfec_decode(S.codec, &bb, S.dlocs, m, S.dcounts, S.dstatus, S.st))) return r;
-        NFEC_HIP(hipMemcpy2DAsync(H, bstride, S.dblk, bstride, (size_t)k * stride, nb, hipMemcpyDeviceToHost, S.st));
-        NFEC_HIP(hipEventRecord(S.done[slot], S.st));
-        return NFEC_OK;
-    };
-    // write the source segments in order (normPrecode.cpp:1129-1175)
-    auto emit = [&](int slot, uint64_t b0, uint32_t nb) -> int {
-        NFEC_HIP(hipEventSynchronize(S.done[slot]));
-        const uint8_t* H = S.hblk[slot];
-        if (b0 == 0) {
-            const uint8_t* m0 = H;
-            for (int i = 0; i < 8; ++i) out_size = (out_size << 8) | m0[i];
-            const size_t maxlen = std::min<size_t>(4096, ss - 12);
-            std::string nm(reinterpret_cast<const char*>(m0 + 8), strnlen(reinterpret_cast<const char*>(m0 + 8), maxlen));
-            if (name_out && name_cap) {
-                const size_t c = std::min(nm.size(), name_cap - 1);
-                std::memcpy(name_out, nm.data(), c);
-                name_out[c] = 0;
-            }
-            const std::string target = out_path ? std::string(out_path) : nm;
-            // every data segment but the meta one, the last cut to the file size (:1156-1161)
-            uint64_t total = 0;
-            if (l.input_segments >= 2) {
-                uint64_t last = out_size % ds;
-                if (last == 0) last = ds;
-                total = (l.input_segments - 2) * ds + last;
-            }
-            int r = outm.open_write(target.c_str(), total);
-            if (r) return r;
-        }
-        // offsets of each block's output in this chunk
-        std::vector<uint64_t> off(nb + 1, 0);
-        for (uint32_t bi = 0; bi < nb; ++bi) {
-            const uint64_t b = b0 + bi;
-            const uint32_t nd = S.hnd[slot][bi];
-            uint64_t bytes = 0;
-            for (uint32_t i = 0; i < nd; ++i) {
-                if (b == 0 && i == 0) continue;
-                uint32_t len = ds;
-                if (b + 1 == l.num_blocks && i + 1 == nd) {
-                    len = (uint32_t)(out_size % ds);
-                    if (len == 0) len = ds;
-                }
-                bytes += len;
-            }
-            off[bi + 1] = off[bi] + bytes;
-        }
-        Threads::run(nb, [&](uint64_t lo, uint64_t hi) {
-            for (uint64_t bi = lo; bi < hi; ++bi) {
-                const uint64_t b = b0 + bi;
-                const uint32_t nd = S.hnd[slot][bi];
-                uint8_t* dst = outm.p + written + off[bi];
-                for (uint32_t i = 0; i < nd; ++i) {
-                    if (b == 0 && i == 0) continue;
-                    uint32_t len = ds;
-                    if (b + 1 == l.num_blocks && i + 1 == nd) {
-                        len = (uint32_t)(out_size % ds);
-                        if (len == 0) len = ds;
+    auto worker = [&](uint32_t wi, int dev, uint64_t blo, uint64_t bhi) -> int {
+        Phases* P = wi == 0 ? &ph : nullptr;
+        int rc = NFEC_OK;
+        {
+            Stage S;
+            rc = S.init(dev, l, stride, cb);
+            auto gather = [&](int slot, uint64_t b0, uint32_t nb) {
+                uint8_t* H = S.hblk[slot];
+                for (uint32_t bi = 0; bi < nb; ++bi)
+                    S.hnd[slot][bi] = (uint16_t)((b0 + bi + 1 == l.num_blocks) ? l.last_block_data : k);
+                Threads::run(nb, tpw, [&](uint64_t lo, uint64_t hi) {
+                    for (uint64_t bi = lo; bi < hi; ++bi) {
+                        const uint64_t b = b0 + bi;
+                        const uint32_t nd = S.hnd[slot][bi];
+                        for (uint32_t t = 0; t < nd + m; ++t)
+                            std::memcpy(H + bi * bstride + (uint64_t)t * stride, in.p + pos[b * n + t] * ss, ss);
                     }
-                    std::memcpy(dst, H + bi * bstride + (uint64_t)i * stride, len);
-                    dst += len;
+                });
+            };
+            auto launch = [&](int slot, uint32_t nb) -> int {
+                uint8_t* H = S.hblk[slot];
+                NFEC_HIP(hipMemcpyAsync(S.dblk, H, (size_t)nb * bstride, hipMemcpyHostToDevice, S.st));
+                NFEC_HIP(hipMemcpyAsync(S.dnd, S.hnd[slot], (size_t)nb * 2, hipMemcpyHostToDevice, S.st));
+                CrcArgs c;
+                c.base = S.dblk;
+                c.block_stride = bstride;
+                c.seg_stride = stride;
+                c.nblocks = nb;
+                c.slots = n;
+                c.len = ds;
+                c.bad = S.dbad;
+                int r;
+                if ((r = launch_crc32_slots(c, S.st))) return r;
+                ErasureListArgs e;
+                e.bad = S.dbad;
+                e.slots = n;
+                e.num_data = S.dnd;
+                e.k = k;
+                e.m = m;
+                e.nblocks = nb;
+                e.locs = S.dlocs;
+                e.stride = m;
+                e.counts = S.dcounts;
+                if ((r = launch_erasure_list(e, S.st))) return r;
+                NFEC_HIP(hipMemcpyAsync(S.hcounts[slot], S.dcounts, (size_t)nb * 2, hipMemcpyDeviceToHost, S.st));
+                NFEC_HIP(hipStreamSynchronize(S.st));
+                for (uint32_t bi = 0; bi < nb; ++bi)
+                    if (S.hcounts[slot][bi] > m)
+                        return fail(NFEC_ERANGE, "npc: decoding encountered block with too many errors");
+                // erased vectors are zeroed before Decode (normPrecode.cpp:1049, :1087)
+                if ((r = launch_zero_slots(S.dblk, bstride, stride, nb, S.dlocs, m, S.dcounts, ds, S.st))) return r;
+                nfec_block_batch bb{};
+                bb.blocks = S.dblk;
+                bb.block_stride = bstride;
+                bb.seg_stride = stride;
+                bb.nblocks = nb;
+                bb.num_data = S.dnd;
+                if ((r = nfec_decode(S.codec, &bb, S.dlocs, m, S.dcounts, S.dstatus, S.st))) return r;
+                NFEC_HIP(hipMemcpy2DAsync(H, bstride, S.dblk, bstride, (size_t)k * stride, nb, hipMemcpyDeviceToHost, S.st));
+                NFEC_HIP(hipEventRecord(S.done[slot], S.st));
+                return NFEC_OK;
+            };
+            // write the source segments (normPrecode.cpp:1129-1175)
+            auto emit = [&](int slot, uint64_t b0, uint32_t nb) -> int {
+                NFEC_HIP(hipEventSynchronize(S.done[slot]));
+                const uint8_t* H = S.hblk[slot];
+                if (b0 == 0) {
+                    const uint8_t* m0 = H;
+                    uint64_t size = 0;
+                    for (int i = 0; i < 8; ++i) size = (size << 8) | m0[i];
+                    const size_t maxlen = std::min<size_t>(4096, ss - 12);
+                    std::string nm(reinterpret_cast<const char*>(m0 + 8),
+                                   strnlen(reinterpret_cast<const char*>(m0 + 8), maxlen));
+                    if (name_out && name_cap) {
+                        const size_t c = std::min(nm.size(), name_cap - 1);
+                        std::memcpy(name_out, nm.data(), c);
+                        name_out[c] = 0;
+                    }
+                    const std::string target = out_path ? std::string(out_path) : nm;
+                    // every data segment but the meta one, the last cut to the file size (:1156-1161)
+                    uint64_t total = 0;
+                    if (l.input_segments >= 2) {
+                        uint64_t last = size % ds;
+                        if (last == 0) last = ds;
+                        total = (l.input_segments - 2) * ds + last;
+                    }
+                    out_size = size;
+                    const int r = outm.open_write(target.c_str(), total);
+                    set_state(r ? -1 : 1);
+                    if (r) return r;
+                } else {
+                    std::unique_lock<std::mutex> lk(omu);
+                    ocv.wait(lk, [&] { return ostate != 0; });
+                    if (ostate < 0) return NFEC_EINVAL;  // worker 0's error is the one reported
                 }
+                Threads::run(nb, tpw, [&](uint64_t lo, uint64_t hi) {
+                    for (uint64_t bi = lo; bi < hi; ++bi) {
+                        const uint64_t b = b0 + bi;
+                        const uint32_t nd = S.hnd[slot][bi];
+                        uint8_t* dst = outm.p + out_offset(b);
+                        uint64_t bytes = 0;
+                        for (uint32_t i = 0; i < nd; ++i) {
+                            if (b == 0 && i == 0) continue;
+                            const uint32_t len = seg_len(b, i, nd);
+                            std::memcpy(dst, H + bi * bstride + (uint64_t)i * stride, len);
+                            dst += len;
+                            bytes += len;
+                        }
+                        written.fetch_add(bytes, std::memory_order_relaxed);
+                    }
+                });
+                return NFEC_OK;
+            };
+            int slot = 0;
+            uint64_t pb0 = 0;
+            uint32_t pnb = 0;
+            if (P) P->mark(0);
+            for (uint64_t b0 = blo; b0 < bhi && !rc; b0 += cb) {
+                const uint32_t nb = (uint32_t)std::min<uint64_t>(cb, bhi - b0);
+                gather(slot, b0, nb);
+                if (P) P->mark(1);
+                if ((rc = launch(slot, nb))) break;
+                if (P) P->mark(2);
+                if (pnb) rc = emit(slot ^ 1, pb0, pnb);
+                if (P) P->mark(3);
+                pb0 = b0;
+                pnb = nb;
+                slot ^= 1;
             }
-        });
-        written += off[nb];
-        return NFEC_OK;
+            if (!rc && pnb) rc = emit(slot ^ 1, pb0, pnb);
+            if (P) P->mark(3);
+        }
+        // the output was never opened: release the workers waiting for it
+        if (wi == 0) set_state(-1);
+        return rc;
     };
-
-    int slot = 0;
-    uint64_t pb0 = 0;
-    uint32_t pnb = 0;
-    ph.mark(0);
-    for (uint64_t b0 = 0; b0 < l.num_blocks && !rc; b0 += cb) {
-        const uint32_t nb = (uint32_t)std::min<uint64_t>(cb, l.num_blocks - b0);
-        gather(slot, b0, nb);
-        ph.mark(1);
-        if ((rc = launch(slot, nb))) break;
-        ph.mark(2);
-        if (pnb) rc = emit(slot ^ 1, pb0, pnb);
-        ph.mark(3);
-        pb0 = b0;
-        pnb = nb;
-        slot ^= 1;
-    }
-    if (!rc && pnb) rc = emit(slot ^ 1, pb0, pnb);
-    ph.mark(3);
+    rc = run_devices(devices, ndev, l.num_blocks, worker);
     ph.report("decode");
-    if (prev_dev >= 0) (void)hipSetDevice(prev_dev);
-    if (!rc && out_bytes) *out_bytes = written;
+    if (!rc && out_bytes) *out_bytes = written.load();
     return rc;
 }
 

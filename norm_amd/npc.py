@@ -2,7 +2,7 @@
 
     python -m norm_amd.npc {encode|decode} input <inFile> [output <outFile>]
            [segment <segmentSize>][block numData][parity numParity]
-           [auto <parityPercentage>][bmax <n>][imax <n>][ibuffer <n>][device <n>]
+           [auto <parityPercentage>][bmax <n>][imax <n>][ibuffer <n>][device <n>[,<n>...]]
 
 The command language is the reference's (NormPrecodeApp::ProcessCommands / CommandType,
 normPrecode.cpp:124-346): commands match by unambiguous prefix, "block" turns auto sizing
@@ -74,22 +74,33 @@ def default_output_name(in_path):
     return name + ".npc"
 
 
-def encode_file(in_path, out_path=None, params=None, device=0):
+def _device_list(device, devices):
+    devs = [int(device)] if devices is None else [int(d) for d in devices]
+    arr = (ctypes.c_int32 * max(1, len(devs)))(*devs)
+    return arr, len(devs)
+
+
+def encode_file(in_path, out_path=None, params=None, device=0, devices=None):
+    """devices: a list of GPUs sharing the pass (contiguous block ranges), else `device` alone"""
     params = params or default_params()
     out_path = out_path or default_output_name(in_path)
-    N.check(N.lib().nfec_npc_encode_file(device, os.fsencode(in_path), os.fsencode(out_path), ctypes.byref(params)),
-            "nfec_npc_encode_file")
+    arr, n = _device_list(device, devices)
+    N.check(N.lib().nfec_npc_encode_file_multi(ctypes.addressof(arr), n, os.fsencode(in_path), os.fsencode(out_path),
+                                               ctypes.byref(params)),
+            "nfec_npc_encode_file_multi")
     return out_path
 
 
-def decode_file(in_path, out_path=None, params=None, device=0):
+def decode_file(in_path, out_path=None, params=None, device=0, devices=None):
     """-> (output path, bytes written)."""
     params = params or default_params()
     nbytes = ctypes.c_uint64()
     name = ctypes.create_string_buffer(4096)
-    N.check(N.lib().nfec_npc_decode_file(device, os.fsencode(in_path), os.fsencode(out_path) if out_path else None,
-                                         ctypes.byref(params), ctypes.byref(nbytes), name, len(name)),
-            "nfec_npc_decode_file")
+    arr, n = _device_list(device, devices)
+    N.check(N.lib().nfec_npc_decode_file_multi(ctypes.addressof(arr), n, os.fsencode(in_path),
+                                               os.fsencode(out_path) if out_path else None,
+                                               ctypes.byref(params), ctypes.byref(nbytes), name, len(name)),
+            "nfec_npc_decode_file_multi")
     return (out_path or name.value.decode(errors="surrogateescape")), nbytes.value
 
 
@@ -109,12 +120,12 @@ def _command_type(cmd):
 def _usage():
     sys.stderr.write("Usage:  npc {encode|decode} input <inFile> [output <outFile>]\n"
                      "            [segment <segmentSize>][block numData][parity numParity]\n"
-                     "            [auto <parityPercentage>][bmax <n>][imax <n>][device <n>]\n")
+                     "            [auto <parityPercentage>][bmax <n>][imax <n>][device <n>[,<n>...]]\n")
 
 
 def main(argv=None):
     argv = list(sys.argv[1:] if argv is None else argv)
-    encode, inp, outp, dev = True, None, None, 0
+    encode, inp, outp, dev = True, None, None, [0]
     kw = {}
     i = 0
     while i < len(argv):
@@ -154,7 +165,7 @@ def main(argv=None):
         elif name == "imax":
             kw["imax"] = int(val)
         elif name == "device":
-            dev = int(val)
+            dev = [int(d) for d in val.split(",")]  # a list shares the pass over those GPUs
         # debug, ibuffer, background: no effect on the output
     if inp is None:
         sys.stderr.write("npc: error: no input file given\n")
@@ -163,9 +174,9 @@ def main(argv=None):
     try:
         params = make_params(**kw)
         if encode:
-            encode_file(inp, outp, params, dev)
+            encode_file(inp, outp, params, devices=dev)
         else:
-            decode_file(inp, outp, params, dev)
+            decode_file(inp, outp, params, devices=dev)
     except (N.NfecError, ValueError) as e:
         sys.stderr.write(f"npc: {e}\n")
         return 1

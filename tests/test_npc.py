@@ -5,6 +5,7 @@ the interleaver map against oracle/npc_ref.py.  GPU: whole files encoded by
 nfec_npc_encode_file are byte-identical to the restated reference loop, and decoded files
 (clean, with repairable damage, with too much damage) match it too.  Format parity is
 unpinned beyond the CRC (see oracle/npc_ref.py)."""
+import ctypes
 import os
 import zlib
 
@@ -217,5 +218,73 @@ def test_cli_round_trip(tmp_path):
         assert npc.main(["decode", "input", "cli.input_bin.npc", "seg", "1000", "block", "30", "parity", "6"]) == 0
         assert (tmp_path / "cli.input.bin").read_bytes() == data
         assert npc.main(["de", "input", "cli.input_bin.npc"]) == 1  # ambiguous command
+    finally:
+        os.chdir(cwd)
+
+
+# ---------------- several devices (contiguous block ranges, one pipeline each) ----------------
+
+def test_device_list_validation_without_gpu(tmp_path):
+    """an empty device list fails before any file or GPU is touched"""
+    p = _params(block=8, parity=2)
+    src, _ = _write(tmp_path, "v.bin", 1000)
+    rc = N.lib().nfec_npc_encode_file_multi(None, 0, os.fsencode(str(src)), os.fsencode(str(tmp_path / "v.npc")),
+                                            ctypes.byref(p))
+    assert rc == N.NFEC_EINVAL
+    assert not (tmp_path / "v.npc").exists()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("devices", [[0, 0], [0, 0, 0]])
+@pytest.mark.parametrize("name,size,kw", [CASES[3], CASES[5], CASES[7]])
+def test_multi_device_files_identical(tmp_path, devices, name, size, kw):
+    """the same pass over a device list ({0, 0}: two pipelines on one GPU) writes the same bytes,
+    encode and damaged decode, as the reference loop"""
+    src, data = _write(tmp_path, f"{name}.bin", size, seed=11)
+    p = _params(**kw)
+    enc = tmp_path / "m.npc"
+    npc.encode_file(str(src), str(enc), p, devices=devices)
+    lay = npc.layout(p, size)
+    want = R.encode(data, src.name, p.segment_size, lay.num_data, lay.num_parity, p.i_max)
+    assert enc.read_bytes() == want
+    dl = npc.layout(p, len(want), encode=False)
+    bad = _corrupt(want, p.segment_size, dl, max(1, dl.num_parity // 2), np.random.default_rng(12), p)
+    enc.write_bytes(bad)
+    out = tmp_path / "m.out"
+    _, nbytes = npc.decode_file(str(enc), str(out), p, devices=devices)
+    want_name, want_out = R.decode(bad, p.segment_size, dl.num_data, dl.num_parity, p.i_max)
+    assert out.read_bytes() == want_out and nbytes == len(want_out)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("where", ["first", "last"])
+def test_multi_device_too_many_errors(tmp_path, where):
+    """an undecodable block in the first range (whose worker opens the output) or the last one
+    fails the whole pass with the reference's fatal error, and no worker is left waiting"""
+    src, _ = _write(tmp_path, "e.bin", 60_000)
+    p = _params(block=10, parity=3)
+    enc = tmp_path / "e.npc"
+    npc.encode_file(str(src), str(enc), p, devices=[0, 0, 0])
+    lay = npc.layout(p, enc.stat().st_size, encode=False)
+    b = bytearray(enc.read_bytes())
+    pos = npc.positions(lay)
+    blk = 0 if where == "first" else lay.num_blocks - 1
+    for t in range(4):  # 4 bad segments > 3 parity
+        b[int(pos[blk * 13 + t]) * p.segment_size + 5] ^= 1
+    enc.write_bytes(bytes(b))
+    with pytest.raises(N.NfecError):
+        npc.decode_file(str(enc), str(tmp_path / "e.out"), p, devices=[0, 0, 0])
+
+
+@pytest.mark.gpu
+def test_cli_device_list(tmp_path):
+    src, data = _write(tmp_path, "d.bin", 90_000, seed=2)
+    cwd = os.getcwd()
+    os.chdir(tmp_path)
+    try:
+        assert npc.main(["encode", "input", str(src), "block", "16", "parity", "4", "device", "0,0"]) == 0
+        src.rename(tmp_path / "orig.bin")
+        assert npc.main(["decode", "input", "d_bin.npc", "block", "16", "parity", "4", "device", "0,0"]) == 0
+        assert (tmp_path / "d.bin").read_bytes() == data
     finally:
         os.chdir(cwd)
