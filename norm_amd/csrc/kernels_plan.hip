@@ -518,11 +518,13 @@ __global__ __launch_bounds__(kWave) void mdp_plan_kernel(MdpPlanArgs a)
     __syncthreads();
     // coefficients: C[r][v] = Dinv_r * gamma_v * Horner_{u}(Lambda_u; w = gamma_v * beta_r)
     const uint32_t cs = a.coef_stride;
-    uint8_t* coef = a.coef + (uint64_t)b * (a.k + a.m) * cs;
+    uint8_t* coef = a.coef16 ? nullptr : a.coef + (uint64_t)b * (a.k + a.m) * cs;
+    uint16_t* coef16 = a.coef16 ? a.coef16 + (uint64_t)b * (a.k + a.m) * cs : nullptr;
     uint16_t* isl = a.in_slots + (uint64_t)b * (a.k + a.m);
     for (uint32_t j = lane; j < ns; j += kWave) {
         isl[j] = surv[j];
-        for (uint32_t r = es; r < cs; ++r) coef[(uint64_t)j * cs + r] = 0;  // padding rows
+        if (coef)
+            for (uint32_t r = es; r < cs; ++r) coef[(uint64_t)j * cs + r] = 0;  // padding rows
     }
     // one (r, slot) pair per lane, r-major: every lane is busy (ns is rarely a multiple of
     // 64) and a wave's lanes share r, so the Lambda row reads are broadcasts
@@ -542,7 +544,11 @@ __global__ __launch_bounds__(kWave) void mdp_plan_kernel(MdpPlanArgs a)
             if (ll != 0xffu) h ^= ex[ll + pw];
             pw = pw >= lw ? pw - lw : pw + 255u - lw;
         }
-        coef[(uint64_t)j * cs + r] = (uint8_t)mul(dinv_s[r], mul(ex[lgamma], h));
+        const uint32_t v = mul(dinv_s[r], mul(ex[lgamma], h));
+        if (coef16)
+            coef16[(uint64_t)j * cs + r] = (uint16_t)(v << 7);
+        else
+            coef[(uint64_t)j * cs + r] = (uint8_t)v;
     }
     uint16_t* osl = a.out_slots + (uint64_t)b * (a.k + a.m);
     for (uint32_t r = lane; r < es; r += kWave) osl[r] = eras[r];

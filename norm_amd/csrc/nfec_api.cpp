@@ -921,7 +921,37 @@ int decode_device(nfec_codec* c, const nfec_block_batch* b, const uint16_t* locs
                         b->block_stride + (uint64_t)(c->k + c->m) * b->seg_stride + c->vec < (1ull << 31);
     const uint32_t E = std::min(c->k, c->m), cst = (E + 1u) & ~1u;
     // (+ RS16 on the tower kernel: stage 2's per-block snippet tables and row offsets)
-    const uint64_t ws_per_block = c->kind == NFEC_MDP ? (uint64_t)n * c->cs
+    // MDP repair on the runtime-coefficient kernel (the plan's matrix as snippet offsets, one
+    // pass over the survivors), else the snippet solve / generic kernel (NFEC_MDP_RT=0)
+    static const bool use_mdp_rt = diag_knob("NFEC_MDP_RT", 1) != 0;
+    auto mdp_rt_args = [&](uint8_t* blocks, uint32_t nb) {
+        Rs8RtArgs r;
+        r.in_base = blocks;
+        r.in_block_stride = b->block_stride;
+        r.in_seg_stride = b->seg_stride;
+        r.out_base = blocks;
+        r.out_block_stride = b->block_stride;
+        r.out_seg_stride = b->seg_stride;
+        r.nblocks = nb;
+        r.vec_bytes = c->vec;
+        r.k = n;                          // columns: the block's survivors, up to k + m
+        r.m = std::min(c->k, c->m);       // rows: its erased source
+        r.per_block = 1;
+        r.blk_cols = c->w_cols.p;
+        r.blk_rows = c->w_rows.p;
+        r.in_slots = c->w_islots.p;
+        r.in_slots_stride = n;
+        r.out_slots = c->w_oslots.p;
+        r.out_slots_stride = n;
+        r.tab = reinterpret_cast<const uint16_t*>(c->w_coef1.p);
+        r.tab_block_stride = (uint64_t)n * c->cs * 2;
+        r.tab_col_stride = c->cs * 2;
+        r.slot_bound = n;
+        return r;
+    };
+    const bool mdp_rt = c->kind == NFEC_MDP && use_mdp_rt && (c->vec % 8) == 0 && !force_generic() &&
+                        rs8_rt_covers(mdp_rt_args(static_cast<uint8_t*>(b->blocks), 1));
+    const uint64_t ws_per_block = c->kind == NFEC_MDP ? (uint64_t)n * c->cs * (mdp_rt ? 2 : 1)
                                   : rt_dec            ? (uint64_t)c->k * cst * 2
                                                       : (uint64_t)dcs * zstride + ((uint64_t)c->k + dcs) * dcs * c->sym +
                                                  (big_plan ? rs_plan_work_bytes(dcs, c->sym) : 0) +
@@ -953,7 +983,7 @@ int decode_device(nfec_codec* c, const nfec_block_batch* b, const uint16_t* locs
     if ((rc = c->w_islots.reserve((size_t)sb * n + 128))) return rc;
     if ((rc = c->w_oslots.reserve((size_t)sb * n + 128))) return rc;
     if (c->kind == NFEC_MDP) {
-        if ((rc = c->w_coef1.reserve((size_t)sb * n * dcs))) return rc;
+        if ((rc = c->w_coef1.reserve((size_t)sb * n * dcs * (mdp_rt ? 2 : 1) + 16))) return rc;
     } else if (rt_dec) {
         if ((rc = c->w_coef1.reserve((size_t)sb * c->k * cst * 2 + 16))) return rc;
     } else {
@@ -1042,6 +1072,13 @@ int decode_device(nfec_codec* c, const nfec_block_batch* b, const uint16_t* locs
             p.out_slots = c->w_oslots.p;
             p.coef_stride = dcs;
             p.coef = c->w_coef1.p;
+            if (mdp_rt) {
+                p.coef16 = reinterpret_cast<uint16_t*>(c->w_coef1.p);
+                if ((rc = launch_mdp_plan(p, s))) return rc;
+                if ((rc = launch_rs8_rt(mdp_rt_args(blocks, nb), s)))
+                    return fail(rc == NFEC_ENOTSUP ? NFEC_EDEVICE : rc, "MDP runtime-coefficient repair launch failed");
+                continue;
+            }
             if ((rc = launch_mdp_plan(p, s))) return rc;
             // blocks with <= 16 erased source vectors: the snippet solve (NFEC_MDP_BS=0: off)
             static const bool use_mdp_bs = diag_knob("NFEC_MDP_BS", 1) != 0;

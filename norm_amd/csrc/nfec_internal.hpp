@@ -465,6 +465,8 @@ struct MdpPlanArgs {
     uint16_t* out_slots = nullptr;           // [b][k+m]
     uint32_t coef_stride = 0;                // padded row count (multiple of 16)
     uint8_t* coef = nullptr;                 // [b][k+m][cs]
+    uint16_t* coef16 = nullptr;              // set: [b][k+m][cs] as snippet offsets (value << 7)
+                                             // for gen_rs8_rt.hip, instead of coef (rows < e only)
 };
 int launch_mdp_plan(const MdpPlanArgs& a, hipStream_t s);
 
