@@ -231,7 +231,11 @@ def main():
         cdst.copy_(csrc)
     stream_copy(cdst, csrc, stream=stream)
     copy_ms = timed(lambda: stream_copy(cdst, csrc, stream=stream), 5)
-    blit_ms = timed(lambda: cdst.copy_(csrc), 5)
+    def blit():
+        with torch.cuda.stream(stream):  # timed() brackets `stream`: the copy must run on it
+            cdst.copy_(csrc)
+
+    blit_ms = timed(blit, 5)
     copy_gbs = 2 * csrc.numel() / (copy_ms * 1e-3) / 1e9
     blit_gbs = 2 * csrc.numel() / (blit_ms * 1e-3) / 1e9
     del csrc, cdst
@@ -266,8 +270,29 @@ def main():
             t = torch.tensor([he], dtype=torch.float64, device=dev)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             he = float(t.item())
+        # the link's own rate on this box: pinned -> device DMA of 1 GiB (and back), the
+        # ceiling of a path that must move every byte it codes over PCIe.  Per step the pipelines
+        # move up 2 bytes per source byte (encode: the k source segments; decode: the k received
+        # ones, nd surviving source + e substitute parity) and down (m + e) / k, so the
+        # host-resident rate is bounded by h2d / 2 whatever the GPU does.
+        lk_h = torch.empty(1 << 30, dtype=torch.uint8, pin_memory=True)
+        lk_d = torch.empty(1 << 30, dtype=torch.uint8, device=dev)
+        with torch.cuda.stream(stream):
+            lk_d.copy_(lk_h, non_blocking=True)
+        def on_stream(dst, src):
+            with torch.cuda.stream(stream):
+                dst.copy_(src, non_blocking=True)
+
+        h2d_ms = timed(lambda: on_stream(lk_d, lk_h), 3)
+        d2h_ms = timed(lambda: on_stream(lk_h, lk_d), 3)
+        del lk_h, lk_d
+        h2d_gbs = (1 << 30) / (h2d_ms * 1e-3) / 1e9
+        up_per_src = 2.0
         host = {
             "value": round(k * vec * hb * world / (he / a.host_steps) / 2**30, 2),
+            "link_h2d_GBps": round(h2d_gbs, 1),
+            "link_d2h_GBps": round((1 << 30) / (d2h_ms * 1e-3) / 1e9, 1),
+            "link_bound_GiBps": round(h2d_gbs * 1e9 / up_per_src * world / 2**30, 2),
             "blocks_per_gpu": hb,
             "unit": "GiB/s",
             "steps": a.host_steps,
@@ -276,6 +301,7 @@ def main():
                     "parity down) + nfec_decode_host (zero-copy slot moves: the 48 surviving source and 16 "
                     "substitute parity segments up, the 16 repaired segments down), overlapped with the kernels",
         }
+        host["frac_of_link_bound"] = round(host["value"] / host["link_bound_GiBps"], 3)
         del hblocks, hnp
 
     ok = None
