@@ -858,25 +858,30 @@ __global__ __launch_bounds__(64 * kPlan2Waves) void rs8_plan_rt_kernel(RsPlanArg
     // lC for the received columns (x_j differs from every erased and parity point)
     for (uint32_t j = lane; j < nd; j += 64) {
         if (ers[j]) continue;
-        const uint32_t x = j == 0 ? 0u : ex[(j - 1) % 255u];
+        const uint32_t x = j == 0 ? 0u : ex[j - 1];  // j < 255
         int32_t acc = -(int32_t)a.lwp[j];
         for (uint32_t t = 0; t < e; ++t) acc += (int32_t)lg[x ^ xs[t]] - (int32_t)lg[x ^ yt[t]];
         acc %= 255;
         lC[j] = (uint8_t)(acc < 0 ? acc + 255 : acc);
     }
     wave_lds_sync();
-    // the matrix, row-fastest (contiguous writes)
+    // the matrix, row-fastest (contiguous writes); (j, s) of entry idx = j * e + s stepped by
+    // 64 entries per iteration without a division
     uint16_t* c1 = reinterpret_cast<uint16_t*>(a.coef1) + (uint64_t)b * k * cst;
+    const uint32_t dj = 64u / e, ds = 64u - dj * e;
+    uint32_t j = lane / e, s = lane - (lane / e) * e;
     for (uint32_t idx = lane; idx < nd * e; idx += 64) {
-        const uint32_t j = idx / e, s = idx - j * e;
         const uint32_t r = ers[j];
         int32_t l;
         if (r)
             l = lA[s] + lB[r - 1] - (int32_t)lg[xs[s] ^ yt[r - 1]];
         else
-            l = lA[s] + (int32_t)lC[j] - (int32_t)lg[xs[s] ^ (j == 0 ? 0u : ex[(j - 1) % 255u])];
+            l = lA[s] + (int32_t)lC[j] - (int32_t)lg[xs[s] ^ (j == 0 ? 0u : ex[j - 1])];
         if (l < 0) l += 255;
         c1[(uint64_t)j * cst + s] = (uint16_t)((uint32_t)ex[l] << 7);
+        j += dj;
+        s += ds;
+        if (s >= e) s -= e, ++j;
     }
     for (uint32_t i = lane; i < e; i += 64) a.out_slots2[(uint64_t)b * k + i] = sE[i];
 }
