@@ -707,7 +707,9 @@ int launch_rt_encode(nfec_codec* c, const nfec_block_batch* b, hipStream_t s)
     a.tab_col_stride = rs8_rt_col_stride(c->m);
     a.accumulate = (b->flags & NFEC_ACCUMULATE) ? 1u : 0u;
     if (b->num_data) {
-        a.per_block = 1;
+        // RS8: flat, each lane's blocks stopping at their own numData (the generator's columns
+        // are the same for every numData); MDP: per block, its table depends on numData
+        a.per_block = mdp ? 1 : 0;
         a.num_data = b->num_data;
         a.out_after_data = 1;
         if (mdp) {

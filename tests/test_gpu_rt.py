@@ -209,3 +209,24 @@ def test_rt_decode_blocks_without_erasures(orc):
                            torch.from_numpy(counts.view(np.int16)).cuda())
     torch.cuda.synchronize()
     assert np.array_equal(st.cpu().numpy(), st_ref) and np.array_equal(dev.cpu().numpy(), ref)
+
+
+@pytest.mark.parametrize("k,m,vec,nb", [(16, 4, 1400, 200), (64, 16, 1408, 50), (100, 3, 8, 700)])
+def test_rt_encode_shortened_flat_bad_counts(orc, k, m, vec, nb):
+    """RS8 shortened batches run flat (item groups across blocks, each lane's pieces stopping at
+    their block's numData); a block whose numData is 0 or past k is left untouched, as the
+    per-block mode leaves it"""
+    rng = np.random.default_rng(vec + nb)
+    nd = rng.integers(1, k + 1, nb).astype(np.uint16)
+    bad = rng.choice(nb, max(2, nb // 10), replace=False)
+    nd_dev = nd.copy()
+    nd_dev[bad[: len(bad) // 2]] = 0
+    nd_dev[bad[len(bad) // 2:]] = k + 1
+    enc = _enc(NFEC_RS8, k, m, vec)
+    host = orc.make_blocks(k, m, vec, nb, num_data=nd)
+    ref = orc.encode_blocks(NFEC_RS8, k, m, vec, host.copy(), nd)
+    ref[bad] = host[bad]
+    dev = torch.from_numpy(host).cuda()
+    enc.encode_blocks(dev, num_data=torch.from_numpy(nd_dev.view(np.int16)).cuda())
+    torch.cuda.synchronize()
+    assert np.array_equal(dev.cpu().numpy(), ref)

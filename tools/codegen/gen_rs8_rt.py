@@ -62,7 +62,8 @@ def quads(q0, n=4):
 
 
 # ---- VGPRs (v0..v127; banks 2/3 = the 8 rows' accumulators, acc_reg(r, i) = acc_reg(0, i) + 16 r) ----
-IN_REGS = [0, 1, 4, 5, 8, 9]          # compiler-placed inputs: 4 load offsets, LDS exchange, LDS out offsets
+IN_REGS = [0, 1, 4, 5, 8, 9, 112, 113, 116, 117]   # compiler-placed inputs: 4 load offsets, LDS exchange,
+                                                   # LDS out offsets, 4 per-piece numData - 1
 FREE = [124, 125]                     # left to the compiler as well (it needs a register beside the inputs)
 SLOT = quads(3)                       # column being loaded -> transposed planes
 S = quads(7)                          # next column's planes (LDS prefetch) / second load slot (G = 1)
@@ -79,7 +80,8 @@ S_C, S_SB, S_BUF, S_COL, S_T0, S_T1, S_T2, S_WV = 50, 51, 52, 53, 54, 55, 56, 57
 S_TBN = 58                            # 2: table address of the column being fetched
 S_OFF = [60, 64]                      # 2 x 4: the entries of a column (8 rows, u16 each)
 S_SLW = 68                            # the slot-list dword being read
-S_LAST = 79
+S_LAST = 77
+S_UNUSED = (69, 70, 71)               # left to the compiler (its SGPR pressure is high around the asm)
 assert S_MASK == 72
 
 
@@ -217,8 +219,19 @@ def uniq(code):
 
 
 def loads(dst):
-    return [f"buffer_load_dwordx2 v[{dst[2 * i]}:{dst[2 * i + 1]}], %[o{i}], s[{S_DESC}:{S_DESC + 3}], s{S_COL} offen"
-            for i in range(4)]
+    """column s[S_C]'s 4 pieces -> dst.  Flat shortened mode (lnd != 0): a piece whose block has
+    numData <= c reads zeros (its offset gets bit 31: past num_records), so each lane's blocks
+    stop at their own numData"""
+    plain = [f"buffer_load_dwordx2 v[{dst[2 * i]}:{dst[2 * i + 1]}], %[o{i}], s[{S_DESC}:{S_DESC + 3}], s{S_COL} offen"
+             for i in range(4)]
+    nd = []
+    for i in range(4):
+        t = TMP[i]
+        nd += [f"v_subrev_u32 v{t}, s{S_C}, %[q{i}]",                          # numData - 1 - c
+               f"v_and_or_b32 v{t}, v{t}, s{S_DESC + 2}, %[o{i}]",              # sign -> bit 31
+               f"buffer_load_dwordx2 v[{dst[2 * i]}:{dst[2 * i + 1]}], v{t}, s[{S_DESC}:{S_DESC + 3}], s{S_COL} offen"]
+    return uniq(["s_bitcmp1_b32 %[acc], 1", "s_cbranch_scc0 Lld_%=_{uid}"] + nd +
+                ["s_branch Lldx_%=_{uid}", "Lld_%=_{uid}:"] + plain + ["Lldx_%=_{uid}:"])
 
 
 def table_fetch(col_sgpr, ebuf, add=None):
@@ -386,7 +399,7 @@ def epilogue():
         d = S_OFF[0] + r
         w = [acc_reg(r, i) for i in range(8)]
         L += transpose(w, epi_pool())
-        L += [f"s_mul_i32 s{S_T1}, s{d}, %[oss]", "s_cmp_eq_u32 %[acc], 0", f"s_cbranch_scc1 Lna{r}_%="]
+        L += [f"s_mul_i32 s{S_T1}, s{d}, %[oss]", "s_bitcmp1_b32 %[acc], 0", f"s_cbranch_scc0 Lna{r}_%="]
         for i in range(4):
             L.append(f"buffer_load_dwordx2 v[{tmp[2 * i]}:{tmp[2 * i + 1]}], v{so[i]}, s[{S_ODESC}:{S_ODESC + 3}], s{S_T1} offen")
         L.append("s_waitcnt vmcnt(0)")
@@ -403,18 +416,19 @@ def epilogue():
 
 def clobbers():
     v = [f'"v{i}"' for i in range(0, V_LAST + 1) if i not in IN_REGS + FREE]
-    s = [f'"s{i}"' for i in range(S_DESC, S_LAST + 1)]
+    s = [f'"s{i}"' for i in range(S_DESC, S_LAST + 1) if i not in S_UNUSED]
     return ", ".join(v + s + ['"m0"', '"scc"', '"memory"'])
 
 
 def main():
     path = sys.argv[1]
     asms = {G: "\\n\"\n            \"".join(body(G)) for G in GS}
-    ins = ", ".join(f'[o{i}] "v"(o[{i}])' for i in range(4))
+    ins = ", ".join([f'[o{i}] "v"(o[{i}])' for i in range(4)] + [f'[q{i}] "v"(q[{i}])' for i in range(4)])
     common = ("[wb] \"s\"(wb), [ob] \"s\"(ob), [ss] \"s\"(a.in_seg_stride), [oss] \"s\"(a.out_seg_stride), "
               "[k] \"s\"(kk), [kl] \"s\"(kl), [nr] \"s\"(nr), [twl] \"s\"(twl), [twh] \"s\"(twh), "
               "[tstep] \"s\"(a.tab_col_stride), [isl] \"s\"(isl), [islot0] \"s\"(a.in_slot0), [osl] \"s\"(osl), "
-              "[oslot] \"s\"(oslot), [acc] \"s\"(a.accumulate), [wv] \"s\"(pw), [iph] \"s\"(iph), [oph] \"s\"(oph), "
+              "[oslot] \"s\"(oslot), [acc] \"s\"(mode), [wv] \"s\"(pw), [iph] \"s\"(iph), [oph] \"s\"(oph), "
+              
               "[lo] \"v\"(lo), [xl] \"v\"(xl), " + ins)
     blocks = []
     for G in GS:
@@ -507,16 +521,24 @@ __device__ __forceinline__ void rt_body(const Rs8RtArgs& a, uint32_t wg)
     const uint32_t b0 = pb ? blk : __builtin_amdgcn_readfirstlane((uint32_t)(min(f0, total - 1) / a.vec_bytes));
     const uint8_t* wb = a.in_base + (uint64_t)b0 * a.in_block_stride;
     const uint8_t* ob = a.out_base + (uint64_t)b0 * a.out_block_stride;
-    uint32_t o[4];
+    // flat shortened mode: every piece's block has its own numData (columns at or past it read
+    // zeros, parity at slot numData + r); numData is 1..k (a.num_data was validated by the host)
+    const uint32_t lnd = !pb && a.num_data ? 1u : 0u;
+    uint32_t o[4], q[4];
     uint32_t* po = lds + (wave * 64u + lane) * 4u;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {{
         const uint64_t f = f0 + (uint64_t)i * 512u + lane * 8u;
         const uint32_t b = pb ? b0 : (uint32_t)(f / a.vec_bytes);
         const uint32_t p = (uint32_t)(f - (uint64_t)(pb ? 0u : b) * a.vec_bytes);
-        const bool ok = live && f < total;
+        const uint32_t raw = lnd && live && f < total ? (uint32_t)a.num_data[b] : a.k;
+        // a block whose numData is 0 or past k is left alone, as in per-block mode
+        const bool ok = live && f < total && raw >= 1u && raw <= a.k;
+        const uint32_t pnd = ok ? raw : 1u;
+        q[i] = pnd - 1u;
         o[i] = ok ? (uint32_t)((uint64_t)(b - b0) * a.in_block_stride) + p : 0x80000000u;
-        po[i] = ok ? (uint32_t)((uint64_t)(b - b0) * a.out_block_stride) + p : 0x80000000u;
+        po[i] = ok ? (uint32_t)((uint64_t)(b - b0) * a.out_block_stride + (uint64_t)(lnd ? pnd : 0u) * a.out_seg_stride) + p
+                   : 0x80000000u;
     }}
     const uint32_t lo = bs::lds_addr(po);
     const uint32_t xl = bs::lds_addr(xch) + gi * (2u * G * {XCH_COL}u) + lane * 8u;
@@ -530,7 +552,8 @@ __device__ __forceinline__ void rt_body(const Rs8RtArgs& a, uint32_t wg)
     const uint16_t* isl = reinterpret_cast<const uint16_t*>(isa & ~(uintptr_t)3);
     const uint16_t* osl = reinterpret_cast<const uint16_t*>(osa & ~(uintptr_t)3);
     const uint32_t iph = (uint32_t)(isa >> 1) & 1u, oph = (uint32_t)(osa >> 1) & 1u;
-    const uint32_t oslot = a.out_slot0 + (a.out_after_data ? nd : 0u) + row0;
+    const uint32_t mode = __builtin_amdgcn_readfirstlane((a.accumulate ? 1u : 0u) | (lnd << 1));  // bit 0: accumulate, bit 1: flat shortened
+    const uint32_t oslot = a.out_slot0 + (a.out_after_data && !lnd ? nd : 0u) + row0;  // (lnd: numData in po)
 {asm_blocks}
 }}
 
