@@ -618,3 +618,32 @@ def test_unfused_gate_across_calls(orc, m):
     run({0, 7, 19})
     run(set())
     run({nb - 1})
+
+
+@pytest.mark.parametrize("pinned", [True, False])
+@pytest.mark.parametrize("bad_nd", [0, 65])
+def test_host_decode_rejects_bad_num_data(orc, pinned, bad_nd):
+    """a host batch whose numData list holds 0 or a count past k fails with NFEC_EINVAL before
+    any slot moves (the zero-copy slot moves size their copies by numData + m), and leaves the
+    caller's buffer alone, pinned or pageable"""
+    import norm_amd as na
+    from norm_amd import _native as N
+
+    k, m, vec, nb = 64, 32, 1400, 8
+    dec = na.NormDecoderRS8()
+    assert dec.Init(k, m, vec)
+    host = orc.make_blocks(k, m, vec, nb)
+    if pinned:
+        t = torch.empty(host.shape, dtype=torch.uint8, pin_memory=True)
+        t.copy_(torch.from_numpy(host))
+        arr = t.numpy()
+    else:
+        arr = host.copy()
+    before = arr.copy()
+    nd = np.full(nb, k, np.uint16)
+    nd[nb - 1] = bad_nd
+    locs = np.zeros((nb, m), np.uint16)
+    counts = np.ones(nb, np.uint16)
+    with pytest.raises(N.NfecError):
+        dec.decode_blocks_host(arr, locs, counts, num_data=nd)
+    assert np.array_equal(arr, before)
