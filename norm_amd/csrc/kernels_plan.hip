@@ -404,13 +404,12 @@ __global__ __launch_bounds__(kWave) void mdp_plan_kernel(MdpPlanArgs a)
     __shared__ uint8_t ex[512];
     __shared__ uint16_t lg[256];
     __shared__ uint8_t lam[512];
-    extern __shared__ uint8_t llamb[];      // [erased row r][u < m]: log of prefix sums Lambda_u(beta_r)
-                                            // (0xff: the sum is 0; logs are < 255)
     // byte-wide: slots, logs and flags are all < 255 (k + m <= 255), and the smaller LDS
     // footprint keeps more of these latency-bound waves resident
     __shared__ uint8_t surv[256];
     __shared__ uint8_t eras[256];
-    __shared__ uint8_t dinv_s[256], lbeta_s[256];
+    __shared__ uint8_t dinv_s[256], lbeta_s[256];  // per erased row: log(Dinv_r beta_r^m), log beta_r
+    __shared__ uint8_t lcol_s[256], lgam_s[256];   // per survivor: log column factor, log gamma_v
     __shared__ uint8_t ers[256];            // erased-slot flags (nvecs <= 255)
     __shared__ uint8_t loc_s[256];          // the block's erasure list (ec <= m < 255)
     __shared__ uint8_t llam[512];           // log lambda_j (0xff: lambda_j = 0)
@@ -492,9 +491,15 @@ __global__ __launch_bounds__(kWave) void mdp_plan_kernel(MdpPlanArgs a)
     }
     if (lane == 0) a.cols[b] = (uint16_t)ns;
     __syncthreads();
-    // per erased row r: beta, Forney denominator, Lambda prefix sums.  Products with powers of
-    // beta are log-domain table terms (exponents stepped in registers), independent of each
-    // other instead of a chain through the running power.
+    // Closed form of the Forney coefficients.  The reference's repair of erased source r from
+    // survivor v is C[r][v] = Dinv_r gamma_v h, h = sum_{u<m} Lambda_u(beta_r) w^(m-1-u),
+    // w = gamma_v beta_r, Lambda_u the prefix sums of the locator's coefficients.  Swapping the
+    // sums, sum_{j<=u<m} w^(m-1-u) = (w^(m-j) + 1) / (w + 1), so (char 2, Lambda(beta_r) = 0, the
+    // lambda_m terms cancel)
+    //     h = (gamma_v beta_r)^m Lambda(1 / gamma_v) / (gamma_v beta_r + 1),
+    //     C[r][v] = [Dinv_r beta_r^m] [gamma_v^(m+1) Lambda(1 / gamma_v)] / (gamma_v beta_r + 1):
+    // a row factor, a column factor and a Cauchy term, O(1) table lookups per entry instead of m
+    // (tests/test_mdp_algebra.py checks the identity against the sum).
     for (uint32_t r = lane; r < es; r += kWave) {
         const uint32_t kk = nvecs - 1 - eras[r];
         const uint32_t lb = (255u - kk) % 255u;  // log beta
@@ -505,18 +510,25 @@ __global__ __launch_bounds__(kWave) void mdp_plan_kernel(MdpPlanArgs a)
             if (ll != 0xffu) denom ^= ex[ll + pj];
             pj = pj + l2 >= 255u ? pj + l2 - 255u : pj + l2;
         }
-        dinv_s[r] = (uint8_t)(denom ? ex[255u - lg[denom]] : 1u);  // GINV[0] = 1 (galois.cpp:39)
+        const uint32_t dinv = denom ? ex[255u - lg[denom]] : 1u;  // GINV[0] = 1 (galois.cpp:39)
         lbeta_s[r] = (uint8_t)lb;
-        uint32_t acc = 0, pu = 0;  // pu = lb * u mod 255
-        for (uint32_t u = 0; u < m; ++u) {
-            const uint32_t ll = llam[u];
-            if (ll != 0xffu) acc ^= ex[ll + pu];
-            pu = pu + lb >= 255u ? pu + lb - 255u : pu + lb;
-            llamb[r * m + u] = acc ? (uint8_t)lg[acc] : (uint8_t)0xff;
+        dinv_s[r] = (uint8_t)((lg[dinv] + (m % 255u) * lb) % 255u);  // log(Dinv_r beta_r^m)
+    }
+    // column factors: log(gamma_v^(m+1) Lambda(1 / gamma_v)), Lambda of degree ec
+    for (uint32_t j = lane; j < ns; j += kWave) {
+        const uint32_t lgam = (nvecs - 1 - surv[j]) % 255u;
+        const uint32_t step = (255u - lgam) % 255u;
+        uint32_t acc = 0, pi = 0;
+        for (uint32_t i = 0; i <= ec; ++i) {
+            const uint32_t ll = llam[i];
+            if (ll != 0xffu) acc ^= ex[ll + pi];
+            pi = pi + step >= 255u ? pi + step - 255u : pi + step;
         }
+        // acc != 0: 1 / gamma_v is not a root (v survived)
+        lcol_s[j] = (uint8_t)(((m + 1u) % 255u * lgam + (acc ? lg[acc] : 0u)) % 255u);
+        lgam_s[j] = (uint8_t)lgam;
     }
     __syncthreads();
-    // coefficients: C[r][v] = Dinv_r * gamma_v * Horner_{u}(Lambda_u; w = gamma_v * beta_r)
     const uint32_t cs = a.coef_stride;
     uint8_t* coef = a.coef16 ? nullptr : a.coef + (uint64_t)b * (a.k + a.m) * cs;
     uint16_t* coef16 = a.coef16 ? a.coef16 + (uint64_t)b * (a.k + a.m) * cs : nullptr;
@@ -526,29 +538,22 @@ __global__ __launch_bounds__(kWave) void mdp_plan_kernel(MdpPlanArgs a)
         if (coef)
             for (uint32_t r = es; r < cs; ++r) coef[(uint64_t)j * cs + r] = 0;  // padding rows
     }
-    // one (r, slot) pair per lane, r-major: every lane is busy (ns is rarely a multiple of
-    // 64) and a wave's lanes share r, so the Lambda row reads are broadcasts
+    // entries [j][r], r fastest (contiguous writes); (j, r) stepped by 64 without a division
+    const uint32_t dj = kWave / es, dr = kWave - dj * es;
+    uint32_t j = lane / es, r = lane - (lane / es) * es;
     for (uint32_t idx = lane; idx < es * ns; idx += kWave) {
-        const uint32_t r = idx / ns, j = idx - r * ns;
-        const uint32_t lgamma = (nvecs - 1 - surv[j]) % 255u;
-        // h = sum_u Lambda_u * w^(m-1-u), w = gamma * beta_r, as independent table terms in
-        // the log domain (a Horner chain would make every step wait on the previous
-        // product's table reads)
-        const uint32_t lw = (lgamma + lbeta_s[r]) % 255u;
-        uint32_t pw = ((m - 1) * lw) % 255u;
-        uint32_t h = 0;
-        const uint8_t* row = llamb + r * m;
-#pragma unroll 4
-        for (uint32_t u = 0; u < m; ++u) {
-            const uint32_t ll = row[u];
-            if (ll != 0xffu) h ^= ex[ll + pw];
-            pw = pw >= lw ? pw - lw : pw + 255u - lw;
-        }
-        const uint32_t v = mul(dinv_s[r], mul(ex[lgamma], h));
+        const uint32_t lw = lgam_s[j] + lbeta_s[r];
+        const uint32_t w1 = ex[lw] ^ 1u;  // gamma_v beta_r + 1, nonzero (v is not erased)
+        int32_t l = (int32_t)dinv_s[r] + (int32_t)lcol_s[j] - (int32_t)lg[w1];
+        if (l < 0) l += 255;
+        const uint32_t v = ex[l];
         if (coef16)
             coef16[(uint64_t)j * cs + r] = (uint16_t)(v << 7);
         else
             coef[(uint64_t)j * cs + r] = (uint8_t)v;
+        j += dj;
+        r += dr;
+        if (r >= es) r -= es, ++j;
     }
     uint16_t* osl = a.out_slots + (uint64_t)b * (a.k + a.m);
     for (uint32_t r = lane; r < es; r += kWave) osl[r] = eras[r];
@@ -571,9 +576,7 @@ int launch_rs_plan(const RsPlanArgs& a, hipStream_t s)
 int launch_mdp_plan(const MdpPlanArgs& a, hipStream_t s)
 {
     if (a.nblocks == 0) return NFEC_OK;
-    // erased source rows are at most min(k, m); k + m <= 255 keeps this under 16 KiB
-    const size_t lds = (size_t)std::min(a.k, a.m) * a.m;
-    hipLaunchKernelGGL(mdp_plan_kernel, dim3(a.nblocks), dim3(kWave), lds, s, a);
+    hipLaunchKernelGGL(mdp_plan_kernel, dim3(a.nblocks), dim3(kWave), 0, s, a);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return hip_fail(e, "mdp_plan launch");
     return NFEC_OK;
