@@ -587,7 +587,11 @@ int launch_rs8_rt(const Rs8RtArgs& in, hipStream_t s)
     Rs8RtArgs a = in;
     // waves per item group by the row capacity: with fewer rows than 8 G (per-block rows below
     // m) the spare waves only load and transpose columns for the others
-    const uint32_t G = a.m <= {R}u ? 1u : a.m <= {2 * R}u ? 2u : 4u;
+    uint32_t G = a.m <= {R}u ? 1u : a.m <= {2 * R}u ? 2u : 4u;
+    // (NFEC_RT_G=1/2/4: that split for every launch, A/B only; NFEC_RT_GPB: per-block launches)
+    static const long g_all = diag_knob("NFEC_RT_G", 0, 0, 4), g_pb = diag_knob("NFEC_RT_GPB", 0, 0, 4);
+    const long gk = a.per_block && g_pb ? g_pb : g_all;
+    if (gk == 1 || gk == 2 || gk == 4) G = (uint32_t)gk;
     a.pass_sets = (a.m + G * {R}u - 1u) / (G * {R}u);
     const uint64_t groups = a.per_block ? (uint64_t)a.nblocks * ((a.vec_bytes + kGroupBytes - 1u) / kGroupBytes)
                                         : ((uint64_t)a.nblocks * a.vec_bytes + kGroupBytes - 1u) / kGroupBytes;
