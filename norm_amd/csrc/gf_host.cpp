@@ -140,7 +140,7 @@ void mdp_encode_matrix(const std::vector<uint8_t>& g, uint32_t m, uint32_t nd, u
 std::vector<uint16_t> rs8_rt_table(const std::vector<uint32_t>& rows, uint32_t k, uint32_t m)
 {
     const uint32_t cs = rs8_rt_col_stride(m) / 2;
-    std::vector<uint16_t> t((size_t)k * cs + 8, 0);
+    std::vector<uint16_t> t((size_t)k * cs + 4 * cs + 64, 0);  // padding: the kernel's touch loads
     for (uint32_t c = 0; c < k; ++c)
         for (uint32_t r = 0; r < m; ++r) t[(size_t)c * cs + r] = (uint16_t)((rows[(size_t)r * k + c] & 0xffu) << 7);
     return t;

@@ -530,30 +530,42 @@ __global__ __launch_bounds__(kWave) void mdp_plan_kernel(MdpPlanArgs a)
     }
     __syncthreads();
     const uint32_t cs = a.coef_stride;
-    uint8_t* coef = a.coef16 ? nullptr : a.coef + (uint64_t)b * (a.k + a.m) * cs;
-    uint16_t* coef16 = a.coef16 ? a.coef16 + (uint64_t)b * (a.k + a.m) * cs : nullptr;
-    uint16_t* isl = a.in_slots + (uint64_t)b * (a.k + a.m);
-    for (uint32_t j = lane; j < ns; j += kWave) {
-        isl[j] = surv[j];
-        if (coef)
-            for (uint32_t r = es; r < cs; ++r) coef[(uint64_t)j * cs + r] = 0;  // padding rows
-    }
-    // entries [j][r], r fastest (contiguous writes); (j, r) stepped by 64 without a division
-    const uint32_t dj = kWave / es, dr = kWave - dj * es;
-    uint32_t j = lane / es, r = lane - (lane / es) * es;
-    for (uint32_t idx = lane; idx < es * ns; idx += kWave) {
-        const uint32_t lw = lgam_s[j] + lbeta_s[r];
-        const uint32_t w1 = ex[lw] ^ 1u;  // gamma_v beta_r + 1, nonzero (v is not erased)
+    const uint32_t nv = a.k + a.m;
+    uint16_t* isl = a.in_slots + (uint64_t)b * nv;
+    for (uint32_t j = lane; j < ns; j += kWave) isl[j] = surv[j];
+    auto entry = [&](uint32_t r, uint32_t j) -> uint32_t {
+        const uint32_t w1 = ex[lgam_s[j] + lbeta_s[r]] ^ 1u;  // gamma_v beta_r + 1, nonzero (v not erased)
         int32_t l = (int32_t)dinv_s[r] + (int32_t)lcol_s[j] - (int32_t)lg[w1];
         if (l < 0) l += 255;
-        const uint32_t v = ex[l];
-        if (coef16)
-            coef16[(uint64_t)j * cs + r] = (uint16_t)(v << 7);
-        else
-            coef[(uint64_t)j * cs + r] = (uint8_t)v;
-        j += dj;
-        r += dr;
-        if (r >= es) r -= es, ++j;
+        return ex[l];
+    };
+    if (a.coef16) {
+        // pass-major snippet offsets for gen_rs8_rt.hip: pass p's rows (rs8_rt_pass_rows), 8
+        // entries per column, columns contiguous
+        uint16_t* c16 = a.coef16 + (uint64_t)b * a.npass16 * nv * 8u;
+        const uint32_t P = rs8_rt_passes(es);
+        for (uint32_t p = 0; p < P; ++p) {
+            uint32_t row0, row1;
+            rs8_rt_pass_rows(es, p, row0, row1);
+            uint16_t* cp = c16 + (uint64_t)p * nv * 8u;
+            for (uint32_t idx = lane; idx < ns * 8u; idx += kWave) {
+                const uint32_t r = row0 + (idx & 7u);
+                cp[idx] = (uint16_t)(r < row1 ? entry(r, idx >> 3) << 7 : 0u);
+            }
+        }
+    } else {
+        uint8_t* coef = a.coef + (uint64_t)b * nv * cs;
+        for (uint32_t j = lane; j < ns; j += kWave)
+            for (uint32_t r = es; r < cs; ++r) coef[(uint64_t)j * cs + r] = 0;  // padding rows
+        // entries [j][r], r fastest (contiguous writes); (j, r) stepped by 64 without a division
+        const uint32_t dj = kWave / es, dr = kWave - dj * es;
+        uint32_t j = lane / es, r = lane - (lane / es) * es;
+        for (uint32_t idx = lane; idx < es * ns; idx += kWave) {
+            coef[(uint64_t)j * cs + r] = (uint8_t)entry(r, j);
+            j += dj;
+            r += dr;
+            if (r >= es) r -= es, ++j;
+        }
     }
     uint16_t* osl = a.out_slots + (uint64_t)b * (a.k + a.m);
     for (uint32_t r = lane; r < es; r += kWave) osl[r] = eras[r];
@@ -752,10 +764,10 @@ __global__ __launch_bounds__(64 * kPlan2Waves) void rs_plan2_kernel(RsPlan2Args 
 //   lC[j] = log b_j + sum_s' log(x_j + x_s') - sum_t log(x_j + y_t)
 // (the partial-fraction solution of a Cauchy system with one more column; lwp = -log b).  Per
 // block: status and rows (e) as rs_plan_kernel<uint8_t>, the column slot list, the erased slots,
-// and the matrix as the kernel's snippet offsets (u16, value << 7) in a compact table coef1
-// [b][j < numData][s < e], column stride cst u16.  One wave per block, four blocks per
-// workgroup sharing the field tables.
-__global__ __launch_bounds__(64 * kPlan2Waves) void rs8_plan_rt_kernel(RsPlanArgs a, uint32_t cst)
+// and the matrix as the kernel's snippet offsets (u16, value << 7) in a pass-major table coef1
+// [b][pass < npass][j < k][8] (Rs8RtArgs::tab_pass_stride).  One wave per block, four blocks
+// per workgroup sharing the field tables.
+__global__ __launch_bounds__(64 * kPlan2Waves) void rs8_plan_rt_kernel(RsPlanArgs a, uint32_t npass)
 {
     constexpr uint32_t kE = 128;  // e <= min(k, m) <= 127 (k + m <= 255)
     __shared__ uint8_t ex[512];
@@ -868,36 +880,42 @@ __global__ __launch_bounds__(64 * kPlan2Waves) void rs8_plan_rt_kernel(RsPlanArg
         lC[j] = (uint8_t)(acc < 0 ? acc + 255 : acc);
     }
     wave_lds_sync();
-    // the matrix, row-fastest (contiguous writes); (j, s) of entry idx = j * e + s stepped by
-    // 64 entries per iteration without a division
-    uint16_t* c1 = reinterpret_cast<uint16_t*>(a.coef1) + (uint64_t)b * k * cst;
-    const uint32_t dj = 64u / e, ds = 64u - dj * e;
-    uint32_t j = lane / e, s = lane - (lane / e) * e;
-    for (uint32_t idx = lane; idx < nd * e; idx += 64) {
-        const uint32_t r = ers[j];
-        int32_t l;
-        if (r)
-            l = lA[s] + lB[r - 1] - (int32_t)lg[xs[s] ^ yt[r - 1]];
-        else
-            l = lA[s] + (int32_t)lC[j] - (int32_t)lg[xs[s] ^ (j == 0 ? 0u : ex[j - 1])];
-        if (l < 0) l += 255;
-        c1[(uint64_t)j * cst + s] = (uint16_t)((uint32_t)ex[l] << 7);
-        j += dj;
-        s += ds;
-        if (s >= e) s -= e, ++j;
+    // the matrix pass-major, as the repair kernel reads it: pass p's rows [row0, row1)
+    // (rs8_rt_pass_rows), per column 8 entries (16 bytes, unused ones zero), columns contiguous
+    uint16_t* c1 = reinterpret_cast<uint16_t*>(a.coef1) + (uint64_t)b * npass * k * 8u;
+    const uint32_t P = rs8_rt_passes(e);
+    for (uint32_t p = 0; p < P; ++p) {
+        uint32_t row0, row1;
+        rs8_rt_pass_rows(e, p, row0, row1);
+        uint16_t* cp = c1 + (uint64_t)p * k * 8u;
+        for (uint32_t idx = lane; idx < nd * 8u; idx += 64) {
+            const uint32_t j = idx >> 3, s = row0 + (idx & 7u);
+            uint32_t v = 0;
+            if (s < row1) {
+                const uint32_t r = ers[j];
+                int32_t l;
+                if (r)
+                    l = lA[s] + lB[r - 1] - (int32_t)lg[xs[s] ^ yt[r - 1]];
+                else
+                    l = lA[s] + (int32_t)lC[j] - (int32_t)lg[xs[s] ^ (j == 0 ? 0u : ex[j - 1])];
+                if (l < 0) l += 255;
+                v = (uint32_t)ex[l] << 7;
+            }
+            cp[idx] = (uint16_t)v;
+        }
     }
     for (uint32_t i = lane; i < e; i += 64) a.out_slots2[(uint64_t)b * k + i] = sE[i];
 }
 
 }  // namespace
 
-int launch_rs8_plan_rt(const RsPlanArgs& a, uint32_t cst, hipStream_t s)
+int launch_rs8_plan_rt(const RsPlanArgs& a, uint32_t npass, hipStream_t s)
 {
     if (a.nblocks == 0) return NFEC_OK;
-    if (a.bits != 8 || a.k + a.m > 255 || !a.lwp || !a.lw || (cst & 1u) || cst < std::min(a.k, a.m))
+    if (a.bits != 8 || a.k + a.m > 255 || !a.lwp || !a.lw || npass < rs8_rt_passes(std::min(a.k, a.m)))
         return NFEC_ENOTSUP;
     hipLaunchKernelGGL(rs8_plan_rt_kernel, dim3((a.nblocks + kPlan2Waves - 1) / kPlan2Waves), dim3(64 * kPlan2Waves),
-                       0, s, a, cst);
+                       0, s, a, npass);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return hip_fail(e, "rs8_plan_rt launch");
     return NFEC_OK;

@@ -365,7 +365,8 @@ int build_codec(nfec_codec* c)
             // the same block maps as runtime-coefficient tables, one per nd (shortened encodes)
             const uint32_t cs = rs8_rt_col_stride(c->m) / 2;
             c->rt_block_bytes = (uint64_t)c->k * cs * 2;
-            std::vector<uint16_t> t((size_t)c->k * c->k * cs + 8, 0);
+            // (+ padding: the kernel's scalar-cache touch reads up to 4 columns past an entry)
+            std::vector<uint16_t> t((size_t)c->k * c->k * cs + 4 * cs + 64, 0);
             for (uint32_t nd = 1; nd <= c->k; ++nd)
                 for (uint32_t col = 0; col < nd; ++col)
                     for (uint32_t r = 0; r < c->m; ++r)
@@ -921,11 +922,12 @@ int decode_device(nfec_codec* c, const nfec_block_batch* b, const uint16_t* locs
     const bool rt_dec = use_rt && !fast && c->kind == NFEC_RS8 && (c->vec % 8) == 0 && c->d_rt.p && c->d_lwp.p &&
                         !force_generic() &&
                         b->block_stride + (uint64_t)(c->k + c->m) * b->seg_stride + c->vec < (1ull << 31);
-    const uint32_t E = std::min(c->k, c->m), cst = (E + 1u) & ~1u;
+    const uint32_t E = std::min(c->k, c->m);
     // (+ RS16 on the tower kernel: stage 2's per-block snippet tables and row offsets)
     // MDP repair on the runtime-coefficient kernel (the plan's matrix as snippet offsets, one
     // pass over the survivors), else the snippet solve / generic kernel (NFEC_MDP_RT=0)
     static const bool use_mdp_rt = diag_knob("NFEC_MDP_RT", 1) != 0;
+    const uint32_t mdp_np = rs8_rt_passes(std::min(c->k, c->m));  // passes of its pass-major table
     auto mdp_rt_args = [&](uint8_t* blocks, uint32_t nb) {
         Rs8RtArgs r;
         r.in_base = blocks;
@@ -946,15 +948,17 @@ int decode_device(nfec_codec* c, const nfec_block_batch* b, const uint16_t* locs
         r.out_slots = c->w_oslots.p;
         r.out_slots_stride = n;
         r.tab = reinterpret_cast<const uint16_t*>(c->w_coef1.p);
-        r.tab_block_stride = (uint64_t)n * c->cs * 2;
-        r.tab_col_stride = c->cs * 2;
+        r.tab_block_stride = (uint64_t)mdp_np * n * 16;
+        r.tab_col_stride = 16;
+        r.tab_pass_stride = (uint64_t)n * 16;
         r.slot_bound = n;
         return r;
     };
     const bool mdp_rt = c->kind == NFEC_MDP && use_mdp_rt && (c->vec % 8) == 0 && !force_generic() &&
                         rs8_rt_covers(mdp_rt_args(static_cast<uint8_t*>(b->blocks), 1));
-    const uint64_t ws_per_block = c->kind == NFEC_MDP ? (uint64_t)n * c->cs * (mdp_rt ? 2 : 1)
-                                  : rt_dec            ? (uint64_t)c->k * cst * 2
+    const uint32_t rt_np = rs8_rt_passes(std::min(c->k, c->m));  // RS8 repair table passes
+    const uint64_t ws_per_block = c->kind == NFEC_MDP ? (mdp_rt ? (uint64_t)mdp_np * n * 16 : (uint64_t)n * c->cs)
+                                  : rt_dec            ? (uint64_t)rt_np * c->k * 16
                                                       : (uint64_t)dcs * zstride + ((uint64_t)c->k + dcs) * dcs * c->sym +
                                                  (big_plan ? rs_plan_work_bytes(dcs, c->sym) : 0) +
                                                  (c->tw ? 2ull * gf16_tw_table_elems(E, E) + 4ull * (E + 12) : 0);
@@ -985,9 +989,9 @@ int decode_device(nfec_codec* c, const nfec_block_batch* b, const uint16_t* locs
     if ((rc = c->w_islots.reserve((size_t)sb * n + 128))) return rc;
     if ((rc = c->w_oslots.reserve((size_t)sb * n + 128))) return rc;
     if (c->kind == NFEC_MDP) {
-        if ((rc = c->w_coef1.reserve((size_t)sb * n * dcs * (mdp_rt ? 2 : 1) + 16))) return rc;
+        if ((rc = c->w_coef1.reserve(mdp_rt ? (size_t)sb * mdp_np * n * 16 + 128 : (size_t)sb * n * dcs))) return rc;
     } else if (rt_dec) {
-        if ((rc = c->w_coef1.reserve((size_t)sb * c->k * cst * 2 + 16))) return rc;
+        if ((rc = c->w_coef1.reserve((size_t)sb * rt_np * c->k * 16 + 128))) return rc;
     } else {
         if ((rc = c->w_coef1.reserve((size_t)sb * c->k * dcs * c->sym))) return rc;
         if ((rc = c->w_coef2.reserve((size_t)sb * dcs * dcs * c->sym))) return rc;
@@ -1076,6 +1080,7 @@ int decode_device(nfec_codec* c, const nfec_block_batch* b, const uint16_t* locs
             p.coef = c->w_coef1.p;
             if (mdp_rt) {
                 p.coef16 = reinterpret_cast<uint16_t*>(c->w_coef1.p);
+                p.npass16 = mdp_np;
                 if ((rc = launch_mdp_plan(p, s))) return rc;
                 if ((rc = launch_rs8_rt(mdp_rt_args(blocks, nb), s)))
                     return fail(rc == NFEC_ENOTSUP ? NFEC_EDEVICE : rc, "MDP runtime-coefficient repair launch failed");
@@ -1322,15 +1327,16 @@ int decode_device(nfec_codec* c, const nfec_block_batch* b, const uint16_t* locs
             r.out_slots = c->w_oslots.p;
             r.out_slots_stride = c->k;
             r.tab = reinterpret_cast<const uint16_t*>(c->w_coef1.p);
-            r.tab_block_stride = (uint64_t)c->k * cst * 2;
-            r.tab_col_stride = cst * 2;
+            r.tab_block_stride = (uint64_t)rt_np * c->k * 16;
+            r.tab_col_stride = 16;
+            r.tab_pass_stride = (uint64_t)c->k * 16;
             r.accumulate = acc;
             r.slot_bound = c->k + c->m;
             if (!rs8_rt_covers(r))
                 return fail(NFEC_ENOTSUP, "runtime-coefficient repair: batch layout past its 2^31 offsets");
             p.lwp = c->d_lwp.p;
             p.lw = c->d_lw.p;
-            if ((rc = launch_rs8_plan_rt(p, cst, s))) return rc;
+            if ((rc = launch_rs8_plan_rt(p, rt_np, s))) return rc;
             if ((rc = launch_rs8_rt(r, s)))
                 return fail(rc == NFEC_ENOTSUP ? NFEC_EDEVICE : rc, "runtime-coefficient repair launch failed");
             continue;

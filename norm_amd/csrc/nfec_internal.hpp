@@ -294,7 +294,10 @@ void gf16_bs_selectors(const std::vector<uint32_t>& parity_rows, uint32_t k, uin
 // coefficient a jump into a 256-entry snippet table.  out[b][oslot(r)] (^)= sum_c coef[c][r] *
 // in[b][islot(c)] for r < rows(b), c < cols(b).  The table holds snippet byte offsets (u16,
 // c << 7): entry (c, r) at tab + [block or count] * tab_block_stride + c * tab_col_stride + 2 r
-// (bytes), padded by 16 bytes past the last entry.
+// (bytes), or, pass-major (tab_pass_stride != 0, the plans' per-block tables), entry i of pass p
+// (row pass_row0(p) + i) at tab + block * tab_block_stride + p * tab_pass_stride +
+// c * tab_col_stride + 2 i: a pass's entries of consecutive columns share scalar-cache lines.
+// Padded by 128 bytes past the last entry (the kernel touches lines ahead of its reads).
 //   flat mode (per_block = 0): item groups run across the blocks; cols = k, rows = m, islot =
 //     in_slot0 + c, oslot = out_slot0 + r (unshortened encode)
 //   per-block mode: item groups inside one block; cols = blk_cols[b] (else num_data[b], else k),
@@ -323,15 +326,27 @@ struct Rs8RtArgs {
     uint64_t tab_block_stride = 0;       // bytes
     uint32_t tab_col_stride = 0;         // bytes, multiple of 4
     uint32_t tab_by_count = 0;
+    uint64_t tab_pass_stride = 0;        // bytes; 0: entries by row (2 r)
     uint32_t accumulate = 0;             // XOR into the output slots
     uint32_t slot_bound = 0;             // slot lists hold slots below this (0: 65536)
     uint32_t pass_sets = 0;              // set by the launcher
 };
 constexpr uint32_t kRs8RtRows = 8;       // parity rows per pass (gen_rs8_rt.py asserts it)
+// rows [row0, row1) of pass p of a block with `rows` rows: the fewest passes of at most 8 rows,
+// rows spread evenly with even boundaries (the kernel's split; plans writing pass-major tables
+// use the same)
+__host__ __device__ inline void rs8_rt_pass_rows(uint32_t rows, uint32_t p, uint32_t& row0, uint32_t& row1)
+{
+    const uint32_t P = rows > kRs8RtRows ? (rows + kRs8RtRows - 1u) / kRs8RtRows : 1u;
+    const uint32_t h = (rows + 1u) / 2u;
+    row0 = p < P ? (2u * (p * h / P) < rows ? 2u * (p * h / P) : rows) : rows;
+    row1 = p < P ? (2u * ((p + 1u) * h / P) < rows ? 2u * ((p + 1u) * h / P) : rows) : rows;
+}
+__host__ __device__ inline uint32_t rs8_rt_passes(uint32_t rows) { return rows > kRs8RtRows ? (rows + kRs8RtRows - 1u) / kRs8RtRows : 1u; }
 int launch_rs8_rt(const Rs8RtArgs& a, hipStream_t s);  // NFEC_ENOTSUP: layout not covered
 bool rs8_rt_covers(const Rs8RtArgs& a);                // launch_rs8_rt would take it
 // snippet-offset table of an m x k generator (row-major parity rows): [c][r] u16, column stride
-// round_up(2m, 4) bytes, 16 bytes of padding
+// round_up(2m, 4) bytes, padded by 4 columns + 128 bytes
 std::vector<uint16_t> rs8_rt_table(const std::vector<uint32_t>& rows, uint32_t k, uint32_t m);
 inline uint32_t rs8_rt_col_stride(uint32_t m) { return (2u * m + 3u) & ~3u; }
 
@@ -384,7 +399,8 @@ int launch_rs_plan(const RsPlanArgs& a, hipStream_t s);
 // RS8 closed-form plan for the runtime-coefficient repair: rs_plan's outputs with coef1 as
 // [b][k][cst] and coef2 as [b][min(k, m)][cst] snippet-offset tables (u16, cst even and >=
 // min(k, m)); needs lwp / lw.  Entries past a block's e are not written.
-int launch_rs8_plan_rt(const RsPlanArgs& a, uint32_t cst, hipStream_t s);
+// writes coef1 pass-major: [block][pass < npass][column < k][8 entries] (u16), npass = passes of min(k, m)
+int launch_rs8_plan_rt(const RsPlanArgs& a, uint32_t npass, hipStream_t s);
 
 // RS decode planning, closed form (RS8, m <= 64): the systematic generator is the Lagrange
 // basis of the points x_j = point(j) evaluated at y_p = point(k+p), so the e x e system
@@ -465,8 +481,9 @@ struct MdpPlanArgs {
     uint16_t* out_slots = nullptr;           // [b][k+m]
     uint32_t coef_stride = 0;                // padded row count (multiple of 16)
     uint8_t* coef = nullptr;                 // [b][k+m][cs]
-    uint16_t* coef16 = nullptr;              // set: [b][k+m][cs] as snippet offsets (value << 7)
-                                             // for gen_rs8_rt.hip, instead of coef (rows < e only)
+    uint16_t* coef16 = nullptr;              // set: snippet offsets (value << 7) for gen_rs8_rt.hip,
+                                             // pass-major [b][pass < npass16][k+m][8], instead of coef
+    uint32_t npass16 = 0;
 };
 int launch_mdp_plan(const MdpPlanArgs& a, hipStream_t s);
 

@@ -80,7 +80,8 @@ S_C, S_SB, S_BUF, S_COL, S_T0, S_T1, S_T2, S_WV = 50, 51, 52, 53, 54, 55, 56, 57
 S_TBN = 58                            # 2: table address of the column being fetched
 S_OFF = [60, 64]                      # 2 x 4: the entries of a column (8 rows, u16 each)
 S_SLW = 68                            # the slot-list dword being read
-S_LAST = 77
+S_TOUCH = 78                          # destination of the scalar-cache touch loads (never read)
+S_LAST = 78
 S_UNUSED = (69, 70, 71)               # left to the compiler (its SGPR pressure is high around the asm)
 assert S_MASK == 72
 
@@ -243,7 +244,8 @@ def table_fetch(col_sgpr, ebuf, add=None):
     else:
         L.append(f"s_mul_i32 s{S_T2}, s{col_sgpr}, %[tstep]")
     L += [f"s_add_u32 s{S_TBN}, %[twl], s{S_T2}", f"s_addc_u32 s{S_TBN + 1}, %[twh], 0",
-          f"s_load_dwordx4 s[{ebuf}:{ebuf + 3}], s[{S_TBN}:{S_TBN + 1}], 0x0"]
+          f"s_load_dwordx4 s[{ebuf}:{ebuf + 3}], s[{S_TBN}:{S_TBN + 1}], 0x0",
+          f"s_load_dword s{S_TOUCH}, s[{S_TBN}:{S_TBN + 1}], %[tpf]"]   # warm a line ahead
     return L
 
 
@@ -426,7 +428,7 @@ def main():
     ins = ", ".join([f'[o{i}] "v"(o[{i}])' for i in range(4)] + [f'[q{i}] "v"(q[{i}])' for i in range(4)])
     common = ("[wb] \"s\"(wb), [ob] \"s\"(ob), [ss] \"s\"(a.in_seg_stride), [oss] \"s\"(a.out_seg_stride), "
               "[k] \"s\"(kk), [kl] \"s\"(kl), [nr] \"s\"(nr), [twl] \"s\"(twl), [twh] \"s\"(twh), "
-              "[tstep] \"s\"(a.tab_col_stride), [isl] \"s\"(isl), [islot0] \"s\"(a.in_slot0), [osl] \"s\"(osl), "
+              "[tstep] \"s\"(a.tab_col_stride), [tpf] \"s\"(tpf), [isl] \"s\"(isl), [islot0] \"s\"(a.in_slot0), [osl] \"s\"(osl), "
               "[oslot] \"s\"(oslot), [acc] \"s\"(mode), [wv] \"s\"(pw), [iph] \"s\"(iph), [oph] \"s\"(oph), "
               
               "[lo] \"v\"(lo), [xl] \"v\"(xl), " + ins)
@@ -451,17 +453,6 @@ static_assert(kRs8RtRows == {R}u, "gen_rs8_rt.py and nfec_internal.hpp disagree 
 namespace {{
 
 constexpr uint32_t kGroupBytes = 2048;   // 64 lanes x 4 pieces x 8 bytes
-
-// rows [row0, row1) of pass p: the fewest passes of at most {R} rows, P = ceil(rows / {R}), rows
-// spread evenly over them (even boundaries: a pass's entries start 4-byte aligned); passes p >= P
-// have none (their waves only load and share columns, or leave)
-__device__ __forceinline__ void pass_rows(uint32_t rows, uint32_t p, uint32_t& row0, uint32_t& row1)
-{{
-    const uint32_t P = max(1u, (rows + {R - 1}u) / {R}u);
-    const uint32_t h = (rows + 1u) / 2u;
-    row0 = p < P ? min(rows, 2u * (p * h / P)) : rows;
-    row1 = p < P ? min(rows, 2u * ((p + 1u) * h / P)) : rows;
-}}
 
 template <int G>
 __device__ __forceinline__ void rt_body(const Rs8RtArgs& a, uint32_t wg)
@@ -511,7 +502,7 @@ __device__ __forceinline__ void rt_body(const Rs8RtArgs& a, uint32_t wg)
         }}
     }}
     uint32_t row0 = 0, row1 = 0;
-    pass_rows(rows, set * G + pw, row0, row1);
+    rs8_rt_pass_rows(rows, set * G + pw, row0, row1);
     const uint32_t nr = __builtin_amdgcn_readfirstlane(row1 - row0);
     if constexpr (G == 1) {{
         if (nr == 0u) return;
@@ -542,9 +533,13 @@ __device__ __forceinline__ void rt_body(const Rs8RtArgs& a, uint32_t wg)
     }}
     const uint32_t lo = bs::lds_addr(po);
     const uint32_t xl = bs::lds_addr(xch) + gi * (2u * G * {XCH_COL}u) + lane * 8u;
-    // table: [column][row] u16 entries, this pass's rows start 2 * row0 bytes in
-    const uint8_t* tb = reinterpret_cast<const uint8_t*>(a.tab) + 2u * row0 +
+    // table: [column][row] u16 entries, this pass's rows start 2 * row0 bytes in; or pass-major
+    const uint8_t* tb = reinterpret_cast<const uint8_t*>(a.tab) +
+                        (a.tab_pass_stride ? (uint64_t)(set * G + pw) * a.tab_pass_stride : 2u * row0) +
                         (pb && a.tab_block_stride ? (uint64_t)(a.tab_by_count ? nd - 1u : blk) * a.tab_block_stride : 0u);
+    // scalar-cache touch distance: per-block tables are read once, so the line 4 columns ahead
+    // is requested early (a dummy load); shared tables stay cached (touch the current line)
+    const uint32_t tpf = __builtin_amdgcn_readfirstlane(pb ? 4u * a.tab_col_stride : 0u);
     const uint32_t twl = (uint32_t)(uintptr_t)tb, twh = (uint32_t)((uintptr_t)tb >> 32);
     // slot lists: 4-byte aligned addresses for the scalar loads, plus the u16 phase
     const uintptr_t isa = pb && a.in_slots ? (uintptr_t)(a.in_slots + (uint64_t)blk * a.in_slots_stride) : 0;
@@ -568,7 +563,7 @@ __global__ __launch_bounds__(256, 4) void rs8_rt_kernel(Rs8RtArgs a)
 bool rs8_rt_covers(const Rs8RtArgs& a)
 {{
     if ((a.vec_bytes & 7u) || a.vec_bytes == 0 || !a.tab || a.k == 0 || (a.tab_col_stride & 3u) ||
-        (a.per_block && (a.tab_block_stride & 3u)))
+        (a.per_block && (a.tab_block_stride & 3u)) || (a.tab_pass_stride & 3u))
         return false;
     // every offset a wave forms stays below 2^31 (a flat item group spans at most
     // 2048 / vec + 2 blocks), as do the slot offsets
