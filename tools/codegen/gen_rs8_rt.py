@@ -501,8 +501,12 @@ __device__ __forceinline__ void rt_body(const Rs8RtArgs& a, uint32_t wg)
             kl = __builtin_amdgcn_readfirstlane(kmax);
         }}
     }}
+    // row pass of this wave: rotated by the workgroup, so that when some waves of an item group
+    // have no rows (rows < 8 G) the busy ones land on different SIMDs from one workgroup to
+    // the next (a workgroup's wave w runs on SIMD w)
+    const uint32_t pr = (pw + (wg / sets) % G) % G;
     uint32_t row0 = 0, row1 = 0;
-    rs8_rt_pass_rows(rows, set * G + pw, row0, row1);
+    rs8_rt_pass_rows(rows, set * G + pr, row0, row1);
     const uint32_t nr = __builtin_amdgcn_readfirstlane(row1 - row0);
     if constexpr (G == 1) {{
         if (nr == 0u) return;
@@ -535,7 +539,7 @@ __device__ __forceinline__ void rt_body(const Rs8RtArgs& a, uint32_t wg)
     const uint32_t xl = bs::lds_addr(xch) + gi * (2u * G * {XCH_COL}u) + lane * 8u;
     // table: [column][row] u16 entries, this pass's rows start 2 * row0 bytes in; or pass-major
     const uint8_t* tb = reinterpret_cast<const uint8_t*>(a.tab) +
-                        (a.tab_pass_stride ? (uint64_t)(set * G + pw) * a.tab_pass_stride : 2u * row0) +
+                        (a.tab_pass_stride ? (uint64_t)(set * G + pr) * a.tab_pass_stride : 2u * row0) +
                         (pb && a.tab_block_stride ? (uint64_t)(a.tab_by_count ? nd - 1u : blk) * a.tab_block_stride : 0u);
     // scalar-cache touch distance: per-block tables are read once, so the line 4 columns ahead
     // is requested early (a dummy load); shared tables stay cached (touch the current line)
