@@ -427,7 +427,7 @@ def main():
     asms = {G: "\\n\"\n            \"".join(body(G)) for G in GS}
     ins = ", ".join([f'[o{i}] "v"(o[{i}])' for i in range(4)] + [f'[q{i}] "v"(q[{i}])' for i in range(4)])
     common = ("[wb] \"s\"(wb), [ob] \"s\"(ob), [ss] \"s\"(a.in_seg_stride), [oss] \"s\"(a.out_seg_stride), "
-              "[k] \"s\"(kk), [kl] \"s\"(kl), [nr] \"s\"(nr), [twl] \"s\"(twl), [twh] \"s\"(twh), "
+              "[k] \"s\"(k), [kl] \"s\"(kl), [nr] \"s\"(nr), [twl] \"s\"(twl), [twh] \"s\"(twh), "
               "[tstep] \"s\"(a.tab_col_stride), [tpf] \"s\"(tpf), [isl] \"s\"(isl), [islot0] \"s\"(a.in_slot0), [osl] \"s\"(osl), "
               "[oslot] \"s\"(oslot), [acc] \"s\"(mode), [wv] \"s\"(pw), [iph] \"s\"(iph), [oph] \"s\"(oph), "
               
@@ -462,17 +462,15 @@ __device__ __forceinline__ void rt_body(const Rs8RtArgs& a, uint32_t wg)
     __shared__ uint64_t xch[(G > 1 ? 4 * 2 * {XCH_COL} / 8 : 1)];  // column planes exchange
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const uint32_t gi = wave / G, pw = wave % G;                // item group in the workgroup, pass in the set
-    const uint32_t sets = a.pass_sets;
-    const uint32_t set = wg % sets;                             // pass sets of one item group are neighbours
-    const uint32_t group = (wg / sets) * NG + gi;
+    const uint32_t gi = wave / G, pw = wave % G;                // item group in the workgroup, wave in the group
+    const uint32_t group = wg * NG + gi;
     const bool pb = a.per_block != 0u;
     const uint32_t chunks = (a.vec_bytes + kGroupBytes - 1u) / kGroupBytes;
     const uint32_t blk = pb ? group / chunks : 0u;
     const uint64_t total = pb ? (uint64_t)a.vec_bytes : (uint64_t)a.nblocks * a.vec_bytes;
     const uint64_t f0 = pb ? (uint64_t)(group - blk * chunks) * kGroupBytes : (uint64_t)group * kGroupBytes;
     const bool live = pb ? blk < a.nblocks : f0 < total;
-    // this wave's columns and rows (0 rows: a helper that only loads and shares)
+    // this item group's columns and rows
     uint32_t kk = a.k, rows = a.m;
     uint32_t nd = a.k;
     if (live && pb) {{
@@ -487,32 +485,21 @@ __device__ __forceinline__ void rt_body(const Rs8RtArgs& a, uint32_t wg)
         if (rows == 0u || kk == 0u || kk > a.k || nd == 0u || nd > a.k) rows = 0u, kk = 0u;
     }}
     if (!live) rows = 0u, kk = 0u;
-    // an item group whose rows all lie before this pass set has nothing to do here
-    if (set * G * {R}u >= rows) rows = 0u, kk = 0u;
-    // the workgroup's step count: every wave runs the same number of barriers (G > 1)
-    uint32_t kl = kk;
+    // the workgroup's largest row and column counts: its waves run the pass sets (8 G rows
+    // each) and steps of the longest item group together, with the same barriers (G > 1)
+    uint32_t kl = kk, rl = rows;
     if constexpr (G > 1) {{
         if (NG > 1) {{
-            __shared__ uint32_t kmax;
-            if (threadIdx.x == 0) kmax = 0u;
+            __shared__ uint32_t kmax, rmax;
+            if (threadIdx.x == 0) kmax = 0u, rmax = 0u;
             __syncthreads();
-            if (lane == 0 && pw == 0) atomicMax(&kmax, kk);
+            if (lane == 0 && pw == 0) atomicMax(&kmax, kk), atomicMax(&rmax, rows);
             __syncthreads();
             kl = __builtin_amdgcn_readfirstlane(kmax);
+            rl = __builtin_amdgcn_readfirstlane(rmax);
         }}
     }}
-    // row pass of this wave: rotated by the workgroup, so that when some waves of an item group
-    // have no rows (rows < 8 G) the busy ones land on different SIMDs from one workgroup to
-    // the next (a workgroup's wave w runs on SIMD w)
-    const uint32_t pr = (pw + (wg / sets) % G) % G;
-    uint32_t row0 = 0, row1 = 0;
-    rs8_rt_pass_rows(rows, set * G + pr, row0, row1);
-    const uint32_t nr = __builtin_amdgcn_readfirstlane(row1 - row0);
-    if constexpr (G == 1) {{
-        if (nr == 0u) return;
-    }} else {{
-        if (kl == 0u) return;  // workgroup-uniform: no group of the workgroup has work in this set
-    }}
+    if (kl == 0u) return;  // workgroup-uniform (G > 1) / this wave (G = 1): nothing to compute
     const uint32_t b0 = pb ? blk : __builtin_amdgcn_readfirstlane((uint32_t)(min(f0, total - 1) / a.vec_bytes));
     const uint8_t* wb = a.in_base + (uint64_t)b0 * a.in_block_stride;
     const uint8_t* ob = a.out_base + (uint64_t)b0 * a.out_block_stride;
@@ -537,23 +524,38 @@ __device__ __forceinline__ void rt_body(const Rs8RtArgs& a, uint32_t wg)
     }}
     const uint32_t lo = bs::lds_addr(po);
     const uint32_t xl = bs::lds_addr(xch) + gi * (2u * G * {XCH_COL}u) + lane * 8u;
-    // table: [column][row] u16 entries, this pass's rows start 2 * row0 bytes in; or pass-major
-    const uint8_t* tb = reinterpret_cast<const uint8_t*>(a.tab) +
-                        (a.tab_pass_stride ? (uint64_t)(set * G + pr) * a.tab_pass_stride : 2u * row0) +
-                        (pb && a.tab_block_stride ? (uint64_t)(a.tab_by_count ? nd - 1u : blk) * a.tab_block_stride : 0u);
+    const uint8_t* tblk = reinterpret_cast<const uint8_t*>(a.tab) +
+                          (pb && a.tab_block_stride ? (uint64_t)(a.tab_by_count ? nd - 1u : blk) * a.tab_block_stride : 0u);
     // scalar-cache touch distance: per-block tables are read once, so the line 4 columns ahead
     // is requested early (a dummy load); shared tables stay cached (touch the current line)
     const uint32_t tpf = __builtin_amdgcn_readfirstlane(pb ? 4u * a.tab_col_stride : 0u);
-    const uint32_t twl = (uint32_t)(uintptr_t)tb, twh = (uint32_t)((uintptr_t)tb >> 32);
     // slot lists: 4-byte aligned addresses for the scalar loads, plus the u16 phase
     const uintptr_t isa = pb && a.in_slots ? (uintptr_t)(a.in_slots + (uint64_t)blk * a.in_slots_stride) : 0;
-    const uintptr_t osa = pb && a.out_slots ? (uintptr_t)(a.out_slots + (uint64_t)blk * a.out_slots_stride + row0) : 0;
     const uint16_t* isl = reinterpret_cast<const uint16_t*>(isa & ~(uintptr_t)3);
-    const uint16_t* osl = reinterpret_cast<const uint16_t*>(osa & ~(uintptr_t)3);
-    const uint32_t iph = (uint32_t)(isa >> 1) & 1u, oph = (uint32_t)(osa >> 1) & 1u;
+    const uint32_t iph = (uint32_t)(isa >> 1) & 1u;
     const uint32_t mode = __builtin_amdgcn_readfirstlane((a.accumulate ? 1u : 0u) | (lnd << 1));  // bit 0: accumulate, bit 1: flat shortened
-    const uint32_t oslot = a.out_slot0 + (a.out_after_data && !lnd ? nd : 0u) + row0;  // (lnd: numData in po)
+    // Pass sets: 8 G rows each, one after another in this workgroup (their second read of a
+    // column hits this XCD's L2), as many as the workgroup's largest row count needs.  The row
+    // pass of a wave is rotated by the workgroup, so that when some waves of an item group have
+    // no rows (rows < 8 G) the busy ones land on different SIMDs from one workgroup to the next.
+    const uint32_t pr = (pw + wg % G) % G;
+    for (uint32_t set = 0; set * G * {R}u < rl; ++set) {{
+        if constexpr (G > 1) {{
+            if (set) __syncthreads();  // the exchange buffers are reused
+        }}
+        uint32_t row0 = 0, row1 = 0;
+        rs8_rt_pass_rows(rows, set * G + pr, row0, row1);
+        const uint32_t nr = __builtin_amdgcn_readfirstlane(row1 - row0);
+        // (an item group whose rows end before this set only keeps the workgroup's barriers)
+        const uint32_t k = __builtin_amdgcn_readfirstlane(set * G * {R}u < rows ? kk : 0u);
+        const uint8_t* tb = tblk + (a.tab_pass_stride ? (uint64_t)(set * G + pr) * a.tab_pass_stride : 2u * row0);
+        const uint32_t twl = (uint32_t)(uintptr_t)tb, twh = (uint32_t)((uintptr_t)tb >> 32);
+        const uintptr_t osa = pb && a.out_slots ? (uintptr_t)(a.out_slots + (uint64_t)blk * a.out_slots_stride + row0) : 0;
+        const uint16_t* osl = reinterpret_cast<const uint16_t*>(osa & ~(uintptr_t)3);
+        const uint32_t oph = (uint32_t)(osa >> 1) & 1u;
+        const uint32_t oslot = a.out_slot0 + (a.out_after_data && !lnd ? nd : 0u) + row0;  // (lnd: numData in po)
 {asm_blocks}
+    }}
 }}
 
 template <int G>
@@ -591,10 +593,10 @@ int launch_rs8_rt(const Rs8RtArgs& in, hipStream_t s)
     static const long g_all = diag_knob("NFEC_RT_G", 0, 0, 4), g_pb = diag_knob("NFEC_RT_GPB", 0, 0, 4);
     const long gk = a.per_block && g_pb ? g_pb : g_all;
     if (gk == 1 || gk == 2 || gk == 4) G = (uint32_t)gk;
-    a.pass_sets = (a.m + G * {R}u - 1u) / (G * {R}u);
+    a.pass_sets = (a.m + G * {R}u - 1u) / (G * {R}u);  // (informational: the kernel loops over them)
     const uint64_t groups = a.per_block ? (uint64_t)a.nblocks * ((a.vec_bytes + kGroupBytes - 1u) / kGroupBytes)
                                         : ((uint64_t)a.nblocks * a.vec_bytes + kGroupBytes - 1u) / kGroupBytes;
-    const uint64_t wgs = (groups + (4u / G) - 1u) / (4u / G) * a.pass_sets;
+    const uint64_t wgs = (groups + (4u / G) - 1u) / (4u / G);
     if (wgs >= (1ull << 31)) return NFEC_ENOTSUP;
     if (G == 1) hipLaunchKernelGGL(rs8_rt_kernel<1>, dim3((uint32_t)wgs), dim3(256), 0, s, a);
     else if (G == 2) hipLaunchKernelGGL(rs8_rt_kernel<2>, dim3((uint32_t)wgs), dim3(256), 0, s, a);
