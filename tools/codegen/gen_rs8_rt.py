@@ -586,9 +586,10 @@ int launch_rs8_rt(const Rs8RtArgs& in, hipStream_t s)
     if (in.nblocks == 0 || in.m == 0) return NFEC_OK;
     if (!rs8_rt_covers(in)) return NFEC_ENOTSUP;
     Rs8RtArgs a = in;
-    // waves per item group by the row capacity: with fewer rows than 8 G (per-block rows below
-    // m) the spare waves only load and transpose columns for the others
-    uint32_t G = a.m <= {R}u ? 1u : a.m <= {2 * R}u ? 2u : 4u;
+    // waves per item group: flat launches by the row count (every wave busy); per-block launches
+    // (the repairs, whose e is usually well below capacity) one wave up to 8 rows, else two
+    // (measured: four waves there leave two mostly idle, profiles/r04/rt_gsplit.jsonl)
+    uint32_t G = a.m <= {R}u ? 1u : (a.m <= {2 * R}u || a.per_block) ? 2u : 4u;
     // (NFEC_RT_G=1/2/4: that split for every launch, A/B only; NFEC_RT_GPB: per-block launches)
     static const long g_all = diag_knob("NFEC_RT_G", 0, 0, 4), g_pb = diag_knob("NFEC_RT_GPB", 0, 0, 4);
     const long gk = a.per_block && g_pb ? g_pb : g_all;
