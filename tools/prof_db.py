@@ -25,6 +25,7 @@ def main():
         s[1] += d
         s[2] = min(s[2], d)
         s[3] = max(s[3], d)
+    print(f"{'calls':>6} {'total_us':>12} {'avg_us':>10} {'min_us':>10} {'max_us':>10}  kernel")
     for n, (k, t, lo, hi) in sorted(st.items(), key=lambda x: -x[1][1]):
         print(f"{k:6d} {t:12.1f} {t / k:10.1f} {lo:10.1f} {hi:10.1f}  {n[:100]}")
 
