@@ -19,4 +19,6 @@ for grp in "${GRPS[@]}"; do
   timeout -s KILL 120 rocprofv3 --pmc $grp --output-format csv -d $OUT/p$i -o pmc -- python3 ${PMC_SCRIPT:-bench.py} $ARGS > $OUT/p$i.log 2>&1 \
       || { echo "pmc pass $i ($grp) failed"; tail -5 $OUT/p$i.log; exit 1; }
 done
-python3 tools/parse_pmc.py $OUT $OUT/pmc_traffic.json > $OUT/summary.json && cat $OUT/pmc_traffic.json
+python3 tools/parse_pmc.py $OUT $OUT/pmc_traffic.json > $OUT/summary.json || exit 1
+# (the traffic file exists for the headline workload only)
+[ ! -f $OUT/pmc_traffic.json ] || cat $OUT/pmc_traffic.json

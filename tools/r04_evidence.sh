@@ -8,9 +8,11 @@ R=${GRAFT_REPO_ROOT:-$(pwd)}
 O=$R/gpurun_out
 mkdir -p $O
 cd $R
+if [ -z "$SKIP_PERCALL" ]; then
 : > $O/percall.jsonl
 for args in "rs8 64 32 1408 16 2000" "rs8 64 16 1408 8 2000" "rs8 16 4 1408 4 2000" "rs16 400 100 1400 50 200" "mdp 64 32 1408 16 500"; do
     timeout -k 10 120 tools/percall/_build/percall $args >> $O/percall.jsonl
 done
+fi
 TAG=c4 timeout -k 10 600 bash tools/pmc_c4.sh > $O/pmc_c4.log 2>&1
 timeout -k 10 300 python3 tools/bench_extra.py --workload c4 > $O/extra_c4.json 2> $O/extra_c4.err
