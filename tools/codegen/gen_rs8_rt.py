@@ -483,6 +483,7 @@ __device__ __forceinline__ void rt_body(const Rs8RtArgs& a, uint32_t wg)
         // a block with nothing to compute reads nothing: a plan writes no slot list or table for
         // a block it rejected or that has no erasure (e = 0), so they must not be read
         if (rows == 0u || kk == 0u || kk > a.k || nd == 0u || nd > a.k) rows = 0u, kk = 0u;
+        if (rows < a.rows_lo || rows > a.rows_hi) rows = 0u, kk = 0u;  // another launch's blocks
     }}
     if (!live) rows = 0u, kk = 0u;
     // the workgroup's largest row and column counts: its waves run the pass sets (8 G rows
@@ -599,7 +600,19 @@ int launch_rs8_rt(const Rs8RtArgs& in, hipStream_t s)
                                         : ((uint64_t)a.nblocks * a.vec_bytes + kGroupBytes - 1u) / kGroupBytes;
     const uint64_t wgs = (groups + (4u / G) - 1u) / (4u / G);
     if (wgs >= (1ull << 31)) return NFEC_ENOTSUP;
-    if (G == 1) hipLaunchKernelGGL(rs8_rt_kernel<1>, dim3((uint32_t)wgs), dim3(256), 0, s, a);
+    if (a.per_block && G == 2 && !gk) {{
+        // per-block rows vary: blocks of at most {R} rows by one wave each (its own columns, no
+        // exchange), the others by two waves sharing columns -- two launches, each skipping the
+        // other's blocks (one wave loses to two from 9 rows up, two waves with one of them idle
+        // lose to one below; profiles/r04/rt_gsplit.jsonl)
+        Rs8RtArgs lo = a, hi = a;
+        lo.rows_hi = {R}u;
+        hi.rows_lo = {R + 1}u;
+        const uint64_t wgs1 = (groups + 3u) / 4u;
+        if (wgs1 >= (1ull << 31)) return NFEC_ENOTSUP;
+        hipLaunchKernelGGL(rs8_rt_kernel<1>, dim3((uint32_t)wgs1), dim3(256), 0, s, lo);
+        hipLaunchKernelGGL(rs8_rt_kernel<2>, dim3((uint32_t)wgs), dim3(256), 0, s, hi);
+    }} else if (G == 1) hipLaunchKernelGGL(rs8_rt_kernel<1>, dim3((uint32_t)wgs), dim3(256), 0, s, a);
     else if (G == 2) hipLaunchKernelGGL(rs8_rt_kernel<2>, dim3((uint32_t)wgs), dim3(256), 0, s, a);
     else hipLaunchKernelGGL(rs8_rt_kernel<4>, dim3((uint32_t)wgs), dim3(256), 0, s, a);
     const hipError_t e = hipGetLastError();
