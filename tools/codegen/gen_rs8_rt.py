@@ -454,12 +454,12 @@ namespace {{
 
 constexpr uint32_t kGroupBytes = 2048;   // 64 lanes x 4 pieces x 8 bytes
 
-template <int G>
+template <int G, int NG>
 __device__ __forceinline__ void rt_body(const Rs8RtArgs& a, uint32_t wg)
 {{
-    constexpr uint32_t NG = 4 / G;                              // item groups per workgroup
-    __shared__ uint32_t lds[4 * 64 * 4];                        // the lanes' output offsets (epilogue)
-    __shared__ uint64_t xch[(G > 1 ? 4 * 2 * {XCH_COL} / 8 : 1)];  // column planes exchange
+    // NG item groups per workgroup, G waves each
+    __shared__ uint32_t lds[G * NG * 64 * 4];                   // the lanes' output offsets (epilogue)
+    __shared__ uint64_t xch[(G > 1 ? NG * 2 * G * {XCH_COL} / 8 : 1)];  // column planes exchange
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t gi = wave / G, pw = wave % G;                // item group in the workgroup, wave in the group
@@ -559,10 +559,10 @@ __device__ __forceinline__ void rt_body(const Rs8RtArgs& a, uint32_t wg)
     }}
 }}
 
-template <int G>
-__global__ __launch_bounds__(256, 4) void rs8_rt_kernel(Rs8RtArgs a)
+template <int G, int NG>
+__global__ __launch_bounds__(64 * G * NG, 4) void rs8_rt_kernel(Rs8RtArgs a)
 {{
-    rt_body<G>(a, bs::wg_index(1));
+    rt_body<G, NG>(a, bs::wg_index(1));
 }}
 
 }}  // namespace
@@ -598,8 +598,18 @@ int launch_rs8_rt(const Rs8RtArgs& in, hipStream_t s)
     a.pass_sets = (a.m + G * {R}u - 1u) / (G * {R}u);  // (informational: the kernel loops over them)
     const uint64_t groups = a.per_block ? (uint64_t)a.nblocks * ((a.vec_bytes + kGroupBytes - 1u) / kGroupBytes)
                                         : ((uint64_t)a.nblocks * a.vec_bytes + kGroupBytes - 1u) / kGroupBytes;
-    const uint64_t wgs = (groups + (4u / G) - 1u) / (4u / G);
+    // item groups per workgroup: four waves per workgroup, except per-block launches of two-wave
+    // groups, one group per workgroup (its barriers then hold only its own two waves, not
+    // another block's; NFEC_RT_PBNG=2: two groups, A/B)
+    static const long pbng = diag_knob("NFEC_RT_PBNG", 1, 1, 2);
+    const uint32_t ng2 = a.per_block ? (uint32_t)pbng : 2u;
+    const uint32_t NGs = G == 1 ? 4u : G == 2 ? ng2 : 1u;
+    const uint64_t wgs = (groups + NGs - 1u) / NGs;
     if (wgs >= (1ull << 31)) return NFEC_ENOTSUP;
+    auto launch2 = [&](const Rs8RtArgs& x) {{
+        if (ng2 == 1) hipLaunchKernelGGL((rs8_rt_kernel<2, 1>), dim3((uint32_t)wgs), dim3(128), 0, s, x);
+        else hipLaunchKernelGGL((rs8_rt_kernel<2, 2>), dim3((uint32_t)wgs), dim3(256), 0, s, x);
+    }};
     if (a.per_block && G == 2 && !gk) {{
         // per-block rows vary: blocks of at most {R} rows by one wave each (its own columns, no
         // exchange), the others by two waves sharing columns -- two launches, each skipping the
@@ -610,11 +620,11 @@ int launch_rs8_rt(const Rs8RtArgs& in, hipStream_t s)
         hi.rows_lo = {R + 1}u;
         const uint64_t wgs1 = (groups + 3u) / 4u;
         if (wgs1 >= (1ull << 31)) return NFEC_ENOTSUP;
-        hipLaunchKernelGGL(rs8_rt_kernel<1>, dim3((uint32_t)wgs1), dim3(256), 0, s, lo);
-        hipLaunchKernelGGL(rs8_rt_kernel<2>, dim3((uint32_t)wgs), dim3(256), 0, s, hi);
-    }} else if (G == 1) hipLaunchKernelGGL(rs8_rt_kernel<1>, dim3((uint32_t)wgs), dim3(256), 0, s, a);
-    else if (G == 2) hipLaunchKernelGGL(rs8_rt_kernel<2>, dim3((uint32_t)wgs), dim3(256), 0, s, a);
-    else hipLaunchKernelGGL(rs8_rt_kernel<4>, dim3((uint32_t)wgs), dim3(256), 0, s, a);
+        hipLaunchKernelGGL((rs8_rt_kernel<1, 4>), dim3((uint32_t)wgs1), dim3(256), 0, s, lo);
+        launch2(hi);
+    }} else if (G == 1) hipLaunchKernelGGL((rs8_rt_kernel<1, 4>), dim3((uint32_t)wgs), dim3(256), 0, s, a);
+    else if (G == 2) launch2(a);
+    else hipLaunchKernelGGL((rs8_rt_kernel<4, 1>), dim3((uint32_t)wgs), dim3(256), 0, s, a);
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? NFEC_OK : hip_fail(e, "rs8 runtime-coefficient product launch");
 }}
