@@ -1,10 +1,13 @@
 """The runtime-coefficient RS8 kernel (gen_rs8_rt.hip) against the oracle, bit-exact: every RS8
 shape the fixed (64, m) kernels do not cover and every shortened batch goes through it
 (NormEncoderRS8::Encode, src/common/normEncoderRS8.cpp:473-483, for k + m <= 255; shortened
-blocks stop at numData, parity at slot numData + r), and MDP blocks of other shapes or lengths
-(normEncoderMDP.cpp:178-211).  Shapes pick each work split: m <= 8 one wave per item group,
-m <= 16 two waves sharing columns, more four (and several pass sets past 32 rows); segments
-longer than one 2 KiB item group; padded strides; accumulate."""
+blocks stop at numData, parity at slot numData + r -- run flat, each 8-byte piece masked by its
+own block's numData), the one-pass repair of those shapes (Decode, :652-757: the plan's closed-form
+e x numData map, then one product; blocks of up to 8 rows on one wave, larger on two), and MDP
+blocks of other shapes or lengths (normEncoderMDP.cpp:178-211).  Shapes pick each work split:
+m <= 8 one wave per item group, m <= 16 two waves sharing columns, more four (and several pass
+sets past 32 rows, looped inside the workgroup); segments longer than one 2 KiB item group;
+padded strides; accumulate."""
 import numpy as np
 import pytest
 
