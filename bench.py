@@ -285,6 +285,23 @@ def main():
 
         h2d_ms = timed(lambda: on_stream(lk_d, lk_h), 3)
         d2h_ms = timed(lambda: on_stream(lk_h, lk_d), 3)
+        # both directions at once, as the pipelines run them (parity and repaired segments come
+        # down while the next chunk goes up): 512 MiB each way on two streams
+        half = 1 << 29
+        s2 = torch.cuda.Stream(device=dev)
+        b0, b1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        torch.cuda.synchronize(dev)
+        b0.record(stream)
+        s2.wait_event(b0)
+        for _ in range(3):
+            with torch.cuda.stream(stream):
+                lk_d[:half].copy_(lk_h[:half], non_blocking=True)
+            with torch.cuda.stream(s2):
+                lk_h[half:].copy_(lk_d[half:], non_blocking=True)
+        stream.wait_stream(s2)
+        b1.record(stream)
+        b1.synchronize()
+        bidir_gbs = 3 * half / (b0.elapsed_time(b1) * 1e-3) / 1e9  # per direction
         del lk_h, lk_d
         h2d_gbs = (1 << 30) / (h2d_ms * 1e-3) / 1e9
         up_per_src = 2.0
@@ -293,6 +310,8 @@ def main():
             "link_h2d_GBps": round(h2d_gbs, 1),
             "link_d2h_GBps": round((1 << 30) / (d2h_ms * 1e-3) / 1e9, 1),
             "link_bound_GiBps": round(h2d_gbs * 1e9 / up_per_src * world / 2**30, 2),
+            "link_bidir_GBps_each_way": round(bidir_gbs, 1),
+            "link_bidir_bound_GiBps": round(bidir_gbs * 1e9 / up_per_src * world / 2**30, 2),
             "blocks_per_gpu": hb,
             "unit": "GiB/s",
             "steps": a.host_steps,
@@ -302,6 +321,7 @@ def main():
                     "substitute parity segments up, the 16 repaired segments down), overlapped with the kernels",
         }
         host["frac_of_link_bound"] = round(host["value"] / host["link_bound_GiBps"], 3)
+        host["frac_of_bidir_bound"] = round(host["value"] / host["link_bidir_bound_GiBps"], 3)
         del hblocks, hnp
 
     ok = None
