@@ -305,13 +305,18 @@ def main():
         del lk_h, lk_d
         h2d_gbs = (1 << 30) / (h2d_ms * 1e-3) / 1e9
         up_per_src = 2.0
+        down_per_src = (m + a.erasures) / k
         host = {
             "value": round(k * vec * hb * world / (he / a.host_steps) / 2**30, 2),
             "link_h2d_GBps": round(h2d_gbs, 1),
             "link_d2h_GBps": round((1 << 30) / (d2h_ms * 1e-3) / 1e9, 1),
             "link_bound_GiBps": round(h2d_gbs * 1e9 / up_per_src * world / 2**30, 2),
             "link_bidir_GBps_each_way": round(bidir_gbs, 1),
-            "link_bidir_bound_GiBps": round(bidir_gbs * 1e9 / up_per_src * world / 2**30, 2),
+            # the step's own mix: (m + e) / k bytes per source byte come down (parity, repaired
+            # segments) while 2 go up; while both directions run each gets the bidirectional
+            # rate, the rest of the upload the one-way rate
+            "link_mixed_bound_GiBps": round(world / ((down_per_src / bidir_gbs + (up_per_src - down_per_src) / h2d_gbs)
+                                                     * 1e-9) / 2**30, 2),
             "blocks_per_gpu": hb,
             "unit": "GiB/s",
             "steps": a.host_steps,
@@ -321,7 +326,7 @@ def main():
                     "substitute parity segments up, the 16 repaired segments down), overlapped with the kernels",
         }
         host["frac_of_link_bound"] = round(host["value"] / host["link_bound_GiBps"], 3)
-        host["frac_of_bidir_bound"] = round(host["value"] / host["link_bidir_bound_GiBps"], 3)
+        host["frac_of_mixed_bound"] = round(host["value"] / host["link_mixed_bound_GiBps"], 3)
         del hblocks, hnp
 
     ok = None
