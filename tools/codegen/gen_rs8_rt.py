@@ -596,6 +596,10 @@ int launch_rs8_rt(const Rs8RtArgs& in, hipStream_t s)
     const long gk = a.per_block && g_pb ? g_pb : g_all;
     if (gk == 1 || gk == 2 || gk == 4) G = (uint32_t)gk;
     a.pass_sets = (a.m + G * {R}u - 1u) / (G * {R}u);  // (informational: the kernel loops over them)
+    // NFEC_RT_PROBE=1 (diagnostic library only, wrong results): every column reads slot 0 of its
+    // block, so the loads hit the cache -- the kernel's time without HBM read latency
+    static const long probe = diag_knob("NFEC_RT_PROBE", 0, 0, 1);
+    if (probe) a.in_seg_stride = 0;
     const uint64_t groups = a.per_block ? (uint64_t)a.nblocks * ((a.vec_bytes + kGroupBytes - 1u) / kGroupBytes)
                                         : ((uint64_t)a.nblocks * a.vec_bytes + kGroupBytes - 1u) / kGroupBytes;
     // item groups per workgroup: four waves per workgroup, except per-block launches of two-wave
