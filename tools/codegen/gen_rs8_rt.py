@@ -587,10 +587,12 @@ int launch_rs8_rt(const Rs8RtArgs& in, hipStream_t s)
     if (in.nblocks == 0 || in.m == 0) return NFEC_OK;
     if (!rs8_rt_covers(in)) return NFEC_ENOTSUP;
     Rs8RtArgs a = in;
-    // waves per item group: flat launches by the row count (every wave busy); per-block launches
-    // (the repairs, whose e is usually well below capacity) one wave up to 8 rows, else two
+    // waves per item group: by the row count when every block has m rows (every wave busy);
+    // launches whose rows differ per block (the repairs, e usually well below capacity) one wave
+    // up to 8 rows, else two
     // (measured: four waves there leave two mostly idle, profiles/r04/rt_gsplit.jsonl)
-    uint32_t G = a.m <= {R}u ? 1u : (a.m <= {2 * R}u || a.per_block) ? 2u : 4u;
+    const bool var_rows = a.per_block && a.blk_rows;  // rows differ per block (the repairs)
+    uint32_t G = a.m <= {R}u ? 1u : (a.m <= {2 * R}u || var_rows) ? 2u : 4u;
     // (NFEC_RT_G=1/2/4: that split for every launch, A/B only; NFEC_RT_GPB: per-block launches)
     static const long g_all = diag_knob("NFEC_RT_G", 0, 0, 4), g_pb = diag_knob("NFEC_RT_GPB", 0, 0, 4);
     const long gk = a.per_block && g_pb ? g_pb : g_all;
@@ -614,7 +616,7 @@ int launch_rs8_rt(const Rs8RtArgs& in, hipStream_t s)
         if (ng2 == 1) hipLaunchKernelGGL((rs8_rt_kernel<2, 1>), dim3((uint32_t)wgs), dim3(128), 0, s, x);
         else hipLaunchKernelGGL((rs8_rt_kernel<2, 2>), dim3((uint32_t)wgs), dim3(256), 0, s, x);
     }};
-    if (a.per_block && G == 2 && !gk) {{
+    if (var_rows && G == 2 && !gk) {{
         // per-block rows vary: blocks of at most {R} rows by one wave each (its own columns, no
         // exchange), the others by two waves sharing columns -- two launches, each skipping the
         // other's blocks (one wave loses to two from 9 rows up, two waves with one of them idle
