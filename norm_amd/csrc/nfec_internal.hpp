@@ -328,6 +328,7 @@ struct Rs8RtArgs {
     uint32_t tab_by_count = 0;
     uint64_t tab_pass_stride = 0;        // bytes; 0: entries by row (2 r)
     uint32_t rows_lo = 0, rows_hi = ~0u; // per-block: only blocks with rows in [lo, hi] (set by the launcher)
+    uint32_t probe_noapply = 0;          // diagnostic probes only (set by the launcher)
     uint32_t accumulate = 0;             // XOR into the output slots
     uint32_t slot_bound = 0;             // slot lists hold slots below this (0: 65536)
     uint32_t pass_sets = 0;              // set by the launcher

@@ -546,7 +546,7 @@ __device__ __forceinline__ void rt_body(const Rs8RtArgs& a, uint32_t wg)
         }}
         uint32_t row0 = 0, row1 = 0;
         rs8_rt_pass_rows(rows, set * G + pr, row0, row1);
-        const uint32_t nr = __builtin_amdgcn_readfirstlane(row1 - row0);
+        const uint32_t nr = a.probe_noapply ? 0u : __builtin_amdgcn_readfirstlane(row1 - row0);
         // (an item group whose rows end before this set only keeps the workgroup's barriers)
         const uint32_t k = __builtin_amdgcn_readfirstlane(set * G * {R}u < rows ? kk : 0u);
         const uint8_t* tb = tblk + (a.tab_pass_stride ? (uint64_t)(set * G + pr) * a.tab_pass_stride : 2u * row0);
@@ -600,8 +600,22 @@ int launch_rs8_rt(const Rs8RtArgs& in, hipStream_t s)
     a.pass_sets = (a.m + G * {R}u - 1u) / (G * {R}u);  // (informational: the kernel loops over them)
     // NFEC_RT_PROBE=1 (diagnostic library only, wrong results): every column reads slot 0 of its
     // block, so the loads hit the cache -- the kernel's time without HBM read latency
-    static const long probe = diag_knob("NFEC_RT_PROBE", 0, 0, 1);
-    if (probe) a.in_seg_stride = 0;
+    // =2: every coefficient the empty snippet (calls kept, their VALU gone: the table reads
+    // one zeroed line); =3: no rows applied (loads, transposes and exchange only)
+    static const long probe = diag_knob("NFEC_RT_PROBE", 0, 0, 3);
+    if (probe == 1) a.in_seg_stride = 0;
+    if (probe == 2) {{
+        static uint16_t* zeros = nullptr;
+        if (!zeros) {{
+            if (hipMalloc(&zeros, 256) != hipSuccess || hipMemset(zeros, 0, 256) != hipSuccess) return NFEC_EDEVICE;
+        }}
+        a.tab = zeros;
+        a.tab_block_stride = 0;
+        a.tab_pass_stride = 0;
+        a.tab_col_stride = 0;
+        a.tab_by_count = 0;
+    }}
+    if (probe == 3) a.probe_noapply = 1;
     const uint64_t groups = a.per_block ? (uint64_t)a.nblocks * ((a.vec_bytes + kGroupBytes - 1u) / kGroupBytes)
                                         : ((uint64_t)a.nblocks * a.vec_bytes + kGroupBytes - 1u) / kGroupBytes;
     // item groups per workgroup: four waves per workgroup, except per-block launches of two-wave
