@@ -81,8 +81,6 @@ S_TBN = 58                            # 2: table address of the column being fet
 S_OFF = [60, 64]                      # 2 x 4: the entries of a column (8 rows, u16 each)
 S_SLW = 68                            # the slot-list dword being read
 S_TOUCH = 78                          # destination of the scalar-cache touch loads (never read)
-S_SNIPB, S_NXT = 69, 70               # chained calls: table B's address (low word), the second target
-CHAIN = [False]                       # emit the chained-call variant (two rows per call/return)
 S_LAST = 78
 S_UNUSED = (69, 70, 71)               # left to the compiler (its SGPR pressure is high around the asm)
 assert S_MASK == 72
@@ -128,26 +126,6 @@ def snippets():
             elif b:
                 out.append(f"v_xor_b32 v{d}, v{d}, v{B[b]}")
         out.append(f"s_setpc_b64 s[{S_RET}:{S_RET + 1}]")
-    if CHAIN[0]:
-        # table B: the same products for row r, then on to row r + 1 (M0 + 16) at the second
-        # target, whose table-A snippet returns to the caller: one taken branch less per pair
-        out.append(".p2align 16")
-        for c in range(256):
-            out.append(f".p2align {SNIP_ALIGN}")
-            if c == 0:
-                out.append("LsnipB_%=:")
-            rows = bitmatrix_rows(c) if c else [0] * 8
-            for i in range(8):
-                a, b = split(rows[i])
-                d = acc_reg(0, i)
-                if a and b:
-                    out.append(f"v_bitop3_b32 v{d}, v{d}, v{A[a]}, v{B[b]} bitop3:0x96")
-                elif a:
-                    out.append(f"v_xor_b32 v{d}, v{d}, v{A[a]}")
-                elif b:
-                    out.append(f"v_xor_b32 v{d}, v{d}, v{B[b]}")
-            out.append("s_add_u32 m0, m0, 16")
-            out.append(f"s_setpc_b64 s[{S_NXT}:{S_NXT + 1}]")
     return out
 
 
@@ -196,18 +174,6 @@ def sweep(nr, x, ebuf):
     targets), or None (generic targets, rows checked against %[nr])"""
     fast = nr is not None
     L = [f"s_mov_b32 s{S_T0}, 0", f"s_set_gpr_idx_on s{S_T0}, gpr_idx(SRC0,DST)"]
-    if fast and CHAIN[0]:
-        for r in range(0, nr, 2):
-            if r + 1 < nr:
-                dw = ebuf + r // 2
-                L += [f"s_pack_lh_b32_b16 s{S_TGT}, s{dw}, s{S_SNIPB}",
-                      f"s_pack_hh_b32_b16 s{S_NXT}, s{dw}, s{S_SNIP}",
-                      f"s_mov_b32 m0, 0x{GPR_MODE | (16 * r):x}",
-                      f"s_swappc_b64 s[{S_RET}:{S_RET + 1}], s[{S_TGT}:{S_TGT + 1}]"]
-            else:
-                L += call(r, fast, ebuf)
-        L += [f"Lsw{x}_%=:", "s_set_gpr_idx_off", "s_nop 1"]
-        return L
     for r in range(nr if fast else R):
         if not fast:
             L += [f"s_cmp_le_u32 %[nr], {r}", f"s_cbranch_scc1 Lsw{x}_%="]
@@ -389,11 +355,6 @@ def body(G):
     # the fast loops pack call targets from the table address's high half: taken when the
     # table starts at a 64 KiB boundary in memory (else the generic loop)
     L += [f"s_and_b32 s{S_T0}, s{S_SNIP}, 0xffff", f"s_cmp_lg_u32 s{S_T0}, 0", "s_cbranch_scc1 Lstepg_%="]
-    if CHAIN[0]:
-        # table B in the same 4 GiB window as table A (one high word for every target)
-        L += [f"s_add_u32 s{S_SNIPB}, s{S_SNIP}, LsnipB_%=-Lsnip0_%=", f"s_addc_u32 s{S_T0}, s{S_SNIP + 1}, 0",
-              f"s_mov_b32 s{S_NXT + 1}, s{S_SNIP + 1}",
-              f"s_cmp_lg_u32 s{S_T0}, s{S_SNIP + 1}", "s_cbranch_scc1 Lstepg_%="]
     for nr in range(R, 0, -1):
         L += [f"s_cmp_eq_u32 %[nr], {nr}", f"s_cbranch_scc1 Lstepr{nr}_%="]
     L.append("s_branch Lstepg_%=")
@@ -403,7 +364,7 @@ def body(G):
     for x, nr in loops:
         L += step_loop_single(x, nr) if G == 1 else step_loop_shared(G, x, nr)
         L.append("s_branch Lepi0_%=")
-    L += ["Lepi0_%=:", "s_cmp_eq_u32 %[nr], 0", "s_cbranch_scc0 Lepn_%="] + jump_end() + ["Lepn_%=:"]
+    L += ["Lepi0_%=:", "s_cmp_eq_u32 %[nr], 0", "s_cbranch_scc1 Lend_%="]
     L += epilogue()
     return L
 
@@ -449,55 +410,39 @@ def epilogue():
         L.append(f"Lna{r}_%=:")
         for i in range(4):
             L.append(f"buffer_store_dwordx2 v[{w[2 * i]}:{w[2 * i + 1]}], v{so[i]}, s[{S_ODESC}:{S_ODESC + 3}], s{S_T1} offen")
-    L += ["Lepi_%=:"] + jump_end()
+    L += ["Lepi_%=:", "s_branch Lend_%="]
     L += snippets()
     L.append("Lend_%=:")
     return L
 
 
-def jump_end():
-    """to Lend past the snippet table(s): a branch while they fit its 16-bit reach, else an
-    absolute jump (the chained variant's two 64 KiB-aligned tables do not)"""
-    if not CHAIN[0]:
-        return ["s_branch Lend_%="]
-    return uniq([f"s_getpc_b64 s[{S_T0}:{S_T1}]", "Ljb_%=_{uid}:",
-                 f"s_add_u32 s{S_T0}, s{S_T0}, Lend_%=-Ljb_%=_{{uid}}", f"s_addc_u32 s{S_T1}, s{S_T1}, 0",
-                 f"s_setpc_b64 s[{S_T0}:{S_T1}]"])
-
-
 def clobbers():
     v = [f'"v{i}"' for i in range(0, V_LAST + 1) if i not in IN_REGS + FREE]
-    s = [f'"s{i}"' for i in range(S_DESC, S_LAST + 1) if CHAIN[0] or i not in S_UNUSED]
+    s = [f'"s{i}"' for i in range(S_DESC, S_LAST + 1) if i not in S_UNUSED]
     return ", ".join(v + s + ['"m0"', '"scc"', '"memory"'])
 
 
 def main():
     path = sys.argv[1]
+    asms = {G: "\\n\"\n            \"".join(body(G)) for G in GS}
     ins = ", ".join([f'[o{i}] "v"(o[{i}])' for i in range(4)] + [f'[q{i}] "v"(q[{i}])' for i in range(4)])
     common = ("[wb] \"s\"(wb), [ob] \"s\"(ob), [ss] \"s\"(a.in_seg_stride), [oss] \"s\"(a.out_seg_stride), "
               "[k] \"s\"(k), [kl] \"s\"(kl), [nr] \"s\"(nr), [twl] \"s\"(twl), [twh] \"s\"(twh), "
               "[tstep] \"s\"(a.tab_col_stride), [tpf] \"s\"(tpf), [isl] \"s\"(isl), [islot0] \"s\"(a.in_slot0), [osl] \"s\"(osl), "
               "[oslot] \"s\"(oslot), [acc] \"s\"(mode), [wv] \"s\"(pw), [iph] \"s\"(iph), [oph] \"s\"(oph), "
+              
               "[lo] \"v\"(lo), [xl] \"v\"(xl), " + ins)
-
-    def variant(chain):
-        CHAIN[0] = chain
-        asms = {G: "\\n\"\n            \"".join(body(G)) for G in GS}
-        blocks = []
-        for G in GS:
-            kw = "if constexpr" if G == GS[0] else "else if constexpr"
-            blocks.append(f"""    {kw} (G == {G}) {{
+    blocks = []
+    for G in GS:
+        kw = "if constexpr" if G == GS[0] else "else if constexpr"
+        blocks.append(f"""    {kw} (G == {G}) {{
         asm volatile(
             "{asms[G]}\\n"
             :
             : {common}
             : {clobbers()});
     }}""")
-        CHAIN[0] = False
-        return "\n".join(blocks)
-
-    # the chained-call variant is built only with -DNFEC_RT_CHAIN (A/B in the diagnostic library)
-    asm_blocks = "#ifdef NFEC_RT_CHAIN\n" + variant(True) + "\n#else\n" + variant(False) + "\n#endif"
+    asm_blocks = "\n".join(blocks)
     src = f"""// GENERATED by tools/codegen/gen_rs8_rt.py -- do not edit by hand.
 // GF(2^8) block-matrix products with runtime coefficients: bit-sliced, snippet jumps.
 #include "nfec_internal.hpp"
