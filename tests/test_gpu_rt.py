@@ -233,3 +233,42 @@ def test_rt_encode_shortened_flat_bad_counts(orc, k, m, vec, nb):
     enc.encode_blocks(dev, num_data=torch.from_numpy(nd_dev.view(np.int16)).cuda())
     torch.cuda.synchronize()
     assert np.array_equal(dev.cpu().numpy(), ref)
+
+
+@pytest.mark.parametrize("k,m,vec,nb,short", [(40, 20, 1400, 300, False), (100, 30, 2056, 60, True),
+                                              (64, 32, 1400, 200, True)])
+def test_rt_decode_mixed_erasure_counts(orc, k, m, vec, nb, short):
+    """one batch whose blocks need 0..m rows: the repair runs blocks of up to 8 rows on one wave
+    and larger ones on two (two launches, each skipping the other's blocks), a block with
+    nothing to repair is left alone, and every byte matches the oracle"""
+    rng = np.random.default_rng(k * 3 + nb)
+    nd = rng.integers(max(1, m // 2), k + 1, nb).astype(np.uint16) if short else np.full(nb, k, np.uint16)
+    host = orc.make_blocks(k, m, vec, nb, num_data=nd if short else None)
+    clean = orc.encode_blocks(NFEC_RS8, k, m, vec, host, nd if short else None)
+    locs = np.zeros((nb, m), np.uint16)
+    counts = np.zeros(nb, np.uint16)
+    rx = clean.copy()
+    for b in range(nb):
+        n = int(nd[b])
+        es = int(rng.integers(0, min(n, m) + 1))        # 0 .. m source erasures
+        ep = int(rng.integers(0, m - es + 1)) if b % 3 == 0 else 0
+        e = np.sort(np.concatenate([rng.choice(n, es, replace=False), n + rng.choice(m, ep, replace=False)]))
+        e = e.astype(np.uint16)[:m]
+        counts[b] = len(e)
+        locs[b, :len(e)] = e
+        for s in e:
+            rx[b, s] = 0
+    counts[0] = 0  # nothing to repair
+    locs[0] = 0
+    rx[0] = clean[0]
+    ref = rx.copy()
+    st_ref = orc.decode_blocks(NFEC_RS8, k, m, vec, ref, locs, counts, nd if short else None)
+    dec = NormDecoderRS8()
+    assert dec.Init(k, m, vec)
+    dev = torch.from_numpy(rx).cuda()
+    st = dec.decode_blocks(dev, torch.from_numpy(locs.view(np.int16)).cuda(),
+                           torch.from_numpy(counts.view(np.int16)).cuda(),
+                           num_data=torch.from_numpy(nd.view(np.int16)).cuda() if short else None)
+    torch.cuda.synchronize()
+    assert np.array_equal(st.cpu().numpy(), st_ref)
+    assert np.array_equal(dev.cpu().numpy(), ref)
