@@ -45,7 +45,7 @@ R = 8                     # rows per wave (pass)
 SNIP_ALIGN = 7            # 128-byte snippet slots
 GPR_MODE = 0x9000         # M0[15:12]: index SRC0 and DST
 MULTI = [a for a in range(1, 16) if bin(a).count("1") >= 2]
-GS = (1, 2, 4)            # waves per item group
+GS = (1, 2, 4, 8)         # waves per item group
 
 
 def q2(q):
@@ -594,9 +594,13 @@ int launch_rs8_rt(const Rs8RtArgs& in, hipStream_t s)
     const bool var_rows = a.per_block && a.blk_rows;  // rows differ per block (the repairs)
     uint32_t G = a.m <= {R}u ? 1u : (a.m <= {2 * R}u || var_rows) ? 2u : 4u;
     // (NFEC_RT_G=1/2/4: that split for every launch, A/B only; NFEC_RT_GPB: per-block launches)
-    static const long g_all = diag_knob("NFEC_RT_G", 0, 0, 4), g_pb = diag_knob("NFEC_RT_GPB", 0, 0, 4);
+    // more than 32 rows (every block the same): eight waves of 8 rows share each column's load
+    // and transpose, one pass set up to 64 rows instead of two (NFEC_RT_G8=0: four waves, A/B)
+    static const long g8 = diag_knob("NFEC_RT_G8", 1);
+    if (G == 4 && g8 && a.m > 4u * {R}u) G = 8;
+    static const long g_all = diag_knob("NFEC_RT_G", 0, 0, 8), g_pb = diag_knob("NFEC_RT_GPB", 0, 0, 8);
     const long gk = a.per_block && g_pb ? g_pb : g_all;
-    if (gk == 1 || gk == 2 || gk == 4) G = (uint32_t)gk;
+    if (gk == 1 || gk == 2 || gk == 4 || gk == 8) G = (uint32_t)gk;
     a.pass_sets = (a.m + G * {R}u - 1u) / (G * {R}u);  // (informational: the kernel loops over them)
     // NFEC_RT_PROBE=1 (diagnostic library only, wrong results): every column reads slot 0 of its
     // block, so the loads hit the cache -- the kernel's time without HBM read latency
@@ -644,7 +648,8 @@ int launch_rs8_rt(const Rs8RtArgs& in, hipStream_t s)
         launch2(hi);
     }} else if (G == 1) hipLaunchKernelGGL((rs8_rt_kernel<1, 4>), dim3((uint32_t)wgs), dim3(256), 0, s, a);
     else if (G == 2) launch2(a);
-    else hipLaunchKernelGGL((rs8_rt_kernel<4, 1>), dim3((uint32_t)wgs), dim3(256), 0, s, a);
+    else if (G == 4) hipLaunchKernelGGL((rs8_rt_kernel<4, 1>), dim3((uint32_t)wgs), dim3(256), 0, s, a);
+    else hipLaunchKernelGGL((rs8_rt_kernel<8, 1>), dim3((uint32_t)wgs), dim3(512), 0, s, a);
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? NFEC_OK : hip_fail(e, "rs8 runtime-coefficient product launch");
 }}
