@@ -488,6 +488,19 @@ __device__ __forceinline__ void rt_body(const Rs8RtArgs& a, uint32_t wg)
     if (!live) rows = 0u, kk = 0u;
     // the workgroup's largest row and column counts: its waves run the pass sets (8 G rows
     // each) and steps of the longest item group together, with the same barriers (G > 1)
+    if (!pb && a.num_data && live) {{
+        // flat shortened: columns past every numData of the item group's blocks read zeros, so
+        // the group stops at their largest (no valid block: nothing to compute or store)
+        const uint32_t bf = (uint32_t)(f0 / a.vec_bytes), bl = (uint32_t)((min(f0 + kGroupBytes, total) - 1u) / a.vec_bytes);
+        uint32_t mx = 0;
+        for (uint32_t b = bf + lane; b <= bl; b += 64u) {{
+            const uint32_t v = a.num_data[b];
+            if (v >= 1u && v <= a.k) mx = max(mx, v);
+        }}
+        for (int off = 32; off > 0; off >>= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, off));
+        kk = __builtin_amdgcn_readfirstlane(mx);
+        if (kk == 0u) rows = 0u;
+    }}
     uint32_t kl = kk, rl = rows;
     if constexpr (G > 1) {{
         if (NG > 1) {{
