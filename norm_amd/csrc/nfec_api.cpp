@@ -911,9 +911,9 @@ int decode_device(nfec_codec* c, const nfec_block_batch* b, const uint16_t* locs
     const uint32_t dcs = c->kind == NFEC_MDP ? c->cs : round_up(std::max(1u, std::min(c->k, c->m)), kRowPad);
     const bool big_plan = c->kind != NFEC_MDP && std::min(c->k, c->m) > 64;
     // RS8 blocks the fused / fixed-shape kernels do not take: a closed-form plan writes each
-    // block's whole repair map (e x numData, rs8_plan_rt_kernel) as a compact snippet table
-    // (columns of cst = min(k, m) rounded up to even entries) and ONE pass of the
-    // runtime-coefficient kernel computes the erased source from the received columns
+    // block's whole repair map (e x numData, rs8_plan_rt_kernel) as a pass-major snippet table
+    // (8 rows per pass, 16 bytes per column) and ONE pass of the runtime-coefficient kernel
+    // computes the erased source from the received columns
     // (NFEC_RT_DEC=1: the one-pass runtime-coefficient repair for those shapes too, for A/B)
     static const bool rt_first = diag_knob("NFEC_RT_DEC", 0) != 0;
     const bool fast = !rt_first && c->kind == NFEC_RS8 && !b->num_data && c->m <= 32 && c->k <= 64 && !force_generic() &&
