@@ -201,6 +201,7 @@ struct nfec_codec {
     std::vector<std::unique_ptr<nfec_codec>> stripes;
     uint32_t cs = 0;  // padded parity-row count
     std::vector<uint32_t> gen;  // m x k parity rows (RS) / LFSR map for a full block (MDP)
+    std::vector<uint8_t> mdp_g; // MDP generator polynomial g[0..m] (the host per-segment step)
 
     // device-resident state
     DevBuf<uint8_t> d_coef;      // encode coefficients, column-major [k][cs] elements
@@ -347,6 +348,7 @@ int build_codec(nfec_codec* c)
         if (c->k + c->m > 255 || c->m == 0) return fail(NFEC_ERANGE, "MDP: numData + numParity > 255");
         std::vector<uint8_t> g;
         mdp_generator_poly(c->m, g);
+        c->mdp_g = g;
         // encode matrices for every block length nd = 1..k: [nd-1][col][cs]
         std::vector<uint8_t> coef((size_t)c->k * c->k * c->cs, 0);
         std::vector<uint8_t> map((size_t)c->m * c->k);
@@ -1824,12 +1826,29 @@ int nfec_encode_segment(nfec_codec* c, uint32_t segment_id, const void* data, vo
 int nfec_encode_segment_host(nfec_codec* c, uint32_t segment_id, const void* data, void* const* parity)
 {
     if (!c || !data || !parity) return fail(NFEC_EINVAL, "null argument");
-    if (c->kind != NFEC_RS8) return fail(NFEC_ENOTSUP, "the host per-segment path is RS8 only");
+    if (c->kind == NFEC_RS16) return fail(NFEC_ENOTSUP, "the host per-segment path is RS8 / MDP only");
     if (segment_id >= c->k) return fail(NFEC_EINVAL, "segmentId >= numData");
     for (uint32_t i = 0; i < c->m; ++i)
         if (!parity[i]) return fail(NFEC_EINVAL, "null parity vector");
     const uint8_t* d = static_cast<const uint8_t*>(data);
     const int isa = host_gf8_isa();
+    if (c->kind == NFEC_MDP) {
+        // the reference's LFSR step: s = data ^ P0 (its scratch copy of P0), then the shift
+        thread_local std::vector<uint8_t> s;
+        s.resize(c->vec);
+        const uint8_t* p0 = static_cast<const uint8_t*>(parity[0]);
+        for (uint32_t j = 0; j < c->vec; ++j) s[j] = d[j] ^ p0[j];
+        const uint32_t m = c->m;
+        for (uint32_t i = 0; i + 1 < m; ++i) {
+            uint8_t* pi = static_cast<uint8_t*>(parity[i]);
+            std::memcpy(pi, parity[i + 1], c->vec);
+            host_gf8_addmul(pi, s.data(), c->mdp_g[m - 1 - i], c->vec, isa);
+        }
+        uint8_t* pl = static_cast<uint8_t*>(parity[m - 1]);
+        std::memset(pl, 0, c->vec);
+        host_gf8_addmul(pl, s.data(), c->mdp_g[0], c->vec, isa);
+        return NFEC_OK;
+    }
     for (uint32_t i = 0; i < c->m; ++i)
         host_gf8_addmul(static_cast<uint8_t*>(parity[i]), d, c->gen[(size_t)i * c->k + segment_id], c->vec, isa);
     return NFEC_OK;

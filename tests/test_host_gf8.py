@@ -1,5 +1,5 @@
 """The host per-segment path (nfec_gf8_addmul_host, the body of nfec_encode_segment_host and of the
-drop-in NormEncoderRS8::Encode): dst ^= c * src in the RS8 field, every form this CPU has (GFNI,
+drop-in NormEncoderRS8::Encode / NormEncoderMDP::Encode): dst ^= c * src in the RS8 field, every form this CPU has (GFNI,
 AVX2, scalar) against the oracle's product table -- the table the reference builds with
 init_mul_table (src/common/normEncoderRS8.cpp:140-149), pinned to galois.cpp's field
 (tests/test_oracle.py).  CPU only: no GPU is involved."""
@@ -88,7 +88,28 @@ def test_encode_segment_host_matches_gpu_and_oracle(orc, k, m, vec):
 
 
 @pytest.mark.gpu
-def test_encode_segment_host_is_rs8_only():
+@pytest.mark.parametrize("k,m,vec", [(64, 32, 1408), (20, 7, 1401), (5, 1, 64)])
+def test_encode_segment_host_mdp_lfsr(orc, k, m, vec):
+    """MDP on the host: the reference's LFSR step per in-order segment (normEncoderMDP.cpp:
+    178-211) over zeroed parity gives the oracle's block parity, as the GPU per-call path does"""
+    import norm_amd as na
+
+    enc = na.NormEncoderMDP()
+    assert enc.Init(k, m, vec)
+    host = orc.make_blocks(k, m, vec, 1)
+    ref = orc.encode_blocks(N.NFEC_MDP, k, m, vec, host.copy())
+    for fn in ("nfec_encode_segment_host", "nfec_encode_segment"):
+        par = [np.zeros(vec, np.uint8) for _ in range(m)]
+        arr = (ctypes.c_void_p * m)(*[p.ctypes.data for p in par])
+        for s in range(k):
+            d = np.ascontiguousarray(host[0, s, :vec])
+            assert getattr(N.lib(), fn)(enc._h, s, d.ctypes.data, arr) == 0
+        for p in range(m):
+            assert np.array_equal(par[p], ref[0, k + p, :vec]), (fn, p)
+
+
+@pytest.mark.gpu
+def test_encode_segment_host_not_rs16():
     import norm_amd as na
 
     enc = na.NormEncoderRS16()
