@@ -245,12 +245,16 @@ enum { NFEC_HOST_GF_SCALAR = 0, NFEC_HOST_GF_AVX2 = 1, NFEC_HOST_GF_GFNI = 2 };
 /* dst[0..bytes) ^= c * src[0..bytes) in the RS8 field (0x11d).  isa: an NFEC_HOST_GF_* form, or
  * < 0 for the best this CPU has.  Returns the form used, NFEC_ENOTSUP when the CPU lacks it. */
 int nfec_gf8_addmul_host(void* dst, const void* src, uint8_t c, size_t bytes, int isa);
+/* ... over `symbols` native-endian 16-bit symbols in the RS16 field (0x1100B); forms: GFNI or
+ * scalar (an AVX2 request runs the scalar form, which is what it returns). */
+int nfec_gf16_addmul_host(void* dst, const void* src, uint16_t c, size_t symbols, int isa);
 /* NormEncoderRS8::Encode (normEncoderRS8.cpp:473-483) on the host: parity_vectors[i] ^=
- * G[k+i][segment_id] * data over vector_size bytes.  MDP (NormEncoderMDP::Encode,
- * normEncoderMDP.cpp:178-211): one LFSR step, s = data ^ parity[0], parity[i] = parity[i+1] ^
- * g[m-1-i] * s, parity[m-1] = g[0] * s -- segments in order, as the reference requires
- * (segment_id is ignored, as there).  RS16: NFEC_ENOTSUP.  Reads only the codec's generator:
- * concurrent calls on one codec are safe (on different blocks). */
+ * G[k+i][segment_id] * data over vector_size bytes.  RS16 (NormEncoderRS16::Encode,
+ * normEncoderRS16.cpp:472-482): the same over vector_size / 2 native-endian symbols, an odd last
+ * byte untouched.  MDP (NormEncoderMDP::Encode, normEncoderMDP.cpp:178-211): one LFSR step,
+ * s = data ^ parity[0], parity[i] = parity[i+1] ^ g[m-1-i] * s, parity[m-1] = g[0] * s --
+ * segments in order, as the reference requires (segment_id is ignored, as there).  Reads only
+ * the codec's generator: concurrent calls on one codec are safe (on different blocks). */
 int nfec_encode_segment_host(nfec_codec* codec, uint32_t segment_id, const void* data,
                              void* const* parity_vectors);
 

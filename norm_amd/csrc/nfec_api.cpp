@@ -1826,12 +1826,19 @@ int nfec_encode_segment(nfec_codec* c, uint32_t segment_id, const void* data, vo
 int nfec_encode_segment_host(nfec_codec* c, uint32_t segment_id, const void* data, void* const* parity)
 {
     if (!c || !data || !parity) return fail(NFEC_EINVAL, "null argument");
-    if (c->kind == NFEC_RS16) return fail(NFEC_ENOTSUP, "the host per-segment path is RS8 / MDP only");
     if (segment_id >= c->k) return fail(NFEC_EINVAL, "segmentId >= numData");
     for (uint32_t i = 0; i < c->m; ++i)
         if (!parity[i]) return fail(NFEC_EINVAL, "null parity vector");
     const uint8_t* d = static_cast<const uint8_t*>(data);
     const int isa = host_gf8_isa();
+    if (c->kind == NFEC_RS16) {
+        // vec / 2 native-endian symbols; an odd last byte is never touched (normEncoderRS16.cpp:479)
+        const size_t nsym = c->vec / 2;
+        const uint16_t* d16 = static_cast<const uint16_t*>(data);
+        for (uint32_t i = 0; i < c->m; ++i)
+            host_gf16_addmul(static_cast<uint16_t*>(parity[i]), d16, c->gen[(size_t)i * c->k + segment_id], nsym, isa);
+        return NFEC_OK;
+    }
     if (c->kind == NFEC_MDP) {
         // the reference's LFSR step: s = data ^ P0 (its scratch copy of P0), then the shift
         thread_local std::vector<uint8_t> s;

@@ -74,6 +74,8 @@ void mdp_encode_matrix(const std::vector<uint8_t>& g, uint32_t m, uint32_t nd, u
 
 // host_gf8.cpp: dst ^= c * src over n bytes on the host CPU (isa: NFEC_HOST_GF_*, < 0 best)
 void host_gf8_addmul(uint8_t* dst, const uint8_t* src, uint32_t c, size_t n, int isa);
+// ... and over nsym 16-bit symbols in the RS16 field (GFNI or scalar)
+void host_gf16_addmul(uint16_t* dst, const uint16_t* src, uint32_t c, size_t nsym, int isa);
 int host_gf8_isa();
 
 // v_perm product tables for one GF(2^8) constant c: 8 dwords (32 bytes)

@@ -63,7 +63,7 @@ int NfecCodecBase::DecodeBlocks(const nfec_block_batch* batch, const uint16_t* e
     void NAME::Encode(unsigned int segmentId, const char* dataVector, char** parityVectorList)   \
     {                                                                                            \
         if (!codec) return;                                                                      \
-        int rc = (KIND != NFEC_RS16 && segment_on_host)                                          \
+        int rc = segment_on_host                                                                 \
                      ? nfec_encode_segment_host(codec, segmentId, dataVector, (void* const*)parityVectorList) \
                      : nfec_encode_segment(codec, segmentId, dataVector, (void* const*)parityVectorList); \
         if (rc != NFEC_OK) std::fprintf(stderr, "nfec: Encode failed: %s\n", nfec_last_error()); \

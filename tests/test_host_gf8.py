@@ -109,12 +109,66 @@ def test_encode_segment_host_mdp_lfsr(orc, k, m, vec):
 
 
 @pytest.mark.gpu
-def test_encode_segment_host_not_rs16():
+@pytest.mark.parametrize("k,m,vec", [(400, 100, 1400), (300, 20, 1401), (10, 4, 64)])
+def test_encode_segment_host_rs16(orc, k, m, vec):
+    """RS16 on the host: vec // 2 native-endian symbols per segment, an odd last byte untouched,
+    block parity equal to the oracle's and to the GPU per-call path"""
     import norm_amd as na
 
     enc = na.NormEncoderRS16()
-    assert enc.Init(10, 4, 64)
-    par = [np.zeros(64, np.uint8) for _ in range(4)]
-    arr = (ctypes.c_void_p * 4)(*[p.ctypes.data for p in par])
-    d = np.zeros(64, np.uint8)
-    assert N.lib().nfec_encode_segment_host(enc._h, 0, d.ctypes.data, arr) == N.NFEC_ENOTSUP
+    assert enc.Init(k, m, vec)
+    host = orc.make_blocks(k, m, vec, 1)
+    ref = orc.encode_blocks(N.NFEC_RS16, k, m, vec, host.copy())
+    for fn in ("nfec_encode_segment_host", "nfec_encode_segment"):
+        par = [np.zeros(vec, np.uint8) for _ in range(m)]
+        arr = (ctypes.c_void_p * m)(*[p.ctypes.data for p in par])
+        for s in range(k):
+            d = np.ascontiguousarray(host[0, s, :vec])
+            assert getattr(N.lib(), fn)(enc._h, s, d.ctypes.data, arr) == 0
+        for p in range(m):
+            assert np.array_equal(par[p], ref[0, k + p, :vec]), (fn, p)
+
+
+# ---- GF(2^16): the RS16 per-segment Encode's product (normEncoderRS16.cpp:472-482) ----
+
+def _gf16_ref(orc, c, x):
+    ex, lg, _ = orc.gf16_tables()
+    x = x.astype(np.int64)
+    out = np.zeros(x.shape, np.uint16)
+    nz = x != 0
+    if c:
+        out[nz] = ex[(int(lg[c]) + lg[x[nz]]) % 65535]
+    return out
+
+
+@pytest.mark.parametrize("form", [N.NFEC_HOST_GF_SCALAR, N.NFEC_HOST_GF_GFNI])
+@pytest.mark.parametrize("n", [0, 1, 15, 16, 17, 700, 701])
+def test_gf16_addmul_matches_oracle(orc, form, n):
+    if form > _best():
+        pytest.skip("this CPU lacks the instructions of that form")
+    rng = np.random.default_rng(n + 7 * form)
+    for c in [0, 1, 2, 0x8000, 0xFFFF] + [int(v) for v in rng.integers(1, 65536, 12)]:
+        buf = rng.integers(0, 65536, n + 3, dtype=np.uint16)
+        src = buf[1:1 + n]                                   # 2-byte aligned, not 32
+        dst_buf = rng.integers(0, 65536, n + 3, dtype=np.uint16)
+        before = dst_buf.copy()
+        rc = N.lib().nfec_gf16_addmul_host(dst_buf[1:].ctypes.data, src.ctypes.data, c, n, form)
+        assert rc == form
+        want = before.copy()
+        want[1:1 + n] ^= _gf16_ref(orc, c, src)
+        assert np.array_equal(dst_buf, want), c
+
+
+def test_gf16_addmul_odd_byte_alignment(orc):
+    """symbols starting at an odd byte address (a pointer the engine may be handed)"""
+    rng = np.random.default_rng(5)
+    raw = rng.integers(0, 256, 2 * 100 + 3, dtype=np.uint8)
+    draw = rng.integers(0, 256, 2 * 100 + 3, dtype=np.uint8)
+    src = raw[1:201]
+    dst = draw[1:201]
+    before = draw.copy()
+    c = 0x1234
+    N.lib().nfec_gf16_addmul_host(dst.ctypes.data, src.ctypes.data, c, 100, -1)
+    want = before.copy()
+    want[1:201] = (before[1:201].view(np.uint16) ^ _gf16_ref(orc, c, src.view(np.uint16))).view(np.uint8)
+    assert np.array_equal(draw, want)
