@@ -67,10 +67,10 @@ int main(int argc, char** argv)
     double t0 = now_us();
     for (unsigned i = 0; i < iters; ++i) enc->Encode(i % k, list[i % k], list.data() + k);
     const double enc_us = (now_us() - t0) / iters;
-    // RS8 and MDP Encode run on the host CPU by default (nfec_encode_segment_host); the GPU round
-    // trip (nfec_encode_segment) beside it
+    // Encode runs on the host CPU by default (nfec_encode_segment_host); the GPU round trip
+    // (nfec_encode_segment) beside it
     double enc_gpu_us = -1;
-    if (!rs16) {
+    {
         NfecCodecBase::SetSegmentEncodeOnHost(false);
         for (unsigned i = 0; i < 8; ++i) enc->Encode(i % k, list[i % k], list.data() + k);
         t0 = now_us();
@@ -137,7 +137,7 @@ int main(int argc, char** argv)
                 "\"decode_us_per_call\": %.2f, \"decode_status\": %d, \"bad\": %d, "
                 "\"oracle_encode_us_per_call\": %.2f, \"oracle_decode_us_per_call\": %.2f}\n",
                 kind, k, m, vec, ne, iters, enc_us, enc_gpu_us,
-                !rs16 ? "host (nfec_encode_segment_host)" : "gpu (nfec_encode_segment)", dec_us, st, bad,
+                "host (nfec_encode_segment_host)", dec_us, st, bad,
                 orc_enc_us, orc_dec_us);
     delete enc;
     delete dec;
