@@ -258,6 +258,19 @@ int nfec_gf16_addmul_host(void* dst, const void* src, uint16_t c, size_t symbols
 int nfec_encode_segment_host(nfec_codec* codec, uint32_t segment_id, const void* data,
                              void* const* parity_vectors);
 
+/* NormDecoderRS8::Decode / NormDecoderRS16::Decode (normEncoderRS8.cpp:652-757, RS16 :650-755)
+ * on the host CPU, same contract as nfec_decode_vectors: the block's closed-form repair map
+ * (the first surviving parities substitute for the erased source, rs8_plan_rt_kernel's algebra)
+ * applied with the GFNI / AVX2 region products, XORed into the erased source buffers.  Returns
+ * erasure_count, 0 when undecodable or the list is not sorted / in range (block untouched),
+ * NFEC_ENOTSUP for MDP and for RS16 codes past the closed form (min(k, m) > 64).  A one-block
+ * repair is tens of microseconds of CPU work, below the GPU round trip for RS8. */
+int nfec_decode_vectors_host(nfec_codec* codec, void* const* vectors, uint32_t num_data,
+                             uint32_t erasure_count, const uint32_t* erasure_locs);
+/* 1 when nfec_decode_vectors_host is the faster path for this call (RS8; RS16 while
+ * erasures x numData x symbols stays below 4 Mi), else 0 (the drop-in Decode's choice). */
+int nfec_decode_host_preferred(const nfec_codec* codec, uint32_t num_data, uint32_t erasure_count);
+
 /* sizeof() of the drop-in class NormEncoder<kind> (decoder = 0) or NormDecoder<kind>
  * (decoder = 1) as the library was compiled (include/norm_fec/normEncoder*.h), 0 for an
  * unknown kind: a NORM build can check that its translation units see the same layout. */

@@ -16,11 +16,16 @@ class NfecCodecBase
     // GPU used by codecs created afterwards in this process (one process per GPU)
     static void SetDevice(int device) { default_device = device; }
     static int GetDevice() { return default_device; }
-    // Where RS8 Encode runs, the incremental sender's per-segment call (normObject.cpp:2038-2052):
-    // on the host CPU (default; nfec_encode_segment_host, a few us per 1.4 KB segment) or as a
-    // GPU round trip (nfec_encode_segment, ~80 us).  Decode and the batch calls use the GPU.
+    // Where Encode runs, the incremental sender's per-segment call (normObject.cpp:2038-2052):
+    // on the host CPU (default; nfec_encode_segment_host, about a microsecond per 1.4 KB
+    // segment) or as a GPU round trip (nfec_encode_segment, ~20-160 us).
     static void SetSegmentEncodeOnHost(bool on) { segment_on_host = on; }
     static bool GetSegmentEncodeOnHost() { return segment_on_host; }
+    // Where a one-block Decode runs (NormSenderNode::Decode, normNode.h:484-487): on the host
+    // CPU when nfec_decode_host_preferred says it is faster (default: RS8, small RS16), else on
+    // the GPU (nfec_decode_vectors).  The batch calls always use the GPU.
+    static void SetDecodeOnHost(bool on) { decode_on_host = on; }
+    static bool GetDecodeOnHost() { return decode_on_host; }
     nfec_codec* Handle() const { return codec; }
     // Batched device-resident calls (see nfec_encode / nfec_decode): the throughput path for
     // block-at-once call sites such as NormObject::CalculateBlockParity (normObject.cpp:2203-2229).
@@ -39,6 +44,7 @@ class NfecCodecBase
     unsigned int vector_size;  // Size of biggest vector to encode
     static int default_device;
     static bool segment_on_host;
+    static bool decode_on_host;
 };
 
 #endif  // NFEC_CODEC_BASE_H

@@ -12,7 +12,9 @@ normEncoderMDP.h) so parity tests read like the reference's own fecTest
 
 On top of the per-call surface, `encode_blocks` / `decode_blocks` take a batch of blocks
 resident in HBM (a torch uint8 CUDA tensor shaped [nblocks, k+m, seg_stride]) -- the
-performance path.  Everything runs through libnfec.so; nothing here computes on the CPU.
+performance path.  Everything runs through libnfec.so; nothing here computes.  (One-block
+Decode follows the drop-in's choice of the library's host CPU path for RS8 and small RS16,
+nfec_decode_vectors_host; Encode here is the GPU round trip, nfec_encode_segment.)
 """
 import ctypes
 
@@ -232,7 +234,10 @@ class _Encoder(_Codec):
 
 
 class _Decoder(_Codec):
-    def Decode(self, vectorList, numData, erasureCount, erasureLocs):
+    def Decode(self, vectorList, numData, erasureCount, erasureLocs, host=None):
+        """NormDecoder::Decode on one block.  host: None -- the drop-in's choice
+        (nfec_decode_host_preferred: the host CPU for RS8 and small RS16, else the GPU);
+        True / False -- force nfec_decode_vectors_host / nfec_decode_vectors."""
         self._need()
         n = numData + self.npar
         arr = (ctypes.c_void_p * n)()
@@ -242,6 +247,11 @@ class _Decoder(_Codec):
             arr[i] = a
             keeps.append(k)
         locs = (ctypes.c_uint32 * max(1, erasureCount))(*list(erasureLocs)[:erasureCount])
+        if host is None:
+            host = N.lib().nfec_decode_host_preferred(self._h, numData, erasureCount) == 1
+        if host:
+            return N.check(N.lib().nfec_decode_vectors_host(self._h, arr, numData, erasureCount, locs),
+                           "nfec_decode_vectors_host")
         rc = N.lib().nfec_decode_vectors(self._h, arr, numData, erasureCount, locs)
         return N.check(rc, "nfec_decode_vectors")
 

@@ -211,6 +211,7 @@ struct nfec_codec {
     DevBuf<uint16_t> d_log;      // field log table (q+1)
     DevBuf<uint8_t> d_mdp_step;  // MDP single LFSR step matrix, column-major [m+1][cs]
     DevBuf<uint16_t> d_lwp, d_lw;  // RS8 closed-form plan constants: log W'(x_j), log W(y_p)
+    std::vector<uint16_t> h_lwp, h_lw;  // the same on the host (nfec_decode_vectors_host)
     // RS8 / MDP products with runtime coefficients (gen_rs8_rt.hip): the generator as snippet
     // offsets [k][m] (RS8), or one [k][m] table per block length nd = 1..k (MDP, shortened)
     DevBuf<uint16_t> d_rt;
@@ -494,6 +495,8 @@ int build_codec(nfec_codec* c)
                 for (uint32_t l = 0; l < c->k; ++l) acc += f.log[pt[c->k + p] ^ pt[l]];
                 lw[p] = (uint16_t)(acc % f.q);
             }
+            c->h_lwp = lwp;
+            c->h_lw = lw;
             if ((rc = c->d_lwp.reserve(c->k))) return rc;
             if ((rc = c->d_lw.reserve(c->m))) return rc;
             NFEC_HIP(hipMemcpy(c->d_lwp.p, lwp.data(), lwp.size() * 2, hipMemcpyHostToDevice));
@@ -1859,6 +1862,101 @@ int nfec_encode_segment_host(nfec_codec* c, uint32_t segment_id, const void* dat
     for (uint32_t i = 0; i < c->m; ++i)
         host_gf8_addmul(static_cast<uint8_t*>(parity[i]), d, c->gen[(size_t)i * c->k + segment_id], c->vec, isa);
     return NFEC_OK;
+}
+
+int nfec_decode_vectors_host(nfec_codec* c, void* const* vectors, uint32_t num_data, uint32_t erasure_count,
+                             const uint32_t* erasure_locs)
+{
+    if (!c || !vectors || (erasure_count && !erasure_locs)) return fail(NFEC_EINVAL, "null argument");
+    c = primary(c);
+    if (c->kind == NFEC_MDP || c->h_lwp.empty()) return fail(NFEC_ENOTSUP, "host decode: RS8, or RS16 with min(k, m) <= 64");
+    if (num_data == 0 || num_data > c->k) return fail(NFEC_EINVAL, "numData out of range");
+    const uint32_t k = c->k, m = c->m, nd = num_data;
+    // the reference's undefined cases (more erasures than parity, unsorted or out-of-range lists)
+    // leave the block alone and return 0, as the GPU plans do
+    if (erasure_count > m) return 0;
+    uint32_t es = 0;
+    for (uint32_t i = 0; i < erasure_count; ++i) {
+        if (erasure_locs[i] >= nd + m || (i && erasure_locs[i] <= erasure_locs[i - 1])) return 0;
+        es += erasure_locs[i] < nd;
+    }
+    if (es == 0) return (int)erasure_count;  // only parity lost: nothing is filled (:732)
+    const bool wide = c->kind == NFEC_RS16;
+    const Field& f = wide ? gf16() : gf8();
+    const int64_t q = f.q;
+    auto md = [&](int64_t v) { v %= q; return v < 0 ? v + q : v; };
+    auto L = [&](uint32_t v) { return (int64_t)f.log[v]; };
+    // substitute parities: the first es surviving ones in slot order (normEncoderRS8.cpp:689-711)
+    std::vector<uint32_t> par;
+    {
+        uint32_t i = es;  // the parity entries of the sorted list follow the source ones
+        for (uint32_t p = 0; p < m && par.size() < es; ++p) {
+            if (i < erasure_count && erasure_locs[i] == nd + p) {
+                ++i;
+                continue;
+            }
+            par.push_back(p);
+        }
+        if (par.size() < es) return 0;  // not enough parity
+    }
+    std::vector<uint32_t> xs(es), yt(es);
+    std::vector<uint8_t> erased(nd, 0);
+    for (uint32_t s = 0; s < es; ++s) {
+        xs[s] = rs_point(f, erasure_locs[s]);
+        yt[s] = rs_point(f, k + par[s]);
+        erased[erasure_locs[s]] = 1;
+    }
+    // A^-1[s][t] = exp(lA[s] + lB[t] - log(x_s + y_t)); the map of a received source column j is
+    // exp(lA[s] + lC[j] - log(x_s + x_j)) (rs8_plan_rt_kernel's algebra, tests/test_rt_algebra.py)
+    std::vector<int64_t> lA(es), lB(es);
+    for (uint32_t s = 0; s < es; ++s) {
+        int64_t a = c->h_lwp[erasure_locs[s]], b = -(int64_t)c->h_lw[par[s]];
+        for (uint32_t t = 0; t < es; ++t) {
+            a += L(xs[s] ^ yt[t]);
+            b += L(yt[s] ^ xs[t]);
+            if (t != s) a -= L(xs[s] ^ xs[t]), b -= L(yt[s] ^ yt[t]);
+        }
+        lA[s] = md(a);
+        lB[s] = md(b);
+    }
+    const int isa = host_gf8_isa();
+    const size_t nsym = wide ? c->vec / 2 : c->vec;  // RS16: an odd last byte is never touched
+    auto addmul = [&](void* dst, const void* src, uint32_t coef) {
+        if (wide)
+            host_gf16_addmul(static_cast<uint16_t*>(dst), static_cast<const uint16_t*>(src), coef, nsym, isa);
+        else
+            host_gf8_addmul(static_cast<uint8_t*>(dst), static_cast<const uint8_t*>(src), coef, nsym, isa);
+    };
+    for (uint32_t j = 0; j < nd; ++j) {
+        if (erased[j] || !vectors[j]) continue;
+        const uint32_t xj = rs_point(f, j);
+        int64_t lc = -(int64_t)c->h_lwp[j];
+        for (uint32_t t = 0; t < es; ++t) lc += L(xj ^ xs[t]) - L(xj ^ yt[t]);
+        lc = md(lc);
+        for (uint32_t s = 0; s < es; ++s)
+            if (vectors[erasure_locs[s]])
+                addmul(vectors[erasure_locs[s]], vectors[j], f.exp[md(lA[s] + lc - L(xs[s] ^ xj))]);
+    }
+    for (uint32_t t = 0; t < es; ++t) {
+        const void* pv = vectors[nd + par[t]];
+        if (!pv) continue;  // a NULL parity reads as zeros, as in the GPU path
+        for (uint32_t s = 0; s < es; ++s)
+            if (vectors[erasure_locs[s]])
+                addmul(vectors[erasure_locs[s]], pv, f.exp[md(lA[s] + lB[t] - L(xs[s] ^ yt[t]))]);
+    }
+    return (int)erasure_count;
+}
+
+int nfec_decode_host_preferred(const nfec_codec* c, uint32_t num_data, uint32_t erasure_count)
+{
+    if (!c) return 0;
+    c = primary(c);
+    if (c->kind == NFEC_MDP || c->h_lwp.empty()) return 0;
+    if (c->kind == NFEC_RS8) return 1;
+    // RS16: the host's GF(2^16) products (~8 G per second with GFNI) win below a few million
+    // (e x numData x symbols); the GPU round trip (~0.1-0.9 ms) above
+    const uint64_t work = (uint64_t)std::min(erasure_count, c->m) * num_data * (c->vec / 2);
+    return work <= (4ull << 20) ? 1 : 0;
 }
 
 int nfec_decode_vectors(nfec_codec* c, void* const* vectors, uint32_t num_data, uint32_t erasure_count,

@@ -14,6 +14,7 @@ NormDecoder::~NormDecoder() {}
 
 int NfecCodecBase::default_device = 0;
 bool NfecCodecBase::segment_on_host = true;
+bool NfecCodecBase::decode_on_host = true;
 
 bool NfecCodecBase::InitCodec(int kind, unsigned int numData, unsigned int numParity, UINT16 vectorSize)
 {
@@ -81,8 +82,11 @@ int NfecCodecBase::DecodeBlocks(const nfec_block_batch* batch, const uint16_t* e
                      unsigned int* erasureLocs)                                                  \
     {                                                                                            \
         if (!codec) return 0;                                                                    \
-        int rc = nfec_decode_vectors(codec, (void* const*)vectorList, numData, erasureCount,     \
-                                     (const uint32_t*)erasureLocs);                              \
+        int rc = (decode_on_host && nfec_decode_host_preferred(codec, numData, erasureCount))    \
+                     ? nfec_decode_vectors_host(codec, (void* const*)vectorList, numData, erasureCount, \
+                                                (const uint32_t*)erasureLocs)                    \
+                     : nfec_decode_vectors(codec, (void* const*)vectorList, numData, erasureCount, \
+                                           (const uint32_t*)erasureLocs);                        \
         if (rc < 0) {                                                                            \
             std::fprintf(stderr, "nfec: Decode failed: %s\n", nfec_last_error());                \
             return 0;                                                                            \
