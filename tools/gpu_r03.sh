@@ -30,7 +30,8 @@ for step in $STEPS; do
       find gpurun_out/prof_$TAG -name '*kernel_stats.csv' | head -1 | xargs -r head -8 ;;
     percall)
       : > gpurun_out/percall_$TAG.jsonl
-      for shape in "rs8 64 16 1408 16 2000" "rs8 64 32 1408 16 2000" "mdp 64 32 1408 16 500" "rs16 400 100 1408 50 100"; do
+      for shape in "rs8 64 32 1408 16 2000" "rs8 64 16 1408 8 2000" "rs8 16 4 1408 4 2000" \
+                   "rs16 400 100 1400 50 200" "rs16 400 20 1400 10 500" "mdp 64 32 1408 16 500"; do
         timeout -k 10 120 tools/percall/_build/percall $shape >> gpurun_out/percall_$TAG.jsonl \
             2>> gpurun_out/percall_$TAG.err || { echo "percall $shape failed"; tail -5 gpurun_out/percall_$TAG.err; exit 7; }
       done
