@@ -27,7 +27,7 @@ def _case(orc, kind, k, m, vec, nd, es, ep, rng, junk=False):
 
 
 def _decode(dec, rx, nd, locs, host, null_parity):
-    vl = [np.ascontiguousarray(rx[s]) for s in range(rx.shape[0])]
+    vl = [rx[s].copy() for s in range(rx.shape[0])]
     if null_parity:
         for s in locs:
             if s >= nd:
@@ -112,7 +112,7 @@ def test_host_decode_undecodable_and_invalid(orc):
     clean, rx, _ = _case(orc, NFEC_RS8, k, m, vec, k, 0, 0, rng)
     for locs in ([0, 1, 2, 3, 21], [3, 1], [0, 25], [5, 5], [0, 1, 2, 3, 4]):
         for host in (True, False):
-            vl = [np.ascontiguousarray(rx[s]) for s in range(k + m)]
+            vl = [rx[s].copy() for s in range(k + m)]
             st = dec.Decode(vl, k, len(locs), locs, host=host)
             assert st == 0, (locs, host)
             for s in range(k + m):
