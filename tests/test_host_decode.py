@@ -74,7 +74,7 @@ def test_host_decode_matches_oracle_and_gpu(orc, kind, k, m, vec, nd, es, ep, ju
 def _oracle_one(orc, kind, k, m, vec, rx, nd, locs):
     ref = rx[None].copy()
     if nd < k:
-        ref = np.concatenate([ref, np.zeros((1, k - nd, vec), np.uint8)], 1)
+        ref = np.concatenate([ref, np.zeros((1, k - nd, ref.shape[2]), np.uint8)], 1)
     nloc = np.zeros((1, m), np.uint16)
     nloc[0, :len(locs)] = locs
     st = orc.decode_blocks(kind, k, m, vec, ref, nloc, np.array([len(locs)], np.uint16),
