@@ -259,16 +259,20 @@ int nfec_encode_segment_host(nfec_codec* codec, uint32_t segment_id, const void*
                              void* const* parity_vectors);
 
 /* NormDecoderRS8::Decode / NormDecoderRS16::Decode (normEncoderRS8.cpp:652-757, RS16 :650-755)
- * on the host CPU, same contract as nfec_decode_vectors: the block's closed-form repair map
- * (the first surviving parities substitute for the erased source, rs8_plan_rt_kernel's algebra)
- * applied with the GFNI / AVX2 region products, XORed into the erased source buffers.  Returns
+ * and NormDecoderMDP::Decode (normEncoderMDP.cpp:300-420) on the host CPU, same contract as
+ * nfec_decode_vectors.  RS: the block's closed-form repair map (the first surviving parities
+ * substitute for the erased source, rs8_plan_rt_kernel's algebra) applied with the GFNI / AVX2
+ * region products, XORed into the erased source buffers.  MDP: the closed-form Forney map
+ * (mdp_plan_kernel's) over the surviving slots, written over the erased source.  Returns
  * erasure_count, 0 when undecodable or the list is not sorted / in range (block untouched),
- * NFEC_ENOTSUP for MDP and for RS16 codes past the closed form (min(k, m) > 64).  A one-block
- * repair is tens of microseconds of CPU work, below the GPU round trip for RS8. */
+ * NFEC_ENOTSUP for RS16 codes past the closed form (min(k, m) > 64).  A one-block repair of a
+ * NORM-sized block is tens of microseconds of CPU work, below the GPU round trip. */
 int nfec_decode_vectors_host(nfec_codec* codec, void* const* vectors, uint32_t num_data,
                              uint32_t erasure_count, const uint32_t* erasure_locs);
-/* 1 when nfec_decode_vectors_host is the faster path for this call (RS8; RS16 while
- * erasures x numData x symbols stays below 4 Mi), else 0 (the drop-in Decode's choice). */
+/* 1 when nfec_decode_vectors_host is the faster path for this call, else 0 (the drop-in
+ * Decode's choice): RS8 while erasures x numData x vector bytes stays within 16 MiB, MDP while
+ * erasures x (numData + numParity) x vector bytes does, RS16 while erasures x numData x symbols
+ * stays within 4 Mi. */
 int nfec_decode_host_preferred(const nfec_codec* codec, uint32_t num_data, uint32_t erasure_count);
 
 /* sizeof() of the drop-in class NormEncoder<kind> (decoder = 0) or NormDecoder<kind>

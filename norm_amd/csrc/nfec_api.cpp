@@ -1864,12 +1864,64 @@ int nfec_encode_segment_host(nfec_codec* c, uint32_t segment_id, const void* dat
     return NFEC_OK;
 }
 
+// MDP one-block repair on the host: the closed-form Forney map of mdp_plan_kernel
+// (kernels_plan.hip; tests/test_mdp_algebra.py), C[r][v] = [Dinv_r beta_r^m] [gamma_v^(m+1)
+// Lambda(1 / gamma_v)] / (gamma_v beta_r + 1) over the surviving slots v, written over the erased
+// source (the reference's syndrome decode, normEncoderMDP.cpp:300-420, reads erased source as
+// zeros and missing parity as absent).  The list is already validated and es > 0.
+static void mdp_decode_host(const nfec_codec* c, void* const* vectors, uint32_t nd, uint32_t ec,
+                            const uint32_t* locs, uint32_t es)
+{
+    const Field& f = gf8();
+    const uint32_t m = c->m, nvecs = nd + m, deg = 2 * m;
+    auto mul = [&](uint32_t x, uint32_t y) -> uint32_t { return (x && y) ? f.exp[f.log[x] + f.log[y]] : 0u; };
+    // erasure locator lambda(x) = prod_i (1 + X_i x), X_i = alpha^(nvecs-1-loc_i)
+    std::vector<uint32_t> lam(deg, 0);
+    lam[0] = 1;
+    for (uint32_t i = 0; i < ec; ++i) {
+        const uint32_t X = f.exp[nvecs - 1 - locs[i]];
+        for (uint32_t j = deg - 1; j > 0; --j) lam[j] ^= mul(X, lam[j - 1]);
+    }
+    // row factors log(Dinv_r beta_r^m), log beta_r
+    std::vector<uint32_t> lrow(es), lbeta(es);
+    for (uint32_t r = 0; r < es; ++r) {
+        const uint32_t lb = (255u - (nvecs - 1 - locs[r])) % 255u;
+        uint32_t denom = 0;
+        for (uint32_t j = 1; j < deg; j += 2)
+            if (lam[j]) denom ^= f.exp[(f.log[lam[j]] + (uint64_t)lb * (j - 1)) % 255u];
+        const uint32_t ldinv = denom ? (255u - f.log[denom]) % 255u : 0u;  // GINV[0] = 1 (galois.cpp:39)
+        lbeta[r] = lb;
+        lrow[r] = (ldinv + (m % 255u) * lb) % 255u;
+    }
+    std::vector<uint8_t> erased(nvecs, 0);
+    for (uint32_t i = 0; i < ec; ++i) erased[locs[i]] = 1;
+    const int isa = host_gf8_isa();
+    for (uint32_t r = 0; r < es; ++r)
+        if (vectors[locs[r]]) std::memset(vectors[locs[r]], 0, c->vec);
+    for (uint32_t v = 0; v < nvecs; ++v) {
+        if (erased[v] || !vectors[v]) continue;  // a NULL survivor reads as zeros, as on the GPU
+        const uint32_t lgam = (nvecs - 1 - v) % 255u, step = (255u - lgam) % 255u;
+        uint32_t acc = 0;
+        for (uint32_t i = 0, pi = 0; i <= ec; ++i, pi = (pi + step) % 255u)
+            if (lam[i]) acc ^= f.exp[f.log[lam[i]] + pi];
+        const uint32_t lcol = ((m + 1u) % 255u * lgam + f.log[acc]) % 255u;  // acc != 0: v survived
+        for (uint32_t r = 0; r < es; ++r) {
+            if (!vectors[locs[r]]) continue;
+            const uint32_t w1 = f.exp[lgam + lbeta[r]] ^ 1u;  // gamma_v beta_r + 1, nonzero
+            const uint32_t l = (lrow[r] + lcol + 255u - f.log[w1]) % 255u;
+            host_gf8_addmul(static_cast<uint8_t*>(vectors[locs[r]]), static_cast<const uint8_t*>(vectors[v]),
+                            f.exp[l], c->vec, isa);
+        }
+    }
+}
+
 int nfec_decode_vectors_host(nfec_codec* c, void* const* vectors, uint32_t num_data, uint32_t erasure_count,
                              const uint32_t* erasure_locs)
 {
     if (!c || !vectors || (erasure_count && !erasure_locs)) return fail(NFEC_EINVAL, "null argument");
     c = primary(c);
-    if (c->kind == NFEC_MDP || c->h_lwp.empty()) return fail(NFEC_ENOTSUP, "host decode: RS8, or RS16 with min(k, m) <= 64");
+    if (c->kind != NFEC_MDP && c->h_lwp.empty())
+        return fail(NFEC_ENOTSUP, "host decode: RS8, MDP, or RS16 with min(k, m) <= 64");
     if (num_data == 0 || num_data > c->k) return fail(NFEC_EINVAL, "numData out of range");
     const uint32_t k = c->k, m = c->m, nd = num_data;
     // the reference's undefined cases (more erasures than parity, unsorted or out-of-range lists)
@@ -1881,6 +1933,10 @@ int nfec_decode_vectors_host(nfec_codec* c, void* const* vectors, uint32_t num_d
         es += erasure_locs[i] < nd;
     }
     if (es == 0) return (int)erasure_count;  // only parity lost: nothing is filled (:732)
+    if (c->kind == NFEC_MDP) {
+        mdp_decode_host(c, vectors, nd, erasure_count, erasure_locs, es);
+        return (int)erasure_count;
+    }
     const bool wide = c->kind == NFEC_RS16;
     const Field& f = wide ? gf16() : gf8();
     const int64_t q = f.q;
@@ -1947,16 +2003,21 @@ int nfec_decode_vectors_host(nfec_codec* c, void* const* vectors, uint32_t num_d
     return (int)erasure_count;
 }
 
+// RS8 / MDP repair products (bytes) up to which one-block Decode stays on the host
+static constexpr uint64_t kHostDecodeBytes = 16ull << 20;
+
 int nfec_decode_host_preferred(const nfec_codec* c, uint32_t num_data, uint32_t erasure_count)
 {
     if (!c) return 0;
     c = primary(c);
-    if (c->kind == NFEC_MDP || c->h_lwp.empty()) return 0;
-    if (c->kind == NFEC_RS8) return 1;
-    // RS16: the host's GF(2^16) products (~8 G per second with GFNI) win below a few million
-    // (e x numData x symbols); the GPU round trip (~0.1-0.9 ms) above
-    const uint64_t work = (uint64_t)std::min(erasure_count, c->m) * num_data * (c->vec / 2);
-    return work <= (4ull << 20) ? 1 : 0;
+    const uint64_t e = std::min(erasure_count, c->m);
+    // products of the repair (erased rows x columns read x symbols): the host's region products
+    // (GF(2^8) ~50 GB/s, GF(2^16) ~8 G symbols/s with GFNI) win below a few million, the GPU
+    // round trip (~0.1-0.9 ms, tools/percall) above
+    if (c->kind == NFEC_MDP) return e * (num_data + c->m) * c->vec <= kHostDecodeBytes ? 1 : 0;
+    if (c->h_lwp.empty()) return 0;
+    if (c->kind == NFEC_RS8) return e * num_data * c->vec <= kHostDecodeBytes ? 1 : 0;
+    return e * num_data * (c->vec / 2) <= (4ull << 20) ? 1 : 0;
 }
 
 int nfec_decode_vectors(nfec_codec* c, void* const* vectors, uint32_t num_data, uint32_t erasure_count,

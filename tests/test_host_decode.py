@@ -10,7 +10,9 @@ import pytest
 
 pytestmark = pytest.mark.gpu
 
-from norm_amd import NFEC_RS8, NFEC_RS16, NormDecoderRS8, NormDecoderRS16  # noqa: E402
+from norm_amd import NFEC_MDP, NFEC_RS8, NFEC_RS16, NormDecoderMDP, NormDecoderRS8, NormDecoderRS16  # noqa: E402
+
+DECODER = {NFEC_RS8: NormDecoderRS8, NFEC_RS16: NormDecoderRS16, NFEC_MDP: NormDecoderMDP}
 
 
 def _case(orc, kind, k, m, vec, nd, es, ep, rng, junk=False):
@@ -48,6 +50,12 @@ CASES = [
     (NFEC_RS16, 400, 20, 1400, 400, 12, 3, False, True),
     (NFEC_RS16, 300, 40, 1401, 250, 30, 5, True, False),
     (NFEC_RS16, 10, 4, 64, 10, 4, 0, False, False),
+    # MDP: erased source arrives zero-filled (normObject.cpp:1579), missing parity NULL
+    (NFEC_MDP, 64, 32, 1408, 64, 16, 0, False, False),
+    (NFEC_MDP, 64, 32, 1400, 50, 10, 6, False, True),
+    (NFEC_MDP, 200, 55, 1401, 150, 30, 20, False, True),
+    (NFEC_MDP, 10, 7, 8, 4, 4, 3, False, False),
+    (NFEC_MDP, 1, 1, 64, 1, 1, 0, False, False),
 ]
 
 
@@ -56,7 +64,7 @@ def test_host_decode_matches_oracle_and_gpu(orc, kind, k, m, vec, nd, es, ep, ju
     rng = np.random.default_rng(k * 131 + m + nd)
     clean, rx, locs = _case(orc, kind, k, m, vec, nd, es, ep, rng, junk)
     st_ref, ref = _oracle_one(orc, kind, k, m, vec, rx, nd, locs)
-    dec = (NormDecoderRS8 if kind == NFEC_RS8 else NormDecoderRS16)()
+    dec = DECODER[kind]()
     assert dec.Init(k, m, vec)
     outs = {}
     for host in (True, False):
@@ -82,9 +90,10 @@ def _oracle_one(orc, kind, k, m, vec, rx, nd, locs):
     return int(st[0]), ref[0]
 
 
-def test_host_decode_random_rs8(orc):
-    """many random RS8 blocks: shapes, shortening, source and parity erasures"""
-    rng = np.random.default_rng(99)
+@pytest.mark.parametrize("kind", [NFEC_RS8, NFEC_MDP])
+def test_host_decode_random(orc, kind):
+    """many random RS8 / MDP blocks: shapes, shortening, source and parity erasures"""
+    rng = np.random.default_rng(99 + kind)
     for it in range(60):
         k = int(rng.integers(1, 120))
         m = int(rng.integers(1, min(100, 255 - k) + 1))
@@ -92,25 +101,27 @@ def test_host_decode_random_rs8(orc):
         nd = int(rng.integers(1, k + 1))
         es = int(rng.integers(0, min(nd, m) + 1))
         ep = int(rng.integers(0, m - es + 1))
-        clean, rx, locs = _case(orc, NFEC_RS8, k, m, vec, nd, es, ep, rng)
-        st_ref, ref = _oracle_one(orc, NFEC_RS8, k, m, vec, rx, nd, locs)
-        dec = NormDecoderRS8()
+        clean, rx, locs = _case(orc, kind, k, m, vec, nd, es, ep, rng)
+        st_ref, ref = _oracle_one(orc, kind, k, m, vec, rx, nd, locs)
+        dec = DECODER[kind]()
         assert dec.Init(k, m, vec)
-        st, vl = _decode(dec, rx, nd, locs, True, False)
+        st, vl = _decode(dec, rx, nd, locs, True, kind == NFEC_MDP)
         assert st == st_ref, (it, k, m, nd, locs)
         for s in range(nd):
             assert np.array_equal(vl[s], ref[s]), (it, s)
 
 
-def test_host_decode_undecodable_and_invalid(orc):
-    """more erasures than surviving parity, unsorted and out-of-range lists: status 0, block
-    untouched, as the GPU path and the reference's defined cases"""
+@pytest.mark.parametrize("kind", [NFEC_RS8, NFEC_MDP])
+def test_host_decode_undecodable_and_invalid(orc, kind):
+    """more erasures than (surviving) parity, unsorted and out-of-range lists: status 0, block
+    untouched, as the GPU path"""
     k, m, vec = 20, 4, 64
-    dec = NormDecoderRS8()
+    dec = DECODER[kind]()
     assert dec.Init(k, m, vec)
     rng = np.random.default_rng(3)
-    clean, rx, _ = _case(orc, NFEC_RS8, k, m, vec, k, 0, 0, rng)
-    for locs in ([0, 1, 2, 3, 21], [3, 1], [0, 25], [5, 5], [0, 1, 2, 3, 4]):
+    clean, rx, _ = _case(orc, kind, k, m, vec, k, 0, 0, rng)
+    bad_lists = [[3, 1], [0, 25], [5, 5], [0, 1, 2, 3, 4]] + ([[0, 1, 2, 3, 21]] if kind == NFEC_RS8 else [])
+    for locs in bad_lists:
         for host in (True, False):
             vl = [rx[s].copy() for s in range(k + m)]
             st = dec.Decode(vl, k, len(locs), locs, host=host)
@@ -120,13 +131,14 @@ def test_host_decode_undecodable_and_invalid(orc):
 
 
 def test_drop_in_policy():
-    """RS8 and small RS16 repairs on the host, big RS16 and MDP on the GPU"""
+    """NORM-sized repairs on the host, big ones on the GPU"""
     from norm_amd import _native as N
-    from norm_amd import NormDecoderMDP
 
     d8, d16, dm = NormDecoderRS8(), NormDecoderRS16(), NormDecoderMDP()
+    b8, bm = NormDecoderRS8(), NormDecoderMDP()
     assert d8.Init(64, 32, 1408) and d16.Init(400, 60, 1400) and dm.Init(64, 32, 1408)
-    assert N.lib().nfec_decode_host_preferred(d8._h, 64, 16) == 1
-    assert N.lib().nfec_decode_host_preferred(d16._h, 400, 10) == 1
-    assert N.lib().nfec_decode_host_preferred(d16._h, 400, 50) == 0
-    assert N.lib().nfec_decode_host_preferred(dm._h, 64, 16) == 0
+    assert b8.Init(128, 127, 8192) and bm.Init(128, 127, 8192)
+    pref = N.lib().nfec_decode_host_preferred
+    assert pref(d8._h, 64, 16) == 1 and pref(dm._h, 64, 16) == 1
+    assert pref(d16._h, 400, 10) == 1 and pref(d16._h, 400, 50) == 0
+    assert pref(b8._h, 128, 100) == 0 and pref(bm._h, 128, 100) == 0

@@ -6,13 +6,15 @@
 // Encode: the sender's per-segment call (normObject.cpp:2038-2052 -> NormEncoderRS8::Encode,
 // normEncoderRS8.cpp:473-483), cycling segmentId over 0..K-1 into zeroed parity.
 // Decode: one block, ERASURES source erasures (zero-filled, normObject.cpp:1579), through
-// NormDecoder::Decode (normEncoderRS8.cpp:652-757): the default path and the GPU round trip.  Prints one JSON line of microseconds per
+// NormDecoder::Decode (normEncoderRS8.cpp:652-757): the default path, the GPU round trip and
+// the host path.  Prints one JSON line of microseconds per
 // call.  Built against libnfec.so (the drop-in headers, as NORM includes them) and the oracle
 // library (test infrastructure; its timing is the CPU reference per call).
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <functional>
 #include <vector>
 
 #include "normEncoderMDP.h"
@@ -90,26 +92,32 @@ int main(int argc, char** argv)
     std::vector<std::vector<char>> keep(ne);
     for (unsigned i = 0; i < ne; ++i) keep[i] = seg[locs[i]];
     int bad = 0, st = 0;
-    auto time_decode = [&]() {
+    auto time_decode = [&](const std::function<int()>& call) {
         double us = 0;
         for (unsigned it = 0; it < iters + 2; ++it) {
             for (unsigned i = 0; i < ne; ++i) std::memset(list[locs[i]], 0, vec);
             const double t = now_us();
-            st = dec->Decode(list.data(), k, ne, locs.data());
+            st = call();
             if (it >= 2) us += now_us() - t;
             for (unsigned i = 0; i < ne; ++i)
                 bad += std::memcmp(list[locs[i]], keep[i].data(), rs16 ? vec & ~1u : vec) != 0;
         }
         return us / iters;
     };
-    // Decode's default path (the drop-in's policy, nfec_decode_host_preferred) and the GPU round
-    // trip (nfec_decode_vectors) beside it
+    auto drop_in = [&]() { return dec->Decode(list.data(), k, ne, locs.data()); };
+    // Decode's default path (the drop-in's policy, nfec_decode_host_preferred), the GPU round
+    // trip (nfec_decode_vectors) and the host path (nfec_decode_vectors_host) beside it
     NfecCodecBase* dbase = dynamic_cast<NfecCodecBase*>(dec);
     const bool dec_host = dbase && nfec_decode_host_preferred(dbase->Handle(), k, ne) == 1;
-    const double dec_us = time_decode();
+    const double dec_us = time_decode(drop_in);
     NfecCodecBase::SetDecodeOnHost(false);
-    const double dec_gpu_us = time_decode();
+    const double dec_gpu_us = time_decode(drop_in);
     NfecCodecBase::SetDecodeOnHost(true);
+    double dec_host_us = -1;
+    if (dbase && nfec_decode_vectors_host(dbase->Handle(), (void* const*)list.data(), k, ne, locs.data()) >= 0)
+        dec_host_us = time_decode([&]() {
+            return nfec_decode_vectors_host(dbase->Handle(), (void* const*)list.data(), k, ne, locs.data());
+        });
 
     // ---- the oracle (CPU restatement of the reference codec), same calls ----
     double orc_enc_us = -1, orc_dec_us = -1;
@@ -145,11 +153,12 @@ int main(int argc, char** argv)
     }
     std::printf("{\"kind\": \"%s\", \"k\": %u, \"m\": %u, \"vec\": %u, \"erasures\": %u, \"iters\": %u, "
                 "\"encode_us_per_call\": %.2f, \"encode_gpu_us_per_call\": %.2f, \"encode_path\": \"%s\", "
-                "\"decode_us_per_call\": %.2f, \"decode_gpu_us_per_call\": %.2f, \"decode_path\": \"%s\", "
+                "\"decode_us_per_call\": %.2f, \"decode_gpu_us_per_call\": %.2f, \"decode_host_us_per_call\": %.2f, "
+                "\"decode_path\": \"%s\", "
                 "\"decode_status\": %d, \"bad\": %d, "
                 "\"oracle_encode_us_per_call\": %.2f, \"oracle_decode_us_per_call\": %.2f}\n",
                 kind, k, m, vec, ne, iters, enc_us, enc_gpu_us,
-                "host (nfec_encode_segment_host)", dec_us, dec_gpu_us,
+                "host (nfec_encode_segment_host)", dec_us, dec_gpu_us, dec_host_us,
                 dec_host ? "host (nfec_decode_vectors_host)" : "gpu (nfec_decode_vectors)", st, bad,
                 orc_enc_us, orc_dec_us);
     delete enc;
