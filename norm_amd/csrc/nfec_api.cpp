@@ -2003,21 +2003,24 @@ int nfec_decode_vectors_host(nfec_codec* c, void* const* vectors, uint32_t num_d
     return (int)erasure_count;
 }
 
-// RS8 / MDP repair products (bytes) up to which one-block Decode stays on the host
-static constexpr uint64_t kHostDecodeBytes = 16ull << 20;
+// Repair products up to which one-block Decode stays on the host: the crossovers of the host
+// path and the GPU round trip measured by tools/percall (profiles/r04/percall.jsonl): RS8 bytes
+// (host ~55-80 GB/s, GPU 0.65-0.77 ms at 128+127 slots), MDP bytes (~90-135 GB/s against
+// 0.86-0.99 ms), RS16 symbols (~8 G/s against 0.5-0.85 ms)
+static constexpr uint64_t kHostDecodeRs8Bytes = 48ull << 20;
+static constexpr uint64_t kHostDecodeMdpBytes = 96ull << 20;
+static constexpr uint64_t kHostDecodeRs16Symbols = 4ull << 20;
 
 int nfec_decode_host_preferred(const nfec_codec* c, uint32_t num_data, uint32_t erasure_count)
 {
     if (!c) return 0;
     c = primary(c);
     const uint64_t e = std::min(erasure_count, c->m);
-    // products of the repair (erased rows x columns read x symbols): the host's region products
-    // (GF(2^8) ~50 GB/s, GF(2^16) ~8 G symbols/s with GFNI) win below a few million, the GPU
-    // round trip (~0.1-0.9 ms, tools/percall) above
-    if (c->kind == NFEC_MDP) return e * (num_data + c->m) * c->vec <= kHostDecodeBytes ? 1 : 0;
+    // products of the repair: erased rows x columns read x symbols
+    if (c->kind == NFEC_MDP) return e * (num_data + c->m) * c->vec <= kHostDecodeMdpBytes ? 1 : 0;
     if (c->h_lwp.empty()) return 0;
-    if (c->kind == NFEC_RS8) return e * num_data * c->vec <= kHostDecodeBytes ? 1 : 0;
-    return e * num_data * (c->vec / 2) <= (4ull << 20) ? 1 : 0;
+    if (c->kind == NFEC_RS8) return e * num_data * c->vec <= kHostDecodeRs8Bytes ? 1 : 0;
+    return e * num_data * (c->vec / 2) <= kHostDecodeRs16Symbols ? 1 : 0;
 }
 
 int nfec_decode_vectors(nfec_codec* c, void* const* vectors, uint32_t num_data, uint32_t erasure_count,
