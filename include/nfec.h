@@ -259,7 +259,7 @@ int nfec_encode_segment_host(nfec_codec* codec, uint32_t segment_id, const void*
                              void* const* parity_vectors);
 
 /* NormDecoderRS8::Decode / NormDecoderRS16::Decode (normEncoderRS8.cpp:652-757, RS16 :650-755)
- * and NormDecoderMDP::Decode (normEncoderMDP.cpp:300-420) on the host CPU, same contract as
+ * and NormDecoderMDP::Decode (normEncoderMDP.cpp:333-430) on the host CPU, same contract as
  * nfec_decode_vectors.  RS: the block's closed-form repair map (the first surviving parities
  * substitute for the erased source, rs8_plan_rt_kernel's algebra) applied with the GFNI / AVX2
  * region products, XORed into the erased source buffers.  MDP: the closed-form Forney map

@@ -1867,7 +1867,7 @@ int nfec_encode_segment_host(nfec_codec* c, uint32_t segment_id, const void* dat
 // MDP one-block repair on the host: the closed-form Forney map of mdp_plan_kernel
 // (kernels_plan.hip; tests/test_mdp_algebra.py), C[r][v] = [Dinv_r beta_r^m] [gamma_v^(m+1)
 // Lambda(1 / gamma_v)] / (gamma_v beta_r + 1) over the surviving slots v, written over the erased
-// source (the reference's syndrome decode, normEncoderMDP.cpp:300-420, reads erased source as
+// source (the reference's syndrome decode, normEncoderMDP.cpp:333-430, reads erased source as
 // zeros and missing parity as absent).  The list is already validated and es > 0.
 static void mdp_decode_host(const nfec_codec* c, void* const* vectors, uint32_t nd, uint32_t ec,
                             const uint32_t* locs, uint32_t es)
