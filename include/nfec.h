@@ -248,6 +248,12 @@ int nfec_gf8_addmul_host(void* dst, const void* src, uint8_t c, size_t bytes, in
 /* ... over `symbols` native-endian 16-bit symbols in the RS16 field (0x1100B); forms: GFNI or
  * scalar (an AVX2 request runs the scalar form, which is what it returns). */
 int nfec_gf16_addmul_host(void* dst, const void* src, uint16_t c, size_t symbols, int isa);
+/* Row dot product, the body of nfec_decode_vectors_host:
+ *   dst[0..n) = (accumulate ? dst : 0) + sum_j coef[j] * src[j][0..n)
+ * over n bytes (bits = 8, RS8 / MDP field) or n native-endian symbols (bits = 16, RS16 field),
+ * one pass over dst.  Returns the form used (as above), NFEC_EINVAL / NFEC_ENOTSUP otherwise. */
+int nfec_gf_dot_host(int bits, void* dst, const void* const* src, const uint16_t* coef, uint32_t ncols,
+                     size_t n, int accumulate, int isa);
 /* NormEncoderRS8::Encode (normEncoderRS8.cpp:473-483) on the host: parity_vectors[i] ^=
  * G[k+i][segment_id] * data over vector_size bytes.  RS16 (NormEncoderRS16::Encode,
  * normEncoderRS16.cpp:472-482): the same over vector_size / 2 native-endian symbols, an odd last

@@ -140,6 +140,7 @@ _SIGS = {
     "nfec_encode_segment_host": (_I, [_P, _U32, _P, _P]),
     "nfec_gf8_addmul_host": (_I, [_P, _P, _U8, ctypes.c_size_t, _I]),
     "nfec_gf16_addmul_host": (_I, [_P, _P, ctypes.c_uint16, ctypes.c_size_t, _I]),
+    "nfec_gf_dot_host": (_I, [_I, _P, _P, _P, ctypes.c_uint32, ctypes.c_size_t, _I, _I]),
     "nfec_decode_vectors_host": (_I, [_P, _P, _U32, _U32, _P]),
     "nfec_decode_host_preferred": (_I, [_P, _U32, _U32]),
     "nfec_decode_vectors": (_I, [_P, _P, _U32, _U32, _P]),

@@ -1864,6 +1864,52 @@ int nfec_encode_segment_host(nfec_codec* c, uint32_t segment_id, const void* dat
     return NFEC_OK;
 }
 
+namespace {
+unsigned host_copy_threads();
+}
+
+// The host repair's products: dst[r] (^)= sum_j coef[r][j] * srcs[j] over nelem bytes (GF(2^8))
+// or symbols (GF(2^16)), row dot products over pieces of the vectors, so a piece of every column
+// stays in cache while all rows take it; a repair of more than 8 MiB of products splits the
+// vectors over host threads (disjoint element ranges, no sharing).
+static void host_rows_apply(bool wide, void* const* dst, uint32_t nrows, const void* const* srcs, uint32_t ncol,
+                            const uint16_t* coef, size_t nelem, bool acc)
+{
+    const int isa = host_gf8_isa();
+    const uint64_t work = (uint64_t)nrows * ncol * nelem * (wide ? 2 : 1);
+    const size_t piece = wide ? 1024 : 2048;
+    auto run = [&](size_t e0, size_t e1) {
+        for (size_t c0 = e0; c0 < e1; c0 += piece) {
+            const size_t len = std::min(piece, e1 - c0);
+            for (uint32_t r = 0; r < nrows; ++r) {
+                if (!dst[r]) continue;
+                if (wide)
+                    host_gf16_dot(static_cast<uint16_t*>(dst[r]) + c0, reinterpret_cast<const uint16_t* const*>(srcs), c0,
+                                  coef + (size_t)r * ncol, ncol, len, acc, isa);
+                else
+                    host_gf8_dot(static_cast<uint8_t*>(dst[r]) + c0, reinterpret_cast<const uint8_t* const*>(srcs), c0,
+                                 coef + (size_t)r * ncol, ncol, len, acc, isa);
+            }
+        }
+    };
+    const unsigned nt = work > (8ull << 20)
+                            ? (unsigned)std::min<uint64_t>(std::min<uint64_t>(host_copy_threads(), work >> 22), nelem / 256)
+                            : 1u;
+    if (nt <= 1) {
+        run(0, nelem);
+        return;
+    }
+    // ranges in multiples of 128 elements
+    const size_t per = ((nelem + nt - 1) / nt + 127) & ~(size_t)127;
+    std::vector<std::thread> th;
+    for (unsigned t = 1; t < nt; ++t) {
+        const size_t e0 = std::min(nelem, t * per), e1 = std::min(nelem, e0 + per);
+        if (e0 < e1) th.emplace_back(run, e0, e1);
+    }
+    run(0, std::min(per, nelem));
+    for (auto& t : th) t.join();
+}
+
 // MDP one-block repair on the host: the closed-form Forney map of mdp_plan_kernel
 // (kernels_plan.hip; tests/test_mdp_algebra.py), C[r][v] = [Dinv_r beta_r^m] [gamma_v^(m+1)
 // Lambda(1 / gamma_v)] / (gamma_v beta_r + 1) over the surviving slots v, written over the erased
@@ -1895,24 +1941,29 @@ static void mdp_decode_host(const nfec_codec* c, void* const* vectors, uint32_t 
     }
     std::vector<uint8_t> erased(nvecs, 0);
     for (uint32_t i = 0; i < ec; ++i) erased[locs[i]] = 1;
-    const int isa = host_gf8_isa();
-    for (uint32_t r = 0; r < es; ++r)
-        if (vectors[locs[r]]) std::memset(vectors[locs[r]], 0, c->vec);
+    std::vector<const void*> srcs;
+    std::vector<uint32_t> lcols, lgams;
     for (uint32_t v = 0; v < nvecs; ++v) {
         if (erased[v] || !vectors[v]) continue;  // a NULL survivor reads as zeros, as on the GPU
         const uint32_t lgam = (nvecs - 1 - v) % 255u, step = (255u - lgam) % 255u;
         uint32_t acc = 0;
         for (uint32_t i = 0, pi = 0; i <= ec; ++i, pi = (pi + step) % 255u)
             if (lam[i]) acc ^= f.exp[f.log[lam[i]] + pi];
-        const uint32_t lcol = ((m + 1u) % 255u * lgam + f.log[acc]) % 255u;  // acc != 0: v survived
-        for (uint32_t r = 0; r < es; ++r) {
-            if (!vectors[locs[r]]) continue;
-            const uint32_t w1 = f.exp[lgam + lbeta[r]] ^ 1u;  // gamma_v beta_r + 1, nonzero
-            const uint32_t l = (lrow[r] + lcol + 255u - f.log[w1]) % 255u;
-            host_gf8_addmul(static_cast<uint8_t*>(vectors[locs[r]]), static_cast<const uint8_t*>(vectors[v]),
-                            f.exp[l], c->vec, isa);
+        srcs.push_back(vectors[v]);
+        lcols.push_back(((m + 1u) % 255u * lgam + f.log[acc]) % 255u);  // acc != 0: v survived
+        lgams.push_back(lgam);
+    }
+    const uint32_t ncol = (uint32_t)srcs.size();
+    std::vector<uint16_t> coef((size_t)es * ncol);
+    std::vector<void*> dst(es);
+    for (uint32_t r = 0; r < es; ++r) {
+        dst[r] = vectors[locs[r]];
+        for (uint32_t j = 0; j < ncol; ++j) {
+            const uint32_t w1 = f.exp[lgams[j] + lbeta[r]] ^ 1u;  // gamma_v beta_r + 1, nonzero
+            coef[(size_t)r * ncol + j] = (uint16_t)f.exp[(lrow[r] + lcols[j] + 255u - f.log[w1]) % 255u];
         }
     }
+    host_rows_apply(false, dst.data(), es, srcs.data(), ncol, coef.data(), c->vec, false);
 }
 
 int nfec_decode_vectors_host(nfec_codec* c, void* const* vectors, uint32_t num_data, uint32_t erasure_count,
@@ -1975,31 +2026,36 @@ int nfec_decode_vectors_host(nfec_codec* c, void* const* vectors, uint32_t num_d
         lA[s] = md(a);
         lB[s] = md(b);
     }
-    const int isa = host_gf8_isa();
-    const size_t nsym = wide ? c->vec / 2 : c->vec;  // RS16: an odd last byte is never touched
-    auto addmul = [&](void* dst, const void* src, uint32_t coef) {
-        if (wide)
-            host_gf16_addmul(static_cast<uint16_t*>(dst), static_cast<const uint16_t*>(src), coef, nsym, isa);
-        else
-            host_gf8_addmul(static_cast<uint8_t*>(dst), static_cast<const uint8_t*>(src), coef, nsym, isa);
-    };
+    // columns: the surviving (non-NULL) source, then the substitute parities (a NULL parity reads
+    // as zeros, as in the GPU path)
+    std::vector<const void*> srcs;
+    std::vector<int64_t> lcol;   // log factor per column
+    std::vector<uint32_t> pts;   // its point
     for (uint32_t j = 0; j < nd; ++j) {
         if (erased[j] || !vectors[j]) continue;
         const uint32_t xj = rs_point(f, j);
         int64_t lc = -(int64_t)c->h_lwp[j];
         for (uint32_t t = 0; t < es; ++t) lc += L(xj ^ xs[t]) - L(xj ^ yt[t]);
-        lc = md(lc);
-        for (uint32_t s = 0; s < es; ++s)
-            if (vectors[erasure_locs[s]])
-                addmul(vectors[erasure_locs[s]], vectors[j], f.exp[md(lA[s] + lc - L(xs[s] ^ xj))]);
+        srcs.push_back(vectors[j]);
+        lcol.push_back(md(lc));
+        pts.push_back(xj);
     }
     for (uint32_t t = 0; t < es; ++t) {
-        const void* pv = vectors[nd + par[t]];
-        if (!pv) continue;  // a NULL parity reads as zeros, as in the GPU path
-        for (uint32_t s = 0; s < es; ++s)
-            if (vectors[erasure_locs[s]])
-                addmul(vectors[erasure_locs[s]], pv, f.exp[md(lA[s] + lB[t] - L(xs[s] ^ yt[t]))]);
+        if (!vectors[nd + par[t]]) continue;
+        srcs.push_back(vectors[nd + par[t]]);
+        lcol.push_back(lB[t]);
+        pts.push_back(yt[t]);
     }
+    const uint32_t ncol = (uint32_t)srcs.size();
+    std::vector<uint16_t> coef((size_t)es * ncol);
+    std::vector<void*> dst(es);
+    for (uint32_t s = 0; s < es; ++s) {
+        dst[s] = vectors[erasure_locs[s]];
+        for (uint32_t j = 0; j < ncol; ++j)
+            coef[(size_t)s * ncol + j] = (uint16_t)f.exp[md(lA[s] + lcol[j] - L(xs[s] ^ pts[j]))];
+    }
+    // RS16: an odd last byte is never touched
+    host_rows_apply(wide, dst.data(), es, srcs.data(), ncol, coef.data(), wide ? c->vec / 2 : c->vec, true);
     return (int)erasure_count;
 }
 

@@ -77,6 +77,12 @@ void host_gf8_addmul(uint8_t* dst, const uint8_t* src, uint32_t c, size_t n, int
 // ... and over nsym 16-bit symbols in the RS16 field (GFNI or scalar)
 void host_gf16_addmul(uint16_t* dst, const uint16_t* src, uint32_t c, size_t nsym, int isa);
 int host_gf8_isa();
+// dst[0..n) = (acc ? dst : 0) + sum_j coef[j] * src[j][off + 0..n) (GF(2^8) bytes / GF(2^16)
+// symbols; off and n in elements); the host repair's row products
+void host_gf8_dot(uint8_t* dst, const uint8_t* const* src, size_t off, const uint16_t* coef, uint32_t nc, size_t n,
+                  bool acc, int isa);
+void host_gf16_dot(uint16_t* dst, const uint16_t* const* src, size_t off, const uint16_t* coef, uint32_t nc,
+                   size_t nsym, bool acc, int isa);
 
 // v_perm product tables for one GF(2^8) constant c: 8 dwords (32 bytes)
 //   t0 = c*{0,1,2,3}   t1 = c*{4,5,6,7}       (low 3 bits)

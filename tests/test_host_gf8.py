@@ -172,3 +172,81 @@ def test_gf16_addmul_odd_byte_alignment(orc):
     want = before.copy()
     want[1:201] = (before[1:201].view(np.uint16) ^ _gf16_ref(orc, c, src.view(np.uint16))).view(np.uint8)
     assert np.array_equal(draw, want)
+
+
+# ---- row dot products (nfec_gf_dot_host): the body of the host one-block repair ----
+
+def _dot(bits, dst, srcs, coef, n, acc, form):
+    arr = (ctypes.c_void_p * max(1, len(srcs)))(*[x.ctypes.data for x in srcs])
+    co = np.ascontiguousarray(coef, np.uint16)
+    return N.lib().nfec_gf_dot_host(bits, dst.ctypes.data, arr, co.ctypes.data, len(srcs), n, int(acc), form)
+
+
+@pytest.mark.parametrize("form", FORMS)
+@pytest.mark.parametrize("n", [0, 1, 31, 32, 127, 128, 129, 1400, 1408, 4100])
+@pytest.mark.parametrize("acc", [False, True])
+def test_gf8_dot_matches_oracle(orc, form, n, acc):
+    if form > _best():
+        pytest.skip("this CPU lacks the instructions of that form")
+    mul = orc.gf8_mul_table()
+    rng = np.random.default_rng(n * 3 + form + 17 * acc)
+    for nc in (0, 1, 5, 64):
+        srcs = [rng.integers(0, 256, n + 3, dtype=np.uint8)[1:1 + n] for _ in range(nc)]
+        coef = rng.integers(0, 256, nc)
+        if nc:
+            coef[0] = 0
+        dst_buf = rng.integers(0, 256, n + 6, dtype=np.uint8)
+        before = dst_buf.copy()
+        assert _dot(8, dst_buf[3:], srcs, coef, n, acc, form) == form
+        want = before[3:3 + n].copy() if acc else np.zeros(n, np.uint8)
+        for x, c in zip(srcs, coef):
+            want ^= mul[int(c)][x]
+        assert np.array_equal(dst_buf[3:3 + n], want), nc
+        assert np.array_equal(dst_buf[:3], before[:3]) and np.array_equal(dst_buf[3 + n:], before[3 + n:])
+
+
+@pytest.mark.parametrize("form", [N.NFEC_HOST_GF_SCALAR, N.NFEC_HOST_GF_GFNI])
+@pytest.mark.parametrize("n", [0, 1, 15, 16, 31, 32, 33, 700, 701])
+@pytest.mark.parametrize("acc", [False, True])
+def test_gf16_dot_matches_oracle(orc, form, n, acc):
+    if form > _best():
+        pytest.skip("this CPU lacks the instructions of that form")
+    rng = np.random.default_rng(n * 5 + form + 11 * acc)
+    for nc in (0, 1, 3, 40):
+        srcs = [rng.integers(0, 65536, n + 2, dtype=np.uint16)[1:1 + n] for _ in range(nc)]
+        coef = rng.integers(0, 65536, nc)
+        if nc > 2:
+            coef[:3] = [0, 1, 0xFFFF]
+        dst_buf = rng.integers(0, 65536, n + 4, dtype=np.uint16)
+        before = dst_buf.copy()
+        assert _dot(16, dst_buf[2:], srcs, coef, n, acc, form) == form
+        want = before[2:2 + n].copy() if acc else np.zeros(n, np.uint16)
+        for x, c in zip(srcs, coef):
+            want ^= _gf16_ref(orc, int(c), x)
+        assert np.array_equal(dst_buf[2:2 + n], want), nc
+        assert np.array_equal(dst_buf[:2], before[:2]) and np.array_equal(dst_buf[2 + n:], before[2 + n:])
+
+
+def test_gf16_matrices_every_byte_half(orc):
+    """the GF(2^16) product's affine matrices come from two 256-entry tables (linear in c): every
+    coefficient of the form c = b and c = b << 8, and sums of them, against log/exp"""
+    if N.NFEC_HOST_GF_GFNI > _best():
+        pytest.skip("no GFNI")
+    rng = np.random.default_rng(9)
+    x = rng.integers(0, 65536, 64, dtype=np.uint16)
+    for c in list(range(256)) + [b << 8 for b in range(256)] + [int(v) for v in rng.integers(0, 65536, 64)]:
+        dst = np.zeros(64, np.uint16)
+        assert N.lib().nfec_gf16_addmul_host(dst.ctypes.data, x.ctypes.data, c, 64, N.NFEC_HOST_GF_GFNI) == N.NFEC_HOST_GF_GFNI
+        assert np.array_equal(dst, _gf16_ref(orc, c, x)), c
+
+
+def test_gf_dot_bad_arguments():
+    src = np.zeros(8, np.uint8)
+    dst = np.zeros(8, np.uint8)
+    arr = (ctypes.c_void_p * 1)(src.ctypes.data)
+    co = np.ones(1, np.uint16)
+    assert N.lib().nfec_gf_dot_host(12, dst.ctypes.data, arr, co.ctypes.data, 1, 8, 0, -1) == N.NFEC_EINVAL
+    assert N.lib().nfec_gf_dot_host(8, None, arr, co.ctypes.data, 1, 8, 0, -1) == N.NFEC_EINVAL
+    nul = (ctypes.c_void_p * 1)(None)
+    assert N.lib().nfec_gf_dot_host(8, dst.ctypes.data, nul, co.ctypes.data, 1, 8, 0, -1) == N.NFEC_EINVAL
+    assert N.lib().nfec_gf_dot_host(8, dst.ctypes.data, arr, co.ctypes.data, 1, 8, 0, 7) == N.NFEC_EINVAL

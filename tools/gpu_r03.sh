@@ -30,7 +30,7 @@ for step in $STEPS; do
       find gpurun_out/prof_$TAG -name '*kernel_stats.csv' | head -1 | xargs -r head -8 ;;
     percall)
       : > gpurun_out/percall_$TAG.jsonl
-      for shape in "rs8 64 32 1408 16 2000" "rs8 64 16 1408 8 2000" "rs8 16 4 1408 4 2000" \
+      for shape in "rs8 64 32 1408 16 2000" "rs8 64 32 1400 16 2000" "rs8 64 16 1408 8 2000" "rs8 16 4 1408 4 2000" \
                    "rs16 400 100 1400 50 200" "rs16 400 20 1400 10 500" "mdp 64 32 1408 16 500" \
                    "rs8 128 127 1408 100 200" "mdp 128 127 1408 100 200" "rs8 128 127 8192 100 50" \
                    "mdp 128 127 8192 100 50" "rs8 200 55 1408 55 200"; do
