@@ -56,6 +56,11 @@ CASES = [
     (NFEC_MDP, 200, 55, 1401, 150, 30, 20, False, True),
     (NFEC_MDP, 10, 7, 8, 4, 4, 3, False, False),
     (NFEC_MDP, 1, 1, 64, 1, 1, 0, False, False),
+    # repairs past 8 MiB of products: the host path splits the vectors over threads
+    (NFEC_RS8, 128, 127, 8192, 128, 100, 20, True, True),
+    (NFEC_RS8, 128, 127, 8190, 120, 90, 30, False, False),
+    (NFEC_MDP, 128, 127, 8192, 128, 100, 20, False, True),
+    (NFEC_RS16, 300, 64, 8000, 300, 64, 0, False, False),
 ]
 
 
