@@ -276,9 +276,9 @@ int nfec_encode_segment_host(nfec_codec* codec, uint32_t segment_id, const void*
 int nfec_decode_vectors_host(nfec_codec* codec, void* const* vectors, uint32_t num_data,
                              uint32_t erasure_count, const uint32_t* erasure_locs);
 /* 1 when nfec_decode_vectors_host is the faster path for this call, else 0 (the drop-in
- * Decode's choice), from the measured crossovers: RS8 while erasures x numData x vector bytes
- * stays within 48 MiB, MDP while erasures x (numData + numParity) x vector bytes stays within
- * 96 MiB, RS16 while erasures x numData x symbols stays within 4 Mi. */
+ * Decode's choice), from the measured latencies: RS8 while erasures x numData x vector bytes
+ * stays within 256 MiB, MDP while erasures x (numData + numParity) x vector bytes stays within
+ * 512 MiB, RS16 (min(k, m) <= 64) while erasures x numData x symbols stays within 64 Mi. */
 int nfec_decode_host_preferred(const nfec_codec* codec, uint32_t num_data, uint32_t erasure_count);
 
 /* sizeof() of the drop-in class NormEncoder<kind> (decoder = 0) or NormDecoder<kind>

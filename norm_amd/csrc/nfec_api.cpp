@@ -2059,13 +2059,14 @@ int nfec_decode_vectors_host(nfec_codec* c, void* const* vectors, uint32_t num_d
     return (int)erasure_count;
 }
 
-// Repair products up to which one-block Decode stays on the host: the crossovers of the host
-// path and the GPU round trip measured by tools/percall (profiles/r04/percall.jsonl): RS8 bytes
-// (host ~55-80 GB/s, GPU 0.65-0.77 ms at 128+127 slots), MDP bytes (~90-135 GB/s against
-// 0.86-0.99 ms), RS16 symbols (~8 G/s against 0.5-0.85 ms)
-static constexpr uint64_t kHostDecodeRs8Bytes = 48ull << 20;
-static constexpr uint64_t kHostDecodeMdpBytes = 96ull << 20;
-static constexpr uint64_t kHostDecodeRs16Symbols = 4ull << 20;
+// Repair products up to which one-block Decode stays on the host, from tools/percall
+// (profiles/r04/percall.jsonl): the host path (row dot products, 8 threads past 8 MiB) beat the
+// GPU round trip at every measured size -- RS8(128,127) x 8192 B with 100 erasures (105 MB of
+// products) 0.36 against 0.79 ms, MDP (209 MB) 0.42 against 0.99 ms, RS16(400,100) with 50
+// erasures (14 M symbol products) 0.31 against 0.86 ms -- so the bounds sit a few times past them.
+static constexpr uint64_t kHostDecodeRs8Bytes = 256ull << 20;
+static constexpr uint64_t kHostDecodeMdpBytes = 512ull << 20;
+static constexpr uint64_t kHostDecodeRs16Symbols = 64ull << 20;
 
 int nfec_decode_host_preferred(const nfec_codec* c, uint32_t num_data, uint32_t erasure_count)
 {

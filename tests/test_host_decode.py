@@ -140,10 +140,11 @@ def test_drop_in_policy():
     from norm_amd import _native as N
 
     d8, d16, dm = NormDecoderRS8(), NormDecoderRS16(), NormDecoderMDP()
-    b8, bm = NormDecoderRS8(), NormDecoderMDP()
+    b8, bm, b16 = NormDecoderRS8(), NormDecoderMDP(), NormDecoderRS16()
     assert d8.Init(64, 32, 1408) and d16.Init(400, 60, 1400) and dm.Init(64, 32, 1408)
-    assert b8.Init(128, 127, 8192) and bm.Init(128, 127, 8192)
+    assert b8.Init(128, 127, 65535) and bm.Init(128, 127, 65535) and b16.Init(4000, 60, 65535)
     pref = N.lib().nfec_decode_host_preferred
     assert pref(d8._h, 64, 16) == 1 and pref(dm._h, 64, 16) == 1
-    assert pref(d16._h, 400, 10) == 1 and pref(d16._h, 400, 50) == 0
-    assert pref(b8._h, 128, 100) == 0 and pref(bm._h, 128, 100) == 0
+    assert pref(d16._h, 400, 10) == 1 and pref(d16._h, 400, 50) == 1
+    assert pref(b8._h, 128, 100) == 0 and pref(bm._h, 128, 100) == 0 and pref(b16._h, 4000, 60) == 0
+    assert pref(b8._h, 128, 10) == 1
