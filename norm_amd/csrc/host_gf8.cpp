@@ -1,5 +1,5 @@
-// host_gf8.cpp -- GF(2^8) region multiply-accumulate on the host CPU, for the one call pattern a
-// GPU cannot serve well: NORM's incremental sender, which calls Encode once per source segment
+// host_gf8.cpp -- GF(2^8) / GF(2^16) region products on the host CPU, for the per-call patterns a
+// GPU cannot serve well.  First NORM's incremental sender, which calls Encode once per source segment
 // and reads the parity without telling the encoder when a block ends
 // (NormObject::NextSenderMsg -> NormSession::SenderEncode, normObject.cpp:2038-2052 ->
 // NormEncoderRS8::Encode, normEncoderRS8.cpp:473-483).  One such call is m products of a
@@ -12,9 +12,10 @@
 //         the field's own products, not GFNI's fixed 0x11b multiply), 32 bytes per instruction;
 //   AVX2: the split-nibble table form, two vpshufb lookups of 16-entry product tables;
 //   scalar: a 256 x 256 product table (the reference's own method, normEncoderRS8.cpp:140-149).
-// c = 0 leaves dst alone, as the reference's addmul macro does (:258-259).  The batch and repair
-// paths stay on the GPU; this serves nfec_encode_segment_host only.  GF(2^16) (RS16 Encode,
-// normEncoderRS16.cpp:472-482) below: GFNI affine transforms per byte half, or log/exp tables.
+// c = 0 leaves dst alone, as the reference's addmul macro does (:258-259).  GF(2^16) (RS16
+// Encode, normEncoderRS16.cpp:472-482) below: GFNI affine transforms on deinterleaved bytes, or
+// log/exp tables.  Row dot products (sum_j c_j * src_j into one destination) serve the one-block
+// host repair (nfec_decode_vectors_host); the batch paths stay on the GPU.
 // (host code only: the library's .cpp files go through the HIP compiler, whose device pass
 // has no x86 builtins)
 #ifndef __HIP_DEVICE_COMPILE__
