@@ -148,3 +148,36 @@ def test_drop_in_policy():
     assert pref(d16._h, 400, 10) == 1 and pref(d16._h, 400, 50) == 1
     assert pref(b8._h, 128, 100) == 0 and pref(bm._h, 128, 100) == 0 and pref(b16._h, 4000, 60) == 0
     assert pref(b8._h, 128, 10) == 1
+
+
+def test_host_decode_concurrent_calls(orc):
+    """one decoder, four caller threads (the host path keeps no per-call state in the codec):
+    every block repaired exactly, including the threaded-size ones"""
+    import threading
+
+    k, m = 128, 127
+    dec = NormDecoderRS8()
+    assert dec.Init(k, m, 8192)
+    jobs = []
+    for i in range(8):
+        rng = np.random.default_rng(700 + i)
+        es = 4 if i % 2 else 100   # 4 erasures: 4 MB of products, one thread; 100: threaded
+        clean, rx, locs = _case(orc, NFEC_RS8, k, m, 8192, k, es, 0, rng)
+        jobs.append((clean, rx, locs))
+    errors = []
+
+    def work(idx):
+        for j in range(idx, len(jobs), 4):
+            clean, rx, locs = jobs[j]
+            for _ in range(3):
+                vl = [rx[s].copy() for s in range(rx.shape[0])]
+                st = dec.Decode(vl, k, len(locs), locs, host=True)
+                if st != len(locs) or any(not np.array_equal(vl[s], clean[0, s]) for s in locs):
+                    errors.append((j, st))
+
+    th = [threading.Thread(target=work, args=(i,)) for i in range(4)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    assert not errors
