@@ -1904,7 +1904,12 @@ static void host_rows_apply(bool wide, void* const* dst, uint32_t nrows, const v
     std::vector<std::thread> th;
     for (unsigned t = 1; t < nt; ++t) {
         const size_t e0 = std::min(nelem, t * per), e1 = std::min(nelem, e0 + per);
-        if (e0 < e1) th.emplace_back(run, e0, e1);
+        if (e0 >= e1) continue;
+        try {
+            th.emplace_back(run, e0, e1);
+        } catch (...) {
+            run(e0, e1);  // no thread to be had: this range on the calling thread
+        }
     }
     run(0, std::min(per, nelem));
     for (auto& t : th) t.join();
