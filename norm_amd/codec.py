@@ -12,9 +12,10 @@ normEncoderMDP.h) so parity tests read like the reference's own fecTest
 
 On top of the per-call surface, `encode_blocks` / `decode_blocks` take a batch of blocks
 resident in HBM (a torch uint8 CUDA tensor shaped [nblocks, k+m, seg_stride]) -- the
-performance path.  Everything runs through libnfec.so; nothing here computes.  (One-block
-Decode follows the drop-in's choice of the library's host CPU path for RS8 and small RS16,
-nfec_decode_vectors_host; Encode here is the GPU round trip, nfec_encode_segment.)
+performance path.  Everything runs through libnfec.so; nothing here computes.  The per-call
+Encode / Decode follow the C++ drop-in's defaults: the library's host CPU paths
+(nfec_encode_segment_host, and nfec_decode_vectors_host unless the repair is very large), with
+host=False for the GPU round trip.
 """
 import ctypes
 
@@ -182,7 +183,9 @@ class _Codec:
 
 
 class _Encoder(_Codec):
-    def Encode(self, segmentId, dataVector, parityVectorList):
+    def Encode(self, segmentId, dataVector, parityVectorList, host=True):
+        """NormEncoder::Encode.  host=True (the drop-in's default): nfec_encode_segment_host, the
+        product on the calling CPU; host=False: the GPU round trip, nfec_encode_segment."""
         self._need()
         daddr, dkeep = _addr_ro(dataVector)
         keeps = []
@@ -191,7 +194,8 @@ class _Encoder(_Codec):
             a, k = _addr_rw(parityVectorList[i])
             arr[i] = a
             keeps.append(k)
-        N.check(N.lib().nfec_encode_segment(self._h, segmentId, daddr, arr), "nfec_encode_segment")
+        fn = "nfec_encode_segment_host" if host else "nfec_encode_segment"
+        N.check(getattr(N.lib(), fn)(self._h, segmentId, daddr, arr), fn)
 
     def encode_blocks(self, blocks, num_data=None, accumulate=False, stream=None):
         """Parity for every block of a device batch (slots [nd, nd+m) of each block)."""

@@ -1829,6 +1829,7 @@ int nfec_encode_segment(nfec_codec* c, uint32_t segment_id, const void* data, vo
 int nfec_encode_segment_host(nfec_codec* c, uint32_t segment_id, const void* data, void* const* parity)
 {
     if (!c || !data || !parity) return fail(NFEC_EINVAL, "null argument");
+    c = primary(c);  // a multi-device codec: the first stripe holds the host tables (mdp_g)
     if (segment_id >= c->k) return fail(NFEC_EINVAL, "segmentId >= numData");
     for (uint32_t i = 0; i < c->m; ++i)
         if (!parity[i]) return fail(NFEC_EINVAL, "null parity vector");

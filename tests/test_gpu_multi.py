@@ -92,26 +92,29 @@ def test_striped_segment_lists_and_async(orc):
             assert np.array_equal(segs[b][s], want[b, s]), (b, s)
 
 
-def test_multi_device_batch_and_per_call(orc):
-    """device batches run on the stripe of their device; per-call Encode/Decode on the first"""
+@pytest.mark.parametrize("kind", [N.NFEC_RS8, N.NFEC_MDP])
+@pytest.mark.parametrize("host_call", [False, True])
+def test_multi_device_batch_and_per_call(orc, kind, host_call):
+    """device batches run on the stripe of their device; per-call Encode/Decode on the first
+    (GPU round trips, or the host paths, which read the first stripe's tables)"""
     k, m, vec, nb = 64, 32, 1400, 33
-    enc, dec = _codecs(N.NFEC_RS8, k, m, vec, [0, 0])
+    enc, dec = _codecs(kind, k, m, vec, [0, 0])
     host = orc.make_blocks(k, m, vec, nb)
-    ref = orc.encode_blocks(N.NFEC_RS8, k, m, vec, host.copy())
+    ref = orc.encode_blocks(kind, k, m, vec, host.copy())
     dev = torch.from_numpy(host).cuda()
     enc.encode_blocks(dev)
     torch.cuda.synchronize()
     assert np.array_equal(dev.cpu().numpy(), ref)
     par = [np.zeros(vec, np.uint8) for _ in range(m)]
     for s in range(k):
-        enc.Encode(s, host[0, s].copy(), par)
+        enc.Encode(s, host[0, s].copy(), par, host=host_call)
     for p in range(m):
         assert np.array_equal(par[p], ref[0, k + p])
     rx, locs, counts = _erase(orc, ref[:1], k, m, 16, 9)
     want = rx.copy()
-    orc.decode_blocks(N.NFEC_RS8, k, m, vec, want, locs, counts)
+    orc.decode_blocks(kind, k, m, vec, want, locs, counts)
     vl = [rx[0, s].copy() for s in range(k + m)]
-    assert dec.Decode(vl, k, 16, [int(x) for x in locs[0, :16]]) == 16
+    assert dec.Decode(vl, k, 16, [int(x) for x in locs[0, :16]], host=host_call) == 16
     for s in range(k):
         assert np.array_equal(vl[s], want[0, s])
 

@@ -274,9 +274,11 @@ def test_decode_rejects_undecodable_blocks(orc):
     assert np.array_equal(out[3], before[3])  # nothing was erased, the repair rewrites the same bytes
 
 
+@pytest.mark.parametrize("host", [False, True])
 @pytest.mark.parametrize("kind", [NFEC_RS8, NFEC_RS16, NFEC_MDP])
-def test_per_call_reference_surface(orc, kind):
-    """Encode()/Decode() with scattered host vectors, exactly as fecTest drives them."""
+def test_per_call_reference_surface(orc, kind, host):
+    """Encode()/Decode() with scattered host vectors, exactly as fecTest drives them: the GPU
+    round trip (host=False) and the host paths (the drop-in's defaults)."""
     k, m, vec = 20, 6, 64
     enc, dec = _codecs(kind, k, m, vec)
     blk = orc.make_blocks(k, m, vec, 1)[0]
@@ -284,7 +286,7 @@ def test_per_call_reference_surface(orc, kind):
     data = [bytearray(blk[s].tobytes()) for s in range(k)]
     parity = [bytearray(vec) for _ in range(m)]
     for s in range(k):
-        enc.Encode(s, bytes(data[s]), parity)
+        enc.Encode(s, bytes(data[s]), parity, host=host)
     assert all(bytes(parity[i]) == ref[k + i].tobytes() for i in range(m))
     vecs = [bytearray(ref[s].tobytes()) for s in range(k + m)]
     erased = [1, 5, 6, k + 2]
@@ -292,26 +294,28 @@ def test_per_call_reference_surface(orc, kind):
         vecs[s] = bytearray(vec)
     vlist = list(vecs)
     vlist[k + 2] = None  # missing parity passed as NULL like NormObject
-    assert dec.Decode(vlist, k, len(erased), erased) == len(erased)
+    assert dec.Decode(vlist, k, len(erased), erased, host=host) == len(erased)
     for s in range(k):
         assert bytes(vlist[s]) == ref[s].tobytes()
 
 
+@pytest.mark.parametrize("host", [False, True])
 @pytest.mark.parametrize("kind", [NFEC_RS8, NFEC_RS16])
 @pytest.mark.parametrize("vec,nd,junk", [(64, 20, False), (64, 20, True), (66, 20, False), (64, 13, False),
                                           (1408, 20, True)])
-def test_per_call_paths(orc, kind, vec, nd, junk):
-    """The per-call Encode/Decode take the batch fast paths for a full block with zero-filled
-    erased buffers (tower kernel / fused repair, overwrite) and the general ones otherwise:
-    a shortened block (numData < k), non-zero erased buffers (the reference XORs the repair
-    into them, normEncoderRS8.cpp:728-755), an odd-multiple vector size (vec % 8 != 0)."""
+def test_per_call_paths(orc, kind, vec, nd, junk, host):
+    """The per-call Encode/Decode on the GPU (host=False) take the batch fast paths for a full
+    block with zero-filled erased buffers (tower kernel / fused repair, overwrite) and the general
+    ones otherwise: a shortened block (numData < k), non-zero erased buffers (the reference XORs
+    the repair into them, normEncoderRS8.cpp:728-755), an odd-multiple vector size
+    (vec % 8 != 0).  host=True: the same calls on the host paths."""
     k, m = 20, 6
     enc, dec = _codecs(kind, k, m, vec)
     blk = orc.make_blocks(k, m, vec, 1, num_data=np.array([nd], np.uint16))[0]
     ref = orc.encode_blocks(kind, k, m, vec, blk[None].copy(), np.array([nd], np.uint16))[0]
     parity = [bytearray(vec) for _ in range(m)]
     for s in range(nd):
-        enc.Encode(s, blk[s, :vec].tobytes(), parity)
+        enc.Encode(s, blk[s, :vec].tobytes(), parity, host=host)
     assert all(bytes(parity[i]) == ref[nd + i, :vec].tobytes() for i in range(m))
     vecs = [bytearray(ref[s, :vec].tobytes()) for s in range(nd + m)]
     erased = [0, 3, nd - 1, nd + 1]
@@ -320,7 +324,7 @@ def test_per_call_paths(orc, kind, vec, nd, junk):
     for s in erased:
         noise[s] = rng.integers(0, 256, vec, dtype=np.uint8).tobytes() if junk else bytes(vec)
         vecs[s] = bytearray(noise[s])
-    assert dec.Decode(vecs, nd, len(erased), erased) == len(erased)
+    assert dec.Decode(vecs, nd, len(erased), erased, host=host) == len(erased)
     nbytes = vec if kind == NFEC_RS8 else vec // 2 * 2
     for s in range(nd):
         want = bytearray(ref[s, :vec].tobytes())
