@@ -4,9 +4,10 @@
  * Drop-in boundary for NORM's FEC plugin layer (reference include/normEncoder.h:38-54):
  * plain pointers, sizes and integer status codes; no C++ or torch types cross it.
  * Every compute entry point runs hand-written gfx950 HIP kernels (a missing/failed GPU yields
- * NFEC_EDEVICE; nothing falls back to the CPU), except the two entry points named *_host in
- * "host CPU per-segment path" below, which are the host path by definition: one Encode call of
- * NORM's incremental sender is a few microseconds of work, less than a GPU round trip.
+ * NFEC_EDEVICE; nothing falls back to the CPU), except the per-call entry points named *_host
+ * ("host CPU per-call paths" below), which are the host path by definition: one Encode call of
+ * NORM's incremental sender, or one block's repair, is microseconds of work, less than a GPU
+ * round trip.  Which of the two a drop-in class calls is its documented policy, not a fallback.
  *
  * Reference interfaces each entry replaces (paths in USNavalResearchLaboratory/norm):
  *   nfec_codec_create(_ex) NormEncoderRS8::Init  src/common/normEncoderRS8.cpp:400-462
@@ -27,6 +28,8 @@
  *                         (include/normEncoder.h:44), host pointers, exact per-call semantics
  *   nfec_decode_vectors   NormDecoder::Decode(vectorList, numData, erasureCount, erasureLocs)
  *                         (include/normEncoder.h:53), host pointers, exact per-call semantics
+ *   nfec_encode_segment_host / nfec_decode_vectors_host
+ *                         the same two calls on the host CPU (GFNI / AVX2 region products)
  */
 #ifndef NFEC_H
 #define NFEC_H
@@ -235,7 +238,7 @@ int nfec_encode_segment(nfec_codec* codec, uint32_t segment_id, const void* data
 /* NormDecoder::Decode: returns erasure_count on success, 0 when undecodable, <0 on error. */
 int nfec_decode_vectors(nfec_codec* codec, void* const* vector_list, uint32_t num_data,
                         uint32_t erasure_count, const uint32_t* erasure_locs);
-/* ---- host CPU per-segment path (NORM's incremental sender) ----
+/* ---- host CPU per-call paths (NORM's incremental sender, one-block repair) ----
  * NormObject::NextSenderMsg calls Encode once per source segment and reads the parity without
  * a call that ends the block (normObject.cpp:2038-2052), so each call must finish on return:
  * m products of one segment, microseconds of CPU work against ~80 us for a GPU round trip
