@@ -2327,38 +2327,6 @@ static uint32_t host_chunk(const nfec_codec* c, uint64_t dbs, uint32_t nblocks)
     return (uint32_t)std::min<uint64_t>(ch, nblocks);
 }
 
-// Chunk sizes of a pinned host batch's pipeline.  Fixed chunks of host_chunk's size pay a
-// per-chunk cost (launches, plans, events: ~0.1 ms) on every chunk, and a fill and a drain (the
-// first upload and the last download run alone) that grow with the chunk.  For the bit-sliced
-// RS8 kernels, whose chunks fill the GPU at any size, the sizes ramp instead: base / 8, / 4,
-// / 2, base, then 4 x base through the middle, and the same steps down at the end -- the fill
-// and drain of a base / 8 chunk with about a quarter of the chunks.  cap: the largest chunk
-// (what a slot must hold).  NFEC_HOST_CHUNK_BLOCKS (tests) keeps fixed chunks.
-static std::vector<uint32_t> host_chunk_plan(const nfec_codec* c, uint64_t dbs, uint32_t nblocks, bool pinned,
-                                             uint32_t& cap)
-{
-    const uint32_t base = host_chunk(c, dbs, nblocks);
-    std::vector<uint32_t> plan;
-    const uint32_t big = 4 * base;
-    const uint32_t head[4] = {base / 8, base / 4, base / 2, base};
-    const uint64_t hs = (uint64_t)head[0] + head[1] + head[2] + head[3];
-    const bool ramp = pinned && !std::getenv("NFEC_HOST_CHUNK_BLOCKS") && c->kind == NFEC_RS8 &&
-                      has_bitsliced(c->k, c->m) && base >= 64 && (uint64_t)big * dbs <= (4ull << 30) &&
-                      nblocks >= 2 * hs + big;
-    if (!ramp) {
-        for (uint32_t b0 = 0; b0 < nblocks; b0 += base) plan.push_back(std::min(base, nblocks - b0));
-        cap = base;
-        return plan;
-    }
-    for (uint32_t h : head) plan.push_back(h);
-    const uint64_t mid = nblocks - 2 * hs;
-    const uint64_t nm = (mid + big - 1) / big;
-    for (uint64_t i = 0; i < nm; ++i) plan.push_back((uint32_t)(mid * (i + 1) / nm - mid * i / nm));
-    for (int i = 3; i >= 0; --i) plan.push_back(head[i]);
-    cap = big;
-    return plan;
-}
-
 static void stage_drain(nfec_codec* c)
 {
     for (auto& s : c->stage.slot)
@@ -2606,9 +2574,8 @@ static int run_host_batch(nfec_codec* c, const nfec_block_batch* hb, const uint1
         return (uint64_t)(top - 1) * ss + c->vec;  // top >= ndmax >= 1
     };
 
-    uint32_t chunk = 0;  // slot capacity in blocks: the largest chunk of the plan
-    const std::vector<uint32_t> plan = host_chunk_plan(c, dbs, hb->nblocks, pinned, chunk);
-    const uint32_t used = std::min<uint32_t>(kHostSlots, (uint32_t)plan.size());
+    const uint32_t chunk = host_chunk(c, dbs, hb->nblocks);
+    const uint32_t used = std::min<uint32_t>(kHostSlots, (hb->nblocks + chunk - 1) / chunk);
     const size_t meta = (size_t)chunk * (1 + lstride + 1);
     HostSlot* sl[kHostSlots] = {};
     for (uint32_t i = 0; i < used; ++i)
@@ -2637,13 +2604,13 @@ static int run_host_batch(nfec_codec* c, const nfec_block_batch* hb, const uint1
         return code;
     };
     uint32_t idx = 0;
-    for (uint32_t b0 = 0; idx < plan.size(); b0 += plan[idx], ++idx) {
+    for (uint32_t b0 = 0; b0 < hb->nblocks; b0 += chunk, ++idx) {
         const uint32_t i = idx % used;
         if ((rc = finish(i))) return bail(rc);
         HostSlot& s = *sl[i];
         Job& j = jobs[i];
         j.b0 = b0;
-        j.nb = plan[idx];
+        j.nb = std::min(chunk, hb->nblocks - b0);
         uint8_t* hsrc = hbase + (uint64_t)b0 * hbs;
         uint64_t dl = dn_len;
         const uint64_t ul = decode ? decode_up_len(b0, j.nb, dl) : up_len;
