@@ -377,6 +377,69 @@ __attribute__((target("avx2,gfni"))) void dot16_gfni(uint16_t* dst, const uint16
     }
 }
 
+// ---- one source into many rows: dst[r][0..n) ^= coef[r * cstride] * src[0..n) ----
+// The per-segment Encode's m products share their source: a 128-byte piece of it stays in
+// registers while every row takes it (one load of the source per piece instead of per row).
+
+__attribute__((target("avx2,gfni"))) void rows_gfni(uint8_t* const* dst, const uint8_t* src, const uint32_t* coef,
+                                                    size_t cstride, uint32_t nr, size_t n)
+{
+    const Gf8HostTables& t = tables();
+    size_t i = 0;
+    for (; i + 128 <= n; i += 128) {
+        const __m256i x0 = _mm256_loadu_si256(reinterpret_cast<const __m256i*>(src + i));
+        const __m256i x1 = _mm256_loadu_si256(reinterpret_cast<const __m256i*>(src + i + 32));
+        const __m256i x2 = _mm256_loadu_si256(reinterpret_cast<const __m256i*>(src + i + 64));
+        const __m256i x3 = _mm256_loadu_si256(reinterpret_cast<const __m256i*>(src + i + 96));
+        for (uint32_t r = 0; r < nr; ++r) {
+            const uint32_t c = coef[r * cstride] & 0xffu;
+            if (!c) continue;
+            const __m256i m = _mm256_set1_epi64x((long long)t.affine[c]);
+            __m256i* d = reinterpret_cast<__m256i*>(dst[r] + i);
+            _mm256_storeu_si256(d, _mm256_xor_si256(_mm256_loadu_si256(d), _mm256_gf2p8affine_epi64_epi8(x0, m, 0)));
+            _mm256_storeu_si256(d + 1, _mm256_xor_si256(_mm256_loadu_si256(d + 1), _mm256_gf2p8affine_epi64_epi8(x1, m, 0)));
+            _mm256_storeu_si256(d + 2, _mm256_xor_si256(_mm256_loadu_si256(d + 2), _mm256_gf2p8affine_epi64_epi8(x2, m, 0)));
+            _mm256_storeu_si256(d + 3, _mm256_xor_si256(_mm256_loadu_si256(d + 3), _mm256_gf2p8affine_epi64_epi8(x3, m, 0)));
+        }
+    }
+    if (i < n)
+        for (uint32_t r = 0; r < nr; ++r) {
+            const uint32_t c = coef[r * cstride] & 0xffu;
+            if (c) addmul_gfni(dst[r] + i, src + i, c, n - i);
+        }
+}
+
+__attribute__((target("avx2,gfni"))) void rows16_gfni(uint16_t* const* dst, const uint16_t* src, const uint32_t* coef,
+                                                      size_t cstride, uint32_t nr, size_t n)
+{
+    const Gf16MatTables& t = gf16_mat_tables();
+    const __m256i deint = gf16_deint(), inter = gf16_inter();
+    size_t i = 0;
+    for (; i + 64 <= n; i += 64) {
+        __m256i x[4];
+        for (int q = 0; q < 4; ++q)
+            x[q] = _mm256_shuffle_epi8(_mm256_loadu_si256(reinterpret_cast<const __m256i*>(src + i + 16 * q)), deint);
+        for (uint32_t r = 0; r < nr; ++r) {
+            const uint32_t c = coef[r * cstride] & 0xffffu;
+            if (!c) continue;
+            const __m256i mm = _mm256_xor_si256(_mm256_loadu_si256(reinterpret_cast<const __m256i*>(&t.lo[c & 0xffu])),
+                                                _mm256_loadu_si256(reinterpret_cast<const __m256i*>(&t.hi[c >> 8])));
+            const __m256i m1 = _mm256_permute4x64_epi64(mm, 0xcc), m2 = _mm256_permute4x64_epi64(mm, 0x66);
+            __m256i* d = reinterpret_cast<__m256i*>(dst[r] + i);
+            for (int q = 0; q < 4; ++q) {
+                const __m256i y = _mm256_xor_si256(_mm256_gf2p8affine_epi64_epi8(x[q], m1, 0),
+                                                   _mm256_shuffle_epi32(_mm256_gf2p8affine_epi64_epi8(x[q], m2, 0), 0x4e));
+                _mm256_storeu_si256(d + q, _mm256_xor_si256(_mm256_loadu_si256(d + q), _mm256_shuffle_epi8(y, inter)));
+            }
+        }
+    }
+    if (i < n)
+        for (uint32_t r = 0; r < nr; ++r) {
+            const uint32_t c = coef[r * cstride] & 0xffffu;
+            if (c) addmul16_gfni(dst[r] + i, src + i, c, n - i);
+        }
+}
+
 }  // namespace
 
 void host_gf16_addmul(uint16_t* dst, const uint16_t* src, uint32_t c, size_t nsym, int isa)
@@ -402,6 +465,22 @@ void host_gf16_dot(uint16_t* dst, const uint16_t* const* src, size_t off, const 
     if ((isa < 0 ? best_isa() : isa) == NFEC_HOST_GF_GFNI) return dot16_gfni(dst, src, off, coef, nc, nsym, acc);
     if (!acc) std::memset(dst, 0, nsym * 2);
     for (uint32_t j = 0; j < nc; ++j) host_gf16_addmul(dst, src[j] + off, coef[j], nsym, isa);
+}
+
+void host_gf8_addmul_rows(uint8_t* const* dst, const uint8_t* src, const uint32_t* coef, size_t cstride, uint32_t nrows,
+                          size_t n, int isa)
+{
+    if (n == 0) return;
+    if ((isa < 0 ? best_isa() : isa) == NFEC_HOST_GF_GFNI) return rows_gfni(dst, src, coef, cstride, nrows, n);
+    for (uint32_t r = 0; r < nrows; ++r) host_gf8_addmul(dst[r], src, coef[r * cstride], n, isa);
+}
+
+void host_gf16_addmul_rows(uint16_t* const* dst, const uint16_t* src, const uint32_t* coef, size_t cstride,
+                           uint32_t nrows, size_t nsym, int isa)
+{
+    if (nsym == 0) return;
+    if ((isa < 0 ? best_isa() : isa) == NFEC_HOST_GF_GFNI) return rows16_gfni(dst, src, coef, cstride, nrows, nsym);
+    for (uint32_t r = 0; r < nrows; ++r) host_gf16_addmul(dst[r], src, coef[r * cstride], nsym, isa);
 }
 
 int host_gf8_isa() { return best_isa(); }

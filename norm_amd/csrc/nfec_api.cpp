@@ -1837,10 +1837,8 @@ int nfec_encode_segment_host(nfec_codec* c, uint32_t segment_id, const void* dat
     const int isa = host_gf8_isa();
     if (c->kind == NFEC_RS16) {
         // vec / 2 native-endian symbols; an odd last byte is never touched (normEncoderRS16.cpp:479)
-        const size_t nsym = c->vec / 2;
-        const uint16_t* d16 = static_cast<const uint16_t*>(data);
-        for (uint32_t i = 0; i < c->m; ++i)
-            host_gf16_addmul(static_cast<uint16_t*>(parity[i]), d16, c->gen[(size_t)i * c->k + segment_id], nsym, isa);
+        host_gf16_addmul_rows(reinterpret_cast<uint16_t* const*>(parity), static_cast<const uint16_t*>(data),
+                              c->gen.data() + segment_id, c->k, c->m, c->vec / 2, isa);
         return NFEC_OK;
     }
     if (c->kind == NFEC_MDP) {
@@ -1860,8 +1858,8 @@ int nfec_encode_segment_host(nfec_codec* c, uint32_t segment_id, const void* dat
         host_gf8_addmul(pl, s.data(), c->mdp_g[0], c->vec, isa);
         return NFEC_OK;
     }
-    for (uint32_t i = 0; i < c->m; ++i)
-        host_gf8_addmul(static_cast<uint8_t*>(parity[i]), d, c->gen[(size_t)i * c->k + segment_id], c->vec, isa);
+    host_gf8_addmul_rows(reinterpret_cast<uint8_t* const*>(parity), d, c->gen.data() + segment_id, c->k, c->m, c->vec,
+                         isa);
     return NFEC_OK;
 }
 

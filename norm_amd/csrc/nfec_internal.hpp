@@ -83,6 +83,11 @@ void host_gf8_dot(uint8_t* dst, const uint8_t* const* src, size_t off, const uin
                   bool acc, int isa);
 void host_gf16_dot(uint16_t* dst, const uint16_t* const* src, size_t off, const uint16_t* coef, uint32_t nc,
                    size_t nsym, bool acc, int isa);
+// dst[r][0..n) ^= coef[r * cstride] * src[0..n) for r < nrows (the per-segment Encode's m rows)
+void host_gf8_addmul_rows(uint8_t* const* dst, const uint8_t* src, const uint32_t* coef, size_t cstride, uint32_t nrows,
+                          size_t n, int isa);
+void host_gf16_addmul_rows(uint16_t* const* dst, const uint16_t* src, const uint32_t* coef, size_t cstride,
+                           uint32_t nrows, size_t nsym, int isa);
 
 // v_perm product tables for one GF(2^8) constant c: 8 dwords (32 bytes)
 //   t0 = c*{0,1,2,3}   t1 = c*{4,5,6,7}       (low 3 bits)
