@@ -21,6 +21,7 @@
 #ifndef __HIP_DEVICE_COMPILE__
 #include <immintrin.h>
 
+#include <algorithm>
 #include <cstring>
 #include <mutex>
 
@@ -414,30 +415,39 @@ __attribute__((target("avx2,gfni"))) void rows16_gfni(uint16_t* const* dst, cons
 {
     const Gf16MatTables& t = gf16_mat_tables();
     const __m256i deint = gf16_deint(), inter = gf16_inter();
-    size_t i = 0;
-    for (; i + 64 <= n; i += 64) {
-        __m256i x[4];
-        for (int q = 0; q < 4; ++q)
-            x[q] = _mm256_shuffle_epi8(_mm256_loadu_si256(reinterpret_cast<const __m256i*>(src + i + 16 * q)), deint);
-        for (uint32_t r = 0; r < nr; ++r) {
-            const uint32_t c = coef[r * cstride] & 0xffffu;
-            if (!c) continue;
+    // rows in groups of 64, their two lane-pair matrices built once per group
+    constexpr uint32_t kGroup = 64;
+    __m256i m1[kGroup], m2[kGroup];
+    for (uint32_t r0 = 0; r0 < nr; r0 += kGroup) {
+        const uint32_t gn = std::min(kGroup, nr - r0);
+        for (uint32_t r = 0; r < gn; ++r) {
+            const uint32_t c = coef[(r0 + r) * cstride] & 0xffffu;
             const __m256i mm = _mm256_xor_si256(_mm256_loadu_si256(reinterpret_cast<const __m256i*>(&t.lo[c & 0xffu])),
                                                 _mm256_loadu_si256(reinterpret_cast<const __m256i*>(&t.hi[c >> 8])));
-            const __m256i m1 = _mm256_permute4x64_epi64(mm, 0xcc), m2 = _mm256_permute4x64_epi64(mm, 0x66);
-            __m256i* d = reinterpret_cast<__m256i*>(dst[r] + i);
-            for (int q = 0; q < 4; ++q) {
-                const __m256i y = _mm256_xor_si256(_mm256_gf2p8affine_epi64_epi8(x[q], m1, 0),
-                                                   _mm256_shuffle_epi32(_mm256_gf2p8affine_epi64_epi8(x[q], m2, 0), 0x4e));
-                _mm256_storeu_si256(d + q, _mm256_xor_si256(_mm256_loadu_si256(d + q), _mm256_shuffle_epi8(y, inter)));
+            m1[r] = _mm256_permute4x64_epi64(mm, 0xcc);  // [A, D, A, D]
+            m2[r] = _mm256_permute4x64_epi64(mm, 0x66);  // [C, B, C, B]
+        }
+        size_t i = 0;
+        for (; i + 64 <= n; i += 64) {
+            __m256i x[4];
+            for (int q = 0; q < 4; ++q)
+                x[q] = _mm256_shuffle_epi8(_mm256_loadu_si256(reinterpret_cast<const __m256i*>(src + i + 16 * q)), deint);
+            for (uint32_t r = 0; r < gn; ++r) {
+                if (!(coef[(r0 + r) * cstride] & 0xffffu)) continue;
+                __m256i* d = reinterpret_cast<__m256i*>(dst[r0 + r] + i);
+                for (int q = 0; q < 4; ++q) {
+                    const __m256i y = _mm256_xor_si256(_mm256_gf2p8affine_epi64_epi8(x[q], m1[r], 0),
+                                                       _mm256_shuffle_epi32(_mm256_gf2p8affine_epi64_epi8(x[q], m2[r], 0), 0x4e));
+                    _mm256_storeu_si256(d + q, _mm256_xor_si256(_mm256_loadu_si256(d + q), _mm256_shuffle_epi8(y, inter)));
+                }
             }
         }
+        if (i < n)
+            for (uint32_t r = r0; r < r0 + gn; ++r) {
+                const uint32_t c = coef[r * cstride] & 0xffffu;
+                if (c) addmul16_gfni(dst[r] + i, src + i, c, n - i);
+            }
     }
-    if (i < n)
-        for (uint32_t r = 0; r < nr; ++r) {
-            const uint32_t c = coef[r * cstride] & 0xffffu;
-            if (c) addmul16_gfni(dst[r] + i, src + i, c, n - i);
-        }
 }
 
 }  // namespace
