@@ -24,6 +24,7 @@
 #include <algorithm>
 #include <cstring>
 #include <mutex>
+#include <vector>
 
 #include "nfec_internal.hpp"
 
@@ -450,6 +451,36 @@ __attribute__((target("avx2,gfni"))) void rows16_gfni(uint16_t* const* dst, cons
     }
 }
 
+// ---- the MDP encoder's LFSR step (normEncoderMDP.cpp:178-211), one pass per 128-byte piece:
+// s = data ^ P0; P_i = P_(i+1) ^ g[m-1-i] * s (i < m-1); P_(m-1) = g[0] * s.  Pieces are
+// independent, so each one reads the old P_(i+1) before it is overwritten, with s in registers.
+
+__attribute__((target("avx2,gfni"))) void mdp_step_gfni(uint8_t* const* par, const uint8_t* data, const uint8_t* g,
+                                                        uint32_t m, size_t n, size_t& done)
+{
+    const Gf8HostTables& t = tables();
+    size_t i = 0;
+    for (; i + 128 <= n; i += 128) {
+        __m256i sv[4];
+        for (int q = 0; q < 4; ++q)
+            sv[q] = _mm256_xor_si256(_mm256_loadu_si256(reinterpret_cast<const __m256i*>(data + i + 32 * q)),
+                                     _mm256_loadu_si256(reinterpret_cast<const __m256i*>(par[0] + i + 32 * q)));
+        for (uint32_t r = 0; r + 1 < m; ++r) {
+            const __m256i mt = _mm256_set1_epi64x((long long)t.affine[g[m - 1 - r]]);
+            const uint8_t* nx = par[r + 1] + i;
+            uint8_t* d = par[r] + i;
+            for (int q = 0; q < 4; ++q)
+                _mm256_storeu_si256(reinterpret_cast<__m256i*>(d + 32 * q),
+                                    _mm256_xor_si256(_mm256_loadu_si256(reinterpret_cast<const __m256i*>(nx + 32 * q)),
+                                                     _mm256_gf2p8affine_epi64_epi8(sv[q], mt, 0)));
+        }
+        const __m256i m0 = _mm256_set1_epi64x((long long)t.affine[g[0]]);
+        for (int q = 0; q < 4; ++q)
+            _mm256_storeu_si256(reinterpret_cast<__m256i*>(par[m - 1] + i + 32 * q), _mm256_gf2p8affine_epi64_epi8(sv[q], m0, 0));
+    }
+    done = i;
+}
+
 }  // namespace
 
 void host_gf16_addmul(uint16_t* dst, const uint16_t* src, uint32_t c, size_t nsym, int isa)
@@ -491,6 +522,24 @@ void host_gf16_addmul_rows(uint16_t* const* dst, const uint16_t* src, const uint
     if (nsym == 0) return;
     if ((isa < 0 ? best_isa() : isa) == NFEC_HOST_GF_GFNI) return rows16_gfni(dst, src, coef, cstride, nrows, nsym);
     for (uint32_t r = 0; r < nrows; ++r) host_gf16_addmul(dst[r], src, coef[r * cstride], nsym, isa);
+}
+
+void host_mdp_step(uint8_t* const* parity, const uint8_t* data, const uint8_t* g, uint32_t m, size_t n, int isa)
+{
+    size_t i = 0;
+    if (m && (isa < 0 ? best_isa() : isa) == NFEC_HOST_GF_GFNI) mdp_step_gfni(parity, data, g, m, n, i);
+    if (i >= n || m == 0) return;
+    // the rest (and the other forms): the same step through a scratch copy of s
+    const size_t len = n - i;
+    thread_local std::vector<uint8_t> sv;
+    sv.resize(len);
+    for (size_t j = 0; j < len; ++j) sv[j] = data[i + j] ^ parity[0][i + j];
+    for (uint32_t r = 0; r + 1 < m; ++r) {
+        std::memcpy(parity[r] + i, parity[r + 1] + i, len);
+        host_gf8_addmul(parity[r] + i, sv.data(), g[m - 1 - r], len, isa);
+    }
+    std::memset(parity[m - 1] + i, 0, len);
+    host_gf8_addmul(parity[m - 1] + i, sv.data(), g[0], len, isa);
 }
 
 int host_gf8_isa() { return best_isa(); }

@@ -1843,19 +1843,7 @@ int nfec_encode_segment_host(nfec_codec* c, uint32_t segment_id, const void* dat
     }
     if (c->kind == NFEC_MDP) {
         // the reference's LFSR step: s = data ^ P0 (its scratch copy of P0), then the shift
-        thread_local std::vector<uint8_t> s;
-        s.resize(c->vec);
-        const uint8_t* p0 = static_cast<const uint8_t*>(parity[0]);
-        for (uint32_t j = 0; j < c->vec; ++j) s[j] = d[j] ^ p0[j];
-        const uint32_t m = c->m;
-        for (uint32_t i = 0; i + 1 < m; ++i) {
-            uint8_t* pi = static_cast<uint8_t*>(parity[i]);
-            std::memcpy(pi, parity[i + 1], c->vec);
-            host_gf8_addmul(pi, s.data(), c->mdp_g[m - 1 - i], c->vec, isa);
-        }
-        uint8_t* pl = static_cast<uint8_t*>(parity[m - 1]);
-        std::memset(pl, 0, c->vec);
-        host_gf8_addmul(pl, s.data(), c->mdp_g[0], c->vec, isa);
+        host_mdp_step(reinterpret_cast<uint8_t* const*>(parity), d, c->mdp_g.data(), c->m, c->vec, isa);
         return NFEC_OK;
     }
     host_gf8_addmul_rows(reinterpret_cast<uint8_t* const*>(parity), d, c->gen.data() + segment_id, c->k, c->m, c->vec,

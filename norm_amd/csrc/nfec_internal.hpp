@@ -88,6 +88,9 @@ void host_gf8_addmul_rows(uint8_t* const* dst, const uint8_t* src, const uint32_
                           size_t n, int isa);
 void host_gf16_addmul_rows(uint16_t* const* dst, const uint16_t* src, const uint32_t* coef, size_t cstride,
                            uint32_t nrows, size_t nsym, int isa);
+// one MDP encoder step (normEncoderMDP.cpp:178-211) over n bytes: s = data ^ P0,
+// P_i = P_(i+1) ^ g[m-1-i] * s for i < m-1, P_(m-1) = g[0] * s (g: the generator polynomial)
+void host_mdp_step(uint8_t* const* parity, const uint8_t* data, const uint8_t* g, uint32_t m, size_t n, int isa);
 
 // v_perm product tables for one GF(2^8) constant c: 8 dwords (32 bytes)
 //   t0 = c*{0,1,2,3}   t1 = c*{4,5,6,7}       (low 3 bits)

@@ -72,5 +72,35 @@ int main()
                 }
                 free(src);
             }
+    // the MDP step against a byte-by-byte restatement
+    for (size_t n = 0; n < 300; n += (n < 40 ? 1 : 7))
+        for (int isa = 0; isa <= 2; ++isa) {
+            const uint32_t m = 1 + rand() % 40;
+            std::vector<uint8_t> g(m + 1);
+            for (auto& v : g) v = rand();
+            uint8_t* data = (uint8_t*)malloc(n ? n : 1);
+            for (size_t q = 0; q < n; ++q) data[q] = rand();
+            std::vector<uint8_t*> a(m);
+            std::vector<std::vector<uint8_t>> b(m, std::vector<uint8_t>(n));
+            for (uint32_t r = 0; r < m; ++r) {
+                a[r] = (uint8_t*)malloc(n ? n : 1);
+                for (size_t q = 0; q < n; ++q) a[r][q] = b[r][q] = rand();
+            }
+            nfec::host_mdp_step(a.data(), data, g.data(), m, n, isa);
+            const nfec::Field& f = nfec::gf8();
+            for (size_t q = 0; q < n; ++q) {
+                const uint32_t sv = data[q] ^ b[0][q];
+                for (uint32_t r = 0; r + 1 < m; ++r) b[r][q] = (uint8_t)(b[r + 1][q] ^ f.mul(g[m - 1 - r], sv));
+                b[m - 1][q] = (uint8_t)f.mul(g[0], sv);
+            }
+            for (uint32_t r = 0; r < m; ++r) {
+                if (n && std::memcmp(a[r], b[r].data(), n) != 0) {
+                    std::printf("mdp step mismatch n %zu isa %d row %u\n", n, isa, r);
+                    return 1;
+                }
+                free(a[r]);
+            }
+            free(data);
+        }
     std::printf("asan driver done\n");
 }
