@@ -32,6 +32,10 @@ int orc_rs8_decode(const uint8_t* enc, unsigned k, unsigned m, unsigned vec, uin
                    unsigned erasure_count, const unsigned* erasure_locs);
 int orc_rs16_decode(const uint16_t* enc, unsigned k, unsigned m, unsigned vec, uint8_t** vectors,
                     unsigned num_data, unsigned erasure_count, const unsigned* erasure_locs);
+int orc_mdp_generator_poly(unsigned m, uint8_t* g);
+void orc_mdp_encode(const uint8_t* g, unsigned m, unsigned vec, const uint8_t* data, uint8_t** parity, uint8_t* scratch);
+int orc_mdp_decode(unsigned m, unsigned vec, uint8_t** dvec, unsigned num_data, unsigned erasure_count,
+                   const unsigned* locs);
 }
 
 static double now_us()
@@ -150,6 +154,27 @@ int main(int argc, char** argv)
             orc_dec_us += now_us() - t;
         }
         orc_dec_us /= iters;
+    } else {
+        // MDP: the reference's in-order LFSR Encode and syndrome / Forney Decode
+        std::vector<uint8_t> g(m + 1), scratch(vec);
+        orc_mdp_generator_poly(m, g.data());
+        uint8_t** ul = reinterpret_cast<uint8_t**>(list.data());
+        const unsigned oit = iters * 4;
+        t0 = now_us();
+        for (unsigned i = 0; i < oit; ++i) orc_mdp_encode(g.data(), m, vec, ul[i % k], ul + k, scratch.data());
+        orc_enc_us = (now_us() - t0) / oit;
+        for (unsigned p = k; p < n; ++p) std::memset(list[p], 0, vec);
+        for (unsigned i = 0; i < k; ++i) orc_mdp_encode(g.data(), m, vec, ul[i], ul + k, scratch.data());
+        for (unsigned p = 0; p < m; ++p) bad += std::memcmp(parity_dropin[p].data(), list[k + p], vec) != 0;
+        orc_dec_us = 0;
+        for (unsigned it = 0; it < iters; ++it) {
+            for (unsigned i = 0; i < ne; ++i) std::memset(list[locs[i]], 0, vec);
+            const double t = now_us();
+            orc_mdp_decode(m, vec, ul, k, ne, locs.data());
+            orc_dec_us += now_us() - t;
+        }
+        orc_dec_us /= iters;
+        for (unsigned i = 0; i < ne; ++i) bad += std::memcmp(list[locs[i]], keep[i].data(), vec) != 0;
     }
     std::printf("{\"kind\": \"%s\", \"k\": %u, \"m\": %u, \"vec\": %u, \"erasures\": %u, \"iters\": %u, "
                 "\"encode_us_per_call\": %.2f, \"encode_gpu_us_per_call\": %.2f, \"encode_path\": \"%s\", "
