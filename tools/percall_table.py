@@ -12,7 +12,7 @@ def fmt(v):
         return "—"
     if v < 1:
         return f"{v:.2f}"
-    if v < 10:
+    if v < 100:
         return f"{v:.1f}"
     if v < 1000:
         return f"{v:.0f}"
