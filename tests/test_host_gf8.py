@@ -250,3 +250,18 @@ def test_gf_dot_bad_arguments():
     nul = (ctypes.c_void_p * 1)(None)
     assert N.lib().nfec_gf_dot_host(8, dst.ctypes.data, nul, co.ctypes.data, 1, 8, 0, -1) == N.NFEC_EINVAL
     assert N.lib().nfec_gf_dot_host(8, dst.ctypes.data, arr, co.ctypes.data, 1, 8, 0, 7) == N.NFEC_EINVAL
+
+
+def test_percall_table_regenerates():
+    """tools/percall_table.py turns the committed per-call measurements into INTEGRATION.md's
+    table: the rows it writes are the ones the document holds"""
+    import os
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    out = subprocess.run([sys.executable, os.path.join(root, "tools", "percall_table.py")], capture_output=True,
+                         text=True, timeout=60)
+    assert out.returncode == 0, out.stderr
+    doc = open(os.path.join(root, "INTEGRATION.md")).read()
+    assert out.stdout.strip() in doc
