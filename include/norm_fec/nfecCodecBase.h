@@ -17,13 +17,13 @@ class NfecCodecBase
     static void SetDevice(int device) { default_device = device; }
     static int GetDevice() { return default_device; }
     // Where Encode runs, the incremental sender's per-segment call (normObject.cpp:2038-2052):
-    // on the host CPU (default; nfec_encode_segment_host, about a microsecond per 1.4 KB
+    // on the host CPU (default; nfec_encode_segment_host, under a microsecond per 1.4 KB
     // segment) or as a GPU round trip (nfec_encode_segment, ~20-160 us).
     static void SetSegmentEncodeOnHost(bool on) { segment_on_host = on; }
     static bool GetSegmentEncodeOnHost() { return segment_on_host; }
     // Where a one-block Decode runs (NormSenderNode::Decode, normNode.h:484-487): on the host
-    // CPU when nfec_decode_host_preferred says it is faster (default: RS8, small RS16), else on
-    // the GPU (nfec_decode_vectors).  The batch calls always use the GPU.
+    // CPU (default, nfec_decode_vectors_host) unless nfec_decode_host_preferred finds the repair
+    // too large for it, else on the GPU (nfec_decode_vectors).  The batch calls always use the GPU.
     static void SetDecodeOnHost(bool on) { decode_on_host = on; }
     static bool GetDecodeOnHost() { return decode_on_host; }
     nfec_codec* Handle() const { return codec; }
