@@ -9,7 +9,9 @@
 //   Init   -> false when numData + numParity > 255 or no gfx950 device is usable
 //   Encode -> parity_i ^= G[k+i][segmentId] * data (normEncoderRS8.cpp:473-483)
 //   Decode -> erasureCount on success, 0 when the block cannot be repaired (:652-757)
-// Every call runs on the GPU through include/nfec.h; per-call Encode/Decode are synchronous.
+// Calls go through include/nfec.h and are synchronous.  Batches run on the GPU; the per-call
+// Encode / Decode run on the host CPU by default (NfecCodecBase::SetSegmentEncodeOnHost /
+// SetDecodeOnHost select the GPU round trip instead).
 #ifndef _NORM_ENCODER_RS8
 #define _NORM_ENCODER_RS8
 

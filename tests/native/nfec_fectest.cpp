@@ -125,6 +125,12 @@ int main(int argc, char* argv[])
 
     if (std::strcmp(kind, "rs8") && std::strcmp(kind, "rs16") && std::strcmp(kind, "mdp")) return 2;
     if (nd == 0 || nd > k) return 2;
+    // NFEC_FECTEST_GPU=1: the per-call GPU round trips instead of the drop-in's host defaults
+    if (const char* g = std::getenv("NFEC_FECTEST_GPU"))
+        if (std::atoi(g) != 0) {
+            NfecCodecBase::SetSegmentEncodeOnHost(false);
+            NfecCodecBase::SetDecodeOnHost(false);
+        }
     NormEncoder* encoder = new_encoder(kind, k, m, vec);
     NormDecoder* decoder = new_decoder(kind, k, m, vec);
     if (!encoder || !decoder) {

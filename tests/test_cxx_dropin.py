@@ -83,8 +83,10 @@ CASES = [
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("gpu_calls", [False, True])
 @pytest.mark.parametrize("kind,k,m,vec,nd,locs,nullpar,src", CASES)
-def test_fectest_matches_oracle(orc, tmp_path, kind, k, m, vec, nd, locs, nullpar, src):
+def test_fectest_matches_oracle(orc, tmp_path, kind, k, m, vec, nd, locs, nullpar, src, gpu_calls):
+    """gpu_calls: the per-call GPU round trips (NFEC_FECTEST_GPU=1) instead of the host defaults"""
     n = nd + m
     if src == "-":
         data = np.zeros((nd, vec), np.uint8)
@@ -96,8 +98,9 @@ def test_fectest_matches_oracle(orc, tmp_path, kind, k, m, vec, nd, locs, nullpa
         inp = str(tmp_path / "in.bin")
         data.tofile(inp)
     out = tmp_path / "out.bin"
+    env = dict(os.environ, NFEC_FECTEST_GPU="1" if gpu_calls else "0")
     r = subprocess.run([EXE, kind, str(k), str(m), str(vec), str(nd), inp, str(out), str(int(nullpar))]
-                       + [str(x) for x in locs], capture_output=True, text=True, timeout=120)
+                       + [str(x) for x in locs], capture_output=True, text=True, timeout=120, env=env)
     dump = np.fromfile(out, np.uint8)
     assert dump.size == 2 * n * vec + 4, r.stderr
     assert "layout_errors=0" in r.stderr, r.stderr  # inline accessors and sizeof agree with the library
