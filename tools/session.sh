@@ -1,0 +1,92 @@
+#!/bin/bash
+# The one GPU session script (round 5 on): each named task runs under its own time limit and the
+# first failure ends the script (no retries).  Output under gpurun_out/$TAG/; the summaries that
+# are judged get copied into profiles/r0N/ by hand afterwards.
+#
+#   TAG=r05a bash tools/session.sh suite bench rs16 ...
+#
+# tasks
+#   suite      pytest -m gpu (the whole GPU suite; PYTEST_K narrows it with a -k expression)
+#   bench      bench.py line, then rocprofv3 --kernel-trace --stats of bench.py --steps 10
+#   rs16       RS16(400,100) 50-erasure repair per 16k blocks under rocprofv3 kernel traces:
+#              source loss, uniform loss over all k + m segments, shortened batches (numData in
+#              [k/2, k]), accumulate, and vec 1460 (vec % 8 != 0); one JSON line each
+#   c4         C4 RS16(4096,256) encode line (with its op roofline) under a kernel trace
+#   pmc_rs16   PMC passes of RS16(400,100) (tools/pmc_r03.sh; instruction mix, cycles, HBM bytes)
+#   pmc_c4     PMC passes of C4 (tools/pmc_c4.sh)
+#   pmc_bench  PMC passes of the headline workload (tools/pmc_r03.sh: HBM bytes for bench.py)
+#   mdp        MDP(64,32) encode + 16-erasure repair line
+#   rs8sweep   RS8 shape sweep (tools/bench_extra.py --workload rs8sweep) under a kernel trace
+#   c5         tools/bench_c5.py --steps 2 (the C5 mix's one-GPU share)
+#   percall    tools/percall per-call latencies (needs tools/percall/_build/percall)
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+R=$(pwd)
+TAG=${TAG:-r05}
+O=$R/gpurun_out/$TAG
+mkdir -p "$O"
+export TMPDIR=/tmp
+
+die() { echo "session: $1 failed (rc $2)"; exit "$2"; }
+
+# rocprofv3 kernel trace + stats of one python command: $1 = name, rest = script and arguments
+prof() {
+    local name=$1; shift
+    (cd /tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/prof_$name" -o "$name" -- \
+        python3 "$@") > "$O/$name.json" 2> "$O/$name.err" || return $?
+    local st
+    st=$(find "$O/prof_$name" -name "${name}_kernel_stats.csv" -print -quit)
+    [ -n "$st" ] && cp "$st" "$O/${name}_kernel_stats.csv"
+    cat "$O/$name.json"
+}
+
+for task in "$@"; do
+    case $task in
+    suite)
+        timeout -k 10 900 python3 -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread \
+            -p no:cacheprovider ${PYTEST_K:+-k "$PYTEST_K"} > "$O/pytest_gpu.log" 2>&1
+        rc=$?
+        tail -n 5 "$O/pytest_gpu.log"
+        [ $rc -eq 0 ] || die suite $rc ;;
+    bench)
+        timeout -k 10 300 python3 bench.py > "$O/bench.json" 2> "$O/bench.err" || die bench $?
+        cat "$O/bench.json"
+        prof bench_k "$R/bench.py" --steps 10 --no-cpu-baseline --host-steps 0 > /dev/null || die bench_prof $? ;;
+    rs16)
+        X=$R/tools/bench_extra.py
+        prof rs16_source "$X" --workload rs16 || die rs16_source $?
+        prof rs16_uniform "$X" --workload rs16 --loss uniform || die rs16_uniform $?
+        prof rs16_short "$X" --workload rs16 --shortened || die rs16_short $?
+        prof rs16_short_uniform "$X" --workload rs16 --shortened --loss uniform || die rs16_short_uniform $?
+        prof rs16_acc "$X" --workload rs16 --accumulate || die rs16_acc $?
+        prof rs16_vec1460 "$X" --workload rs16 --vec 1460 || die rs16_vec1460 $?
+        prof rs16_vec1460_uniform "$X" --workload rs16 --vec 1460 --loss uniform || die rs16_vec1460_uniform $? ;;
+    c4)
+        prof c4 "$R/tools/bench_extra.py" --workload c4 || die c4 $? ;;
+    pmc_rs16)
+        PMC_SCRIPT=tools/bench_extra.py PMC_ARGS="--workload rs16 --steps 1 --warmup 1" \
+        PMC_GROUPS="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_BRANCH SQ_INSTS_LDS SQ_INSTS_SMEM SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR;SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_SCA;GRBM_GUI_ACTIVE GRBM_COUNT;FETCH_SIZE;WRITE_SIZE" \
+        TAG=${TAG}_rs16 timeout -k 10 900 bash tools/pmc_r03.sh > "$O/pmc_rs16.log" 2>&1 || die pmc_rs16 $?
+        cp "$R/gpurun_out/pmc_${TAG}_rs16/summary.json" "$O/pmc_rs16_summary.json" ;;
+    pmc_c4)
+        TAG=${TAG}_c4 timeout -k 10 900 bash tools/pmc_c4.sh > "$O/pmc_c4.log" 2>&1 || die pmc_c4 $?
+        cp "$R/gpurun_out/pmc_${TAG}_c4/summary.json" "$O/pmc_c4_summary.json" ;;
+    pmc_bench)
+        TAG=${TAG}_bench timeout -k 10 900 bash tools/pmc_r03.sh > "$O/pmc_bench.log" 2>&1 || die pmc_bench $?
+        cp "$R/gpurun_out/pmc_${TAG}_bench/summary.json" "$O/pmc_bench_summary.json" ;;
+    mdp)
+        timeout -k 10 300 python3 tools/bench_extra.py --workload mdp > "$O/mdp.json" 2> "$O/mdp.err" || die mdp $?
+        cat "$O/mdp.json" ;;
+    rs8sweep)
+        prof rs8sweep "$R/tools/bench_extra.py" --workload rs8sweep || die rs8sweep $? ;;
+    c5)
+        timeout -k 10 600 python3 tools/bench_c5.py --steps 2 > "$O/c5.json" 2> "$O/c5.err" || die c5 $?
+        cat "$O/c5.json" ;;
+    percall)
+        : > "$O/percall.jsonl"
+        for args in "rs8 64 32 1408 16 2000" "rs8 64 16 1408 8 2000" "rs8 16 4 1408 4 2000" "rs16 400 100 1400 50 200" "mdp 64 32 1408 16 500"; do
+            timeout -k 10 120 tools/percall/_build/percall $args >> "$O/percall.jsonl" || die percall $?
+        done ;;
+    *)
+        echo "session: unknown task $task"; exit 2 ;;
+    esac
+done
