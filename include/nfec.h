@@ -73,7 +73,7 @@ typedef struct nfec_codec nfec_codec;
 
 typedef struct nfec_codec_info {
     int32_t kind;         /* NFEC_RS8 / NFEC_RS16 / NFEC_MDP */
-    int32_t device;       /* HIP device ordinal the codec lives on */
+    int32_t device;       /* HIP device ordinal the codec lives on (-1: host-only codec) */
     uint32_t num_data;    /* k (ndata)  */
     uint32_t num_parity;  /* m (npar)   */
     uint32_t vector_size; /* bytes per segment vector processed (vectorSize given to Init) */
@@ -122,13 +122,18 @@ int nfec_codec_create(int device, int kind, uint32_t num_data, uint32_t num_pari
                       uint32_t vector_size, nfec_codec** out);
 
 /* Codec options (nfec_codec_config.flags): correct alternatives of the RS16 kernels, chosen per
- * codec (the tests run both; the defaults are the faster ones). */
+ * codec (the tests run both; the defaults are the faster ones), and a codec without a GPU. */
 enum {
     NFEC_OPT_RS16_SHARED_TABLES = 1u << 0, /* RS16 products on the shared-LDS-table kernel
                                               instead of the tower-field one */
     NFEC_OPT_RS16_TOEPLITZ_OFF = 1u << 1,  /* RS16 encode never uses the Toeplitz split */
-    NFEC_OPT_RS16_TOEPLITZ_ON = 1u << 2    /* ... uses it whenever the shape allows it, not
+    NFEC_OPT_RS16_TOEPLITZ_ON = 1u << 2,   /* ... uses it whenever the shape allows it, not
                                               only where it needs fewer passes */
+    NFEC_OPT_HOST_ONLY = 1u << 3           /* no device at all (a NORM node without a usable
+                                              gfx950): Init's math on the host, and only the host
+                                              per-call paths (nfec_encode_segment_host,
+                                              nfec_decode_vectors_host) run; every GPU entry
+                                              returns NFEC_EDEVICE.  No device list. */
 };
 
 /* One codec over one or several GPUs of a node.  With several devices the codec holds the

@@ -13,9 +13,23 @@
 class NfecCodecBase
 {
   public:
-    // GPU used by codecs created afterwards in this process (one process per GPU)
-    static void SetDevice(int device) { default_device = device; }
+    // GPU used by codecs created afterwards in this process (one process per GPU); clears a
+    // device list set by SetDevices
+    static void SetDevice(int device) { default_device = device; num_devices = 0; }
     static int GetDevice() { return default_device; }
+    // Several GPUs for codecs created afterwards (at most kMaxDevices; a device may repeat):
+    // Init creates one codec striped over them (nfec_codec_create_ex), so a single-process
+    // caller -- one NORM session's encoder (normSession.cpp:834-889) -- spreads its host batches
+    // over the node's GPUs in contiguous block ranges.  count <= 1 means SetDevice(devices[0]).
+    enum { kMaxDevices = 64 };
+    static bool SetDevices(const int* devices, int count);
+    static int GetDevices(int* devices, int cap);  // the list (count returned; 1: the one device)
+    // With no usable gfx950 device, Init still succeeds when both per-call paths are on the host
+    // (the defaults): the codec is host-only (NFEC_OPT_HOST_ONLY), Encode / Decode run on the CPU
+    // and the batch calls return NFEC_EDEVICE.  SetHostFallback(false) makes Init fail instead.
+    static void SetHostFallback(bool on) { host_fallback = on; }
+    static bool GetHostFallback() { return host_fallback; }
+    bool IsHostOnly() const;
     // Where Encode runs, the incremental sender's per-segment call (normObject.cpp:2038-2052):
     // on the host CPU (default; nfec_encode_segment_host, under a microsecond per 1.4 KB
     // segment) or as a GPU round trip (nfec_encode_segment, ~20-160 us).
@@ -43,8 +57,11 @@ class NfecCodecBase
     unsigned int npar;         // No. of parity packets (n-k)
     unsigned int vector_size;  // Size of biggest vector to encode
     static int default_device;
+    static int device_list[kMaxDevices];
+    static int num_devices;     // 0: default_device alone
     static bool segment_on_host;
     static bool decode_on_host;
+    static bool host_fallback;
 };
 
 #endif  // NFEC_CODEC_BASE_H

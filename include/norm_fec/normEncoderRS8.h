@@ -6,7 +6,8 @@
 // -I<nfec>/include/norm_fec ahead of NORM's include/ they compile against these declarations,
 // which the library's constructors and methods were compiled from too.
 // Public surface = the reference's (normEncoderRS8.h:10-22, :36-45):
-//   Init   -> false when numData + numParity > 255 or no gfx950 device is usable
+//   Init   -> false when numData + numParity > 255; without a usable gfx950 device it builds a
+//             host-only codec (per-call Encode / Decode on the CPU; NfecCodecBase::SetHostFallback)
 //   Encode -> parity_i ^= G[k+i][segmentId] * data (normEncoderRS8.cpp:473-483)
 //   Decode -> erasureCount on success, 0 when the block cannot be repaired (:652-757)
 // Calls go through include/nfec.h and are synchronous.  Batches run on the GPU; the per-call

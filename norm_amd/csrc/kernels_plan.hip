@@ -311,11 +311,15 @@ __global__ __launch_bounds__(kWave) void rs16_plan_cf_kernel(RsPlanArgs a)
         if (np_s < es) { ok = false; status = 0; }
     }
     const uint32_t e = ok ? es : 0;
-    const bool by_encode = a.rows1 && e > 0 && nd == k && listP[e - 1] == nd + e - 1;
+    // by_row (the tower decode): every block is repaired from the stage-1 encode's z rows
+    // 0..P_last (its last substitute parity row), the inverse laid out by parity row
+    const bool by_row = a.by_row && a.rows1 && e > 0;
+    const bool by_encode = by_row || (a.rows1 && e > 0 && nd == k && listP[e - 1] == nd + e - 1);
+    const uint32_t ncol = by_row ? (uint32_t)listP[e - 1] - nd + 1u : e;  // stage-2 columns
     if (lane == 0) {
         if (a.status) a.status[b] = status;
         a.rows[b] = (int32_t)e;
-        a.cols2[b] = (uint16_t)e;
+        a.cols2[b] = (uint16_t)ncol;
         if (a.rows1) a.rows1[b] = by_encode ? 0 : (int32_t)e;
     }
     if (e == 0) return;
@@ -369,28 +373,55 @@ __global__ __launch_bounds__(kWave) void rs16_plan_cf_kernel(RsPlanArgs a)
         lB[i] = bcc < 0 ? bcc + q : bcc;
     }
     __syncthreads();
-    uint16_t* coef2 = reinterpret_cast<uint16_t*>(a.coef2) + (uint64_t)b * cs * cs;
-    for (uint32_t idx = lane; idx < cs * cs; idx += kWave) {
-        const uint32_t t = idx / cs, s = idx % cs;  // column t (input z_t), row s (output)
-        uint16_t v = 0;
-        if (t < e && s < e) {
-            int32_t l = lA[s] + lB[t] - (int32_t)lg[xs[s] ^ yt[t]];
-            l %= q;
-            if (l < 0) l += q;
-            v = ex[l];
+    uint16_t* coef2 = reinterpret_cast<uint16_t*>(a.coef2) + (uint64_t)b * (a.coef2_block ? a.coef2_block : (uint64_t)cs * cs);
+    if (by_row) {
+        // column = parity row P_t - nd (z row), rows s < e; the lost parity rows below P_last
+        // get zero columns
+        for (uint32_t idx = lane; idx < ncol * e; idx += kWave) {
+            const uint32_t col = idx / e, s = idx - col * e;
+            uint32_t lo = 0, hi = e;  // first t with listP[t] - nd >= col
+            while (lo < hi) {
+                const uint32_t mid = (lo + hi) >> 1;
+                if ((uint32_t)listP[mid] - nd < col) lo = mid + 1;
+                else hi = mid;
+            }
+            uint16_t v = 0;
+            if (lo < e && (uint32_t)listP[lo] - nd == col) {
+                int32_t l = lA[s] + lB[lo] - (int32_t)lg[xs[s] ^ yt[lo]];
+                l %= q;
+                if (l < 0) l += q;
+                v = ex[l];
+            }
+            coef2[(uint64_t)col * cs + s] = v;
         }
-        coef2[idx] = v;
+    } else {
+        for (uint32_t idx = lane; idx < cs * cs; idx += kWave) {
+            const uint32_t t = idx / cs, s = idx % cs;  // column t (input z_t), row s (output)
+            uint16_t v = 0;
+            if (t < e && s < e) {
+                int32_t l = lA[s] + lB[t] - (int32_t)lg[xs[s] ^ yt[t]];
+                l %= q;
+                if (l < 0) l += q;
+                v = ex[l];
+            }
+            coef2[idx] = v;
+        }
     }
     uint16_t* oslots = a.out_slots2 + (uint64_t)b * k;
     for (uint32_t s = lane; s < e; s += kWave) oslots[s] = listE[s];
     if (by_encode) {
-        // the stage-1 encode reads every source slot: the erased ones must read as zero
-        if (lane == 0) atomicMax(a.rmax, e);
+        // stage 1 computes z rows 0..ncol - 1; in overwrite mode the encode must read the erased
+        // source as zero (zero_base), with accumulate it reads their contents X and stage 2,
+        // writing A^-1 z = d_E ^ X over them, gives exactly the reference's XOR
+        if (lane == 0) atomicMax(a.rmax, ncol);
+        if (!a.zero_base) return;
         uint8_t* blk = a.zero_base + (uint64_t)b * a.zero_block_stride;
-        const uint32_t words = a.zero_vec >> 3;
+        // zero_vec: the even byte count of the symbols (a tail past the last 8-byte word too)
+        const uint32_t words = a.zero_vec >> 3, tail = (a.zero_vec & 7u) >> 1;
         for (uint32_t s = 0; s < e; ++s) {
             uint2* p = reinterpret_cast<uint2*>(blk + (uint64_t)listE[s] * a.zero_seg_stride);
             for (uint32_t w = lane; w < words; w += kWave) p[w] = make_uint2(0u, 0u);
+            if (lane < tail) reinterpret_cast<uint16_t*>(p + words)[lane] = 0;
         }
     }
 }

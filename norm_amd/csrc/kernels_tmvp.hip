@@ -153,8 +153,8 @@ namespace {
 // A^-1 (coef2, column t = z row t, row s = erased output s) becomes the kernel's snippet table
 // [t][sweep][s][2] as gf16_tw_offsets lays out an encode's generator (the kernel spreads the
 // block's e rows over its passes itself), and the output rows' byte offsets row_off[b][s] =
-// erased slot s * seg_stride.  One workgroup per block; columns and rows at or past the block's
-// e are never read.
+// erased slot s * seg_stride.  One workgroup per block; columns at or past the block's column
+// count (cols[b], else e) and rows at or past its e are never read.
 __device__ __forceinline__ uint32_t gf8_mul_11d(uint32_t a, uint32_t b)
 {
     uint32_t r = 0;
@@ -176,10 +176,11 @@ __global__ __launch_bounds__(256) void tw_dec_tables_kernel(TwDecTablesArgs a)
     for (uint32_t r = threadIdx.x; r < a.M + 12u; r += blockDim.x)
         ro[r] = (int32_t)r < e ? (uint32_t)a.out_slots[(uint64_t)b * a.slots_stride + r] * a.seg_stride : 0u;
     if (e <= 0) return;
-    const uint32_t ue = (uint32_t)e;
-    for (uint32_t idx = threadIdx.x; idx < ue * ue; idx += blockDim.x) {
+    const uint32_t ue = (uint32_t)e, nc = a.cols ? (uint32_t)a.cols[b] : ue;
+    const uint16_t* c2 = a.coef2 + (uint64_t)b * (a.coef2_block ? a.coef2_block : (uint64_t)a.dcs * a.dcs);
+    for (uint32_t idx = threadIdx.x; idx < nc * ue; idx += blockDim.x) {
         const uint32_t t = idx / ue, row = idx - t * ue;
-        const uint32_t g = a.coef2[((uint64_t)b * a.dcs + t) * a.dcs + row];
+        const uint32_t g = c2[(uint64_t)t * a.dcs + row];
         uint32_t tt = 0;
 #pragma unroll
         for (int k = 0; k < 16; ++k)

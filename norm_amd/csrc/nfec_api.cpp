@@ -221,6 +221,8 @@ struct nfec_codec {
     // RS16 products by the tower-field kernel (gen_gf16_tw.hip) instead of the shared-table one:
     // snippet offsets [k][gf16_tw_passes(m)][48]; the Toeplitz split's three products likewise
     bool tw = false;
+    // NFEC_OPT_HOST_ONLY: no device, no device tables; only the host per-call paths run
+    bool host_only = false;
     DevBuf<uint16_t> d_twoff, d_tmvp_tw;
     // RS16 encode by the Toeplitz split (kernels_tmvp.hip): offsets of the three products, each
     // [k/2+1][m_pad(m/2)][48], then the constants' row masks (c_j [k][16], W [m][16], G0 [m][16])
@@ -303,9 +305,15 @@ int upload(DevBuf<uint8_t>& d, const void* src, size_t bytes)
     return NFEC_OK;
 }
 
+int host_only_fail()
+{
+    return fail(NFEC_EDEVICE, "host-only codec (NFEC_OPT_HOST_ONLY): no GPU path");
+}
+
 int check_batch(const nfec_codec* c, const nfec_block_batch* b)
 {
     if (!c || !b) return fail(NFEC_EINVAL, "null codec or batch");
+    if (c->host_only) return host_only_fail();
     if (b->nblocks == 0) return NFEC_OK;
     if (!b->blocks) return fail(NFEC_EINVAL, "null blocks pointer");
     if ((reinterpret_cast<uintptr_t>(b->blocks) & 7) || (b->seg_stride & 7) || (b->block_stride & 7))
@@ -338,13 +346,74 @@ static int launch_rs16_product(const nfec_codec* c, const Gf16T3Args& t, hipStre
     return c->tw ? launch_gf16_tw_encode(t, s) : launch_gf16_t3_encode(t, s);
 }
 
+// one RS16 product on the tower kernel over a whole vector of t.vec_bytes (even) bytes: its
+// 8-byte pieces on the tower kernel, the 2-6 byte tail past them on the tail kernel
+// (kernels_gf16tail.hip), so any NORM vector size (segmentSize + 8) stays off the exp-table kernel
+static bool rs16_tw_full_covers(const Gf16T3Args& t)
+{
+    const uint32_t even = t.vec_bytes & ~1u, body = even & ~7u;
+    if (even == 0) return false;
+    Gf16T3Args b = t;
+    b.vec_bytes = body;
+    return (body == 0 || gf16_tw_covers(b)) && gf16_tw_tail_covers(t, even - body);
+}
+
+static int launch_rs16_tw_full(const Gf16T3Args& t, hipStream_t s)
+{
+    const uint32_t even = t.vec_bytes & ~1u, body = even & ~7u;
+    if (body) {
+        Gf16T3Args b = t;
+        b.vec_bytes = body;
+        const int rc = launch_gf16_tw_encode(b, s);
+        if (rc) return rc;
+    }
+    return launch_gf16_tw_tail(t, body, even - body, s);
+}
+
 // ---- codec construction ----
+// log W'(x_j) over the k source points and log W(y_p) at the parity points: the constants of
+// the closed-form plans (rs_plan2_kernel for RS8, rs16_plan_cf_kernel for RS16, the host repair)
+static void plan_constants(nfec_codec* c, const Field& f)
+{
+    std::vector<uint16_t> lwp(c->k), lw(c->m);
+    std::vector<uint32_t> pt(c->k + c->m);
+    for (uint32_t j = 0; j < c->k + c->m; ++j) pt[j] = rs_point(f, j);
+    for (uint32_t j = 0; j < c->k; ++j) {
+        uint64_t acc = 0;
+        for (uint32_t l = 0; l < c->k; ++l)
+            if (l != j) acc += f.log[pt[j] ^ pt[l]];
+        lwp[j] = (uint16_t)(acc % f.q);
+    }
+    for (uint32_t p = 0; p < c->m; ++p) {
+        uint64_t acc = 0;
+        for (uint32_t l = 0; l < c->k; ++l) acc += f.log[pt[c->k + p] ^ pt[l]];
+        lw[p] = (uint16_t)(acc % f.q);
+    }
+    c->h_lwp = lwp;
+    c->h_lw = lw;
+}
+
 int build_codec(nfec_codec* c)
 {
     const bool wide = c->kind == NFEC_RS16;
     c->sym = wide ? 2 : 1;
     c->cs = round_up(std::max(c->m, 1u), kRowPad);
     const Field& f = wide ? gf16() : gf8();
+    if (c->host_only) {
+        // what the host per-call paths read: the generator (MDP: the polynomial and the full
+        // block's LFSR map) and the closed-form plan constants
+        if (c->kind == NFEC_MDP) {
+            if (c->k + c->m > 255 || c->m == 0) return fail(NFEC_ERANGE, "MDP: numData + numParity > 255");
+            mdp_generator_poly(c->m, c->mdp_g);
+            std::vector<uint8_t> map((size_t)c->m * c->k);
+            mdp_encode_matrix(c->mdp_g, c->m, c->k, map.data());
+            c->gen.assign(map.begin(), map.end());
+            return NFEC_OK;
+        }
+        if (rs_generator(wide ? 16 : 8, c->k, c->m, c->gen)) return fail(NFEC_ERANGE, "RS: numData/numParity exceeds code limits");
+        if (!wide || std::min(c->k, c->m) <= kPlanCfMaxE) plan_constants(c, f);
+        return NFEC_OK;
+    }
     if (c->kind == NFEC_MDP) {
         if (c->k + c->m > 255 || c->m == 0) return fail(NFEC_ERANGE, "MDP: numData + numParity > 255");
         std::vector<uint8_t> g;
@@ -479,28 +548,11 @@ int build_codec(nfec_codec* c)
             }
         }
         if (!wide || std::min(c->k, c->m) <= kPlanCfMaxE) {
-            // log W'(x_j) over the k source points and log W(y_p) at the parity points (the
-            // closed-form plans: rs_plan2_kernel for RS8, rs16_plan_cf_kernel for RS16)
-            std::vector<uint16_t> lwp(c->k), lw(c->m);
-            std::vector<uint32_t> pt(c->k + c->m);
-            for (uint32_t j = 0; j < c->k + c->m; ++j) pt[j] = rs_point(f, j);
-            for (uint32_t j = 0; j < c->k; ++j) {
-                uint64_t acc = 0;
-                for (uint32_t l = 0; l < c->k; ++l)
-                    if (l != j) acc += f.log[pt[j] ^ pt[l]];
-                lwp[j] = (uint16_t)(acc % f.q);
-            }
-            for (uint32_t p = 0; p < c->m; ++p) {
-                uint64_t acc = 0;
-                for (uint32_t l = 0; l < c->k; ++l) acc += f.log[pt[c->k + p] ^ pt[l]];
-                lw[p] = (uint16_t)(acc % f.q);
-            }
-            c->h_lwp = lwp;
-            c->h_lw = lw;
+            plan_constants(c, f);
             if ((rc = c->d_lwp.reserve(c->k))) return rc;
             if ((rc = c->d_lw.reserve(c->m))) return rc;
-            NFEC_HIP(hipMemcpy(c->d_lwp.p, lwp.data(), lwp.size() * 2, hipMemcpyHostToDevice));
-            NFEC_HIP(hipMemcpy(c->d_lw.p, lw.data(), lw.size() * 2, hipMemcpyHostToDevice));
+            NFEC_HIP(hipMemcpy(c->d_lwp.p, c->h_lwp.data(), c->h_lwp.size() * 2, hipMemcpyHostToDevice));
+            NFEC_HIP(hipMemcpy(c->d_lw.p, c->h_lw.data(), c->h_lw.size() * 2, hipMemcpyHostToDevice));
         }
     }
     // field tables
@@ -792,12 +844,16 @@ int encode_device(nfec_codec* c, const nfec_block_batch* b, hipStream_t s)
             const int rc = rs16_tmvp_encode(c, b, s);
             if (rc != NFEC_ENOTSUP) return rc;
         }
-        if ((c->d_t3off.p || c->tw) && !b->num_data) {
+        if (c->tw || (c->d_t3off.p && !b->num_data)) {
+            // the tower kernel takes shortened batches (numData masking per 8-byte piece, parity at
+            // slot numData + r) and any even vector size (tail kernel); the shared-table kernel
+            // unshortened batches with vec % 8 = 0 only
             Gf16T3Args t;
             t.base = static_cast<const uint8_t*>(b->blocks);
             t.block_stride = b->block_stride;
             t.seg_stride = b->seg_stride;
             t.nblocks = b->nblocks;
+            t.num_data = c->tw ? b->num_data : nullptr;
             t.k = c->k;
             t.m = c->m;
             t.m_pad = gf16_t3_rows_padded(c->m);
@@ -805,7 +861,8 @@ int encode_device(nfec_codec* c, const nfec_block_batch* b, hipStream_t s)
             t.offs = c->d_t3off.p;
             t.tw = c->d_twoff.p;
             t.accumulate = acc;
-            const int rc = launch_rs16_product(c, t, s);
+            const int rc = !c->tw ? launch_rs16_product(c, t, s)
+                           : rs16_tw_full_covers(t) ? launch_rs16_tw_full(t, s) : NFEC_ENOTSUP;
             if (rc != NFEC_ENOTSUP) return rc;
         }
         if (use_bs16 && c->d_sel16.p) {
@@ -898,6 +955,185 @@ int encode_device(nfec_codec* c, const nfec_block_batch* b, hipStream_t s)
     return launch_gf8_matmul(a, false, s);
 }
 
+// ---- RS16 decode on the tower kernel, every block ----
+// The reference replaces each erased source row of its decoding matrix by the generator row of
+// the next surviving parity (normEncoderRS16.cpp:658-716; shortened blocks :675-693) and applies
+// the inverse's erased rows (:726-753).  Here, per block, with P_t the substitute parity rows
+// and P_last the last of them:
+//   stage 1 (flat, the encode itself): z_r = parity row r ^ sum_{c < nd} G[r][c] d_c for every
+//           r <= P_last of any block (rows_lim = the batch's largest P_last + 1), with the erased
+//           source read as zero (the plan zeroes it) -- so z_{P_t} = sum_s G[P_t][E_s] d_{E_s};
+//           shortened blocks mask their columns at numData per 8-byte piece and read their
+//           parity at slot numData + r;
+//   stage 2 (per block): d_E = A^-1 z over the block's z rows 0..P_last, the inverse laid out by
+//           parity row (columns of lost parity rows are zero), written over the erased source.
+// With NFEC_ACCUMULATE the erased source is not zeroed: stage 1 then reads its contents X and
+// z = A (d_E ^ X), so stage 2's A^-1 z = d_E ^ X written over X is the reference's XOR.  Lost
+// parity (uniform loss), shortened blocks, accumulate and any even vector size (the tail kernel)
+// all run here; the round-2 exp-table kernel is left for layouts past the tower kernel's 2^31
+// offsets and codecs on the shared-table kernel.
+static bool rs16_twdec_covers(const nfec_codec* c, const nfec_block_batch* b)
+{
+    static const bool on = diag_knob("NFEC_RS16_TWDEC", 1) != 0;
+    if (!on || c->kind != NFEC_RS16 || !c->tw || !c->d_lwp.p || std::min(c->k, c->m) > kPlanCfMaxE) return false;
+    const uint32_t zstride = round_up(c->vec, 8);
+    Gf16T3Args t1;  // stage 1's layout (one block: the bounds do not depend on the count)
+    t1.base = static_cast<const uint8_t*>(b->blocks);
+    t1.block_stride = b->block_stride;
+    t1.seg_stride = b->seg_stride;
+    t1.nblocks = 1;
+    t1.num_data = b->num_data;
+    t1.k = c->k;
+    t1.m = c->m;
+    t1.vec_bytes = c->vec & ~1u;
+    t1.tw = c->d_twoff.p;
+    t1.accumulate = 1;
+    t1.out_base = reinterpret_cast<uint8_t*>(16);  // (any non-null: the z rows' layout)
+    t1.out_block_stride = (uint64_t)c->m * zstride;
+    t1.out_seg_stride = zstride;
+    t1.acc_base = t1.base;
+    t1.acc_block_stride = b->block_stride;
+    t1.acc_seg_stride = b->seg_stride;
+    t1.acc_slot0 = b->num_data ? 0u : c->k;
+    t1.acc_after_data = b->num_data ? 1u : 0u;
+    // stage 2 writes 32-bit row offsets (erased slot * seg_stride)
+    return rs16_tw_full_covers(t1) && (uint64_t)(c->k + c->m) * b->seg_stride + c->vec < (1ull << 31);
+}
+
+static int decode_rs16_tw(nfec_codec* c, const nfec_block_batch* b, const uint16_t* locs, uint32_t lstride,
+                          const uint16_t* counts, int32_t* status, hipStream_t s)
+{
+    const bool acc = b->flags & NFEC_ACCUMULATE;
+    const uint32_t zstride = round_up(c->vec, 8);
+    const uint32_t M2 = std::min(c->k, c->m);              // erased source rows at most
+    const uint32_t dcs = round_up(std::max(1u, M2), kRowPad);
+    const uint64_t zblk = (uint64_t)c->m * zstride;        // z rows 0..m-1
+    const uint64_t c2blk = (uint64_t)c->m * dcs;           // inverse by parity row: [m][dcs]
+    const size_t tw2_elems = gf16_tw_table_elems(c->m, M2);  // stage-2 table: m columns, M2 rows
+    const uint64_t per_block = zblk + 2ull * c2blk + 2ull * tw2_elems + 4ull * (M2 + 12) + 2ull * c->k + 64;
+    uint32_t cap = std::min(b->nblocks, sub_batch(per_block, 8ull << 30, 65536u));
+    const uint64_t held = c->w_z.n + c->w_coef2.n + 2ull * c->w_tw2.n;
+    if ((uint64_t)cap * per_block > held) {
+        size_t free_b = 0, total_b = 0;
+        if (hipMemGetInfo(&free_b, &total_b) == hipSuccess)
+            cap = std::min(cap, sub_batch(per_block, ((uint64_t)free_b + held) / 2, 65536u));
+        else
+            (void)hipGetLastError();
+    }
+    const uint32_t npass = (b->nblocks + cap - 1) / std::max(cap, 1u);
+    const uint32_t sb = std::max(1u, (b->nblocks + npass - 1) / std::max(npass, 1u));
+    int rc;
+    if ((rc = c->w_rows.reserve(sb))) return rc;
+    if ((rc = c->w_rows1.reserve(sb))) return rc;
+    if ((rc = c->w_cols.reserve(sb))) return rc;
+    if ((rc = c->w_rmax.reserve(1))) return rc;
+    if (!status && (rc = c->w_status.reserve(sb))) return rc;
+    if ((rc = c->w_oslots.reserve((size_t)sb * c->k + 128))) return rc;
+    if ((rc = c->w_z.reserve((size_t)sb * zblk))) return rc;
+    if ((rc = c->w_coef2.reserve((size_t)sb * c2blk * 2))) return rc;
+    if ((rc = c->w_tw2.reserve((size_t)sb * tw2_elems))) return rc;
+    if ((rc = c->w_rowoff.reserve((size_t)sb * (M2 + 12)))) return rc;
+    uint16_t phi[16];
+    uint32_t lam = 0;
+    gf16_tw_field(phi, &lam);
+    for (uint32_t b0 = 0; b0 < b->nblocks; b0 += sb) {
+        const uint32_t nb = std::min(sb, b->nblocks - b0);
+        uint8_t* blocks = static_cast<uint8_t*>(b->blocks) + (uint64_t)b0 * b->block_stride;
+        const uint16_t* nd = b->num_data ? b->num_data + b0 : nullptr;
+        int32_t* st = status ? status + b0 : c->w_status.p;
+        NFEC_HIP(hipMemsetAsync(c->w_rmax.p, 0, sizeof(uint32_t), s));
+        RsPlanArgs p;
+        p.bits = 16;
+        p.k = c->k;
+        p.m = c->m;
+        p.nblocks = nb;
+        p.num_data = nd;
+        p.erasure_locs = locs + (uint64_t)b0 * lstride;
+        p.erasure_stride = lstride;
+        p.erasure_counts = counts + b0;
+        p.gen_parity = c->d_gen.p;
+        p.exp_tab = c->d_exp.p;
+        p.log_tab = c->d_log.p;
+        p.status = st;
+        p.rows = c->w_rows.p;
+        p.out_slots2 = c->w_oslots.p;
+        p.cols2 = c->w_cols.p;
+        p.coef_stride = dcs;
+        p.coef2 = c->w_coef2.p;
+        p.coef2_block = c2blk;
+        p.lwp = c->d_lwp.p;
+        p.lw = c->d_lw.p;
+        p.by_row = 1;
+        p.rows1 = c->w_rows1.p;
+        p.rmax = c->w_rmax.p;
+        p.zero_base = acc ? nullptr : blocks;
+        p.zero_block_stride = b->block_stride;
+        p.zero_seg_stride = b->seg_stride;
+        p.zero_vec = c->vec & ~1u;
+        if ((rc = launch_rs_plan(p, s))) return rc;
+        // stage 1: z rows 0..rows_lim-1 of every block by the encode, XORed with its parity rows
+        Gf16T3Args t;
+        t.base = blocks;
+        t.block_stride = b->block_stride;
+        t.seg_stride = b->seg_stride;
+        t.nblocks = nb;
+        t.num_data = nd;
+        t.k = c->k;
+        t.m = c->m;
+        t.vec_bytes = c->vec & ~1u;
+        t.tw = c->d_twoff.p;
+        t.accumulate = 1;
+        t.out_base = c->w_z.p;
+        t.out_block_stride = zblk;
+        t.out_seg_stride = zstride;
+        t.out_slot0 = 0;
+        t.acc_base = blocks;
+        t.acc_block_stride = b->block_stride;
+        t.acc_seg_stride = b->seg_stride;
+        t.acc_slot0 = nd ? 0u : c->k;
+        t.acc_after_data = nd ? 1u : 0u;
+        t.rows_lim = c->w_rmax.p;
+        if ((rc = launch_rs16_tw_full(t, s))) return rc == NFEC_ENOTSUP ? fail(NFEC_EDEVICE, "tower decode stage 1") : rc;
+        // stage 2: the per-block tables of A^-1 by parity row, then d_E = A^-1 z
+        TwDecTablesArgs d;
+        d.coef2 = reinterpret_cast<const uint16_t*>(c->w_coef2.p);
+        d.dcs = dcs;
+        d.coef2_block = c2blk;
+        d.rows = c->w_rows.p;
+        d.cols = c->w_cols.p;
+        d.out_slots = c->w_oslots.p;
+        d.slots_stride = c->k;
+        d.seg_stride = b->seg_stride;
+        d.nblocks = nb;
+        d.M = M2;
+        d.tw = c->w_tw2.p;
+        d.tw_block_stride = tw2_elems;
+        d.row_off = c->w_rowoff.p;
+        std::copy(phi, phi + 16, d.phi);
+        d.lam = lam;
+        if ((rc = launch_tw_dec_tables(d, s))) return rc;
+        Gf16T3Args t2;
+        t2.base = c->w_z.p;
+        t2.block_stride = zblk;
+        t2.seg_stride = zstride;
+        t2.nblocks = nb;
+        t2.k = c->m;   // columns: z rows 0..P_last (blk_cols)
+        t2.m = M2;     // rows: the block's e erased source (blk_rows)
+        t2.vec_bytes = c->vec & ~1u;
+        t2.tw = c->w_tw2.p;
+        t2.tw_block_stride = tw2_elems;
+        t2.blk_rows = c->w_rows.p;
+        t2.blk_cols = c->w_cols.p;
+        t2.row_off = c->w_rowoff.p;
+        t2.row_off_stride = M2 + 12;
+        t2.out_base = blocks;
+        t2.out_block_stride = b->block_stride;
+        t2.out_seg_stride = b->seg_stride;
+        if ((rc = launch_rs16_tw_full(t2, s))) return rc == NFEC_ENOTSUP ? fail(NFEC_EDEVICE, "tower decode stage 2") : rc;
+    }
+    return NFEC_OK;
+}
+
 // ---- decode on a device batch ----
 // caller_locked: the caller already holds c->mu (nfec_decode_vectors keeps it for the whole
 // per-call decode, staging included)
@@ -909,6 +1145,7 @@ int decode_device(nfec_codec* c, const nfec_block_batch* b, const uint16_t* locs
     if (c->kind == NFEC_MDP && acc) return fail(NFEC_ENOTSUP, "MDP decode requires zero-filled erased segments");
     std::unique_lock<std::mutex> lk(c->mu, std::defer_lock);
     if (!caller_locked) lk.lock();
+    if (rs16_twdec_covers(c, b)) return decode_rs16_tw(c, b, locs, lstride, counts, status, s);
     const uint32_t n = c->k + c->m;
     const uint32_t zstride = round_up(c->vec, 8);
     // RS decode rows: at most min(k, m) source erasures are solved per block, so the plan's
@@ -1512,6 +1749,22 @@ namespace {
 int create_one(int device, int kind, uint32_t num_data, uint32_t num_parity, uint32_t vector_size, uint32_t opts,
                nfec_codec** out)
 {
+    if (opts & NFEC_OPT_HOST_ONLY) {
+        // no device is touched: Init's math and the host per-call paths only
+        std::unique_ptr<nfec_codec> c(new nfec_codec);
+        c->kind = kind;
+        c->device = -1;
+        c->opts = opts;
+        c->k = num_data;
+        c->m = num_parity;
+        c->vec = vector_size;
+        c->host_only = true;
+        c->async.device = -1;
+        const int rc = build_codec(c.get());
+        if (rc) return rc;
+        *out = c.release();
+        return NFEC_OK;
+    }
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev) {
         (void)hipGetLastError();
@@ -1580,8 +1833,11 @@ int nfec_codec_create_ex(const nfec_codec_config* cfg, nfec_codec** out)
     if (kind != NFEC_RS8 && kind != NFEC_RS16 && kind != NFEC_MDP) return fail(NFEC_EINVAL, "unknown codec kind");
     if (cfg->num_data == 0 || cfg->num_parity == 0) return fail(NFEC_EINVAL, "numData and numParity must be > 0");
     if (cfg->vector_size == 0 || cfg->vector_size > 65535) return fail(NFEC_EINVAL, "vectorSize must be in [1, 65535]");
-    if (cfg->flags & ~(uint32_t)(NFEC_OPT_RS16_SHARED_TABLES | NFEC_OPT_RS16_TOEPLITZ_OFF | NFEC_OPT_RS16_TOEPLITZ_ON))
+    if (cfg->flags & ~(uint32_t)(NFEC_OPT_RS16_SHARED_TABLES | NFEC_OPT_RS16_TOEPLITZ_OFF | NFEC_OPT_RS16_TOEPLITZ_ON |
+                                 NFEC_OPT_HOST_ONLY))
         return fail(NFEC_EINVAL, "unknown option flag");
+    if ((cfg->flags & NFEC_OPT_HOST_ONLY) && cfg->num_devices > 1)
+        return fail(NFEC_EINVAL, "a host-only codec takes no device list");
     if ((cfg->flags & NFEC_OPT_RS16_TOEPLITZ_OFF) && (cfg->flags & NFEC_OPT_RS16_TOEPLITZ_ON))
         return fail(NFEC_EINVAL, "Toeplitz split both on and off");
     const uint32_t nd = cfg->num_devices ? cfg->num_devices : 1;
@@ -1742,6 +1998,7 @@ int nfec_encode_segment(nfec_codec* c, uint32_t segment_id, const void* data, vo
 {
     if (!c || !data || !parity) return fail(NFEC_EINVAL, "null argument");
     c = primary(c);
+    if (c->host_only) return host_only_fail();
     if (segment_id >= c->k) return fail(NFEC_EINVAL, "segmentId >= numData");
     for (uint32_t i = 0; i < c->m; ++i)
         if (!parity[i]) return fail(NFEC_EINVAL, "null parity vector");
@@ -1794,10 +2051,10 @@ int nfec_encode_segment(nfec_codec* c, uint32_t segment_id, const void* data, vo
         t.nblocks = 1;
         t.k = 1;
         t.m = c->m;
-        t.vec_bytes = c->vec;
+        t.vec_bytes = c->vec & ~1u;
         t.tw = c->tw ? c->d_twoff.p + (size_t)segment_id * 4u * c->m : nullptr;
         t.accumulate = 1;
-        rc = c->tw && (c->vec % 8) == 0 && gf16_tw_covers(t) ? launch_gf16_tw_encode(t, st) : NFEC_ENOTSUP;
+        rc = c->tw && rs16_tw_full_covers(t) ? launch_rs16_tw_full(t, st) : NFEC_ENOTSUP;
         if (rc != NFEC_ENOTSUP && rc) return rc;
         if (rc == NFEC_ENOTSUP) {
             Gf16MatmulArgs a;
@@ -2064,6 +2321,7 @@ int nfec_decode_host_preferred(const nfec_codec* c, uint32_t num_data, uint32_t 
 {
     if (!c) return 0;
     c = primary(c);
+    if (c->host_only) return c->kind == NFEC_MDP || !c->h_lwp.empty() ? 1 : 0;
     const uint64_t e = std::min(erasure_count, c->m);
     // products of the repair: erased rows x columns read x symbols
     if (c->kind == NFEC_MDP) return e * (num_data + c->m) * c->vec <= kHostDecodeMdpBytes ? 1 : 0;
@@ -2077,6 +2335,7 @@ int nfec_decode_vectors(nfec_codec* c, void* const* vectors, uint32_t num_data, 
 {
     if (!c || !vectors || (erasure_count && !erasure_locs)) return fail(NFEC_EINVAL, "null argument");
     c = primary(c);
+    if (c->host_only) return host_only_fail();
     if (num_data == 0 || num_data > c->k) return fail(NFEC_EINVAL, "numData out of range");
     if (erasure_count > c->m) return 0;
     DeviceGuard g(c->device);
@@ -2709,6 +2968,7 @@ static int run_host_vectors(nfec_codec* c, void* const* vecs, uint32_t nblocks, 
                             uint32_t flags, bool decode)
 {
     if (!c || (nblocks && !vecs)) return fail(NFEC_EINVAL, "null codec or vector list");
+    if (primary(c)->host_only) return host_only_fail();
     if (decode && (!locs || !counts || lstride == 0)) return fail(NFEC_EINVAL, "bad erasure arrays");
     if (nblocks == 0) return NFEC_OK;
     if (!c->stripes.empty())
@@ -2942,6 +3202,7 @@ int submit_vectors(nfec_codec* c, void* const* vecs, uint32_t nblocks, const uin
     if (!out) return fail(NFEC_EINVAL, "null request pointer");
     *out = nullptr;
     if (!c || (nblocks && !vecs)) return fail(NFEC_EINVAL, "null codec or vector list");
+    if (primary(c)->host_only) return host_only_fail();
     if (decode && (!locs || !counts || lstride == 0)) return fail(NFEC_EINVAL, "bad erasure arrays");
     const uint64_t n = (uint64_t)c->k + c->m;
     auto tab = std::make_shared<std::vector<void*>>(vecs, vecs + n * nblocks);

@@ -216,7 +216,9 @@ struct Gf16T3Args {
     uint64_t block_stride = 0;
     uint32_t seg_stride = 0;
     uint32_t nblocks = 0;
-    const uint16_t* num_data = nullptr;  // must be null (unshortened batches only)
+    // per block numData (tower kernel, flat mode only: columns at or past it read as zeros; the
+    // shared-table kernel takes unshortened batches only)
+    const uint16_t* num_data = nullptr;
     uint32_t k = 0, m = 0, m_pad = 0;    // m_pad = gf16_t3_rows_padded(m)
     uint32_t vec_bytes = 0;              // multiple of 8
     const uint16_t* offs = nullptr;      // [k + 1][m_pad][48] LDS offsets (gf16_t3_offsets)
@@ -230,16 +232,20 @@ struct Gf16T3Args {
     const uint8_t* acc_base = nullptr;
     uint64_t acc_block_stride = 0;
     uint32_t acc_seg_stride = 0, acc_slot0 = 0;
+    // with num_data: output / accumulate row r at slot slot0 + numData + r (encode: the parity
+    // after the block's numData sources; decode stage 1: the received parity rows)
+    uint32_t out_after_data = 0, acc_after_data = 0;
     const uint32_t* rows_lim = nullptr;  // device word: rows needed (<= m), null: m
     // column map: column c is read from slot ((c >> col_shift) * col_chunk + (c & col_mask) +
     // col_base) (identity by default); in_slots bounds the slots read (0: k + m)
     uint32_t col_shift = 31, col_mask = 0xFFFFFFFFu, col_chunk = 0, col_base = 0, in_slots = 0;
     const uint16_t* tw = nullptr;   // [k][2][m][2] snippet offsets (gf16_tw_offsets)
     // per-block mode (RS16 decode stage 2 on the tower kernel): item groups stay inside one
-    // block; block b has its own table (tw + b * tw_block_stride), e = blk_rows[b] rows and
-    // columns, and its rows' output byte offsets row_off[b * row_off_stride + r] (from out_base
-    // + b * out_block_stride); no accumulate source
+    // block; block b has its own table (tw + b * tw_block_stride), e = blk_rows[b] rows,
+    // blk_cols[b] columns (null: e), and its rows' output byte offsets row_off[b *
+    // row_off_stride + r] (from out_base + b * out_block_stride); no accumulate source
     const int32_t* blk_rows = nullptr;
+    const uint16_t* blk_cols = nullptr;
     uint64_t tw_block_stride = 0;
     const uint32_t* row_off = nullptr;
     uint32_t row_off_stride = 0;
@@ -284,19 +290,28 @@ int launch_gf16_tw_multi(const Gf16T3Args* e, uint32_t n, hipStream_t s);
 void gf16_tw_offsets(const std::vector<uint32_t>& parity_rows, uint32_t k, uint32_t m, uint16_t* out);
 uint32_t gf16_tw_passes(uint32_t m);  // passes of the tower kernel for m rows (a multiple of 4)
 size_t gf16_tw_table_elems(uint32_t k, uint32_t m);  // u16 elements of a k-column, m-row table
-void gf16_tw_field(uint16_t phi_cols[16], uint32_t* lam);  // the tower isomorphism's constants
+// the tower isomorphism's constants: phi's columns (phi(x^i)), lam, and phi^-1's columns (optional)
+void gf16_tw_field(uint16_t phi_cols[16], uint32_t* lam, uint16_t* phi_inv_cols = nullptr);
+// the segment tails of the same products: bytes [off, off + bytes) of every segment (even, at
+// most 6: the part of vec & ~1 past the tower kernel's 8-byte pieces), same arguments and
+// layouts as launch_gf16_tw_encode (flat or per-block mode, numData, accumulate; a.vec_bytes is
+// ignored; no column map).  kernels_gf16tail.hip
+int launch_gf16_tw_tail(const Gf16T3Args& a, uint32_t off, uint32_t bytes, hipStream_t s);
+bool gf16_tw_tail_covers(const Gf16T3Args& a, uint32_t bytes);  // launch_gf16_tw_tail would take it
 // RS16 decode stage 2 on the tower kernel: per-block snippet tables and output row offsets from
 // the plan's e x e inverses (kernels_tmvp.hip)
 struct TwDecTablesArgs {
-    const uint16_t* coef2 = nullptr;  // [b][dcs][dcs] inverse, column-major ([t][s])
+    const uint16_t* coef2 = nullptr;  // [b][columns][dcs] inverse, column-major ([t][s])
     uint32_t dcs = 0;
+    uint64_t coef2_block = 0;         // elements per block (0: dcs * dcs)
     const int32_t* rows = nullptr;    // e per block
+    const uint16_t* cols = nullptr;   // columns per block (null: e)
     const uint16_t* out_slots = nullptr;  // [b][slots_stride] erased source slots
     uint32_t slots_stride = 0;
     uint32_t seg_stride = 0;          // output segment stride (bytes)
-    uint32_t nblocks = 0, M = 0;      // M rows / columns at most (min(k, m))
+    uint32_t nblocks = 0, M = 0;      // M rows at most (min(k, m))
     uint64_t tw_block_stride = 0;     // u16 elements per block table
-    uint16_t* tw = nullptr;           // [b][gf16_tw_table_elems(M, M)]: [t][sweep][row][2]
+    uint16_t* tw = nullptr;           // [b][gf16_tw_table_elems(columns, M)]: [t][sweep][row][2]
     uint32_t* row_off = nullptr;      // [b][M + 12]
     uint16_t phi[16] = {};
     uint32_t lam = 0;
@@ -399,9 +414,17 @@ struct RsPlanArgs {
     // *rmax to e and zeroes the erased source slots (zero_*: the batch).  Others: rows1 = e.
     int32_t* rows1 = nullptr;
     uint32_t* rmax = nullptr;
+    // by_row (tower decode, rs16_plan_cf_kernel): EVERY decodable block is repaired by encode,
+    // whatever its substitute parities or numData: stage 1 computes z rows 0..P_last (the block's
+    // last substitute parity row - nd), *rmax rises to P_last + 1, cols2 = P_last + 1, and coef2
+    // is laid out by parity row (column P_t - nd holds A^-1's column t, lost rows zero).
+    // zero_base null: the erased source is not zeroed (accumulate: stage 2 overwrites with
+    // d_E ^ X, see rs16_plan_cf_kernel)
+    uint32_t by_row = 0;
+    uint64_t coef2_block = 0;           // coef2 elements per block (0: coef_stride^2)
     uint8_t* zero_base = nullptr;
     uint64_t zero_block_stride = 0;
-    uint32_t zero_seg_stride = 0, zero_vec = 0;   // zero_vec: bytes, multiple of 8
+    uint32_t zero_seg_stride = 0, zero_vec = 0;   // zero_vec: bytes (even; rs_plan_kernel: multiple of 8)
     // RS16 closed form (rs16_plan_cf_kernel, when both are set and min(k, m) <= kPlanCfMaxE):
     // A^-1 from the Cauchy form of the Lagrange generator instead of Gauss-Jordan
     const uint16_t* lwp = nullptr;      // [k] log W'(x_j)

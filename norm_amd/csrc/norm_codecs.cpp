@@ -13,14 +13,57 @@ NormEncoder::~NormEncoder() {}
 NormDecoder::~NormDecoder() {}
 
 int NfecCodecBase::default_device = 0;
+int NfecCodecBase::device_list[NfecCodecBase::kMaxDevices] = {};
+int NfecCodecBase::num_devices = 0;
 bool NfecCodecBase::segment_on_host = true;
 bool NfecCodecBase::decode_on_host = true;
+bool NfecCodecBase::host_fallback = true;
+
+bool NfecCodecBase::SetDevices(const int* devices, int count)
+{
+    if (count < 1 || count > kMaxDevices || !devices) return false;
+    default_device = devices[0];
+    num_devices = count > 1 ? count : 0;
+    for (int i = 0; i < count; ++i) device_list[i] = devices[i];
+    return true;
+}
+
+int NfecCodecBase::GetDevices(int* devices, int cap)
+{
+    const int n = num_devices ? num_devices : 1;
+    for (int i = 0; devices && i < n && i < cap; ++i) devices[i] = num_devices ? device_list[i] : default_device;
+    return n;
+}
+
+bool NfecCodecBase::IsHostOnly() const
+{
+    nfec_codec_info info;
+    return codec && nfec_codec_get_info(codec, &info) == NFEC_OK && info.device < 0;
+}
 
 bool NfecCodecBase::InitCodec(int kind, unsigned int numData, unsigned int numParity, UINT16 vectorSize)
 {
     DestroyCodec();
     nfec_codec* c = 0;
-    int rc = nfec_codec_create(default_device, kind, numData, numParity, vectorSize, &c);
+    nfec_codec_config cfg;
+    cfg.kind = kind;
+    cfg.num_data = numData;
+    cfg.num_parity = numParity;
+    cfg.vector_size = vectorSize;
+    int32_t devs[kMaxDevices];
+    const int n = num_devices ? num_devices : 1;
+    for (int i = 0; i < n; ++i) devs[i] = num_devices ? device_list[i] : default_device;
+    cfg.devices = devs;
+    cfg.num_devices = (uint32_t)n;
+    cfg.flags = 0;
+    int rc = nfec_codec_create_ex(&cfg, &c);
+    if (rc == NFEC_EDEVICE && host_fallback && segment_on_host && decode_on_host) {
+        // no usable gfx950: a host-only codec still serves NORM's per-call Encode / Decode
+        cfg.devices = 0;
+        cfg.num_devices = 0;
+        cfg.flags = NFEC_OPT_HOST_ONLY;
+        rc = nfec_codec_create_ex(&cfg, &c);
+    }
     if (rc != NFEC_OK) {
         // the reference logs PL_FATAL and returns false (normEncoderRS8.cpp:405-409)
         std::fprintf(stderr, "nfec: Init(%u, %u, %u) failed: %s\n", numData, numParity, (unsigned)vectorSize,

@@ -2,7 +2,8 @@
 // restated against the GPU drop-in classes and driven through NormEncoder* / NormDecoder*
 // base-class pointers, the way NORM's engine holds its codecs (normSession.h:791,
 // normNode.h:649).  Test infrastructure: built by tests/native/Makefile against libnfec.so
-// only (plain g++, no HIP headers), run by tests/test_cxx_dropin.py on the GPU box.
+// only (plain g++, no HIP headers), run by tests/test_cxx_dropin.py on the GPU box and, with
+// host-only codecs (no usable gfx950: the per-call paths on the CPU), in the CPU suite.
 //
 //   nfec_fectest KIND K M VEC NUMDATA IN OUT NULLPAR [LOC ...]
 //     KIND     rs8 | rs16 | mdp
@@ -131,11 +132,30 @@ int main(int argc, char* argv[])
             NfecCodecBase::SetSegmentEncodeOnHost(false);
             NfecCodecBase::SetDecodeOnHost(false);
         }
+    // NFEC_FECTEST_DEVICES=0,0,...: one codec striped over that device list (SetDevices, the
+    // class-level route to nfec_codec_create_ex for a single NORM session's encoder)
+    if (const char* dl = std::getenv("NFEC_FECTEST_DEVICES")) {
+        int devs[NfecCodecBase::kMaxDevices], nd_ = 0;
+        for (const char* p = dl; *p && nd_ < NfecCodecBase::kMaxDevices;) {
+            devs[nd_++] = std::atoi(p);
+            while (*p && *p != ',') ++p;
+            if (*p == ',') ++p;
+        }
+        if (!NfecCodecBase::SetDevices(devs, nd_)) return 2;
+    }
     NormEncoder* encoder = new_encoder(kind, k, m, vec);
     NormDecoder* decoder = new_decoder(kind, k, m, vec);
     if (!encoder || !decoder) {
         std::fprintf(stderr, "fect: Init(%u, %u, %u) failed\n", k, m, vec);
         return 3;
+    }
+    {
+        // where the codecs live: host-only (no usable gfx950, NFEC_OPT_HOST_ONLY) or the GPU list
+        NfecCodecBase* eb = dynamic_cast<NfecCodecBase*>(encoder);
+        NfecCodecBase* db = dynamic_cast<NfecCodecBase*>(decoder);
+        std::fprintf(stderr, "fect: host_only=%d/%d devices=%d/%d\n", eb->IsHostOnly() ? 1 : 0,
+                     db->IsHostOnly() ? 1 : 0, nfec_codec_num_devices(eb->Handle(), 0, 0),
+                     nfec_codec_num_devices(db->Handle(), 0, 0));
     }
     // Destroy / Init again through the vtable: Destroy must leave the codec reusable
     encoder->Destroy();

@@ -82,11 +82,38 @@ CASES = [
 ]
 
 
-@pytest.mark.gpu
-@pytest.mark.parametrize("gpu_calls", [False, True])
+def _no_gpu():
+    from norm_amd import _native as N
+
+    return N.lib().nfec_device_count() == 0
+
+
 @pytest.mark.parametrize("kind,k,m,vec,nd,locs,nullpar,src", CASES)
-def test_fectest_matches_oracle(orc, tmp_path, kind, k, m, vec, nd, locs, nullpar, src, gpu_calls):
-    """gpu_calls: the per-call GPU round trips (NFEC_FECTEST_GPU=1) instead of the host defaults"""
+def test_fectest_host_only_matches_oracle(orc, tmp_path, kind, k, m, vec, nd, locs, nullpar, src):
+    """No GPU (this container): Init builds host-only codecs (NFEC_OPT_HOST_ONLY) and the
+    drop-in's per-call Encode / Decode run on the CPU -- the same bytes as the oracle."""
+    if not _no_gpu():
+        pytest.skip("a gfx950 is visible: the GPU variants below cover this box")
+    err = _run_fectest(orc, tmp_path, kind, k, m, vec, nd, locs, nullpar, src, {"NFEC_FECTEST_GPU": "0"})
+    assert "host_only=1/1" in err, err
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", ["host_calls", "gpu_calls", "gpu_calls_2dev"])
+@pytest.mark.parametrize("kind,k,m,vec,nd,locs,nullpar,src", CASES)
+def test_fectest_matches_oracle(orc, tmp_path, kind, k, m, vec, nd, locs, nullpar, src, mode):
+    """host_calls: the drop-in's host per-call defaults on a GPU codec; gpu_calls: the per-call
+    GPU round trips (NFEC_FECTEST_GPU=1); gpu_calls_2dev: the same on a codec striped over the
+    device list {0, 0} (NfecCodecBase::SetDevices, NFEC_FECTEST_DEVICES)"""
+    env = {"NFEC_FECTEST_GPU": "0" if mode == "host_calls" else "1"}
+    if mode == "gpu_calls_2dev":
+        env["NFEC_FECTEST_DEVICES"] = "0,0"
+    err = _run_fectest(orc, tmp_path, kind, k, m, vec, nd, locs, nullpar, src, env)
+    assert "host_only=0/0" in err, err
+    assert ("devices=2/2" if mode == "gpu_calls_2dev" else "devices=1/1") in err, err
+
+
+def _run_fectest(orc, tmp_path, kind, k, m, vec, nd, locs, nullpar, src, env_extra):
     n = nd + m
     if src == "-":
         data = np.zeros((nd, vec), np.uint8)
@@ -98,7 +125,7 @@ def test_fectest_matches_oracle(orc, tmp_path, kind, k, m, vec, nd, locs, nullpa
         inp = str(tmp_path / "in.bin")
         data.tofile(inp)
     out = tmp_path / "out.bin"
-    env = dict(os.environ, NFEC_FECTEST_GPU="1" if gpu_calls else "0")
+    env = dict(os.environ, **env_extra)
     r = subprocess.run([EXE, kind, str(k), str(m), str(vec), str(nd), inp, str(out), str(int(nullpar))]
                        + [str(x) for x in locs], capture_output=True, text=True, timeout=120, env=env)
     dump = np.fromfile(out, np.uint8)
@@ -134,3 +161,4 @@ def test_fectest_matches_oracle(orc, tmp_path, kind, k, m, vec, nd, locs, nullpa
         assert r.returncode == 0, r.stderr
         nbytes = vec & ~1 if kind == "rs16" else vec  # RS16 never repairs an odd last byte
         assert np.array_equal(rx[:nd, :nbytes], data[:, :nbytes])
+    return r.stderr

@@ -420,12 +420,28 @@ def col_offset():
             f"s_add_u32 s{S_COL}, s{S_COL}, s{S_T2}", f"s_add_u32 s{S_COL}, s{S_COL}, %[cbb]"]
 
 
+_uid = [0]
+
+
 def loads():
+    """column s[S_C]'s 8 pieces -> the slot.  Flat shortened mode (bit 0 of %[md]): a piece whose
+    block has numData <= c reads zeros (its offset gets bit 31: past num_records; %[q<i>] =
+    the piece's numData - 1), so each piece's block stops at its own numData"""
     x = slot()
     if "noload" in FLAGS:
         return []
-    return [f"buffer_load_dwordx2 v[{x[2 * i]}:{x[2 * i + 1]}], %[o{i}], s[{S_DESC}:{S_DESC + 3}], s{S_COL} offen"
-            for i in range(8)]
+    _uid[0] += 1
+    u = _uid[0]
+    plain = [f"buffer_load_dwordx2 v[{x[2 * i]}:{x[2 * i + 1]}], %[o{i}], s[{S_DESC}:{S_DESC + 3}], s{S_COL} offen"
+             for i in range(8)]
+    masked = []
+    for i in range(8):
+        t = V_CA + i   # the combinations are free while a column loads
+        masked += [f"v_subrev_u32 v{t}, s{S_C}, %[q{i}]",                      # numData - 1 - c
+                   f"v_and_or_b32 v{t}, v{t}, s{S_DESC + 2}, %[o{i}]",          # sign -> bit 31
+                   f"buffer_load_dwordx2 v[{x[2 * i]}:{x[2 * i + 1]}], v{t}, s[{S_DESC}:{S_DESC + 3}], s{S_COL} offen"]
+    return ([f"s_bitcmp1_b32 %[md], 0", f"s_cbranch_scc0 Lldp{u}_%="] + masked +
+            [f"s_branch Lldx{u}_%=", f"Lldp{u}_%=:"] + plain + [f"Lldx{u}_%=:"])
 
 
 def xch_addr(j=None, sgpr=None):
@@ -611,12 +627,12 @@ def main():
         FLAGS = f
         asms[v] = "\\n\"\n            \"".join(body())
     FLAGS = ()
-    ins = ", ".join(f'[o{i}] "v"(o[{i}])' for i in range(8))
+    ins = ", ".join([f'[o{i}] "v"(o[{i}])' for i in range(8)] + [f'[q{i}] "v"(q[{i}])' for i in range(8)])
     common = """[wb] "s"(wb), [ss] "s"(a.seg_stride), [k] "s"(kk), [tw] "s"(tw), [tstep] "s"(tstep), [t1off] "s"(t1off), [nr] "s"(nr),
               [csh] "s"(a.col_shift), [cmk] "s"(a.col_mask), [cck] "s"(cck), [cbb] "s"(cbb),
               [acc] "s"(a.accumulate), [ob] "s"(ob), [ab] "s"(ab), [oslot] "s"(a.out_slot0 + row0),
               [oss] "s"(a.out_seg_stride), [aslot] "s"(a.acc_slot0 + row0), [ass] "s"(a.acc_seg_stride),
-              [wv] "s"(wave), [rp] "s"(rp), [lo] "v"(lo), [xl] "v"(xl), """ + ins
+              [wv] "s"(wave), [rp] "s"(rp), [md] "s"(md), [lo] "v"(lo), [xl] "v"(xl), """ + ins
     blocks = []
     for v in variants:
         kw = "if constexpr" if v == 0 else "else if constexpr"
@@ -647,6 +663,7 @@ def main():
     else:
         tw_variant = "constexpr int tw_variant() { return 0; }"
     phi_cols = ", ".join(f"0x{c:04x}" for c in PHI)
+    phi_inv_cols = ", ".join(f"0x{c:04x}" for c in PHI_INV)
     src = f"""// GENERATED by tools/codegen/gen_gf16_tw.py -- do not edit by hand.
 // RS16 products through the tower field GF((2^8)^2): bit-sliced, GF(2^8) snippet jumps.
 // Isomorphism: lam = 0x{LAM:02x}, beta = 0x{BETA:04x} (phi(x^i) = beta^i).
@@ -674,14 +691,19 @@ __device__ __forceinline__ void tw_body(const Gf16T3Args& a, uint32_t wg)
     const uint32_t group = wg / quads, quad = wg - group * quads;
     // flat mode: item groups run over the batch's bytes across blocks (one coefficient table);
     // per-block mode (blk_rows): each group lies in one block, which has its own table, row
-    // count e (also its column count) and output row offsets
+    // count e, column count (blk_cols, else e) and output row offsets
     const bool pb = a.blk_rows != nullptr;
     const uint32_t chunks = (a.vec_bytes + {GROUP_BYTES - 1}u) / {GROUP_BYTES}u;
     const uint32_t pblk = pb ? group / chunks : 0u;
     const uint64_t total = pb ? (uint64_t)a.vec_bytes : (uint64_t)a.nblocks * a.vec_bytes;
     const uint64_t f0 = pb ? (uint64_t)(group - pblk * chunks) * {GROUP_BYTES}u : (uint64_t)group * {GROUP_BYTES}u;
     if ((pb && pblk >= a.nblocks) || f0 >= total) return;  // workgroup-uniform, as the next exits
-    // rows actually needed (decode stage 1: the largest erasure count among the blocks it
+    // flat shortened mode (num_data): every piece's block has its own numData; columns at or
+    // past it read zeros, and the output / accumulate rows may sit after it (out_after_data /
+    // acc_after_data: slot numData + r).  The item group runs to the largest numData among its
+    // blocks; a block whose numData is 0 or past k is left alone.
+    const uint32_t lnd = !pb && a.num_data ? 1u : 0u;
+    // rows actually needed (decode stage 1: the last substitute-parity row among the blocks it
     // serves, written by the plan; per-block mode: the block's e); workgroups past them leave
     // at once, waves past them only load, transpose and share their columns
     uint32_t rlim = a.m, kk = a.k;
@@ -689,29 +711,46 @@ __device__ __forceinline__ void tw_body(const Gf16T3Args& a, uint32_t wg)
     if (pb) {{
         const int32_t e = (int32_t)__builtin_amdgcn_readfirstlane((uint32_t)a.blk_rows[pblk]);
         rlim = e > 0 ? min(rlim, (uint32_t)e) : 0u;
-        kk = min(kk, rlim);
+        kk = a.blk_cols ? min(kk, (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)a.blk_cols[pblk])) : min(kk, rlim);
+    }} else if (lnd) {{
+        const uint32_t bf = (uint32_t)(f0 / a.vec_bytes), bl = (uint32_t)((min(f0 + {GROUP_BYTES}u, total) - 1u) / a.vec_bytes);
+        uint32_t mx = 0;
+        for (uint32_t b = bf + lane; b <= bl; b += 64u) {{
+            const uint32_t v = a.num_data[b];
+            if (v >= 1u && v <= a.k) mx = max(mx, v);
+        }}
+        for (int off = 32; off > 0; off >>= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, off));
+        kk = __builtin_amdgcn_readfirstlane(mx);
     }}
     // the rows in play spread evenly over whole workgroups of four passes (the table holds any
     // row range); the launch sized the grid for a.m rows, so later workgroups may leave
     const uint32_t npass = gf16_tw_passes_dev(rlim);
-    if (rlim == 0u || quad * 4u >= npass) return;
+    if (rlim == 0u || kk == 0u || quad * 4u >= npass) return;
     const uint32_t pass = quad * 4u + wave;
     const uint32_t row0 = pass * rlim / npass, row1 = (pass + 1u) * rlim / npass;
     const uint32_t nr = __builtin_amdgcn_readfirstlane(row1 - row0);
     const uint32_t b0 = pb ? pblk : __builtin_amdgcn_readfirstlane((uint32_t)(f0 / a.vec_bytes));
     const uint8_t* wb = a.base + (uint64_t)b0 * a.block_stride;
-    uint32_t o[8];
+    uint32_t o[8], q[8];
     uint32_t* po = lds + (wave * 64u + lane) * 16u;
 #pragma unroll
     for (int i = 0; i < 8; ++i) {{
         const uint64_t f = f0 + (uint64_t)i * 512u + lane * 8u;
         const uint32_t b = pb ? b0 : (uint32_t)(f / a.vec_bytes);
         const uint32_t p = (uint32_t)(f - (uint64_t)(pb ? 0u : b) * a.vec_bytes);
-        const bool ok = f < total;
+        const uint32_t raw = lnd && f < total ? (uint32_t)a.num_data[b] : a.k;
+        const bool ok = f < total && raw >= 1u && raw <= a.k;
+        const uint32_t pnd = ok ? raw : 1u;
+        q[i] = pnd - 1u;
         o[i] = ok ? (uint32_t)((uint64_t)(b - b0) * a.block_stride) + p : 0x80000000u;
-        po[i] = ok ? (uint32_t)((uint64_t)(b - b0) * a.out_block_stride) + p : 0x80000000u;
-        po[8 + i] = ok ? (uint32_t)((uint64_t)(b - b0) * a.acc_block_stride) + p : 0x80000000u;
+        po[i] = ok ? (uint32_t)((uint64_t)(b - b0) * a.out_block_stride +
+                                (a.out_after_data ? (uint64_t)pnd * a.out_seg_stride : 0u)) + p
+                   : 0x80000000u;
+        po[8 + i] = ok ? (uint32_t)((uint64_t)(b - b0) * a.acc_block_stride +
+                                    (a.acc_after_data ? (uint64_t)pnd * a.acc_seg_stride : 0u)) + p
+                       : 0x80000000u;
     }}
+    const uint32_t md = __builtin_amdgcn_readfirstlane(lnd);
     const uint32_t lo = bs::lds_addr(po);
     const uint32_t xl = bs::lds_addr(xch) + lane * 8u;
     // table [column][sweep][row][2 entries]: this pass's rows start 2 * row0 elements in
@@ -747,29 +786,35 @@ __global__ __launch_bounds__({64 * NWAVES}, 2) void gf16_tw_multi_kernel(Gf16T3M
 // checks the shape, fills the default output / accumulate layouts and the pass count
 int tw_prepare(const Gf16T3Args& a, Gf16T3Args& b, uint64_t& wgs)
 {{
-    if ((a.vec_bytes & 7u) || a.vec_bytes == 0 || !a.tw || a.num_data || a.k == 0)
+    // (numData masking is a flat-mode feature; the column map is the Toeplitz split's, unshortened)
+    if ((a.vec_bytes & 7u) || a.vec_bytes == 0 || !a.tw || a.k == 0 || (a.num_data && (a.blk_rows || a.col_chunk)))
         return NFEC_ENOTSUP;
-    // every piece offset of a group ({GROUP_BYTES} bytes of flat positions) plus slot offsets within 2^31
-    const uint64_t nbg = {GROUP_BYTES}u / a.vec_bytes + 2u;
-    const uint64_t in_slots = a.in_slots ? a.in_slots : (uint64_t)a.k + a.m;
-    if (nbg * a.block_stride + in_slots * a.seg_stride >= (1ull << 31) ||
-        (a.out_base && nbg * a.out_block_stride + (uint64_t)(a.out_slot0 + a.m) * a.out_seg_stride >= (1ull << 31)) ||
-        (a.acc_base && nbg * a.acc_block_stride + (uint64_t)(a.acc_slot0 + a.m) * a.acc_seg_stride >= (1ull << 31)))
-        return NFEC_ENOTSUP;
-    const uint64_t total = (uint64_t)a.nblocks * a.vec_bytes;
     b = a;
-    if (!b.out_base) {{  // encode: parity in place, slot k + r; accumulate against it
+    if (!b.out_base) {{  // encode: parity in place, slot k + r (numData + r when shortened); accumulate against it
         b.out_base = const_cast<uint8_t*>(a.base);
         b.out_block_stride = a.block_stride;
         b.out_seg_stride = a.seg_stride;
-        b.out_slot0 = a.k;
+        b.out_slot0 = a.num_data ? 0u : a.k;
+        b.out_after_data = a.num_data ? 1u : 0u;
     }}
     if (!b.acc_base) {{
         b.acc_base = b.out_base;
         b.acc_block_stride = b.out_block_stride;
         b.acc_seg_stride = b.out_seg_stride;
         b.acc_slot0 = b.out_slot0;
+        b.acc_after_data = b.out_after_data;
     }}
+    if (!a.num_data) b.out_after_data = b.acc_after_data = 0u;
+    // every piece offset of a group ({GROUP_BYTES} bytes of flat positions) plus slot offsets within 2^31
+    const uint64_t nbg = {GROUP_BYTES}u / a.vec_bytes + 2u;
+    const uint64_t in_slots = a.in_slots ? a.in_slots : (uint64_t)a.k + a.m;
+    const uint64_t oslots = (uint64_t)b.out_slot0 + (b.out_after_data ? a.k : 0u) + a.m;
+    const uint64_t aslots = (uint64_t)b.acc_slot0 + (b.acc_after_data ? a.k : 0u) + a.m;
+    if (nbg * a.block_stride + in_slots * a.seg_stride >= (1ull << 31) ||
+        nbg * b.out_block_stride + oslots * b.out_seg_stride >= (1ull << 31) ||
+        nbg * b.acc_block_stride + aslots * b.acc_seg_stride >= (1ull << 31))
+        return NFEC_ENOTSUP;
+    const uint64_t total = (uint64_t)a.nblocks * a.vec_bytes;
     b.passes = gf16_tw_passes(a.m);
     // per-block mode: one table and one set of row offsets per block, no accumulate source
     if (a.blk_rows && (!a.row_off || !a.tw_block_stride || a.accumulate)) return NFEC_ENOTSUP;
@@ -780,6 +825,7 @@ int tw_prepare(const Gf16T3Args& a, Gf16T3Args& b, uint64_t& wgs)
 }}
 
 const uint16_t kPhiCol[16] = {{{phi_cols}}};
+const uint16_t kPhiInvCol[16] = {{{phi_inv_cols}}};
 
 }}  // namespace
 
@@ -827,9 +873,10 @@ int launch_gf16_tw_encode(const Gf16T3Args& a, hipStream_t s)
     return e == hipSuccess ? NFEC_OK : hip_fail(e, "gf16 tower encode launch");
 }}
 
-void gf16_tw_field(uint16_t phi_cols[16], uint32_t* lam)
+void gf16_tw_field(uint16_t phi_cols[16], uint32_t* lam, uint16_t* phi_inv_cols)
 {{
     for (int i = 0; i < 16; ++i) phi_cols[i] = kPhiCol[i];
+    for (int i = 0; phi_inv_cols && i < 16; ++i) phi_inv_cols[i] = kPhiInvCol[i];
     *lam = 0x{LAM:02x}u;
 }}
 
