@@ -294,6 +294,19 @@ int nfec_decode_host_preferred(const nfec_codec* codec, uint32_t num_data, uint3
  * unknown kind: a NORM build can check that its translation units see the same layout. */
 size_t nfec_dropin_sizeof(int kind, int decoder);
 
+/* The host worker pool every host-batch copy of 4 MiB or more runs on (one per process): its
+ * workers (the cores the job may use -- the affinity mask capped by the cgroup cpu.max quota --
+ * or NFEC_HOST_THREADS, at most 64), the usable and the visible cores.  All stripes of all codecs
+ * share it; smaller copies run on the calling thread. */
+int nfec_host_threads(uint32_t* pool, uint32_t* usable_cores, uint32_t* visible_cores);
+/* Host-side rate probe of the segment-list gather (no GPU): nstripes driver threads, one per
+ * would-be device, each gather their contiguous block range [i*B/N, (i+1)*B/N) of the pointer
+ * table vectors[b*slots + s] (slots vectors of vector_size bytes per block) into staging of their
+ * own in the pipelines' 128 MiB chunks, through the same pool as nfec_*_host_vectors.  *seconds:
+ * the mean wall time of one pass over all blocks; *max_active (may be NULL): the most copy
+ * pieces that ran at once during the probe (at most the pool's size). */
+int nfec_util_gather_probe(void* const* vectors, uint32_t nblocks, uint32_t slots, uint32_t vector_size,
+                           uint32_t nstripes, uint32_t reps, double* seconds, uint32_t* max_active);
 /* ---- synthetic workload utilities (device kernels; SURVEY.md 8d definitions) ----
  * fill: source slots [0, numData) of every block with the splitmix64 stream
  *       word w of (block b, slot s) = mix(seed ^ ((b0+b)<<20) ^ s + (w+1)*0x9E3779B97F4A7C15).

@@ -149,6 +149,9 @@ _SIGS = {
     "nfec_util_erasures": (_I, [_P, _U32, _P, _U32, _U32, _U32, _U64, _U64, _P]),
     "nfec_util_zero_slots": (_I, [ctypes.POINTER(BlockBatch), _P, _U32, _P, _U32, _P]),
     "nfec_util_stream_copy": (_I, [_P, _P, _U64, _P]),
+    "nfec_host_threads": (_I, [ctypes.POINTER(_U32), ctypes.POINTER(_U32), ctypes.POINTER(_U32)]),
+    "nfec_util_gather_probe": (_I, [_P, _U32, _U32, _U32, _U32, _U32, ctypes.POINTER(ctypes.c_double),
+                                    ctypes.POINTER(_U32)]),
     "nfec_fti_write": (_I, [ctypes.POINTER(Fti), _P, ctypes.c_size_t]),
     "nfec_fti_read": (_I, [_U8, _P, ctypes.c_size_t, ctypes.POINTER(Fti)]),
     "nfec_payload_id_length": (_I, [_U8]),

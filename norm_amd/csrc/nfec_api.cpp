@@ -14,6 +14,7 @@
 #include <map>
 #include <memory>
 #include <thread>
+#include <chrono>
 #include <vector>
 
 #include "bitslice.hpp"
@@ -2143,20 +2144,12 @@ static void host_rows_apply(bool wide, void* const* dst, uint32_t nrows, const v
         run(0, nelem);
         return;
     }
-    // ranges in multiples of 128 elements
+    // ranges in multiples of 128 elements, on the process's host pool
     const size_t per = ((nelem + nt - 1) / nt + 127) & ~(size_t)127;
-    std::vector<std::thread> th;
-    for (unsigned t = 1; t < nt; ++t) {
+    host_parallel_for(nt, [&](unsigned t) {
         const size_t e0 = std::min(nelem, t * per), e1 = std::min(nelem, e0 + per);
-        if (e0 >= e1) continue;
-        try {
-            th.emplace_back(run, e0, e1);
-        } catch (...) {
-            run(e0, e1);  // no thread to be had: this range on the calling thread
-        }
-    }
-    run(0, std::min(per, nelem));
-    for (auto& t : th) t.join();
+        if (e0 < e1) run(e0, e1);
+    });
 }
 
 // MDP one-block repair on the host: the closed-form Forney map of mdp_plan_kernel
@@ -2439,15 +2432,9 @@ uint8_t* host_device_ptr(const void* p)
     return static_cast<uint8_t*>(at.devicePointer);
 }
 
-unsigned host_copy_threads()
-{
-    static const unsigned n = [] {
-        unsigned t = 8;
-        if (const char* v = std::getenv("NFEC_HOST_THREADS")) t = (unsigned)std::max(1, std::atoi(v));
-        return std::min<unsigned>(t, 64);
-    }();
-    return n;
-}
+// pieces one host copy is cut into (at least 4 MiB each): as many as the process's host pool
+// has workers, which every concurrent call (and stripe) shares
+unsigned host_copy_threads() { return host_pool_size(); }
 
 // rows x width bytes, strided on both sides, split over host threads for large copies
 void copy2d(uint8_t* dst, uint64_t dpitch, const uint8_t* src, uint64_t spitch, uint64_t width, uint32_t rows)
@@ -2467,15 +2454,11 @@ void copy2d(uint8_t* dst, uint64_t dpitch, const uint8_t* src, uint64_t spitch, 
         run(0, rows);
         return;
     }
-    std::vector<std::thread> th;
-    th.reserve(nt - 1);
     const uint32_t per = (rows + nt - 1) / nt;
-    for (unsigned t = 1; t < nt; ++t) {
+    host_parallel_for(nt, [&](unsigned t) {
         const uint32_t r0 = std::min<uint32_t>(rows, t * per), r1 = std::min<uint32_t>(rows, r0 + per);
-        if (r0 < r1) th.emplace_back(run, r0, r1);
-    }
-    run(0, std::min(per, rows));
-    for (auto& t : th) t.join();
+        if (r0 < r1) run(r0, r1);
+    });
 }
 
 }  // namespace
@@ -2723,9 +2706,18 @@ static int run_striped(nfec_codec* c, uint32_t nblocks, F fn)
         rcs[i] = hi > lo ? fn(c->stripes[i].get(), lo, hi - lo) : NFEC_OK;
         if (rcs[i] < 0) errs[i] = last_error_cstr();
     };
+    // one driver thread per stripe (they mostly wait on their GPU; the copies go to the host pool)
     std::vector<std::thread> th;
-    for (uint32_t i = 1; i < ns; ++i) th.emplace_back(one, i);
+    std::vector<uint32_t> inline_ranges;
+    for (uint32_t i = 1; i < ns; ++i) {
+        try {
+            th.emplace_back(one, i);
+        } catch (...) {
+            inline_ranges.push_back(i);  // no thread to be had: that range on the calling thread
+        }
+    }
     one(0);
+    for (uint32_t i : inline_ranges) one(i);
     for (auto& t : th) t.join();
     for (uint32_t i = 0; i < ns; ++i)
         if (rcs[i] < 0) return fail(rcs[i], errs[i]);
@@ -2951,14 +2943,31 @@ void parallel_blocks(uint32_t nb, uint64_t bytes, F fn)
         fn(0u, nb);
         return;
     }
-    std::vector<std::thread> th;
     const uint32_t per = (nb + nt - 1) / nt;
-    for (unsigned t = 1; t < nt; ++t) {
+    host_parallel_for(nt, [&](unsigned t) {
         const uint32_t b0 = std::min<uint32_t>(nb, t * per), b1 = std::min<uint32_t>(nb, b0 + per);
-        if (b0 < b1) th.emplace_back(fn, b0, b1);
-    }
-    fn(0u, std::min(per, nb));
-    for (auto& t : th) t.join();
+        if (b0 < b1) fn(b0, b1);
+    });
+}
+
+// the segment-list gather of blocks [b0, b0 + nb): block b's slots [0, numData_b + extra) from
+// its pointer list (vecs[b * n + s]; NULL: zero) into dst + (b - b0) * dbs + s * ss, on the host
+// pool.  extra: m when the parity is read too (decode, accumulate), else 0.
+void gather_segments(uint8_t* dst, uint64_t dbs, uint64_t ss, void* const* vecs, uint32_t n, uint32_t b0, uint32_t nb,
+                     const uint16_t* num_data, uint32_t k, uint32_t extra, uint32_t vec)
+{
+    parallel_blocks(nb, (uint64_t)nb * n * vec, [&](uint32_t i0, uint32_t i1) {
+        for (uint32_t i = i0; i < i1; ++i) {
+            const uint32_t b = b0 + i;
+            const uint32_t up = (num_data ? num_data[b] : k) + extra;
+            uint8_t* d = dst + (uint64_t)i * dbs;
+            for (uint32_t q = 0; q < up; ++q) {
+                const void* p = vecs[(uint64_t)b * n + q];
+                if (p) std::memcpy(d + q * ss, p, vec);
+                else std::memset(d + q * ss, 0, vec);
+            }
+        }
+    });
 }
 
 }  // namespace
@@ -3009,21 +3018,9 @@ static int run_host_vectors(nfec_codec* c, void* const* vecs, uint32_t nblocks, 
     } jobs[kHostSlots];
     const uint64_t blk_bytes = (uint64_t)n * c->vec;
     auto gather = [&](HostSlot& s, const Job& j) {
-        parallel_blocks(j.nb, (uint64_t)j.nb * blk_bytes, [&](uint32_t i0, uint32_t i1) {
-            for (uint32_t i = i0; i < i1; ++i) {
-                const uint32_t b = j.b0 + i;
-                const uint32_t nd = num_data ? num_data[b] : c->k;
-                // encode without accumulate reads the source only; everything else reads the
-                // whole listed block (absent parity is zero, as MDP's decoder treats it)
-                const uint32_t up = (!decode && !acc) ? nd : nd + c->m;
-                uint8_t* dst = s.pin + (uint64_t)i * dbs;
-                for (uint32_t q = 0; q < up; ++q) {
-                    const void* p = vecs[(uint64_t)b * n + q];
-                    if (p) std::memcpy(dst + q * ss, p, c->vec);
-                    else std::memset(dst + q * ss, 0, c->vec);
-                }
-            }
-        });
+        // encode without accumulate reads the source only; everything else reads the whole
+        // listed block (absent parity is zero, as MDP's decoder treats it)
+        gather_segments(s.pin, dbs, ss, vecs, n, j.b0, j.nb, num_data, c->k, (!decode && !acc) ? 0u : c->m, c->vec);
     };
     auto scatter = [&](HostSlot& s, const Job& j) {
         parallel_blocks(j.nb, (uint64_t)j.nb * (uint64_t)c->m * c->vec, [&](uint32_t i0, uint32_t i1) {
@@ -3287,6 +3284,52 @@ int nfec_util_zero_slots(const nfec_block_batch* b, const uint16_t* locs, uint32
     if (!b || !b->blocks || !locs || !counts) return fail(NFEC_EINVAL, "null argument");
     return launch_zero_slots(static_cast<uint8_t*>(b->blocks), b->block_stride, b->seg_stride, b->nblocks, locs,
                              stride, counts, vector_size, static_cast<hipStream_t>(stream));
+}
+
+int nfec_host_threads(uint32_t* pool, uint32_t* usable_cores, uint32_t* visible_cores)
+{
+    if (pool) *pool = host_pool_workers();
+    if (usable_cores) *usable_cores = host_usable_cores();
+    if (visible_cores) *visible_cores = host_visible_cores();
+    return NFEC_OK;
+}
+
+int nfec_util_gather_probe(void* const* vectors, uint32_t nblocks, uint32_t slots, uint32_t vector_size,
+                           uint32_t nstripes, uint32_t reps, double* seconds, uint32_t* max_active)
+{
+    if (!vectors || !seconds || nblocks == 0 || slots == 0 || vector_size == 0 || nstripes == 0 || nstripes > 64 ||
+        reps == 0)
+        return fail(NFEC_EINVAL, "bad argument");
+    const uint64_t ss = round_up(vector_size, 8u), dbs = (uint64_t)slots * ss;
+    const uint32_t chunk = (uint32_t)std::max<uint64_t>(1, (128ull << 20) / dbs);  // the pipelines' 128 MiB chunks
+    std::vector<std::unique_ptr<uint8_t, void (*)(void*)>> stage;
+    for (uint32_t i = 0; i < nstripes; ++i) {
+        const uint64_t nb = (uint64_t)nblocks * (i + 1) / nstripes - (uint64_t)nblocks * i / nstripes;
+        void* p = nullptr;
+        const size_t bytes = (size_t)std::max<uint64_t>(1, std::min<uint64_t>(nb, chunk)) * dbs;
+        if (posix_memalign(&p, 4096, bytes)) return fail(NFEC_ENOMEM, "probe staging");
+        std::memset(p, 0, bytes);  // touched before timing
+        stage.emplace_back(static_cast<uint8_t*>(p), std::free);
+    }
+    auto stripe = [&](uint32_t i) {
+        const uint32_t lo = (uint32_t)((uint64_t)nblocks * i / nstripes), hi = (uint32_t)((uint64_t)nblocks * (i + 1) / nstripes);
+        for (uint32_t b0 = lo; b0 < hi; b0 += chunk)
+            gather_segments(stage[i].get(), dbs, ss, vectors, slots, b0, std::min(chunk, hi - b0), nullptr, slots, 0,
+                            vector_size);
+    };
+    auto pass = [&] {
+        std::vector<std::thread> th;
+        for (uint32_t i = 1; i < nstripes; ++i) th.emplace_back(stripe, i);
+        stripe(0);
+        for (auto& t : th) t.join();
+    };
+    pass();  // untimed: first touches of the pool, the table and the staging
+    if (max_active) host_pool_max_active(true);
+    const auto t0 = std::chrono::steady_clock::now();
+    for (uint32_t r = 0; r < reps; ++r) pass();
+    *seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() / reps;
+    if (max_active) *max_active = host_pool_max_active(false);
+    return NFEC_OK;
 }
 
 int nfec_util_stream_copy(void* dst, const void* src, uint64_t bytes, void* stream)

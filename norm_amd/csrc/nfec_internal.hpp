@@ -6,6 +6,8 @@
 #include <cstddef>
 #include <cstdint>
 #include <cstdlib>
+#include <cstring>
+#include <functional>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -43,6 +45,20 @@ inline long diag_knob(const char* name, long def, long lo = 0, long hi = 1)
     return def;
 #endif
 }
+
+// ---------------------------------------------------------------------------------
+// Host worker pool (host_pool.cpp): one per process, sized to the cores the job may use (the
+// affinity mask capped by the cgroup cpu.max quota; NFEC_HOST_THREADS overrides, at most 64).
+// host_parallel_for runs fn(0..n-1) on it and returns when all are done; every host-batch copy
+// of every codec and stripe shares these workers, so N stripes never put more than
+// host_pool_size() copy threads on the cores.
+// ---------------------------------------------------------------------------------
+unsigned host_visible_cores();
+unsigned host_usable_cores();
+unsigned host_pool_size();
+unsigned host_pool_workers();  // workers actually running (starts the pool)
+unsigned host_pool_max_active(bool reset);  // most pool pieces that ran at once (since the last reset)
+void host_parallel_for(unsigned n, const std::function<void(unsigned)>& fn);
 
 // ---------------------------------------------------------------------------------
 // Host field arithmetic (gf_host.cpp).  GF(2^8) on 0x11d and GF(2^16) on 0x1100B with
