@@ -102,9 +102,9 @@ typedef struct nfec_block_batch {
 
 /* ---- version / device ---- */
 int nfec_abi_version(void);
-/* SHA-256 (hex) of the sources this library was built from: the files of norm_amd/csrc, then the
- * .h files of include and include/norm_fec, each list sorted by path, contents concatenated
- * (norm_amd/Makefile). */
+/* SHA-256 (hex) of the sources this library was built from: the .cpp/.hip/.hpp/.h files of
+ * norm_amd/csrc, then the .h files of include and include/norm_fec, each list sorted by path,
+ * contents concatenated (norm_amd/Makefile). */
 const char* nfec_build_id(void);
 /* number of visible gfx950 devices (0 when none) */
 int nfec_device_count(void);
@@ -143,7 +143,9 @@ enum {
  * thread and one staging pipeline per device, no exchange between the ranges: the in-process
  * form of SURVEY 8e's block striping for single-process callers such as one NORM session
  * (normSession.cpp:834-889) or npc (normPrecode.cpp:588-880).  A device batch (nfec_encode /
- * nfec_decode) runs on the first listed device that holds it (NFEC_EINVAL when none does);
+ * nfec_decode) runs on the first listed device that holds it (NFEC_EINVAL when a device
+ * allocation is on none of them; a batch in host-mapped or registered host memory runs on the
+ * first device, as a one-device codec would take it);
  * per-call work (nfec_encode_segment / nfec_decode_vectors) on the first device. */
 typedef struct nfec_codec_config {
     int32_t kind;             /* NFEC_RS8 / NFEC_RS16 / NFEC_MDP */

@@ -205,12 +205,13 @@ def check(rc, what):
 
 def source_build_id(root=None):
     """SHA-256 of the library's sources in this tree, computed as norm_amd/Makefile computes
-    nfec_build_id(): csrc/* then include/*.h and include/norm_fec/*.h, each sorted by path."""
+    nfec_build_id(): csrc/*.{cpp,hip,hpp,h} then include/*.h and include/norm_fec/*.h, each sorted by path."""
     import glob
     import hashlib
 
     root = root or os.path.dirname(_HERE)
-    csrc = sorted(p for p in glob.glob(os.path.join(root, "norm_amd", "csrc", "*")) if os.path.isfile(p))
+    csrc = sorted(p for ext in ("cpp", "hip", "hpp", "h")
+                  for p in glob.glob(os.path.join(root, "norm_amd", "csrc", "*." + ext)))
     inc = sorted(glob.glob(os.path.join(root, "include", "*.h")) + glob.glob(os.path.join(root, "include", "norm_fec", "*.h")))
     h = hashlib.sha256()
     for path in csrc + inc:

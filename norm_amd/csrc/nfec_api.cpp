@@ -1794,15 +1794,20 @@ int create_one(int device, int kind, uint32_t num_data, uint32_t num_parity, uin
 const nfec_codec* primary(const nfec_codec* c) { return c->stripes.empty() ? c : c->stripes[0].get(); }
 nfec_codec* primary(nfec_codec* c) { return c->stripes.empty() ? c : c->stripes[0].get(); }
 
-// the stripe whose device holds a device batch (a single-device codec: itself)
+// the stripe whose device holds a device batch (a single-device codec: itself).  Only device
+// allocations name a device: a batch in host-mapped or registered host memory (which the GPU
+// reads over PCIe, as a single-device codec would pass it through) or in memory HIP does not
+// know runs on the first stripe, so a codec's device list does not change which batches it takes.
 nfec_codec* stripe_for(nfec_codec* c, const void* dev_ptr)
 {
     if (c->stripes.empty()) return c;
     hipPointerAttribute_t at;
+    std::memset(&at, 0, sizeof(at));
     if (hipPointerGetAttributes(&at, dev_ptr) != hipSuccess) {
         (void)hipGetLastError();
-        return nullptr;
+        return c->stripes[0].get();
     }
+    if (at.type != hipMemoryTypeDevice) return c->stripes[0].get();
     for (auto& st : c->stripes)
         if (st->device == at.device) return st.get();
     return nullptr;

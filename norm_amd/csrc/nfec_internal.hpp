@@ -20,6 +20,7 @@ namespace nfec {
 // Error plumbing: the ABI never throws; failures set a thread-local message.
 // ---------------------------------------------------------------------------------
 void set_error(const std::string& msg);
+const char* last_error_cstr();  // this thread's last message
 int fail(int code, const std::string& msg);
 int hip_fail(hipError_t e, const char* what);
 
@@ -346,7 +347,9 @@ void gf16_bs_selectors(const std::vector<uint32_t>& parity_rows, uint32_t k, uin
 // c * tab_col_stride + 2 i: a pass's entries of consecutive columns share scalar-cache lines.
 // Padded by 128 bytes past the last entry (the kernel touches lines ahead of its reads).
 //   flat mode (per_block = 0): item groups run across the blocks; cols = k, rows = m, islot =
-//     in_slot0 + c, oslot = out_slot0 + r (unshortened encode)
+//     in_slot0 + c, oslot = out_slot0 + r (unshortened encode); with num_data (shortened encode,
+//     "flat shortened") each 8-byte piece takes its own block's numData: columns at or past it
+//     read as zeros and its parity row r lands at slot numData + r
 //   per-block mode: item groups inside one block; cols = blk_cols[b] (else num_data[b], else k),
 //     rows = blk_rows[b] (<= 0: skip; else m); islot = in_slots[b][c] or in_slot0 + c; oslot =
 //     out_slots[b][r] or out_slot0 (+ num_data[b] with out_after_data) + r; table per block

@@ -184,7 +184,11 @@ struct Threads {
         std::vector<std::thread> pool;
         for (unsigned i = 0; i < t; ++i) {
             const uint64_t lo = n * i / t, hi = n * (i + 1) / t;
-            pool.emplace_back([=] { f(lo, hi); });
+            try {
+                pool.emplace_back([=] { f(lo, hi); });
+            } catch (...) {
+                f(lo, hi);  // no thread to be had: this range on the calling thread
+            }
         }
         for (auto& th : pool) th.join();
     }
@@ -360,13 +364,27 @@ int run_devices(const int32_t* devices, uint32_t ndev, uint64_t nblocks, F worke
         if (prev >= 0) (void)hipSetDevice(prev);
         return rc;
     }
+    // each worker's error message is thread-local: keep it and set it again on the calling thread
+    // for the first failing worker (as nfec_api.cpp's run_striped does)
     std::vector<int> rcs(ndev, NFEC_OK);
+    std::vector<std::string> errs(ndev);
+    auto one = [&](uint32_t i) {
+        rcs[i] = worker(i, devices[i], nblocks * i / ndev, nblocks * (i + 1) / ndev);
+        if (rcs[i] < 0) errs[i] = last_error_cstr();
+    };
     std::vector<std::thread> th;
-    for (uint32_t i = 0; i < ndev; ++i)
-        th.emplace_back([&, i] { rcs[i] = worker(i, devices[i], nblocks * i / ndev, nblocks * (i + 1) / ndev); });
+    std::vector<uint32_t> inline_ranges;
+    for (uint32_t i = 0; i < ndev; ++i) {
+        try {
+            th.emplace_back(one, i);
+        } catch (...) {
+            inline_ranges.push_back(i);  // no thread to be had: that range on the calling thread
+        }
+    }
+    for (uint32_t i : inline_ranges) one(i);
     for (auto& t : th) t.join();
-    for (int rc : rcs)
-        if (rc) return rc;
+    for (uint32_t i = 0; i < ndev; ++i)
+        if (rcs[i]) return rcs[i] < 0 ? fail(rcs[i], errs[i]) : rcs[i];
     return NFEC_OK;
 }
 

@@ -129,3 +129,17 @@ def test_bad_device_list_fails():
     cfg.num_devices = 2
     h = ctypes.c_void_p()
     assert N.lib().nfec_codec_create_ex(ctypes.byref(cfg), ctypes.byref(h)) == N.NFEC_EDEVICE and not h
+
+
+def test_multi_device_codec_takes_host_mapped_batches(orc):
+    """a device batch in pinned (host-mapped) host memory names no device: a {0, 0} codec runs it
+    on its first stripe, as a one-device codec passes it through -- same bytes either way"""
+    k, m, vec, nb = 16, 4, 64, 5
+    host = orc.make_blocks(k, m, vec, nb)
+    ref = orc.encode_blocks(N.NFEC_RS8, k, m, vec, host.copy())
+    for devices in ([0], [0, 0]):
+        enc, _ = _codecs(N.NFEC_RS8, k, m, vec, devices)
+        pinned = torch.from_numpy(host.copy()).pin_memory()
+        enc.encode_blocks(pinned)
+        torch.cuda.synchronize()
+        assert np.array_equal(pinned.numpy(), ref), devices

@@ -128,7 +128,7 @@ DEC = [
     (32, 16, 1408, 17, 10, 6, False),
     (128, 32, 1400, 9, 20, 5, False),
     (200, 55, 136, 7, 40, 10, True),
-    (64, 32, 1400, 40, 16, 0, True),      # the headline shape, shortened: generic path
+    (64, 32, 1400, 40, 16, 0, True),      # the headline shape, shortened: the one-pass runtime-coefficient repair
     (3, 100, 64, 9, 3, 50, False),        # m > k
     (127, 128, 72, 3, 100, 27, False),    # e = 100: four waves, several pass sets per stage
     (64, 20, 4096, 5, 12, 3, False),      # two item groups per segment
