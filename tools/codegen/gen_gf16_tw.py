@@ -29,7 +29,12 @@ After the last column each row goes back through phi^-1 and the transpose and is
 with the accumulate source when asked).  Workgroup = 4 independent waves (consecutive jobs:
 passes of one item group share their column reads through L2).
 
-Usage: gen_gf16_tw.py OUT.hip [--diag]
+Usage: gen_gf16_tw.py OUT.hip [--diag] [--rows N]
+
+--rows N (default 11): parity rows per wave.  11 rows hold 176 accumulator VGPRs (244 in all: 2
+waves per SIMD); 6 rows 96 (164 in all: 3 waves per SIMD, more waves to hide the snippet calls'
+branch redirects, at more column work per row).  The library built from it must be compiled with
+-DNFEC_TW_ROWS=N.
 """
 import os
 import sys
@@ -67,6 +72,15 @@ S_C, S_COL, S_T0, S_T1, S_T2 = 64, 65, 66, 67, 68
 S_OFF = 72               # 24: the column's table entries (sweep 0: 72..83, sweep 1: 84..95)
 S_LAST = 95
 MASKS = {8: 0x00FF00FF, 4: 0x0F0F0F0F, 2: 0x33333333, 1: 0x55555555}
+
+def set_rows(n):
+    """parity rows per wave and what follows from it"""
+    global ROWS, V_LAST, SPECIAL_ROWS
+    ROWS = n
+    V_LAST = ACC0 + 16 * ROWS - 1
+    # pass row counts with their own (unchecked) step loop
+    SPECIAL_ROWS = tuple(range(ROWS, max(ROWS - 6, 0), -1))
+
 
 # timing probes (wrong parity on purpose), diagnostic library only (--diag, NFEC_TW_VARIANT=<id>):
 #   "nosweep"  no jumps: loads, transpose, phi and combinations only
@@ -409,7 +423,7 @@ S_TB = 96                        # 2: table base (this pass's entries of column 
 S_TBN = 98                       # 2: table address of the column being fetched
 S_LAST4 = 99
 XCH_BUF = 4 * 8 * 64 * 8         # bytes per exchange buffer (4 columns)
-SPECIAL_ROWS = (11, 10, 9, 8, 7, 6)   # pass row counts with their own (unchecked) step loop
+SPECIAL_ROWS = (11, 10, 9, 8, 7, 6)   # pass row counts with their own (unchecked) step loop (set_rows)
 
 
 def col_offset():
@@ -434,10 +448,16 @@ def loads():
     u = _uid[0]
     plain = [f"buffer_load_dwordx2 v[{x[2 * i]}:{x[2 * i + 1]}], %[o{i}], s[{S_DESC}:{S_DESC + 3}], s{S_COL} offen"
              for i in range(8)]
-    masked = []
+    # the pieces' numData - 1 (u16 pairs in LDS at %[lq]); the combinations are free while a
+    # column loads
+    q = [V_CB + 1 + i for i in range(4)]   # (64-bit register pairs start at even registers)
+    masked = [f"ds_read_b64 v[{q[0]}:{q[1]}], %[lq]", f"ds_read_b64 v[{q[2]}:{q[3]}], %[lq] offset:8",
+              "s_waitcnt lgkmcnt(0)"]
     for i in range(8):
-        t = V_CA + i   # the combinations are free while a column loads
-        masked += [f"v_subrev_u32 v{t}, s{S_C}, %[q{i}]",                      # numData - 1 - c
+        t = V_CA + i
+        src = q[i // 2]
+        masked += [f"v_lshrrev_b32 v{t}, 16, v{src}" if i & 1 else f"v_and_b32 v{t}, 0xffff, v{src}",
+                   f"v_subrev_u32 v{t}, s{S_C}, v{t}",                          # numData - 1 - c
                    f"v_and_or_b32 v{t}, v{t}, s{S_DESC + 2}, %[o{i}]",          # sign -> bit 31
                    f"buffer_load_dwordx2 v[{x[2 * i]}:{x[2 * i + 1]}], v{t}, s[{S_DESC}:{S_DESC + 3}], s{S_COL} offen"]
     return ([f"s_bitcmp1_b32 %[md], 0", f"s_cbranch_scc0 Lldp{u}_%="] + masked +
@@ -620,6 +640,10 @@ def main():
     global FLAGS
     diag = "--diag" in sys.argv
     args = [a for a in sys.argv[1:] if a != "--diag"]
+    if "--rows" in args:
+        i = args.index("--rows")
+        set_rows(int(args[i + 1]))
+        del args[i:i + 2]
     path = args[0]
     variants = DIAG_VARIANTS if diag else VARIANTS
     asms = {}
@@ -627,12 +651,12 @@ def main():
         FLAGS = f
         asms[v] = "\\n\"\n            \"".join(body())
     FLAGS = ()
-    ins = ", ".join([f'[o{i}] "v"(o[{i}])' for i in range(8)] + [f'[q{i}] "v"(q[{i}])' for i in range(8)])
+    ins = ", ".join(f'[o{i}] "v"(o[{i}])' for i in range(8))
     common = """[wb] "s"(wb), [ss] "s"(a.seg_stride), [k] "s"(kk), [tw] "s"(tw), [tstep] "s"(tstep), [t1off] "s"(t1off), [nr] "s"(nr),
               [csh] "s"(a.col_shift), [cmk] "s"(a.col_mask), [cck] "s"(cck), [cbb] "s"(cbb),
               [acc] "s"(a.accumulate), [ob] "s"(ob), [ab] "s"(ab), [oslot] "s"(a.out_slot0 + row0),
               [oss] "s"(a.out_seg_stride), [aslot] "s"(a.acc_slot0 + row0), [ass] "s"(a.acc_seg_stride),
-              [wv] "s"(wave), [rp] "s"(rp), [md] "s"(md), [lo] "v"(lo), [xl] "v"(xl), """ + ins
+              [wv] "s"(wave), [rp] "s"(rp), [md] "s"(md), [lo] "v"(lo), [xl] "v"(xl), [lq] "v"(lq), """ + ins
     blocks = []
     for v in variants:
         kw = "if constexpr" if v == 0 else "else if constexpr"
@@ -662,6 +686,8 @@ def main():
 }""" % len(variants)
     else:
         tw_variant = "constexpr int tw_variant() { return 0; }"
+    # waves per SIMD the register file allows (512 VGPRs per lane, allocated in granules of 8)
+    WAVES_PER_SIMD = min(8, 512 // ((V_LAST + 1 + 7) // 8 * 8))
     phi_cols = ", ".join(f"0x{c:04x}" for c in PHI)
     phi_inv_cols = ", ".join(f"0x{c:04x}" for c in PHI_INV)
     src = f"""// GENERATED by tools/codegen/gen_gf16_tw.py -- do not edit by hand.
@@ -683,7 +709,9 @@ __device__ __forceinline__ uint32_t gf16_tw_passes_dev(uint32_t m)
 template <int V>
 __device__ __forceinline__ void tw_body(const Gf16T3Args& a, uint32_t wg)
 {{
-    __shared__ uint32_t lds[{NWAVES} * 64 * 16];       // the lanes' store offsets (epilogue)
+    // per lane: 8 output and 8 accumulate-source offsets (epilogue), then the 8 pieces' numData - 1
+    // as u16 pairs (flat shortened loads)
+    __shared__ uint32_t lds[{NWAVES} * 64 * 20];
     __shared__ uint64_t xch[2 * {XCH_BUF // 8}];       // column planes exchange (body)
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -732,7 +760,7 @@ __device__ __forceinline__ void tw_body(const Gf16T3Args& a, uint32_t wg)
     const uint32_t b0 = pb ? pblk : __builtin_amdgcn_readfirstlane((uint32_t)(f0 / a.vec_bytes));
     const uint8_t* wb = a.base + (uint64_t)b0 * a.block_stride;
     uint32_t o[8], q[8];
-    uint32_t* po = lds + (wave * 64u + lane) * 16u;
+    uint32_t* po = lds + (wave * 64u + lane) * 20u;
 #pragma unroll
     for (int i = 0; i < 8; ++i) {{
         const uint64_t f = f0 + (uint64_t)i * 512u + lane * 8u;
@@ -750,8 +778,11 @@ __device__ __forceinline__ void tw_body(const Gf16T3Args& a, uint32_t wg)
                                     (a.acc_after_data ? (uint64_t)pnd * a.acc_seg_stride : 0u)) + p
                        : 0x80000000u;
     }}
+#pragma unroll
+    for (int i = 0; i < 4; ++i) po[16 + i] = (q[2 * i] & 0xFFFFu) | (q[2 * i + 1] << 16);
     const uint32_t md = __builtin_amdgcn_readfirstlane(lnd);
     const uint32_t lo = bs::lds_addr(po);
+    const uint32_t lq = lo + 64u;
     const uint32_t xl = bs::lds_addr(xch) + lane * 8u;
     // table [column][sweep][row][2 entries]: this pass's rows start 2 * row0 elements in
     const uint16_t* tw = a.tw + (uint64_t)b0 * (pb ? a.tw_block_stride : 0u) + 2u * row0;
@@ -765,7 +796,7 @@ __device__ __forceinline__ void tw_body(const Gf16T3Args& a, uint32_t wg)
 }}
 
 template <int V>
-__global__ __launch_bounds__({64 * NWAVES}, 2) void gf16_tw_encode_kernel(Gf16T3Args a)
+__global__ __launch_bounds__({64 * NWAVES}, {WAVES_PER_SIMD}) void gf16_tw_encode_kernel(Gf16T3Args a)
 {{
     tw_body<V>(a, bs::wg_index(1));
 }}
@@ -773,12 +804,12 @@ __global__ __launch_bounds__({64 * NWAVES}, 2) void gf16_tw_encode_kernel(Gf16T3
 // several independent products in one grid (the RS16 Toeplitz split, rs16_tmvp): workgroup
 // ranges [wg_end[i-1], wg_end[i]) run problem i, so their tails share one launch
 template <int V>
-__global__ __launch_bounds__({64 * NWAVES}, 2) void gf16_tw_multi_kernel(Gf16T3Multi mm)
+__global__ __launch_bounds__({64 * NWAVES}, {WAVES_PER_SIMD}) void gf16_tw_multi_kernel(Gf16T3Multi mm)
 {{
     const uint32_t wg = bs::wg_index(1);
-    if (wg < mm.wg_end[0]) tw_body<V>(mm.e[0], wg);
-    else if (wg < mm.wg_end[1]) tw_body<V>(mm.e[1], wg - mm.wg_end[0]);
-    else tw_body<V>(mm.e[2], wg - mm.wg_end[1]);
+    // one body instance (three would hold three argument sets live: more registers, fewer waves)
+    const uint32_t i = wg < mm.wg_end[0] ? 0u : wg < mm.wg_end[1] ? 1u : 2u;
+    tw_body<V>(mm.e[i], wg - (i ? mm.wg_end[i - 1] : 0u));
 }}
 
 {tw_variant}
