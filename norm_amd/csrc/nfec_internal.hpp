@@ -301,7 +301,7 @@ bool gf16_t3_covers(const Gf16T3Args& a);  // launch_gf16_t3_encode would take i
 int launch_gf16_t3_multi(const Gf16T3Args* e, uint32_t n, hipStream_t s);  // n <= 3 independent products
 // the same products through the tower field GF((2^8)^2) (gen_gf16_tw.hip): reads a.tw, not a.offs
 #ifndef NFEC_TW_ROWS
-#define NFEC_TW_ROWS 11  // parity rows per wave of the tower kernel (gen_gf16_tw.py --rows)
+#define NFEC_TW_ROWS 6  // parity rows per wave of the tower kernel (gen_gf16_tw.py --rows)
 #endif
 constexpr uint32_t kGf16TwRowsPerPass = NFEC_TW_ROWS;
 int launch_gf16_tw_encode(const Gf16T3Args& a, hipStream_t s);  // NFEC_ENOTSUP: shape not covered

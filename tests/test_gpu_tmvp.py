@@ -1,7 +1,7 @@
 """RS16 encode by the Toeplitz split (kernels_tmvp.hip + gen_gf16_t3.hip multi launch) against
 the oracle on the GPU, bit-exact.  NFEC_OPT_RS16_TOEPLITZ_ON forces the split for shapes where
-it is allowed but not chosen by default (NFEC_OPT_RS16_TOEPLITZ_OFF: never); (256, 64) and C4
-take it by default."""
+it is allowed but not chosen by default (NFEC_OPT_RS16_TOEPLITZ_OFF: never); (128, 32), (512, 128)
+and C4 take it by default (fewer passes of the tower kernel's 6 rows per wave)."""
 
 import numpy as np
 import pytest
@@ -26,14 +26,15 @@ CASES = [
     (64, 16, 1400, 1400, 5, "1", True),
     (128, 32, 64, 64, 37, "1", True),     # several item groups, short segments
     (128, 32, 1408, 1416, 3, "1", True),  # padded segment stride
-    (256, 64, 1400, 1400, 4, None, True),  # chosen by default (3 x 1 pass of 128 columns < 2 x 256)
+    (128, 32, 1400, 1400, 4, None, True),  # chosen by default (3 x 4 passes of 64 columns < 8 x 128)
+    (256, 64, 1400, 1400, 4, None, False),  # same pass count either way (3 x 8 x 128 = 12 x 256): not chosen
     (256, 64, 1400, 1400, 4, "0", False),
-    (512, 128, 64, 64, 2, "1", True),     # three passes of 44 rows per product
+    (512, 128, 64, 64, 2, "1", True),     # several passes per product
     (32, 8, 8, 8, 7, "1", True),          # one item per segment, chunk width 4
     (96, 16, 72, 72, 5, "1", True),       # three chunk pairs
     (1024, 64, 1400, 1400, 2, "1", True),
     (2048, 128, 64, 64, 2, "1", True),    # same pass count either way: forced
-    (1024, 64, 64, 64, 3, None, True),    # chosen by default (3 x 1 pass of 512 < 2 x 1024)
+    (512, 128, 64, 64, 3, None, True),    # chosen by default (3 x 12 passes of 256 < 24 x 512)
     (96, 24, 1400, 1400, 3, "1", False),  # m / 2 not a power of two: not allowed
     (100, 20, 1400, 1400, 3, "1", False),  # k not a multiple of m
 ]

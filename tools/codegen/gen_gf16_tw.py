@@ -31,10 +31,11 @@ passes of one item group share their column reads through L2).
 
 Usage: gen_gf16_tw.py OUT.hip [--diag] [--rows N]
 
---rows N (default 11): parity rows per wave.  11 rows hold 176 accumulator VGPRs (244 in all: 2
-waves per SIMD); 6 rows 96 (164 in all: 3 waves per SIMD, more waves to hide the snippet calls'
-branch redirects, at more column work per row).  The library built from it must be compiled with
--DNFEC_TW_ROWS=N.
+--rows N (default 6): parity rows per wave.  6 rows hold 96 accumulator VGPRs (164 in all: 3 waves
+per SIMD, which hide the snippet calls' branch redirects: RS16(400,100) encode 27.1 -> 22.9 ms,
+C4 133.4 -> 125.8 ms against 11 rows, profiles/r05/tw_rows_ab); 11 rows hold 176 (244 in all: 2
+waves per SIMD, less column work per row; the round-3/4 kernel).  A library built from another
+value must be compiled with -DNFEC_TW_ROWS=N.
 """
 import os
 import sys
@@ -44,7 +45,7 @@ from gen_rs8_bitsliced import bitmatrix_rows  # noqa: E402
 from gen_rs8_bitsliced import mul as gf8_mul  # noqa: E402  (the RS8 field, 0x11d)
 
 P16 = 0x1100B            # the reference's GF(2^16) polynomial
-ROWS = 11                # parity rows per wave (pass)
+ROWS = 6                 # parity rows per wave (pass); set_rows() below fixes what follows from it
 NWAVES = 4               # independent waves per workgroup
 GROUP_BYTES = 4096       # flat bytes per item group: 64 lanes x 8 pieces x 8 bytes
 SNIP_ALIGN = 7           # 128-byte snippet slots
@@ -59,7 +60,7 @@ V_CA = 42                # 11: combinations of planes 0..3 of the source
 V_CB = 53                # 11: combinations of planes 4..7
 V_TMP = [64, 65, 66, 67]
 ACC0 = 68                # row r: out0 planes ACC0 + 16 r + (0..7), out1 + 8
-V_LAST = ACC0 + 16 * ROWS - 1   # 243
+V_LAST = ACC0 + 16 * ROWS - 1   # 163 at 6 rows
 # (register pairs of loads and stores must start at even registers; v9 stays unused so the
 # compiler places the nine inputs in v0..v8)
 MULTI = [a for a in range(1, 16) if bin(a).count("1") >= 2]
@@ -423,7 +424,7 @@ S_TB = 96                        # 2: table base (this pass's entries of column 
 S_TBN = 98                       # 2: table address of the column being fetched
 S_LAST4 = 99
 XCH_BUF = 4 * 8 * 64 * 8         # bytes per exchange buffer (4 columns)
-SPECIAL_ROWS = (11, 10, 9, 8, 7, 6)   # pass row counts with their own (unchecked) step loop (set_rows)
+SPECIAL_ROWS = (6, 5, 4, 3, 2, 1)   # pass row counts with their own (unchecked) step loop (set_rows)
 
 
 def col_offset():

@@ -12,7 +12,8 @@
 #              source loss, uniform loss over all k + m segments, shortened batches (numData in
 #              [k/2, k]), accumulate, and vec 1460 (vec % 8 != 0); one JSON line each
 #   c4         C4 RS16(4096,256) encode line (with its op roofline) under a kernel trace
-#   pmc_rs16   PMC passes of RS16(400,100) (tools/pmc_r03.sh; instruction mix, cycles, HBM bytes)
+#   pmc_rs16   PMC passes of the RS16(400,100) encode (tools/pmc_r03.sh; instruction mix, cycles,
+#              HBM bytes) -> pmc_tw_rs16_summary.json, which bench_extra's op roofline reads
 #   pmc_c4     PMC passes of C4 (tools/pmc_c4.sh)
 #   pmc_bench  PMC passes of the headline workload (tools/pmc_r03.sh: HBM bytes for bench.py)
 #   mdp        MDP(64,32) encode + 16-erasure repair line
@@ -63,10 +64,18 @@ for task in "$@"; do
     c4)
         prof c4 "$R/tools/bench_extra.py" --workload c4 || die c4 $? ;;
     pmc_rs16)
-        PMC_SCRIPT=tools/bench_extra.py PMC_ARGS="--workload rs16 --steps 1 --warmup 1" \
+        # the encode alone (--erasures 0), so the tower kernel's counters are the encode's
+        PMC_SCRIPT=tools/bench_extra.py PMC_ARGS="--workload rs16 --erasures 0 --steps 1 --warmup 1" \
         PMC_GROUPS="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_BRANCH SQ_INSTS_LDS SQ_INSTS_SMEM SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR;SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_SCA;GRBM_GUI_ACTIVE GRBM_COUNT;FETCH_SIZE;WRITE_SIZE" \
         TAG=${TAG}_rs16 timeout -k 10 900 bash tools/pmc_r03.sh > "$O/pmc_rs16.log" 2>&1 || die pmc_rs16 $?
-        cp "$R/gpurun_out/pmc_${TAG}_rs16/summary.json" "$O/pmc_rs16_summary.json" ;;
+        python3 - "$R/gpurun_out/pmc_${TAG}_rs16/summary.json" "$O/pmc_tw_rs16_summary.json" <<'PY' || die pmc_rs16 $?
+import json, sys
+d = json.load(open(sys.argv[1]))
+d["_workload"] = {"workload": "rs16", "k": 400, "m": 100, "vec": 1400, "blocks": 16384,
+                  "counters": "rocprofv3 --pmc, one group per pass (tools/session.sh pmc_rs16); encode only; per-launch averages"}
+json.dump(d, open(sys.argv[2], "w"), indent=1, sort_keys=True)
+PY
+        ;;
     pmc_c4)
         TAG=${TAG}_c4 timeout -k 10 900 bash tools/pmc_c4.sh > "$O/pmc_c4.log" 2>&1 || die pmc_c4 $?
         cp "$R/gpurun_out/pmc_${TAG}_c4/summary.json" "$O/pmc_c4_summary.json" ;;
