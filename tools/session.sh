@@ -20,6 +20,9 @@
 #   rs8sweep   RS8 shape sweep (tools/bench_extra.py --workload rs8sweep) under a kernel trace
 #   c5         tools/bench_c5.py --steps 2 (the C5 mix's one-GPU share)
 #   percall    tools/percall per-call latencies (needs tools/percall/_build/percall)
+#   ab         A/B of the product library against AB_LIB (another build of the same sources, e.g.
+#              a generator option, loaded through NFEC_LIBRARY): the RS16 GPU tests on AB_LIB,
+#              then rs16 and c4 lines from both, alternating, AB_REPS times (default 2)
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 R=$(pwd)
 TAG=${TAG:-r05}
@@ -94,6 +97,21 @@ PY
         : > "$O/percall.jsonl"
         for args in "rs8 64 32 1408 16 2000" "rs8 64 16 1408 8 2000" "rs8 16 4 1408 4 2000" "rs16 400 100 1400 50 200" "mdp 64 32 1408 16 500"; do
             timeout -k 10 120 tools/percall/_build/percall $args >> "$O/percall.jsonl" || die percall $?
+        done ;;
+    ab)
+        [ -n "$AB_LIB" ] || die "ab (AB_LIB unset)" 2
+        NFEC_LIBRARY=$R/$AB_LIB timeout -k 10 600 python3 -u -m pytest -x -q --timeout 120 --timeout-method thread \
+            -p no:cacheprovider tests/test_gpu_rs16_tw.py tests/test_gpu_rs16_kernels.py tests/test_c4_c5.py -m gpu \
+            > "$O/pytest_ab.log" 2>&1 || { tail -n 20 "$O/pytest_ab.log"; die ab_tests 1; }
+        tail -n 1 "$O/pytest_ab.log"
+        for i in $(seq 1 "${AB_REPS:-2}"); do
+            for w in rs16 c4; do
+                timeout -k 10 300 python3 tools/bench_extra.py --workload $w > "$O/${w}_a_$i.json" || die ab $?
+                NFEC_LIBRARY=$R/$AB_LIB timeout -k 10 300 python3 tools/bench_extra.py --workload $w > "$O/${w}_b_$i.json" || die ab $?
+            done
+        done
+        for f in "$O"/*_[ab]_*.json; do
+            python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print(sys.argv[1], d.get('encode_ms'), d.get('decode_ms'))" "$f"
         done ;;
     *)
         echo "session: unknown task $task"; exit 2 ;;
