@@ -126,7 +126,7 @@ def test_toeplitz_host_pipeline_chunks(orc, pinned, monkeypatch):
     """Host-resident encode through the split: four chunks over the three slot streams share
     the codec's scratch (ordered by its event)."""
     k, m, vec, nb = 256, 64, 1400, 10
-    enc = _encoder(k, m, vec, None)
+    enc = _encoder(k, m, vec, "1")
     assert enc.features() & NFEC_FEATURE_RS16_TOEPLITZ
     host = orc.make_blocks(k, m, vec, nb)
     ref = orc.encode_blocks(orc.RS16, k, m, vec, host.copy())
