@@ -173,10 +173,10 @@ def test_register_map_is_disjoint():
 
 @pytest.mark.parametrize("m", [1, 4, 11, 12, 44, 45, 50, 100, 128, 200, 256])
 def test_pass_partition(m):
-    """rows spread evenly over whole workgroups of four passes, at most ROWS rows per pass,
+    """rows spread evenly over whole workgroups of NWAVES passes, at most ROWS rows per pass,
     every row in exactly one pass (the kernel's row0/nr and gf16_tw_offsets use the same split)"""
     P = g.n_passes(m)
-    assert P % 4 == 0 and P >= 4
+    assert P % g.NWAVES == 0 and P >= g.NWAVES
     rows = []
     for p in range(P):
         lo, hi = g.pass_rows(m, P, p)

@@ -46,7 +46,7 @@ from gen_rs8_bitsliced import mul as gf8_mul  # noqa: E402  (the RS8 field, 0x11
 
 P16 = 0x1100B            # the reference's GF(2^16) polynomial
 ROWS = 6                 # parity rows per wave (pass); set_rows() below fixes what follows from it
-NWAVES = 4               # independent waves per workgroup
+NWAVES = 4               # waves per workgroup (passes of one item group sharing its columns; --waves)
 GROUP_BYTES = 4096       # flat bytes per item group: 64 lanes x 8 pieces x 8 bytes
 SNIP_ALIGN = 7           # 128-byte snippet slots
 TBL_HALF = 48            # 16-bit table entries per (column, pass): 11 rows x 4 + 4 padding
@@ -73,6 +73,13 @@ S_C, S_COL, S_T0, S_T1, S_T2 = 64, 65, 66, 67, 68
 S_OFF = 72               # 24: the column's table entries (sweep 0: 72..83, sweep 1: 84..95)
 S_LAST = 95
 MASKS = {8: 0x00FF00FF, 4: 0x0F0F0F0F, 2: 0x33333333, 1: 0x55555555}
+
+def set_waves(n):
+    """waves per workgroup and what follows from it"""
+    global NWAVES, XCH_BUF
+    NWAVES = n
+    XCH_BUF = NWAVES * 8 * 64 * 8
+
 
 def set_rows(n):
     """parity rows per wave and what follows from it"""
@@ -423,7 +430,7 @@ S_SB, S_BUF, S_WV = 69, 70, 71   # step's first column; exchange buffer byte off
 S_TB = 96                        # 2: table base (this pass's entries of column 0)
 S_TBN = 98                       # 2: table address of the column being fetched
 S_LAST4 = 99
-XCH_BUF = 4 * 8 * 64 * 8         # bytes per exchange buffer (4 columns)
+XCH_BUF = NWAVES * 8 * 64 * 8    # bytes per exchange buffer (NWAVES columns; set_waves)
 SPECIAL_ROWS = (6, 5, 4, 3, 2, 1)   # pass row counts with their own (unchecked) step loop (set_rows)
 
 
@@ -505,7 +512,7 @@ def apply_col(j, x, nrows):
     L += sweep(0, y, nrows)
     L.append("s_waitcnt lgkmcnt(0)")
     L += [f"v_mov_b32 v{V_W + i}, v{V_S + i}" for i in range(8)]
-    if j < 3:
+    if j < NWAVES - 1:
         L += [f"s_add_u32 s{S_T2}, s{S_SB}, {j + 1}", f"s_cmp_lt_u32 s{S_T2}, %[k]", f"s_cbranch_scc0 Lnf{y}_%="]
         L += fetch(j + 1, 0)
         L.append(f"Lnf{y}_%=:")
@@ -529,15 +536,15 @@ def step_loop(x, nrows):
         L.append(f"ds_write_b64 v{V_TMP[0]}, v[{V_S + 2 * p}:{V_S + 2 * p + 1}] offset:{512 * (4 + p)}")
     L.append(f"Lnotr{x}_%=:")
     # the wave's column of the next step goes into the (now free) slot
-    L += [f"s_add_u32 s{S_C}, s{S_C}, 4", f"s_cmp_lt_u32 s{S_C}, %[k]", f"s_cbranch_scc0 Lnl{x}_%="]
+    L += [f"s_add_u32 s{S_C}, s{S_C}, {NWAVES}", f"s_cmp_lt_u32 s{S_C}, %[k]", f"s_cbranch_scc0 Lnl{x}_%="]
     L += col_offset() + loads()
     L += [f"Lnl{x}_%=:", "s_waitcnt lgkmcnt(0)", "s_barrier"]
     if nrows is None:
         L += ["s_cmp_eq_u32 %[nr], 0", f"s_cbranch_scc1 Lend{x}_%="]
     L += fetch(0, 0)
-    for j in range(4):
+    for j in range(NWAVES):
         L += apply_col(j, x, nrows)
-    L += [f"Lend{x}_%=:", f"s_xor_b32 s{S_BUF}, s{S_BUF}, {XCH_BUF}", f"s_add_u32 s{S_SB}, s{S_SB}, 4",
+    L += [f"Lend{x}_%=:", f"s_xor_b32 s{S_BUF}, s{S_BUF}, {XCH_BUF}", f"s_add_u32 s{S_SB}, s{S_SB}, {NWAVES}",
           f"s_cmp_lt_u32 s{S_SB}, %[k]", f"s_cbranch_scc1 Lstep{x}_%="]
     return L
 
@@ -624,7 +631,7 @@ def pass_rows(m, passes, p):
 def n_passes(m):
     """passes of a product with m rows: the fewest of at most ROWS rows, rounded up to whole
     workgroups of four"""
-    return (((m + ROWS - 1) // ROWS) + 3) // 4 * 4
+    return (((m + ROWS - 1) // ROWS) + NWAVES - 1) // NWAVES * NWAVES
 
 
 def clobbers(last_s=None):
@@ -644,6 +651,10 @@ def main():
     if "--rows" in args:
         i = args.index("--rows")
         set_rows(int(args[i + 1]))
+        del args[i:i + 2]
+    if "--waves" in args:
+        i = args.index("--waves")
+        set_waves(int(args[i + 1]))
         del args[i:i + 2]
     path = args[0]
     variants = DIAG_VARIANTS if diag else VARIANTS
@@ -704,7 +715,7 @@ namespace {{
 
 __device__ __forceinline__ uint32_t gf16_tw_passes_dev(uint32_t m)
 {{
-    return ((m + {ROWS - 1}u) / {ROWS}u + 3u) / 4u * 4u;
+    return ((m + {ROWS - 1}u) / {ROWS}u + {NWAVES - 1}u) / {NWAVES}u * {NWAVES}u;
 }}
 
 template <int V>
@@ -716,7 +727,7 @@ __device__ __forceinline__ void tw_body(const Gf16T3Args& a, uint32_t wg)
     __shared__ uint64_t xch[2 * {XCH_BUF // 8}];       // column planes exchange (body)
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const uint32_t quads = a.passes / 4u;
+    const uint32_t quads = a.passes / {NWAVES}u;   // workgroups per item group
     const uint32_t group = wg / quads, quad = wg - group * quads;
     // flat mode: item groups run over the batch's bytes across blocks (one coefficient table);
     // per-block mode (blk_rows): each group lies in one block, which has its own table, row
@@ -754,8 +765,8 @@ __device__ __forceinline__ void tw_body(const Gf16T3Args& a, uint32_t wg)
     // the rows in play spread evenly over whole workgroups of four passes (the table holds any
     // row range); the launch sized the grid for a.m rows, so later workgroups may leave
     const uint32_t npass = gf16_tw_passes_dev(rlim);
-    if (rlim == 0u || kk == 0u || quad * 4u >= npass) return;
-    const uint32_t pass = quad * 4u + wave;
+    if (rlim == 0u || kk == 0u || quad * {NWAVES}u >= npass) return;
+    const uint32_t pass = quad * {NWAVES}u + wave;
     const uint32_t row0 = pass * rlim / npass, row1 = (pass + 1u) * rlim / npass;
     const uint32_t nr = __builtin_amdgcn_readfirstlane(row1 - row0);
     const uint32_t b0 = pb ? pblk : __builtin_amdgcn_readfirstlane((uint32_t)(f0 / a.vec_bytes));
@@ -852,7 +863,7 @@ int tw_prepare(const Gf16T3Args& a, Gf16T3Args& b, uint64_t& wgs)
     if (a.blk_rows && (!a.row_off || !a.tw_block_stride || a.accumulate)) return NFEC_ENOTSUP;
     const uint64_t groups = a.blk_rows ? (uint64_t)a.nblocks * ((a.vec_bytes + {GROUP_BYTES - 1}u) / {GROUP_BYTES}u)
                                        : (total + {GROUP_BYTES - 1}u) / {GROUP_BYTES}u;
-    wgs = groups * (b.passes / 4u);
+    wgs = groups * (b.passes / {NWAVES}u);
     return wgs >= (1ull << 31) ? NFEC_ENOTSUP : NFEC_OK;
 }}
 
@@ -914,7 +925,7 @@ void gf16_tw_field(uint16_t phi_cols[16], uint32_t* lam, uint16_t* phi_inv_cols)
 
 uint32_t gf16_tw_passes(uint32_t m)
 {{
-    return ((m + {ROWS - 1}u) / {ROWS}u + 3u) / 4u * 4u;
+    return ((m + {ROWS - 1}u) / {ROWS}u + {NWAVES - 1}u) / {NWAVES}u * {NWAVES}u;
 }}
 
 size_t gf16_tw_table_elems(uint32_t k, uint32_t m)
