@@ -129,11 +129,13 @@ enum {
     NFEC_OPT_RS16_TOEPLITZ_OFF = 1u << 1,  /* RS16 encode never uses the Toeplitz split */
     NFEC_OPT_RS16_TOEPLITZ_ON = 1u << 2,   /* ... uses it whenever the shape allows it, not
                                               only where it needs fewer passes */
-    NFEC_OPT_HOST_ONLY = 1u << 3           /* no device at all (a NORM node without a usable
+    NFEC_OPT_HOST_ONLY = 1u << 3,          /* no device at all (a NORM node without a usable
                                               gfx950): Init's math on the host, and only the host
                                               per-call paths (nfec_encode_segment_host,
                                               nfec_decode_vectors_host) run; every GPU entry
                                               returns NFEC_EDEVICE.  No device list. */
+    NFEC_OPT_RS16_TOEPLITZ_ONE_LEVEL = 1u << 4  /* the Toeplitz split at one Karatsuba level at
+                                                   most (default: two where they save passes) */
 };
 
 /* One codec over one or several GPUs of a node.  With several devices the codec holds the
@@ -163,6 +165,8 @@ int nfec_codec_get_info(const nfec_codec* codec, nfec_codec_info* out);
  *   NFEC_FEATURE_RS16_TOEPLITZ: unshortened, overwriting RS16 encodes use the Toeplitz split of
  *   the generator (three (m/2)-row products over k/2 columns). */
 #define NFEC_FEATURE_RS16_TOEPLITZ 1
+/* ... at two Karatsuba levels: nine (m/4)-row products over k/4 columns (tower kernel) */
+#define NFEC_FEATURE_RS16_TOEPLITZ2 2
 int nfec_codec_features(const nfec_codec* codec);
 /* Copies the m x k parity rows of the systematic generator (row p = generator row k+p),
  * row-major, elements of symbol_bytes each.  MDP: the m x k matrix of the LFSR code for a

@@ -18,8 +18,9 @@ HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "nfec.h")
 NFEC_RS8, NFEC_RS16, NFEC_MDP = 1, 2, 3
 NFEC_OK, NFEC_EINVAL, NFEC_ENOMEM, NFEC_EDEVICE, NFEC_ERANGE, NFEC_ENOTSUP = 0, -1, -2, -3, -4, -5
 NFEC_ACCUMULATE = 1
-NFEC_FEATURE_RS16_TOEPLITZ = 1
+NFEC_FEATURE_RS16_TOEPLITZ, NFEC_FEATURE_RS16_TOEPLITZ2 = 1, 2
 NFEC_OPT_RS16_SHARED_TABLES, NFEC_OPT_RS16_TOEPLITZ_OFF, NFEC_OPT_RS16_TOEPLITZ_ON, NFEC_OPT_HOST_ONLY = 1, 2, 4, 8
+NFEC_OPT_RS16_TOEPLITZ_ONE_LEVEL = 16
 NFEC_HOST_GF_SCALAR, NFEC_HOST_GF_AVX2, NFEC_HOST_GF_GFNI = 0, 1, 2
 
 

@@ -123,7 +123,126 @@ __global__ __launch_bounds__(256, 4) void tmvp_postscale_kernel(Rs16TmvpArgs a)
     store16(o, r1, a.block_stride, m);
 }
 
+// ---- two Karatsuba levels (rs16_tmvp_plan_levels, levels = 2) ----
+// Scratch per block (sc, sc_block_stride; columns of vec bytes): the level-1 pair sums v at
+// [0, k/2) (virtual column q*cw + i), the level-2 scaled sums s_0, s_1, s_2 at k/2 + X*k/4 + u
+// (u = q*hw + i, i < hw), then the nine hw-row products at k/2 + 3k/4 + e*hw + p.
+__device__ __forceinline__ uint32_t tmvp2_prow0(const Rs16TmvpArgs& a) { return a.k / 2u + 3u * (a.k / 4u); }
+
+// per (q, i < hw): u_j = c_j d_j for j = a0, a1 = a0 + hw, b0 = a0 + cw, b1 = b0 + hw, then
+//   v at q cw + i = u_a0 + u_b0, at q cw + hw + i = u_a1 + u_b1   (the level-1 pair sums, halves)
+//   s_0 = both pair sums, s_1 = u_b0 + u_b1, s_2 = u_a0 + u_a1      (level 2's alpha inputs)
+// (the products are linear, so the sums are taken after transposing back to symbols)
+__global__ __launch_bounds__(256, 3) void tmvp2_prescale_kernel(Rs16TmvpArgs a)
+{
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t wid = __builtin_amdgcn_readfirstlane(blockIdx.x * 4u + (threadIdx.x >> 6));
+    const uint32_t quarter = a.k / 4u;
+    const uint32_t u = wid % quarter, chunk = wid / quarter;
+    const uint32_t ipb = a.vec / 8u, items = a.nblocks * ipb;
+    if (chunk * 512u >= items) return;
+    const uint32_t q = u / a.hw, i = u - q * a.hw;
+    const uint32_t a0 = 2u * q * a.cw + i;
+    const uint32_t col[4] = {a0, a0 + a.hw, a0 + a.cw, a0 + a.cw + a.hw};  // a0, a1, b0, b1
+    ItemMap m;
+    map_items(chunk, lane, items, ipb, m);
+    uint32_t r[4][16];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+        uint32_t x[16];
+        load16(x, a.base + (uint64_t)col[t] * a.seg_stride, a.block_stride, m);
+        bs16::transpose(x);
+#pragma unroll
+        for (int p = 0; p < 16; ++p) r[t][p] = 0;
+        bs16::mulc_acc(x, r[t], a.cmat + 16u * col[t]);
+        bs16::transpose(r[t]);
+    }
+    uint32_t v0[16], v1[16], o[16];
+#pragma unroll
+    for (int p = 0; p < 16; ++p) v0[p] = r[0][p] ^ r[2][p], v1[p] = r[1][p] ^ r[3][p];
+    uint8_t* sc = a.sc;
+    store16(v0, sc + (uint64_t)(q * a.cw + i) * a.vec, a.sc_block_stride, m);
+    store16(v1, sc + (uint64_t)(q * a.cw + a.hw + i) * a.vec, a.sc_block_stride, m);
+#pragma unroll
+    for (int p = 0; p < 16; ++p) o[p] = v0[p] ^ v1[p];
+    store16(o, sc + (uint64_t)(a.k / 2u + u) * a.vec, a.sc_block_stride, m);
+#pragma unroll
+    for (int p = 0; p < 16; ++p) o[p] = r[2][p] ^ r[3][p];
+    store16(o, sc + (uint64_t)(a.k / 2u + quarter + u) * a.vec, a.sc_block_stride, m);
+#pragma unroll
+    for (int p = 0; p < 16; ++p) o[p] = r[0][p] ^ r[1][p];
+    store16(o, sc + (uint64_t)(a.k / 2u + 2u * quarter + u) * a.vec, a.sc_block_stride, m);
+}
+
+// per p < hw: level-1 product X's rows p (top) and hw + p (bottom) are P_aX + P_bX and
+// P_aX + P_gX (products e = 3X, 3X + 1, 3X + 2); parity rows p and hw + p (R0) take X = 0, 1,
+// rows cw + p and cw + hw + p (R1) take X = 0, 2, then W(y_r) and G[r][0] d_0 as at one level
+__global__ __launch_bounds__(256, 3) void tmvp2_postscale_kernel(Rs16TmvpArgs a)
+{
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t wid = __builtin_amdgcn_readfirstlane(blockIdx.x * 4u + (threadIdx.x >> 6));
+    const uint32_t p = wid % a.hw, chunk = wid / a.hw;
+    const uint32_t ipb = a.vec / 8u, items = a.nblocks * ipb;
+    if (chunk * 512u >= items) return;
+    ItemMap m;
+    map_items(chunk, lane, items, ipb, m);
+    const uint8_t* pr = a.sc + (uint64_t)(tmvp2_prow0(a) + p) * a.vec;  // product e at + e * hw * vec
+    // sums over (R0 top, R0 bottom, R1 top, R1 bottom) of the nine products (e = 3X + {a, b, g})
+    constexpr uint8_t uses[9] = {0xF, 0x5, 0xA, 0x3, 0x1, 0x2, 0xC, 0x4, 0x8};
+    uint32_t sum[4][16], x[16];
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int j = 0; j < 16; ++j) sum[t][j] = 0;
+#pragma unroll
+    for (int e = 0; e < 9; ++e) {
+        load16(x, pr + (uint64_t)e * a.hw * a.vec, a.sc_block_stride, m);
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+            if (uses[e] & (1u << t))
+#pragma unroll
+                for (int j = 0; j < 16; ++j) sum[t][j] ^= x[j];
+    }
+    uint32_t d0[16];
+    load16(d0, a.base, a.block_stride, m);
+    bs16::transpose(d0);
+    const uint32_t rows[4] = {p, a.hw + p, a.cw + p, a.cw + a.hw + p};
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+        bs16::transpose(sum[t]);
+        uint32_t o[16];
+#pragma unroll
+        for (int j = 0; j < 16; ++j) o[j] = 0;
+        bs16::mulc_acc(sum[t], o, a.wmat + 16u * rows[t]);
+        bs16::mulc_acc(d0, o, a.gmat + 16u * rows[t]);
+        bs16::transpose(o);
+        store16(o, const_cast<uint8_t*>(a.base) + (uint64_t)(a.k + rows[t]) * a.seg_stride, a.block_stride, m);
+    }
+}
+
 }  // namespace
+
+int launch_tmvp2_prescale(const Rs16TmvpArgs& a, hipStream_t s)
+{
+    const uint64_t items = (uint64_t)a.nblocks * (a.vec / 8u);
+    const uint64_t waves = (items + 511) / 512 * (a.k / 4);
+    if (!a.hw || !a.sc || items >= (1ull << 32) || waves >= (1ull << 32)) return NFEC_ENOTSUP;
+    if (waves == 0) return NFEC_OK;
+    hipLaunchKernelGGL(tmvp2_prescale_kernel, dim3((uint32_t)((waves + 3) / 4)), dim3(256), 0, s, a);
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? NFEC_OK : hip_fail(e, "tmvp level-2 prescale launch");
+}
+
+int launch_tmvp2_postscale(const Rs16TmvpArgs& a, hipStream_t s)
+{
+    const uint64_t items = (uint64_t)a.nblocks * (a.vec / 8u);
+    const uint64_t waves = (items + 511) / 512 * a.hw;
+    if (!a.hw || !a.sc || items >= (1ull << 32) || waves >= (1ull << 32)) return NFEC_ENOTSUP;
+    if (waves == 0) return NFEC_OK;
+    hipLaunchKernelGGL(tmvp2_postscale_kernel, dim3((uint32_t)((waves + 3) / 4)), dim3(256), 0, s, a);
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? NFEC_OK : hip_fail(e, "tmvp level-2 postscale launch");
+}
 
 int launch_tmvp_prescale(const Rs16TmvpArgs& a, hipStream_t s)
 {

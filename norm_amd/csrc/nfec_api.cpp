@@ -228,6 +228,7 @@ struct nfec_codec {
     // RS16 encode by the Toeplitz split (kernels_tmvp.hip): offsets of the three products, each
     // [k/2+1][m_pad(m/2)][48], then the constants' row masks (c_j [k][16], W [m][16], G0 [m][16])
     bool tmvp = false;
+    int tmvp_levels = 0;           // Karatsuba levels of the split: 1 (3 products) or 2 (9, tower kernel)
     DevBuf<uint16_t> d_tmvp_off, d_tmvp_mat;
     std::mutex tmvp_mu;            // one Toeplitz encode at a time per codec: they share w_tmvp
     DevBuf<uint8_t> w_tmvp;        // prescaled pair sums + P1 rows of a sub-batch
@@ -511,29 +512,39 @@ int build_codec(nfec_codec* c)
             NFEC_HIP(hipMemcpy(c->d_t3off.p, off.data(), off.size() * 2, hipMemcpyHostToDevice));
         }
         // RS16: the Toeplitz split of the generator, three (m/2)-row products over k/2 columns
-        // instead of one m-row product over k (kernels_tmvp.hip), where its passes are fewer:
-        // NFEC_OPT_RS16_TOEPLITZ_OFF never, NFEC_OPT_RS16_TOEPLITZ_ON whenever the shape allows
-        // it (tests), neither when it pays (NFEC_RS16_TMVP=0/1/-1 overrides, diagnostic library)
+        // (one Karatsuba level) or, on the tower kernel, nine (m/4)-row products over k/4 columns
+        // (two levels) instead of one m-row product over k (kernels_tmvp.hip), where its passes
+        // are fewer: NFEC_OPT_RS16_TOEPLITZ_OFF never, NFEC_OPT_RS16_TOEPLITZ_ON whenever the
+        // shape allows it, at the most levels allowed (tests), neither when it pays;
+        // NFEC_OPT_RS16_TOEPLITZ_ONE_LEVEL caps it at one level (NFEC_RS16_TMVP=0/1/-1 overrides,
+        // diagnostic library)
         if (wide && use_gf16_t3() && (c->vec % 8) == 0) {
             const int mode = (int)diag_knob("NFEC_RS16_TMVP",
                                             (c->opts & NFEC_OPT_RS16_TOEPLITZ_OFF)  ? 0
                                             : (c->opts & NFEC_OPT_RS16_TOEPLITZ_ON) ? 1
                                                                                     : -1,
                                             -1, 1);
-            const uint32_t cw = c->m / 2;
+            const uint32_t cw = c->m / 2, hw = cw / 2;
             const uint32_t rpp = kGf16T3RowsPerPass;
-            const bool pays = c->tw ? 3ull * gf16_tw_passes(cw) * (c->k / 2) < (uint64_t)gf16_tw_passes(c->m) * c->k
-                                    : 3ull * ((cw + rpp - 1) / rpp) * (c->k / 2) < (uint64_t)((c->m + rpp - 1) / rpp) * c->k;
-            std::vector<uint32_t> prod[3];
+            // column passes of each form (the products' cost is about one column step per pass)
+            const uint64_t l0 = c->tw ? (uint64_t)gf16_tw_passes(c->m) * c->k : (uint64_t)((c->m + rpp - 1) / rpp) * c->k;
+            const uint64_t l1 = c->tw ? 3ull * gf16_tw_passes(cw) * (c->k / 2) : 3ull * ((cw + rpp - 1) / rpp) * (c->k / 2);
+            const bool two_ok = c->tw && hw >= 1 && !(c->opts & NFEC_OPT_RS16_TOEPLITZ_ONE_LEVEL);
+            const uint64_t l2 = two_ok ? 9ull * gf16_tw_passes(hw) * (c->k / 4) : ~0ull;
+            int levels = 0;
+            if (mode == 1) levels = two_ok ? 2 : 1;
+            else if (mode != 0) levels = l2 < std::min(l0, l1) ? 2 : l1 < l0 ? 1 : 0;
+            const int nprod = levels == 2 ? 9 : 3;
+            std::vector<uint32_t> prod[9];
             std::vector<uint16_t> cm, wm, gm;
-            if (mode != 0 && (mode == 1 || pays) && rs16_tmvp_plan(c->k, c->m, c->gen, prod, cm, wm, gm)) {
-                const uint32_t half = c->k / 2, mp = gf16_t3_rows_padded(cw);
-                const size_t one = c->tw ? gf16_tw_table_elems(half, cw)
-                                         : (size_t)(half + 1) * mp * 48;
-                std::vector<uint16_t> off(3 * one);
-                for (int e = 0; e < 3; ++e) {
-                    if (c->tw) gf16_tw_offsets(prod[e], half, cw, off.data() + e * one);
-                    else gf16_t3_offsets(prod[e], half, cw, off.data() + e * one);
+            if (levels && rs16_tmvp_plan_levels(c->k, c->m, c->gen, levels, prod, cm, wm, gm)) {
+                const uint32_t cols = levels == 2 ? c->k / 4 : c->k / 2, rows = levels == 2 ? hw : cw;
+                const uint32_t mp = gf16_t3_rows_padded(rows);
+                const size_t one = c->tw ? gf16_tw_table_elems(cols, rows) : (size_t)(cols + 1) * mp * 48;
+                std::vector<uint16_t> off(nprod * one);
+                for (int e = 0; e < nprod; ++e) {
+                    if (c->tw) gf16_tw_offsets(prod[e], cols, rows, off.data() + e * one);
+                    else gf16_t3_offsets(prod[e], cols, rows, off.data() + e * one);
                 }
                 std::vector<uint16_t> mat;
                 mat.insert(mat.end(), cm.begin(), cm.end());
@@ -546,6 +557,7 @@ int build_codec(nfec_codec* c)
                 NFEC_HIP(hipMemcpy(c->d_tmvp_mat.p, mat.data(), mat.size() * 2, hipMemcpyHostToDevice));
                 NFEC_HIP(hipEventCreateWithFlags(&c->tmvp_done, hipEventDisableTiming));
                 c->tmvp = true;
+                c->tmvp_levels = levels;
             }
         }
         if (!wide || std::min(c->k, c->m) <= kPlanCfMaxE) {
@@ -639,8 +651,116 @@ static bool use_asm()
 // pairs, the three shared-table products in one launch, and the postscale into the parity.
 // The sub-batch scratch is the codec's, so calls are ordered: each waits (on its stream) for
 // the previous one's end.
+// Two Karatsuba levels (tower kernel only): the level-2 prescale writes the pair sums and the
+// scaled sums into the block's scratch, one launch runs the nine (m/4)-row products (their alpha
+// parts over the scaled sums, the beta / gamma parts over the pair sums' halves (X = 0) or the
+// source columns themselves through column maps (X = 1, 2)) into the scratch, and the level-2
+// postscale combines them into the m parity rows (kernels_tmvp.hip; gf_host.cpp,
+// rs16_tmvp_plan_levels).
+static int rs16_tmvp2_encode(nfec_codec* c, const nfec_block_batch* b, hipStream_t s)
+{
+    const uint32_t k = c->k, m = c->m, cw = m / 2, hw = cw / 2, half = k / 2, quarter = k / 4, vec = c->vec;
+    const uint32_t prow0 = half + 3 * quarter;                  // first product row in the scratch
+    const uint64_t per_block = (uint64_t)(prow0 + 9 * hw) * vec;
+    std::lock_guard<std::mutex> lk(c->tmvp_mu);
+    size_t free_b = 0, total_b = 0;
+    if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) {
+        (void)hipGetLastError();
+        free_b = 0;
+    }
+    const uint64_t budget = std::min<uint64_t>(16ull << 30, ((uint64_t)free_b + c->w_tmvp.n) / 2);
+    const uint64_t cap = std::max<uint64_t>(1, budget / per_block);
+    const uint64_t nsub = (b->nblocks + cap - 1) / cap;
+    const uint32_t sb = (uint32_t)std::max<uint64_t>(1, (b->nblocks + nsub - 1) / std::max<uint64_t>(nsub, 1));
+    if (c->w_tmvp.reserve((size_t)sb * per_block) != NFEC_OK) {
+        (void)hipGetLastError();
+        return NFEC_ENOTSUP;  // no room for the scratch: the one-product encode takes the batch
+    }
+    NFEC_HIP(hipStreamWaitEvent(s, c->tmvp_done, 0));
+    bool queued = false;
+    auto leave = [&](int code) {
+        if (queued && hipEventRecord(c->tmvp_done, s) != hipSuccess && code == NFEC_OK)
+            code = hip_fail(hipGetLastError(), "tmvp event");
+        return code;
+    };
+    const size_t one_tw = gf16_tw_table_elems(quarter, hw);
+    uint32_t hshift = 0;
+    while ((1u << hshift) < hw) ++hshift;
+    int rc;
+    for (uint32_t b0 = 0; b0 < b->nblocks; b0 += sb) {
+        const uint32_t nb = std::min(sb, b->nblocks - b0);
+        uint8_t* blocks = static_cast<uint8_t*>(b->blocks) + (uint64_t)b0 * b->block_stride;
+        Rs16TmvpArgs a;
+        a.base = blocks;
+        a.block_stride = b->block_stride;
+        a.seg_stride = b->seg_stride;
+        a.nblocks = nb;
+        a.vec = vec;
+        a.k = k;
+        a.cw = cw;
+        a.hw = hw;
+        a.sc = c->w_tmvp.p;
+        a.sc_block_stride = per_block;
+        a.cmat = c->d_tmvp_mat.p;
+        a.wmat = c->d_tmvp_mat.p + (size_t)k * 16;
+        a.gmat = c->d_tmvp_mat.p + (size_t)(k + m) * 16;
+        Gf16T3Args e[9];
+        for (int X = 0; X < 3; ++X)
+            for (int t = 0; t < 3; ++t) {
+                Gf16T3Args& g = e[3 * X + t];
+                g.nblocks = nb;
+                g.k = quarter;
+                g.m = hw;
+                g.vec_bytes = vec;
+                g.tw = c->d_tmvp_tw.p + (3 * X + t) * one_tw;
+                g.out_base = a.sc;
+                g.out_block_stride = per_block;
+                g.out_seg_stride = vec;
+                g.out_slot0 = prow0 + (3 * X + t) * hw;
+                if (t == 0) {
+                    // alpha: the scaled sums s_X, plain columns of the scratch
+                    g.base = a.sc;
+                    g.block_stride = per_block;
+                    g.seg_stride = vec;
+                    g.col_base = half + X * quarter;
+                    g.in_slots = prow0;
+                    continue;
+                }
+                // beta (t = 1: second halves) / gamma (t = 2: first halves) through a column map:
+                // level-2 column q * hw + i -> slot (q * chunk) + base + i
+                g.col_shift = hshift;
+                g.col_mask = hw - 1;
+                if (X == 0) {  // the pair sums in the scratch, chunks of cw
+                    g.base = a.sc;
+                    g.block_stride = per_block;
+                    g.seg_stride = vec;
+                    g.col_chunk = cw;
+                    g.col_base = t == 1 ? hw : 0;
+                    g.in_slots = prow0;
+                } else {       // the source columns, chunk pairs of 2 cw: X = 1 the pairs' b halves
+                    g.base = blocks;
+                    g.block_stride = b->block_stride;
+                    g.seg_stride = b->seg_stride;
+                    g.col_chunk = 2 * cw;
+                    g.col_base = (X == 1 ? cw : 0) + (t == 1 ? hw : 0);
+                    g.in_slots = k + m;
+                }
+            }
+        // a shape the kernels do not cover shows on the first sub-batch, before any parity byte
+        // is written: NFEC_ENOTSUP then hands the batch to the one-product encode
+        if ((rc = launch_tmvp2_prescale(a, s)))
+            return leave(rc == NFEC_ENOTSUP && b0 == 0 ? rc : fail(rc, "tmvp level-2 prescale"));
+        queued = true;
+        if ((rc = launch_gf16_tw_multi(e, 9, s)))
+            return leave(rc == NFEC_ENOTSUP && b0 == 0 ? rc : fail(rc, "tmvp level-2 products"));
+        if ((rc = launch_tmvp2_postscale(a, s))) return leave(fail(rc, "tmvp level-2 postscale"));
+    }
+    return leave(NFEC_OK);
+}
+
 int rs16_tmvp_encode(nfec_codec* c, const nfec_block_batch* b, hipStream_t s)
 {
+    if (c->tmvp_levels == 2) return rs16_tmvp2_encode(c, b, s);
     const uint32_t k = c->k, m = c->m, cw = m / 2, half = k / 2, vec = c->vec;
     // sub-batches of at most 16 GiB of scratch (C4's 4,096 blocks: one, 12.5 GB) and at most
     // half of the device memory free now (plus the scratch this codec already holds), of equal
@@ -1840,7 +1960,7 @@ int nfec_codec_create_ex(const nfec_codec_config* cfg, nfec_codec** out)
     if (cfg->num_data == 0 || cfg->num_parity == 0) return fail(NFEC_EINVAL, "numData and numParity must be > 0");
     if (cfg->vector_size == 0 || cfg->vector_size > 65535) return fail(NFEC_EINVAL, "vectorSize must be in [1, 65535]");
     if (cfg->flags & ~(uint32_t)(NFEC_OPT_RS16_SHARED_TABLES | NFEC_OPT_RS16_TOEPLITZ_OFF | NFEC_OPT_RS16_TOEPLITZ_ON |
-                                 NFEC_OPT_HOST_ONLY))
+                                 NFEC_OPT_HOST_ONLY | NFEC_OPT_RS16_TOEPLITZ_ONE_LEVEL))
         return fail(NFEC_EINVAL, "unknown option flag");
     if ((cfg->flags & NFEC_OPT_HOST_ONLY) && cfg->num_devices > 1)
         return fail(NFEC_EINVAL, "a host-only codec takes no device list");
@@ -1923,7 +2043,8 @@ int nfec_codec_get_info(const nfec_codec* c, nfec_codec_info* out)
 int nfec_codec_features(const nfec_codec* c)
 {
     if (!c) return fail(NFEC_EINVAL, "null argument");
-    return primary(c)->tmvp ? NFEC_FEATURE_RS16_TOEPLITZ : 0;
+    const nfec_codec* p = primary(c);
+    return (p->tmvp ? NFEC_FEATURE_RS16_TOEPLITZ : 0) | (p->tmvp_levels == 2 ? NFEC_FEATURE_RS16_TOEPLITZ2 : 0);
 }
 
 int nfec_codec_get_generator(const nfec_codec* c, void* host_out, size_t bytes)

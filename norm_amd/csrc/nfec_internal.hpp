@@ -271,6 +271,14 @@ struct Gf16T3Multi {
     Gf16T3Args e[3];
     uint32_t wg_end[3] = {0, 0, 0};
 };
+// several independent products in one tower-kernel launch (the Toeplitz split: 3 at one level,
+// 9 at two): workgroups [wg_end[i-1], wg_end[i]) run problem i
+constexpr uint32_t kTwMultiMax = 9;
+struct Gf16TwMulti {
+    Gf16T3Args e[kTwMultiMax];
+    uint32_t wg_end[kTwMultiMax] = {};
+    uint32_t n = 0;
+};
 constexpr uint32_t kGf16T3RowsPerPass = 44;  // 11 row waves x 4 rows (gen_gf16_t3.py asserts it)
 constexpr uint32_t gf16_t3_rows_padded(uint32_t m)
 {
@@ -291,11 +299,23 @@ struct Rs16TmvpArgs {
     const uint16_t* cmat = nullptr; // [k][16] row masks of c_j (c_0 = 0)
     const uint16_t* wmat = nullptr; // [m][16] of W(y_p)
     const uint16_t* gmat = nullptr; // [m][16] of G[p][0]
+    // two Karatsuba levels: hw = m / 4, and one scratch per block (sc + b * sc_block_stride,
+    // columns of vec bytes): pair sums [0, k/2), scaled sums s_X at k/2 + X k/4, the nine
+    // hw-row products from k/2 + 3k/4 (kernels_tmvp.hip, tmvp2_*)
+    uint32_t hw = 0;
+    uint8_t* sc = nullptr;
+    uint64_t sc_block_stride = 0;
 };
 bool rs16_tmvp_plan(uint32_t k, uint32_t m, const std::vector<uint32_t>& gen, std::vector<uint32_t> prod[3],
                     std::vector<uint16_t>& cmat, std::vector<uint16_t>& wmat, std::vector<uint16_t>& gmat);
+// levels 1 (prod[0..2], (m/2) x (k/2) each) or 2 (prod[0..8], (m/4) x (k/4) each; gf_host.cpp)
+bool rs16_tmvp_plan_levels(uint32_t k, uint32_t m, const std::vector<uint32_t>& gen, int levels,
+                           std::vector<uint32_t>* prod, std::vector<uint16_t>& cmat, std::vector<uint16_t>& wmat,
+                           std::vector<uint16_t>& gmat);
 int launch_tmvp_prescale(const Rs16TmvpArgs& a, hipStream_t s);
 int launch_tmvp_postscale(const Rs16TmvpArgs& a, hipStream_t s);
+int launch_tmvp2_prescale(const Rs16TmvpArgs& a, hipStream_t s);
+int launch_tmvp2_postscale(const Rs16TmvpArgs& a, hipStream_t s);
 int launch_gf16_t3_encode(const Gf16T3Args& a, hipStream_t s);  // NFEC_ENOTSUP: shape not covered
 bool gf16_t3_covers(const Gf16T3Args& a);  // launch_gf16_t3_encode would take it
 int launch_gf16_t3_multi(const Gf16T3Args* e, uint32_t n, hipStream_t s);  // n <= 3 independent products
@@ -306,7 +326,7 @@ int launch_gf16_t3_multi(const Gf16T3Args* e, uint32_t n, hipStream_t s);  // n 
 constexpr uint32_t kGf16TwRowsPerPass = NFEC_TW_ROWS;
 int launch_gf16_tw_encode(const Gf16T3Args& a, hipStream_t s);  // NFEC_ENOTSUP: shape not covered
 bool gf16_tw_covers(const Gf16T3Args& a);
-int launch_gf16_tw_multi(const Gf16T3Args* e, uint32_t n, hipStream_t s);
+int launch_gf16_tw_multi(const Gf16T3Args* e, uint32_t n, hipStream_t s);  // n <= kTwMultiMax
 void gf16_tw_offsets(const std::vector<uint32_t>& parity_rows, uint32_t k, uint32_t m, uint16_t* out);
 uint32_t gf16_tw_passes(uint32_t m);  // passes of the tower kernel for m rows (a multiple of 4)
 size_t gf16_tw_table_elems(uint32_t k, uint32_t m);  // u16 elements of a k-column, m-row table

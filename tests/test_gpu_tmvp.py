@@ -1,7 +1,10 @@
-"""RS16 encode by the Toeplitz split (kernels_tmvp.hip + gen_gf16_t3.hip multi launch) against
-the oracle on the GPU, bit-exact.  NFEC_OPT_RS16_TOEPLITZ_ON forces the split for shapes where
-it is allowed but not chosen by default (NFEC_OPT_RS16_TOEPLITZ_OFF: never); (128, 32), (512, 128)
-and C4 take it by default (fewer passes of the tower kernel's 6 rows per wave)."""
+"""RS16 encode by the Toeplitz split (kernels_tmvp.hip + the tower kernel's multi launch) against
+the oracle on the GPU, bit-exact, at one Karatsuba level (three (m/2)-row products) and two
+(nine (m/4)-row products).  NFEC_OPT_RS16_TOEPLITZ_ON forces the split, at the most levels the
+shape allows, where it is not chosen by default (NFEC_OPT_RS16_TOEPLITZ_OFF: never;
+NFEC_OPT_RS16_TOEPLITZ_ONE_LEVEL: one level at most); by default the codec takes the form with the
+fewest passes of the tower kernel's 6 rows per wave: one level for (128, 32) and (512, 128), two
+for (256, 64) and C4."""
 
 import numpy as np
 import pytest
@@ -11,39 +14,54 @@ pytestmark = pytest.mark.gpu
 torch = pytest.importorskip("torch")
 
 from norm_amd import NFEC_RS16, NormDecoderRS16, NormEncoderRS16  # noqa: E402
-from norm_amd._native import (NFEC_FEATURE_RS16_TOEPLITZ, NFEC_OPT_RS16_TOEPLITZ_OFF,  # noqa: E402
-                              NFEC_OPT_RS16_TOEPLITZ_ON)
+from norm_amd._native import (NFEC_FEATURE_RS16_TOEPLITZ, NFEC_FEATURE_RS16_TOEPLITZ2,  # noqa: E402
+                              NFEC_OPT_RS16_TOEPLITZ_OFF, NFEC_OPT_RS16_TOEPLITZ_ON,
+                              NFEC_OPT_RS16_TOEPLITZ_ONE_LEVEL)
+
+OPTS = {None: 0, "0": NFEC_OPT_RS16_TOEPLITZ_OFF, "1": NFEC_OPT_RS16_TOEPLITZ_ON,
+        "1L1": NFEC_OPT_RS16_TOEPLITZ_ON | NFEC_OPT_RS16_TOEPLITZ_ONE_LEVEL, "L1": NFEC_OPT_RS16_TOEPLITZ_ONE_LEVEL}
 
 
 def _encoder(k, m, vec, force):
-    enc = NormEncoderRS16(options={None: 0, "0": NFEC_OPT_RS16_TOEPLITZ_OFF, "1": NFEC_OPT_RS16_TOEPLITZ_ON}[force])
+    enc = NormEncoderRS16(options=OPTS[force])
     assert enc.Init(k, m, vec)
     return enc
 
 
+def _levels(enc):
+    f = enc.features()
+    return 2 if f & NFEC_FEATURE_RS16_TOEPLITZ2 else 1 if f & NFEC_FEATURE_RS16_TOEPLITZ else 0
+
+
 CASES = [
-    # k, m, vec, seg_stride, nblocks, force, expect split
-    (64, 16, 1400, 1400, 5, "1", True),
-    (128, 32, 64, 64, 37, "1", True),     # several item groups, short segments
-    (128, 32, 1408, 1416, 3, "1", True),  # padded segment stride
-    (128, 32, 1400, 1400, 4, None, True),  # chosen by default (3 x 4 passes of 64 columns < 8 x 128)
-    (256, 64, 1400, 1400, 4, None, False),  # same pass count either way (3 x 8 x 128 = 12 x 256): not chosen
-    (256, 64, 1400, 1400, 4, "0", False),
-    (512, 128, 64, 64, 2, "1", True),     # several passes per product
-    (32, 8, 8, 8, 7, "1", True),          # one item per segment, chunk width 4
-    (96, 16, 72, 72, 5, "1", True),       # three chunk pairs
-    (1024, 64, 1400, 1400, 2, "1", True),
-    (2048, 128, 64, 64, 2, "1", True),    # same pass count either way: forced
-    (512, 128, 64, 64, 3, None, True),    # chosen by default (3 x 12 passes of 256 < 24 x 512)
-    (96, 24, 1400, 1400, 3, "1", False),  # m / 2 not a power of two: not allowed
-    (100, 20, 1400, 1400, 3, "1", False),  # k not a multiple of m
+    # k, m, vec, seg_stride, nblocks, force, expected Karatsuba levels (0: no split)
+    (64, 16, 1400, 1400, 5, "1", 2),
+    (64, 16, 1400, 1400, 5, "1L1", 1),
+    (128, 32, 64, 64, 37, "1", 2),        # several item groups, short segments
+    (128, 32, 64, 64, 37, "1L1", 1),
+    (128, 32, 1408, 1416, 3, "1", 2),     # padded segment stride
+    (128, 32, 1400, 1400, 4, None, 1),    # one level by default (3 x 4 passes of 64 < 8 x 128 < 9 x 4 x 32)
+    (256, 64, 1400, 1400, 4, None, 2),    # two levels by default (9 x 4 x 64 < 3 x 8 x 128 = 12 x 256)
+    (256, 64, 1400, 1400, 4, "L1", 0),    # at one level the same pass count as no split: not chosen
+    (256, 64, 1400, 1400, 4, "0", 0),
+    (512, 128, 64, 64, 2, "1", 2),        # several passes per product
+    (512, 128, 64, 64, 2, "1L1", 1),
+    (32, 8, 8, 8, 7, "1", 2),             # one item per segment, chunk width 4, level-2 halves of 2
+    (32, 8, 8, 8, 7, "1L1", 1),
+    (16, 4, 64, 64, 3, "1", 2),           # the smallest level-2 shape: halves of one column
+    (96, 16, 72, 72, 5, "1", 2),          # three chunk pairs
+    (1024, 64, 1400, 1400, 2, "1", 2),
+    (2048, 128, 64, 64, 2, "1", 2),
+    (512, 128, 64, 64, 3, None, 1),       # one level by default (3 x 12 x 256 < 24 x 512; two levels tie)
+    (96, 24, 1400, 1400, 3, "1", 0),      # m / 2 not a power of two: not allowed
+    (100, 20, 1400, 1400, 3, "1", 0),     # k not a multiple of m
 ]
 
 
-@pytest.mark.parametrize("k,m,vec,stride,nb,force,split", CASES)
-def test_toeplitz_encode_matches_oracle(orc, k, m, vec, stride, nb, force, split):
+@pytest.mark.parametrize("k,m,vec,stride,nb,force,levels", CASES)
+def test_toeplitz_encode_matches_oracle(orc, k, m, vec, stride, nb, force, levels):
     enc = _encoder(k, m, vec, force)
-    assert bool(enc.features() & NFEC_FEATURE_RS16_TOEPLITZ) == split
+    assert _levels(enc) == levels
     host = orc.make_blocks(k, m, vec, nb, seg_stride=stride)
     host[:, k:, :] = 0xA5  # overwrite semantics: stale parity must not leak through
     ref = orc.encode_blocks(orc.RS16, k, m, vec, host.copy())  # zeroes the parity, then Encode()s

@@ -117,3 +117,68 @@ def test_bitsliced_constant_multiply(gf, tmp_path):
     out = subprocess.run([str(exe)], input="\n".join(lines) + "\n", capture_output=True, text=True, check=True).stdout
     got = [[int(v) for v in ln.split()] for ln in out.strip().splitlines()]
     assert got == expect
+
+
+def _level2(gf, k, m, d, G, w, c, t):
+    """Two Karatsuba levels (kernels_tmvp.hip, rs16_tmvp_plan with two levels): level 1 as above;
+    level 2 splits each of the three (m/2)-row products the same way within each cw-wide chunk of
+    its columns, whose cw x cw blocks are Toeplitz: nine (m/4)-row products over k/4 columns.
+    The diag(c) of P1 / P2 moves to their data side for the alpha products (sums of scaled
+    columns) and stays in the coefficients of the beta / gamma products (raw columns)."""
+    _, _, _, mul = gf
+    cw, hw, nq = m // 2, m // 4, k // m
+    S = d.shape[1]
+    # N_X[p][a] for p < cw over level-1 virtual column (q, i), i < cw: the Toeplitz parts
+    N = [lambda p, q, i: t(p, 2 * q * cw + i),
+         lambda p, q, i: t(p, 2 * q * cw + cw + i) ^ t(p, 2 * q * cw + i),
+         lambda p, q, i: t(p + cw, 2 * q * cw + i) ^ t(p, 2 * q * cw + i)]
+    # level-1 inputs: z_0 = c_a d_a + c_b d_b, z_1 = c_b d_b, z_2 = c_a d_a (per (q, i))
+    col = {0: None, 1: lambda q, i: 2 * q * cw + cw + i, 2: lambda q, i: 2 * q * cw + i}
+
+    def z(X, q, i, s):
+        a, b = 2 * q * cw + i, 2 * q * cw + cw + i
+        if X == 0:
+            return mul(c[a], int(d[a, s])) ^ mul(c[b], int(d[b, s]))
+        j = col[X](q, i)
+        return mul(c[j], int(d[j, s]))
+
+    P = [np.zeros((cw, S), np.int64) for _ in range(3)]
+    for X in range(3):
+        pa = np.zeros((hw, S), np.int64)
+        pb = np.zeros_like(pa)
+        pg = np.zeros_like(pa)
+        for q in range(nq):
+            for i in range(hw):
+                for p in range(hw):
+                    al = N[X](p, q, i)
+                    be = N[X](p, q, hw + i)       # top-right block
+                    ga = N[X](hw + p, q, i)       # bottom-left block
+                    assert N[X](hw + p, q, hw + i) == al   # bottom-right = top-left (Toeplitz)
+                    for s in range(S):
+                        z0, z1 = z(X, q, i, s), z(X, q, hw + i, s)
+                        pa[p, s] ^= mul(al, z0 ^ z1)
+                        pb[p, s] ^= mul(be ^ al, z1)
+                        pg[p, s] ^= mul(ga ^ al, z0)
+        P[X][:hw] = pa ^ pb
+        P[X][hw:] = pa ^ pg
+    out = np.zeros((m, S), np.int64)
+    for p in range(cw):
+        for s in range(S):
+            out[p, s] = mul(w[p], int(P[0][p, s] ^ P[1][p, s])) ^ mul(int(G[p][0]), int(d[0, s]))
+            out[p + cw, s] = mul(w[p + cw], int(P[0][p, s] ^ P[2][p, s])) ^ mul(int(G[p + cw][0]), int(d[0, s]))
+    return out
+
+
+@pytest.mark.parametrize("k,m", [(16, 8), (32, 8), (64, 16)])
+def test_two_karatsuba_levels_reproduce_product(orc, gf, k, m):
+    _, _, _, mul = gf
+    G = orc.generator(orc.RS16, k, m)[k:]
+    w, c, t = _factors(gf, k, m)
+    rng = np.random.default_rng(11)
+    d = rng.integers(0, 65536, size=(k, 2))
+    ref = np.zeros((m, 2), np.int64)
+    for p in range(m):
+        for j in range(k):
+            for s in range(2):
+                ref[p, s] ^= mul(int(G[p][j]), int(d[j, s]))
+    assert np.array_equal(_level2(gf, k, m, d, G, w, c, t), ref)
