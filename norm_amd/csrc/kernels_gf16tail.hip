@@ -83,34 +83,49 @@ __global__ __launch_bounds__(kTailRowsPerWg) void gf16_tw_tail_kernel(Gf16T3Args
     const uint8_t* in = a.base + (uint64_t)blk * a.block_stride + off;
     const uint16_t* tab = a.tw + (pb ? (uint64_t)blk * a.tw_block_stride : 0u);
     uint32_t acc0[kTailMaxSym] = {0, 0, 0}, acc1[kTailMaxSym] = {0, 0, 0};
-    for (uint32_t c = 0; c < kk; ++c) {
-        // the column's tail symbols in the tower basis (uniform across the workgroup)
-        const uint16_t* x = reinterpret_cast<const uint16_t*>(in + (uint64_t)c * a.seg_stride);
-        uint32_t lx0[kTailMaxSym], lx1[kTailMaxSym];
+    // columns in batches of 8, their loads issued together (the loop is latency-bound otherwise):
+    // a column's tail symbols as one 8-byte load (the segment stride is a multiple of 8 and at
+    // least vec, so the 8 bytes at the tail offset stay inside the slot), uniform across the
+    // workgroup; the row's two table dwords
+    const uint32_t* tab32 = reinterpret_cast<const uint32_t*>(tab);
+    for (uint32_t c0 = 0; c0 < kk; c0 += 8u) {
+        uint2 xv[8];
+        uint32_t e0[8], e1[8];
 #pragma unroll
-        for (uint32_t s = 0; s < kTailMaxSym; ++s) {
-            const uint32_t v = s < nsym ? (uint32_t)x[s] : 0u;
-            const uint32_t t = (uint32_t)ph0[v & 255u] ^ (uint32_t)ph1[v >> 8];
-            lx0[s] = lg[t & 255u];
-            lx1[s] = lg[t >> 8];
+        for (uint32_t j = 0; j < 8u; ++j) {
+            const uint32_t c = min(c0 + j, kk - 1u);
+            xv[j] = *reinterpret_cast<const uint2*>(in + (uint64_t)c * a.seg_stride);
+            const uint64_t eb = ((uint64_t)c * 4u * a.m + 2u * r) / 2u;  // dword index of (c, sweep 0, r)
+            e0[j] = live ? tab32[eb] : 0u;
+            e1[j] = live ? tab32[eb + a.m] : 0u;
         }
-        if (!live) continue;
-        // entries (c0, c1) of sweep 0 and (lam c1, c0 ^ c1) of sweep 1, each (value << 7)
-        const uint64_t eb = (uint64_t)c * 4u * a.m + 2u * r;
-        const uint32_t e0 = (uint32_t)tab[eb] | ((uint32_t)tab[eb + 1] << 16);
-        const uint32_t e1 = (uint32_t)tab[eb + 2u * a.m] | ((uint32_t)tab[eb + 2u * a.m + 1] << 16);
-        const uint32_t l00 = lg[(e0 >> 7) & 255u], l01 = lg[e0 >> 23];  // x0 -> out0, out1
-        const uint32_t l10 = lg[(e1 >> 7) & 255u], l11 = lg[e1 >> 23];  // x1 -> out0, out1
 #pragma unroll
-        for (uint32_t s = 0; s < kTailMaxSym; ++s) {
-            const uint32_t a0 = lx0[s], a1 = lx1[s];
-            if (a0 != kNoLog) {
-                if (l00 != kNoLog) acc0[s] ^= ex[a0 + l00];
-                if (l01 != kNoLog) acc1[s] ^= ex[a0 + l01];
+        for (uint32_t j = 0; j < 8u; ++j) {
+            if (c0 + j >= kk) break;
+            // the column's tail symbols in the tower basis
+            uint32_t lx0[kTailMaxSym], lx1[kTailMaxSym];
+#pragma unroll
+            for (uint32_t s = 0; s < kTailMaxSym; ++s) {
+                const uint32_t w = s < 2u ? xv[j].x : xv[j].y;
+                const uint32_t v = s < nsym ? (w >> (16u * (s & 1u))) & 0xFFFFu : 0u;
+                const uint32_t t = (uint32_t)ph0[v & 255u] ^ (uint32_t)ph1[v >> 8];
+                lx0[s] = lg[t & 255u];
+                lx1[s] = lg[t >> 8];
             }
-            if (a1 != kNoLog) {
-                if (l10 != kNoLog) acc0[s] ^= ex[a1 + l10];
-                if (l11 != kNoLog) acc1[s] ^= ex[a1 + l11];
+            // entries (c0, c1) of sweep 0 and (lam c1, c0 ^ c1) of sweep 1, each (value << 7)
+            const uint32_t l00 = lg[(e0[j] >> 7) & 255u], l01 = lg[e0[j] >> 23];  // x0 -> out0, out1
+            const uint32_t l10 = lg[(e1[j] >> 7) & 255u], l11 = lg[e1[j] >> 23];  // x1 -> out0, out1
+#pragma unroll
+            for (uint32_t s = 0; s < kTailMaxSym; ++s) {
+                const uint32_t a0 = lx0[s], a1 = lx1[s];
+                if (a0 != kNoLog) {
+                    if (l00 != kNoLog) acc0[s] ^= ex[a0 + l00];
+                    if (l01 != kNoLog) acc1[s] ^= ex[a0 + l01];
+                }
+                if (a1 != kNoLog) {
+                    if (l10 != kNoLog) acc0[s] ^= ex[a1 + l10];
+                    if (l11 != kNoLog) acc1[s] ^= ex[a1 + l11];
+                }
             }
         }
     }
