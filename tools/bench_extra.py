@@ -165,13 +165,20 @@ def rs16_op_roofline(enc, k, m, nb, vec, enc_ms):
     import glob
     import norm_amd as na
 
-    split = bool(enc.features() & na.NFEC_FEATURE_RS16_TOEPLITZ)
+    from norm_amd import _native as N
+
+    f = enc.features()
+    split = bool(f & N.NFEC_FEATURE_RS16_TOEPLITZ)
+    two = bool(f & N.NFEC_FEATURE_RS16_TOEPLITZ2)
     name = "gf16_tw_multi_kernel" if split else "gf16_tw_encode_kernel"
-    out = {"kernel": name + (" (Toeplitz split: 3 tower-field products of m/2 rows over k/2 columns)"
-                             if split else " (tower-field products, snippet calls)"),
+    form = (" (Toeplitz split, two Karatsuba levels: 9 tower-field products of m/4 rows over k/4 columns)" if two
+            else " (Toeplitz split: 3 tower-field products of m/2 rows over k/2 columns)" if split
+            else " (tower-field products, snippet calls)")
+    out = {"kernel": name + form,
            "gf16_macs_per_s": float("%.4g" % (k * m * (vec // 2) * nb / (enc_ms * 1e-3))),
            "macs_note": "k*m*symbols of the generator product per second"
-                        + (" (the split computes 3/4 of them)" if split else "")}
+                        + (" (the split computes 9/16 of them)" if two else " (the split computes 3/4 of them)" if split
+                           else "")}
     src = None
     for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "r0*", "pmc_tw_*summary.json")), reverse=True):
         d = json.load(open(path))
