@@ -816,11 +816,13 @@ __global__ __launch_bounds__({64 * NWAVES}, {WAVES_PER_SIMD}) void gf16_tw_encod
 // several independent products in one grid (the RS16 Toeplitz split, rs16_tmvp): workgroup
 // ranges [wg_end[i-1], wg_end[i]) run problem i, so their tails share one launch
 template <int V>
-__global__ __launch_bounds__({64 * NWAVES}, {WAVES_PER_SIMD}) void gf16_tw_multi_kernel(Gf16T3Multi mm)
+__global__ __launch_bounds__({64 * NWAVES}, {WAVES_PER_SIMD}) void gf16_tw_multi_kernel(Gf16TwMulti mm)
 {{
     const uint32_t wg = bs::wg_index(1);
-    // one body instance (three would hold three argument sets live: more registers, fewer waves)
-    const uint32_t i = wg < mm.wg_end[0] ? 0u : wg < mm.wg_end[1] ? 1u : 2u;
+    // one body instance (one per problem would hold their argument sets live: more registers,
+    // fewer waves); the problem index is workgroup-uniform
+    uint32_t i = 0;
+    while (i + 1u < mm.n && wg >= mm.wg_end[i]) ++i;
     tw_body<V>(mm.e[i], wg - (i ? mm.wg_end[i - 1] : 0u));
 }}
 
@@ -881,12 +883,13 @@ bool gf16_tw_covers(const Gf16T3Args& a)
 
 int launch_gf16_tw_multi(const Gf16T3Args* e, uint32_t n, hipStream_t s)
 {{
-    if (n == 0 || n > 3) return NFEC_EINVAL;
-    Gf16T3Multi mm;
+    if (n == 0 || n > kTwMultiMax) return NFEC_EINVAL;
+    Gf16TwMulti mm;
+    mm.n = n;
     uint64_t end = 0;
-    for (uint32_t i = 0; i < 3; ++i) {{
+    for (uint32_t i = 0; i < n; ++i) {{
         uint64_t w = 0;
-        if (i < n && e[i].nblocks) {{
+        if (e[i].nblocks) {{
             const int rc = tw_prepare(e[i], mm.e[i], w);
             if (rc) return rc;
         }}
