@@ -111,10 +111,20 @@ def _store(lane):
     return out
 
 
-@pytest.mark.parametrize("k,rows,seed", [(1, 1, 3), (3, 11, 4), (5, 4, 5)])
-def test_column_flow_matches_gf16_products(k, rows, seed):
-    """the kernel's per-column sequence (transpose, phi, combos, row snippets on x0, x1 ->
-    S -> W, combos, row snippets) and its epilogue (phi^-1, transpose), row targets by index"""
+@pytest.mark.parametrize("k,rows,seed,prefetch", [(1, 1, 3, True), (3, 11, 4, True), (5, 4, 5, True),
+                                                  (5, 7, 6, False)])
+def test_column_flow_matches_gf16_products(k, rows, seed, prefetch):
+    """the kernel's per-column sequence (transpose, phi, [x1 planes through the LDS exchange],
+    combos, row snippets on x0, x1 -> W, combos, row snippets) and its epilogue (phi^-1,
+    transpose), row targets by index; both register layouts"""
+    g.set_prefetch(prefetch)
+    try:
+        _column_flow(k, rows, seed)
+    finally:
+        g.set_prefetch(True)
+
+
+def _column_flow(k, rows, seed):
     rnd = random.Random(seed)
     data = [[rnd.randrange(1 << 16) for _ in range(32)] for _ in range(k)]
     data[0][:4] = [0, 1, 0xFFFF, 0x8000]
@@ -128,12 +138,14 @@ def test_column_flow_matches_gf16_products(k, rows, seed):
         _load(lane, data[c])
         lane.run(g.transpose16(g.slot(), g.V_TMP))
         lane.run(g.phi_code())
+        x1 = [lane.v[r] for r in g.x1_regs()]   # (written to the exchange before the combinations)
         lane.run(g.combos_code())
         for r in range(rows):
             e = [v >> g.SNIP_ALIGN for v in g.table_entries(G[r][c])]
             lane.run(snip[e[0]], idx=16 * r)
             lane.run(snip[e[1]], idx=16 * r + 8)
-        lane.run([f"v_mov_b32 v{g.V_W + i}, v{g.V_S + i}" for i in range(8)])
+        for i in range(8):
+            lane.v[g.V_W + i] = x1[i]
         lane.run(g.combos_code())
         for r in range(rows):
             e = [v >> g.SNIP_ALIGN for v in g.table_entries(G[r][c])]
@@ -160,15 +172,32 @@ def test_snippets_fit_their_slots():
         assert size <= 1 << g.SNIP_ALIGN
 
 
-def test_register_map_is_disjoint():
-    regions = [range(g.V_SLOT, g.V_SLOT + 16), range(g.V_W, g.V_W + 8), range(g.V_S, g.V_S + 8),
-               range(g.V_CA, g.V_CA + 11), range(g.V_CB, g.V_CB + 11), g.V_TMP,
-               range(g.ACC0, g.V_LAST + 1)]
-    seen = set()
-    for r in regions:
-        for v in r:
-            assert v not in seen and 10 <= v <= 255
-            seen.add(v)
+@pytest.mark.parametrize("rows,prefetch", [(6, True), (7, False), (6, False), (4, True), (11, True)])
+def test_register_map_is_disjoint(rows, prefetch):
+    """the VGPR regions of each layout are disjoint, above the asm's inputs (v0..v3), with the
+    pairs of loads, stores and LDS reads at even registers and the occupancy the layout is for"""
+    try:
+        g.set_prefetch(prefetch)
+        g.set_rows(rows)
+        regions = [range(g.V_SLOT, g.V_SLOT + 16), range(g.V_W, g.V_W + 8),
+                   range(g.V_CA, g.V_CA + 11), range(g.V_CB, g.V_CB + 11), g.V_TMP,
+                   range(g.ACC0, g.V_LAST + 1)]
+        if prefetch:
+            regions.append(range(g.V_S, g.V_S + 8))
+        seen = set()
+        for r in regions:
+            for v in r:
+                assert v not in seen and 4 <= v <= 255
+                seen.add(v)
+        assert g.V_SLOT % 2 == 0 and g.V_W % 2 == 0 and g.V_CA % 2 == 0 and (g.V_CB + 1) % 2 == 0
+        assert g.V_X1 % 2 == 0 and (not prefetch or g.V_S % 2 == 0)
+        if rows == 7 or rows == 6:
+            assert g.V_LAST < 168   # three waves per SIMD
+        if rows == 4:
+            assert g.V_LAST < 128   # four
+    finally:
+        g.set_prefetch(True)
+        g.set_rows(6)
 
 
 @pytest.mark.parametrize("m", [1, 4, 11, 12, 44, 45, 50, 100, 128, 200, 256])

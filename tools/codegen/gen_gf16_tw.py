@@ -53,16 +53,27 @@ TBL_HALF = 48            # 16-bit table entries per (column, pass): 11 rows x 4 
 GPR_MODE = 0x9000        # M0[15:12]: index SRC0 and DST
 
 # ---- VGPRs ----
-V_SLOT = 10              # 16: raw column (loads) -> transposed planes; epilogue: output planes
-V_W = 26                 # 8: current source planes (x0, then x1); epilogue: store offsets
-V_S = 34                 # 8: x1 while x0 is applied; epilogue: accumulate-source offsets
-V_CA = 42                # 11: combinations of planes 0..3 of the source
-V_CB = 53                # 11: combinations of planes 4..7
-V_TMP = [64, 65, 66, 67]
-ACC0 = 68                # row r: out0 planes ACC0 + 16 r + (0..7), out1 + 8
-V_LAST = ACC0 + 16 * ROWS - 1   # 163 at 6 rows
-# (register pairs of loads and stores must start at even registers; v9 stays unused so the
-# compiler places the nine inputs in v0..v8)
+# v0..v3: the asm's three inputs (lo, xl, lq; placed by the compiler below the first clobber)
+PREFETCH = True          # x1 / next x0 planes read into S while a sweep runs (--noprefetch: into W after it)
+
+
+def layout():
+    """register map for ROWS and PREFETCH (set_rows / set_prefetch call it)"""
+    global V_SLOT, V_W, V_S, V_X1, V_CA, V_CB, V_TMP, ACC0, V_LAST
+    V_SLOT = 4           # 16: raw column (loads) -> transposed planes; epilogue: output planes
+    V_W = 20             # 8: current source planes (x0, then x1); epilogue: store offsets
+    V_S = 28 if PREFETCH else None   # 8: x1 while x0 is applied (prefetch only)
+    V_CA = 36 if PREFETCH else 28    # 11: combinations of planes 0..3 of the source
+    V_CB = V_CA + 11     # 11: combinations of planes 4..7
+    V_X1 = V_S if PREFETCH else V_CA  # phi's x1 planes before the exchange write
+    V_TMP = [V_CB + 11 + i for i in range(4)]
+    ACC0 = V_CB + 15     # row r: out0 planes ACC0 + 16 r + (0..7), out1 + 8
+    V_LAST = ACC0 + 16 * ROWS - 1
+
+
+layout()
+# (register pairs of loads, stores and LDS reads start at even registers: V_SLOT, V_W, V_S,
+# V_CA and V_CB + 1 are even)
 MULTI = [a for a in range(1, 16) if bin(a).count("1") >= 2]
 
 # ---- SGPRs (clobbered) ----
@@ -74,6 +85,12 @@ S_OFF = 72               # 24: the column's table entries (sweep 0: 72..83, swee
 S_LAST = 95
 MASKS = {8: 0x00FF00FF, 4: 0x0F0F0F0F, 2: 0x33333333, 1: 0x55555555}
 
+def set_prefetch(on):
+    global PREFETCH
+    PREFETCH = on
+    layout()
+
+
 def set_waves(n):
     """waves per workgroup and what follows from it"""
     global NWAVES, XCH_BUF
@@ -83,9 +100,9 @@ def set_waves(n):
 
 def set_rows(n):
     """parity rows per wave and what follows from it"""
-    global ROWS, V_LAST, SPECIAL_ROWS
+    global ROWS, SPECIAL_ROWS
     ROWS = n
-    V_LAST = ACC0 + 16 * ROWS - 1
+    layout()
     # pass row counts with their own (unchecked) step loop
     SPECIAL_ROWS = tuple(range(ROWS, max(ROWS - 6, 0), -1))
 
@@ -298,13 +315,13 @@ def w_regs():
     return [V_W + i for i in range(8)]
 
 
-def s_regs():
-    return [V_S + i for i in range(8)]
+def x1_regs():
+    return [V_X1 + i for i in range(8)]
 
 
 def phi_code():
-    """transposed planes (slot) -> x0 planes (W) and x1 planes (S)"""
-    return xor_network(row_masks(PHI), slot(), w_regs() + s_regs())
+    """transposed planes (slot) -> x0 planes (W) and x1 planes (S, or CA without the prefetch)"""
+    return xor_network(row_masks(PHI), slot(), w_regs() + x1_regs())
 
 
 def phi_inv_code(r):
@@ -446,29 +463,31 @@ _uid = [0]
 
 
 def loads():
-    """column s[S_C]'s 8 pieces -> the slot.  Flat shortened mode (bit 0 of %[md]): a piece whose
-    block has numData <= c reads zeros (its offset gets bit 31: past num_records; %[q<i>] =
-    the piece's numData - 1), so each piece's block stops at its own numData"""
+    """column s[S_C]'s 8 pieces -> the slot.  The pieces' byte offsets come from LDS (%[lo] + 80,
+    shared by the workgroup's waves).  Flat shortened mode (bit 0 of %[md]): a piece whose block
+    has numData <= c reads zeros (its offset gets bit 31: past num_records; q = the piece's
+    numData - 1, u16 pairs at %[lq]), so each piece's block stops at its own numData"""
     x = slot()
     if "noload" in FLAGS:
         return []
     _uid[0] += 1
     u = _uid[0]
-    plain = [f"buffer_load_dwordx2 v[{x[2 * i]}:{x[2 * i + 1]}], %[o{i}], s[{S_DESC}:{S_DESC + 3}], s{S_COL} offen"
-             for i in range(8)]
-    # the pieces' numData - 1 (u16 pairs in LDS at %[lq]); the combinations are free while a
-    # column loads
-    q = [V_CB + 1 + i for i in range(4)]   # (64-bit register pairs start at even registers)
+    o = [V_CA + i for i in range(8)]       # (free: the combinations are rebuilt per column)
+    q = [V_CB + 1 + i for i in range(4)]
+    t = V_CB + 5
+    L = [f"ds_read_b128 v[{o[0]}:{o[3]}], %[lo] offset:80", f"ds_read_b128 v[{o[4]}:{o[7]}], %[lo] offset:96"]
+    plain = ["s_waitcnt lgkmcnt(0)"]
+    plain += [f"buffer_load_dwordx2 v[{x[2 * i]}:{x[2 * i + 1]}], v{o[i]}, s[{S_DESC}:{S_DESC + 3}], s{S_COL} offen"
+              for i in range(8)]
     masked = [f"ds_read_b64 v[{q[0]}:{q[1]}], %[lq]", f"ds_read_b64 v[{q[2]}:{q[3]}], %[lq] offset:8",
               "s_waitcnt lgkmcnt(0)"]
     for i in range(8):
-        t = V_CA + i
         src = q[i // 2]
         masked += [f"v_lshrrev_b32 v{t}, 16, v{src}" if i & 1 else f"v_and_b32 v{t}, 0xffff, v{src}",
                    f"v_subrev_u32 v{t}, s{S_C}, v{t}",                          # numData - 1 - c
-                   f"v_and_or_b32 v{t}, v{t}, s{S_DESC + 2}, %[o{i}]",          # sign -> bit 31
-                   f"buffer_load_dwordx2 v[{x[2 * i]}:{x[2 * i + 1]}], v{t}, s[{S_DESC}:{S_DESC + 3}], s{S_COL} offen"]
-    return ([f"s_bitcmp1_b32 %[md], 0", f"s_cbranch_scc0 Lldp{u}_%="] + masked +
+                   f"v_and_or_b32 v{o[i]}, v{t}, s{S_DESC + 2}, v{o[i]}",       # sign -> bit 31
+                   f"buffer_load_dwordx2 v[{x[2 * i]}:{x[2 * i + 1]}], v{o[i]}, s[{S_DESC}:{S_DESC + 3}], s{S_COL} offen"]
+    return (L + [f"s_bitcmp1_b32 %[md], 0", f"s_cbranch_scc0 Lldp{u}_%="] + masked +
             [f"s_branch Lldx{u}_%=", f"Lldp{u}_%=:"] + plain + [f"Lldx{u}_%=:"])
 
 
@@ -481,16 +500,19 @@ def xch_addr(j=None, sgpr=None):
             f"v_add_u32 v{V_TMP[0]}, s{S_T0}, %[xl]"], 0
 
 
-def fetch(j, n):
-    """planes of source x_n of column slot j -> S (LDS), table entries of sweep n -> their half"""
+def fetch_planes(j, n, dst):
+    """planes of source x_n of column slot j -> dst (LDS)"""
     code, base = xch_addr(j)
+    return code + [f"ds_read_b64 v[{dst + 2 * p}:{dst + 2 * p + 1}], v{V_TMP[0]} offset:{base + 512 * (4 * n + p)}"
+                   for p in range(4)]
+
+
+def fetch_entries(j, n):
+    """table entries of sweep n of column slot j -> their half of the entry registers"""
     L = []
     if n == 0:  # a new column: its table address
         L += [f"s_add_u32 s{S_T2}, s{S_SB}, {j}", f"s_mul_i32 s{S_T2}, s{S_T2}, %[tstep]",
               f"s_add_u32 s{S_TBN}, s{S_TB}, s{S_T2}", f"s_addc_u32 s{S_TBN + 1}, s{S_TB + 1}, 0"]
-    L += code
-    for p in range(4):
-        L.append(f"ds_read_b64 v[{V_S + 2 * p}:{V_S + 2 * p + 1}], v{V_TMP[0]} offset:{base + 512 * (4 * n + p)}")
     o = S_OFF + 12 * n
     if n == 1:  # the column's sweep-1 entries follow its m sweep-0 rows
         L += [f"s_add_u32 s{S_TBN}, s{S_TBN}, %[t1off]", f"s_addc_u32 s{S_TBN + 1}, s{S_TBN + 1}, 0"]
@@ -499,12 +521,37 @@ def fetch(j, n):
     return L
 
 
+def fetch(j, n):
+    """prefetch form: planes of x_n of column slot j -> S, table entries of sweep n -> their half"""
+    if n == 0:
+        return fetch_entries(j, 0)[:4] + fetch_planes(j, 0, V_S) + fetch_entries(j, 0)[4:]
+    return fetch_planes(j, 1, V_S) + fetch_entries(j, 1)
+
+
 def apply_col(j, x, nrows):
-    """apply column slot j of the step (entering with x0's planes and sweep-0 entries in flight)"""
+    """apply column slot j of the step (prefetch: entering with x0's planes in S and the sweep-0
+    entries in flight; else with the entries in flight only)"""
     y = f"{x}{j}"
     L = []
     if j:
         L += [f"s_add_u32 s{S_T2}, s{S_SB}, {j}", f"s_cmp_lt_u32 s{S_T2}, %[k]", f"s_cbranch_scc0 Lend{x}_%="]
+    if not PREFETCH:
+        # each sweep's planes go straight into W once the previous sweep is done (the LDS latency
+        # is exposed to this wave; the SIMD's other waves run meanwhile)
+        L += fetch_planes(j, 0, V_W)
+        L.append("s_waitcnt lgkmcnt(0)")
+        L += fetch_entries(j, 1)
+        L += combos_code()
+        L += sweep(0, y, nrows)
+        L += fetch_planes(j, 1, V_W)
+        L.append("s_waitcnt lgkmcnt(0)")
+        if j < NWAVES - 1:
+            L += [f"s_add_u32 s{S_T2}, s{S_SB}, {j + 1}", f"s_cmp_lt_u32 s{S_T2}, %[k]", f"s_cbranch_scc0 Lnf{y}_%="]
+            L += fetch_entries(j + 1, 0)
+            L.append(f"Lnf{y}_%=:")
+        L += combos_code()
+        L += sweep(1, y, nrows)
+        return L
     L.append("s_waitcnt lgkmcnt(0)")
     L += [f"v_mov_b32 v{V_W + i}, v{V_S + i}" for i in range(8)]
     L += fetch(j, 1)
@@ -533,7 +580,7 @@ def step_loop(x, nrows):
     for p in range(4):
         L.append(f"ds_write_b64 v{V_TMP[0]}, v[{V_W + 2 * p}:{V_W + 2 * p + 1}] offset:{512 * p}")
     for p in range(4):
-        L.append(f"ds_write_b64 v{V_TMP[0]}, v[{V_S + 2 * p}:{V_S + 2 * p + 1}] offset:{512 * (4 + p)}")
+        L.append(f"ds_write_b64 v{V_TMP[0]}, v[{V_X1 + 2 * p}:{V_X1 + 2 * p + 1}] offset:{512 * (4 + p)}")
     L.append(f"Lnotr{x}_%=:")
     # the wave's column of the next step goes into the (now free) slot
     L += [f"s_add_u32 s{S_C}, s{S_C}, {NWAVES}", f"s_cmp_lt_u32 s{S_C}, %[k]", f"s_cbranch_scc0 Lnl{x}_%="]
@@ -541,7 +588,7 @@ def step_loop(x, nrows):
     L += [f"Lnl{x}_%=:", "s_waitcnt lgkmcnt(0)", "s_barrier"]
     if nrows is None:
         L += ["s_cmp_eq_u32 %[nr], 0", f"s_cbranch_scc1 Lend{x}_%="]
-    L += fetch(0, 0)
+    L += fetch(0, 0) if PREFETCH else fetch_entries(0, 0)
     for j in range(NWAVES):
         L += apply_col(j, x, nrows)
     L += [f"Lend{x}_%=:", f"s_xor_b32 s{S_BUF}, s{S_BUF}, {XCH_BUF}", f"s_add_u32 s{S_SB}, s{S_SB}, {NWAVES}",
@@ -590,7 +637,6 @@ def epilogue():
           f"s_mov_b32 s{S_ADESC + 3}, 0x00020000"]
     for i in range(8):
         L.append(f"ds_read_b32 v{V_W + i}, %[lo] offset:{4 * i}")
-        L.append(f"ds_read_b32 v{V_S + i}, %[lo] offset:{32 + 4 * i}")
     # the rows' output byte offsets (the table entries' registers are free now): per-block mode
     # from the row table, else (oslot + r) * oss
     L += ["s_cmp_eq_u64 %[rp], 0", "s_cbranch_scc1 Lflat_%=",
@@ -609,8 +655,11 @@ def epilogue():
         L += [f"s_mov_b32 s{S_T1}, s{S_OFF + r}",
               "s_cmp_eq_u32 %[acc], 0", f"s_cbranch_scc1 Lna{r}_%=",
               f"s_add_u32 s{S_T2}, %[aslot], {r}", f"s_mul_i32 s{S_T2}, s{S_T2}, %[ass]"]
+        # the accumulate source's piece offsets (LDS) in the loads' own destination registers
+        L += [f"ds_read_b32 v{tmp[2 * i]}, %[lo] offset:{32 + 4 * i}" for i in range(8)]
+        L.append("s_waitcnt lgkmcnt(0)")
         for i in range(8):
-            L.append(f"buffer_load_dwordx2 v[{tmp[2 * i]}:{tmp[2 * i + 1]}], v{V_S + i}, s[{S_ADESC}:{S_ADESC + 3}], s{S_T2} offen")
+            L.append(f"buffer_load_dwordx2 v[{tmp[2 * i]}:{tmp[2 * i + 1]}], v{tmp[2 * i]}, s[{S_ADESC}:{S_ADESC + 3}], s{S_T2} offen")
         L.append("s_waitcnt vmcnt(0)")
         for i in range(16):
             L.append(f"v_xor_b32 v{x[i]}, v{x[i]}, v{tmp[i]}")
@@ -652,6 +701,9 @@ def main():
         i = args.index("--rows")
         set_rows(int(args[i + 1]))
         del args[i:i + 2]
+    if "--noprefetch" in args:
+        set_prefetch(False)
+        args.remove("--noprefetch")
     if "--waves" in args:
         i = args.index("--waves")
         set_waves(int(args[i + 1]))
@@ -663,12 +715,11 @@ def main():
         FLAGS = f
         asms[v] = "\\n\"\n            \"".join(body())
     FLAGS = ()
-    ins = ", ".join(f'[o{i}] "v"(o[{i}])' for i in range(8))
     common = """[wb] "s"(wb), [ss] "s"(a.seg_stride), [k] "s"(kk), [tw] "s"(tw), [tstep] "s"(tstep), [t1off] "s"(t1off), [nr] "s"(nr),
               [csh] "s"(a.col_shift), [cmk] "s"(a.col_mask), [cck] "s"(cck), [cbb] "s"(cbb),
               [acc] "s"(a.accumulate), [ob] "s"(ob), [ab] "s"(ab), [oslot] "s"(a.out_slot0 + row0),
               [oss] "s"(a.out_seg_stride), [aslot] "s"(a.acc_slot0 + row0), [ass] "s"(a.acc_seg_stride),
-              [wv] "s"(wave), [rp] "s"(rp), [md] "s"(md), [lo] "v"(lo), [xl] "v"(xl), [lq] "v"(lq), """ + ins
+              [wv] "s"(wave), [rp] "s"(rp), [md] "s"(md), [lo] "v"(lo), [xl] "v"(xl), [lq] "v"(lq)"""
     blocks = []
     for v in variants:
         kw = "if constexpr" if v == 0 else "else if constexpr"
@@ -721,9 +772,10 @@ __device__ __forceinline__ uint32_t gf16_tw_passes_dev(uint32_t m)
 template <int V>
 __device__ __forceinline__ void tw_body(const Gf16T3Args& a, uint32_t wg)
 {{
-    // per lane: 8 output and 8 accumulate-source offsets (epilogue), then the 8 pieces' numData - 1
-    // as u16 pairs (flat shortened loads)
-    __shared__ uint32_t lds[{NWAVES} * 64 * 20];
+    // per lane, shared by the workgroup's waves (each writes the same values and reads only
+    // what it wrote itself, so no barrier): 8 output and 8 accumulate-source offsets (epilogue),
+    // the 8 pieces' numData - 1 as u16 pairs (flat shortened loads), the 8 pieces' offsets
+    __shared__ uint32_t lds[64 * 28];
     __shared__ uint64_t xch[2 * {XCH_BUF // 8}];       // column planes exchange (body)
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -771,8 +823,8 @@ __device__ __forceinline__ void tw_body(const Gf16T3Args& a, uint32_t wg)
     const uint32_t nr = __builtin_amdgcn_readfirstlane(row1 - row0);
     const uint32_t b0 = pb ? pblk : __builtin_amdgcn_readfirstlane((uint32_t)(f0 / a.vec_bytes));
     const uint8_t* wb = a.base + (uint64_t)b0 * a.block_stride;
-    uint32_t o[8], q[8];
-    uint32_t* po = lds + (wave * 64u + lane) * 20u;
+    uint32_t q[8];
+    uint32_t* po = lds + lane * 28u;
 #pragma unroll
     for (int i = 0; i < 8; ++i) {{
         const uint64_t f = f0 + (uint64_t)i * 512u + lane * 8u;
@@ -782,7 +834,7 @@ __device__ __forceinline__ void tw_body(const Gf16T3Args& a, uint32_t wg)
         const bool ok = f < total && raw >= 1u && raw <= a.k;
         const uint32_t pnd = ok ? raw : 1u;
         q[i] = pnd - 1u;
-        o[i] = ok ? (uint32_t)((uint64_t)(b - b0) * a.block_stride) + p : 0x80000000u;
+        po[20 + i] = ok ? (uint32_t)((uint64_t)(b - b0) * a.block_stride) + p : 0x80000000u;
         po[i] = ok ? (uint32_t)((uint64_t)(b - b0) * a.out_block_stride +
                                 (a.out_after_data ? (uint64_t)pnd * a.out_seg_stride : 0u)) + p
                    : 0x80000000u;

@@ -20,9 +20,11 @@
 #   rs8sweep   RS8 shape sweep (tools/bench_extra.py --workload rs8sweep) under a kernel trace
 #   c5         tools/bench_c5.py --steps 2 (the C5 mix's one-GPU share)
 #   percall    tools/percall per-call latencies (needs tools/percall/_build/percall)
-#   ab         A/B of the product library against AB_LIB (another build of the same sources, e.g.
-#              a generator option, loaded through NFEC_LIBRARY): the RS16 GPU tests on AB_LIB,
-#              then rs16 and c4 lines from both, alternating, AB_REPS times (default 2)
+#   ab         A/B of the product library against AB_LIBS (other builds of the same sources, e.g.
+#              tools/ab_build.sh with a generator option, loaded through NFEC_LIBRARY): the RS16 GPU
+#              tests on each (AB_K: a -k expression, e.g. to skip the split-level expectations of a
+#              build with another row count), then rs16 and c4 lines from all, alternating,
+#              AB_REPS times (default 2)
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 R=$(pwd)
 TAG=${TAG:-r05}
@@ -99,19 +101,25 @@ PY
             timeout -k 10 120 tools/percall/_build/percall $args >> "$O/percall.jsonl" || die percall $?
         done ;;
     ab)
-        [ -n "$AB_LIB" ] || die "ab (AB_LIB unset)" 2
-        NFEC_LIBRARY=$R/$AB_LIB timeout -k 10 600 python3 -u -m pytest -x -q --timeout 120 --timeout-method thread \
-            -p no:cacheprovider tests/test_gpu_rs16_tw.py tests/test_gpu_rs16_kernels.py tests/test_c4_c5.py -m gpu \
-            > "$O/pytest_ab.log" 2>&1 || { tail -n 20 "$O/pytest_ab.log"; die ab_tests 1; }
-        tail -n 1 "$O/pytest_ab.log"
+        [ -n "$AB_LIBS" ] || die "ab (AB_LIBS unset)" 2
+        for L in $AB_LIBS; do
+            n=$(basename "$L" .so)
+            NFEC_LIBRARY=$R/$L timeout -k 10 600 python3 -u -m pytest -x -q --timeout 120 --timeout-method thread \
+                -p no:cacheprovider tests/test_gpu_rs16_tw.py tests/test_gpu_rs16_kernels.py tests/test_gpu_tmvp.py \
+                tests/test_c4_c5.py -m gpu ${AB_K:+-k "$AB_K"} > "$O/pytest_$n.log" 2>&1 || { tail -n 20 "$O/pytest_$n.log"; die ab_tests_$n 1; }
+            echo "$n: $(tail -n 1 "$O/pytest_$n.log")"
+        done
         for i in $(seq 1 "${AB_REPS:-2}"); do
             for w in rs16 c4; do
-                timeout -k 10 300 python3 tools/bench_extra.py --workload $w > "$O/${w}_a_$i.json" || die ab $?
-                NFEC_LIBRARY=$R/$AB_LIB timeout -k 10 300 python3 tools/bench_extra.py --workload $w > "$O/${w}_b_$i.json" || die ab $?
+                timeout -k 10 300 python3 tools/bench_extra.py --workload $w > "$O/${w}_product_$i.json" || die ab $?
+                for L in $AB_LIBS; do
+                    n=$(basename "$L" .so)
+                    NFEC_LIBRARY=$R/$L timeout -k 10 300 python3 tools/bench_extra.py --workload $w > "$O/${w}_${n}_$i.json" || die ab $?
+                done
             done
         done
-        for f in "$O"/*_[ab]_*.json; do
-            python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print(sys.argv[1], d.get('encode_ms'), d.get('decode_ms'))" "$f"
+        for f in "$O"/rs16_*_[0-9].json "$O"/c4_*_[0-9].json; do
+            python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print(sys.argv[1].rsplit('/',1)[1], d.get('encode_ms'), d.get('decode_ms'))" "$f"
         done ;;
     *)
         echo "session: unknown task $task"; exit 2 ;;
