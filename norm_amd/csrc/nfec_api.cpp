@@ -220,7 +220,7 @@ struct nfec_codec {
     DevBuf<uint16_t> d_sel16;      // RS16 bit-sliced encode table offsets [k][m][64] (may be absent)
     DevBuf<uint16_t> d_t3off;      // RS16 shared-table encode LDS offsets [k+1][m_pad][48]
     // RS16 products by the tower-field kernel (gen_gf16_tw.hip) instead of the shared-table one:
-    // snippet offsets [k][gf16_tw_passes(m)][48]; the Toeplitz split's three products likewise
+    // snippet offsets [k][sweep][m][2] (gf16_tw_table_elems); the Toeplitz split's products likewise
     bool tw = false;
     // NFEC_OPT_HOST_ONLY: no device, no device tables; only the host per-call paths run
     bool host_only = false;
@@ -526,11 +526,13 @@ int build_codec(nfec_codec* c)
                                             -1, 1);
             const uint32_t cw = c->m / 2, hw = cw / 2;
             const uint32_t rpp = kGf16T3RowsPerPass;
-            // column passes of each form (the products' cost is about one column step per pass)
-            const uint64_t l0 = c->tw ? (uint64_t)gf16_tw_passes(c->m) * c->k : (uint64_t)((c->m + rpp - 1) / rpp) * c->k;
-            const uint64_t l1 = c->tw ? 3ull * gf16_tw_passes(cw) * (c->k / 2) : 3ull * ((cw + rpp - 1) / rpp) * (c->k / 2);
+            // column passes of each form (the products' cost is about one column step per pass;
+            // on the tower kernel weighted by the cost of a pass of the configuration a launch
+            // of that many rows takes, gf16_tw_cost)
+            const uint64_t l0 = c->tw ? gf16_tw_cost(c->m) * c->k : (uint64_t)((c->m + rpp - 1) / rpp) * c->k;
+            const uint64_t l1 = c->tw ? 3ull * gf16_tw_cost(cw) * (c->k / 2) : 3ull * ((cw + rpp - 1) / rpp) * (c->k / 2);
             const bool two_ok = c->tw && hw >= 1 && !(c->opts & NFEC_OPT_RS16_TOEPLITZ_ONE_LEVEL);
-            const uint64_t l2 = two_ok ? 9ull * gf16_tw_passes(hw) * (c->k / 4) : ~0ull;
+            const uint64_t l2 = two_ok ? 9ull * gf16_tw_cost(hw) * (c->k / 4) : ~0ull;
             int levels = 0;
             if (mode == 1) levels = two_ok ? 2 : 1;
             else if (mode != 0) levels = l2 < std::min(l0, l1) ? 2 : l1 < l0 ? 1 : 0;

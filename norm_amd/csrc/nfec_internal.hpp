@@ -320,15 +320,15 @@ int launch_gf16_t3_encode(const Gf16T3Args& a, hipStream_t s);  // NFEC_ENOTSUP:
 bool gf16_t3_covers(const Gf16T3Args& a);  // launch_gf16_t3_encode would take it
 int launch_gf16_t3_multi(const Gf16T3Args* e, uint32_t n, hipStream_t s);  // n <= 3 independent products
 // the same products through the tower field GF((2^8)^2) (gen_gf16_tw.hip): reads a.tw, not a.offs
-#ifndef NFEC_TW_ROWS
-#define NFEC_TW_ROWS 6  // parity rows per wave of the tower kernel (gen_gf16_tw.py --rows)
-#endif
-constexpr uint32_t kGf16TwRowsPerPass = NFEC_TW_ROWS;
 int launch_gf16_tw_encode(const Gf16T3Args& a, hipStream_t s);  // NFEC_ENOTSUP: shape not covered
 bool gf16_tw_covers(const Gf16T3Args& a);
 int launch_gf16_tw_multi(const Gf16T3Args* e, uint32_t n, hipStream_t s);  // n <= kTwMultiMax
 void gf16_tw_offsets(const std::vector<uint32_t>& parity_rows, uint32_t k, uint32_t m, uint16_t* out);
-uint32_t gf16_tw_passes(uint32_t m);  // passes of the tower kernel for m rows (a multiple of 4)
+// The library holds the kernel in several configurations (rows per wave: 6 at 3 waves per SIMD,
+// 4 at 4); each launch takes the cheapest for its rows (gen_gf16_tw.py CONFIGS / PASS_COST).
+uint32_t gf16_tw_passes(uint32_t m, uint32_t rows);  // passes for m rows at `rows` per wave (a multiple of 4)
+uint32_t gf16_tw_rows(uint32_t m);   // the configuration a launch of m rows takes
+uint64_t gf16_tw_cost(uint32_t m);   // its relative cost per column (pass cost x passes)
 size_t gf16_tw_table_elems(uint32_t k, uint32_t m);  // u16 elements of a k-column, m-row table
 // the tower isomorphism's constants: phi's columns (phi(x^i)), lam, and phi^-1's columns (optional)
 void gf16_tw_field(uint16_t phi_cols[16], uint32_t* lam, uint16_t* phi_inv_cols = nullptr);

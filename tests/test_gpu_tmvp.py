@@ -3,8 +3,9 @@ the oracle on the GPU, bit-exact, at one Karatsuba level (three (m/2)-row produc
 (nine (m/4)-row products).  NFEC_OPT_RS16_TOEPLITZ_ON forces the split, at the most levels the
 shape allows, where it is not chosen by default (NFEC_OPT_RS16_TOEPLITZ_OFF: never;
 NFEC_OPT_RS16_TOEPLITZ_ONE_LEVEL: one level at most); by default the codec takes the form with the
-fewest passes of the tower kernel's 6 rows per wave: one level for (128, 32) and (512, 128), two
-for (256, 64) and C4."""
+lowest pass cost (gf16_tw_cost: each product's rows on the cheaper of the tower kernel's 6-row and
+4-row configurations, a 4-row pass costing 0.73 of a 6-row one): one level for (128, 32), two for
+(256, 64), (512, 128) and C4."""
 
 import numpy as np
 import pytest
@@ -40,9 +41,10 @@ CASES = [
     (128, 32, 64, 64, 37, "1", 2),        # several item groups, short segments
     (128, 32, 64, 64, 37, "1L1", 1),
     (128, 32, 1408, 1416, 3, "1", 2),     # padded segment stride
-    (128, 32, 1400, 1400, 4, None, 1),    # one level by default (3 x 4 passes of 64 < 8 x 128 < 9 x 4 x 32)
-    (256, 64, 1400, 1400, 4, None, 2),    # two levels by default (9 x 4 x 64 < 3 x 8 x 128 = 12 x 256)
-    (256, 64, 1400, 1400, 4, "L1", 0),    # at one level the same pass count as no split: not chosen
+    # pass costs: 4 passes of 4 rows 292, 8 passes 584, 16 passes 1168, 6-row passes 100 each
+    (128, 32, 1400, 1400, 4, None, 1),    # one level by default (3 x 292 x 64 < 584 x 128 < 9 x 292 x 32)
+    (256, 64, 1400, 1400, 4, None, 2),    # two levels by default (9 x 292 x 64 < 3 x 584 x 128 < 1168 x 256)
+    (256, 64, 1400, 1400, 4, "L1", 1),    # at most one level: 3 x 584 x 128 < 1168 x 256
     (256, 64, 1400, 1400, 4, "0", 0),
     (512, 128, 64, 64, 2, "1", 2),        # several passes per product
     (512, 128, 64, 64, 2, "1L1", 1),
@@ -52,7 +54,7 @@ CASES = [
     (96, 16, 72, 72, 5, "1", 2),          # three chunk pairs
     (1024, 64, 1400, 1400, 2, "1", 2),
     (2048, 128, 64, 64, 2, "1", 2),
-    (512, 128, 64, 64, 3, None, 1),       # one level by default (3 x 12 x 256 < 24 x 512; two levels tie)
+    (512, 128, 64, 64, 3, None, 2),       # two levels by default (9 x 584 x 128 < 3 x 1168 x 256 < 2336 x 512)
     (96, 24, 1400, 1400, 3, "1", 0),      # m / 2 not a power of two: not allowed
     (100, 20, 1400, 1400, 3, "1", 0),     # k not a multiple of m
 ]

@@ -29,13 +29,17 @@ After the last column each row goes back through phi^-1 and the transpose and is
 with the accumulate source when asked).  Workgroup = 4 independent waves (consecutive jobs:
 passes of one item group share their column reads through L2).
 
-Usage: gen_gf16_tw.py OUT.hip [--diag] [--rows N]
+Usage: gen_gf16_tw.py OUT.hip [--diag] [--rows N] [--noprefetch] [--waves N]
 
---rows N (default 6): parity rows per wave.  6 rows hold 96 accumulator VGPRs (164 in all: 3 waves
-per SIMD, which hide the snippet calls' branch redirects: RS16(400,100) encode 27.1 -> 22.9 ms,
-C4 133.4 -> 125.8 ms against 11 rows, profiles/r05/tw_rows_ab); 11 rows hold 176 (244 in all: 2
-waves per SIMD, less column work per row; the round-3/4 kernel).  A library built from another
-value must be compiled with -DNFEC_TW_ROWS=N.
+The library holds the kernel in the configurations of CONFIGS (rows per wave), and each launch
+takes the one with the lowest PASS_COST x passes for its rows.  6 rows hold 96 accumulator VGPRs
+(164 in all: 3 waves per SIMD, which hide the snippet calls' branch redirects: RS16(400,100)
+encode 27.1 -> 22.9 ms, C4 133.4 -> 125.8 ms against 11 rows, profiles/r05/tw_rows_ab); 4 rows
+hold 64 (125 in all: 4 waves per SIMD, more column work per row: C4's 64-row products 0.946x the
+6-row time, RS16(400,100)'s 100 rows 1.044x, profiles/r05/tw_rows4_ab).  --rows N builds one
+configuration of N rows (A/B builds, tools/ab_build.sh; 11 rows: the round-3/4 kernel at 2 waves
+per SIMD).  --noprefetch reads each sweep's planes into W after the previous sweep instead of
+into S during it (8 VGPRs fewer, 16 moves per column fewer; measured neutral at 6 rows).
 """
 import os
 import sys
@@ -55,6 +59,12 @@ GPR_MODE = 0x9000        # M0[15:12]: index SRC0 and DST
 # ---- VGPRs ----
 # v0..v3: the asm's three inputs (lo, xl, lq; placed by the compiler below the first clobber)
 PREFETCH = True          # x1 / next x0 planes read into S while a sweep runs (--noprefetch: into W after it)
+# The library holds one kernel per configuration (rows per wave, prefetch) and each launch takes
+# the one with the lowest PASS_COST x passes: 6 rows fit 3 waves per SIMD (164 VGPRs), 4 rows 4
+# (125).  A pass of the 4-row kernel costs ~0.73 of a 6-row one (profiles/r05/tw_rows4_ab/: C4's
+# 64-row products 16 passes vs 12, 0.946x the time; RS16(400, 100) 28 vs 20, 1.044x).
+CONFIGS = [(6, True), (4, True)]
+PASS_COST = {6: 100, 4: 73}
 
 
 def layout():
@@ -689,54 +699,91 @@ def clobbers(last_s=None):
     return ", ".join(v + s + ['"m0"', '"scc"', '"memory"'])
 
 
+def asm_block(cond, text, last_s):
+    return f"""    {cond} {{
+        asm volatile(
+            "{text}\\n"
+            :
+            : {ASM_INPUTS}
+            : {clobbers(last_s)});
+    }}"""
+
+
+ASM_INPUTS = """[wb] "s"(wb), [ss] "s"(a.seg_stride), [k] "s"(kk), [tw] "s"(tw), [tstep] "s"(tstep), [t1off] "s"(t1off), [nr] "s"(nr),
+              [csh] "s"(a.col_shift), [cmk] "s"(a.col_mask), [cck] "s"(cck), [cbb] "s"(cbb),
+              [acc] "s"(a.accumulate), [ob] "s"(ob), [ab] "s"(ab), [oslot] "s"(a.out_slot0 + row0),
+              [oss] "s"(a.out_seg_stride), [aslot] "s"(a.acc_slot0 + row0), [ass] "s"(a.acc_seg_stride),
+              [wv] "s"(wave), [rp] "s"(rp), [md] "s"(md), [lo] "v"(lo), [xl] "v"(xl), [lq] "v"(lq)"""
+
+
 def main():
     if "--search" in sys.argv:
         lam, beta, _, _ = choose_tower()
         print(f"LAM, BETA = 0x{lam:02X}, 0x{beta:04X}")
         return
-    global FLAGS
+    global FLAGS, CONFIGS
     diag = "--diag" in sys.argv
     args = [a for a in sys.argv[1:] if a != "--diag"]
-    if "--rows" in args:
-        i = args.index("--rows")
-        set_rows(int(args[i + 1]))
-        del args[i:i + 2]
-    if "--noprefetch" in args:
-        set_prefetch(False)
+    prefetch = "--noprefetch" not in args
+    if not prefetch:
         args.remove("--noprefetch")
+    CONFIGS = [(r, prefetch) for r, _ in CONFIGS]
+    if "--rows" in args:   # one configuration only (A/B builds)
+        i = args.index("--rows")
+        CONFIGS = [(int(args[i + 1]), prefetch)]
+        del args[i:i + 2]
     if "--waves" in args:
         i = args.index("--waves")
         set_waves(int(args[i + 1]))
         del args[i:i + 2]
     path = args[0]
     variants = DIAG_VARIANTS if diag else VARIANTS
-    asms = {}
-    for v, f in variants.items():
-        FLAGS = f
-        asms[v] = "\\n\"\n            \"".join(body())
-    FLAGS = ()
-    common = """[wb] "s"(wb), [ss] "s"(a.seg_stride), [k] "s"(kk), [tw] "s"(tw), [tstep] "s"(tstep), [t1off] "s"(t1off), [nr] "s"(nr),
-              [csh] "s"(a.col_shift), [cmk] "s"(a.col_mask), [cck] "s"(cck), [cbb] "s"(cbb),
-              [acc] "s"(a.accumulate), [ob] "s"(ob), [ab] "s"(ab), [oslot] "s"(a.out_slot0 + row0),
-              [oss] "s"(a.out_seg_stride), [aslot] "s"(a.acc_slot0 + row0), [ass] "s"(a.acc_seg_stride),
-              [wv] "s"(wave), [rp] "s"(rp), [md] "s"(md), [lo] "v"(lo), [xl] "v"(xl), [lq] "v"(lq)"""
-    blocks = []
-    for v in variants:
-        kw = "if constexpr" if v == 0 else "else if constexpr"
-        blocks.append(f"""    {kw} (V == {v}) {{
-        asm volatile(
-            "{asms[v]}\\n"
-            :
-            : {common}
-            : {clobbers(S_LAST4)});
-    }}""")
+    blocks, kernels, waves = [], [], {}
+    for ci, (rows, pf) in enumerate(CONFIGS):
+        set_prefetch(pf)
+        set_rows(rows)
+        # waves per SIMD the register file allows (512 VGPRs per lane, allocated in granules of 8)
+        waves[rows] = min(8, 512 // ((V_LAST + 1 + 7) // 8 * 8))
+        for v, f in variants.items():
+            FLAGS = f
+            text = "\\n\"\n            \"".join(body())
+            kw = "if constexpr" if not blocks else "else if constexpr"
+            blocks.append(asm_block(f"{kw} (R == {rows} && V == {v})", text, S_LAST4))
+        FLAGS = ()
+        kernels.append(f"""template <int V>
+__global__ __launch_bounds__({64 * NWAVES}, {waves[rows]}) void gf16_tw_encode_kernel_r{rows}(Gf16T3Args a)
+{{
+    tw_body<{rows}, V>(a, bs::wg_index(1));
+}}
+
+// several independent products in one grid (the RS16 Toeplitz split, rs16_tmvp): workgroup
+// ranges [wg_end[i-1], wg_end[i]) run problem i, so their tails share one launch
+template <int V>
+__global__ __launch_bounds__({64 * NWAVES}, {waves[rows]}) void gf16_tw_multi_kernel_r{rows}(Gf16TwMulti mm)
+{{
+    const uint32_t wg = bs::wg_index(1);
+    // one body instance (one per problem would hold their argument sets live: more registers,
+    // fewer waves); the problem index is workgroup-uniform
+    uint32_t i = 0;
+    while (i + 1u < mm.n && wg >= mm.wg_end[i]) ++i;
+    tw_body<{rows}, V>(mm.e[i], wg - (i ? mm.wg_end[i - 1] : 0u));
+}}""")
+    set_prefetch(True)
+    set_rows(6)
     asm_blocks = "\n".join(blocks)
+    kernel_defs = "\n\n".join(kernels)
 
     def cases(kern, grid, arg):
-        return "\n".join(f"    case {v}: hipLaunchKernelGGL({kern}<{v}>, dim3((uint32_t){grid}), "
-                         f"dim3({64 * NWAVES}), 0, s, {arg}); break;" for v in variants)
+        out = []
+        for rows, _ in CONFIGS:
+            inner = "\n".join(f"        case {v}: hipLaunchKernelGGL({kern}_r{rows}<{v}>, dim3((uint32_t){grid}), "
+                               f"dim3({64 * NWAVES}), 0, s, {arg}); break;" for v in variants)
+            out.append(f"    case {rows}:\n        switch (tw_variant()) {{\n{inner}\n        }}\n        break;")
+        return "\n".join(out)
     enc_cases = cases("gf16_tw_encode_kernel", "wgs", "b")
     multi_cases = cases("gf16_tw_multi_kernel", "end", "mm")
+    cfg_rows = ", ".join(str(r) for r, _ in CONFIGS)
+    cfg_cost = ", ".join(str(PASS_COST.get(r, 100)) for r, _ in CONFIGS)
     if diag:
         tw_variant = """int tw_variant()
 {
@@ -749,8 +796,6 @@ def main():
 }""" % len(variants)
     else:
         tw_variant = "constexpr int tw_variant() { return 0; }"
-    # waves per SIMD the register file allows (512 VGPRs per lane, allocated in granules of 8)
-    WAVES_PER_SIMD = min(8, 512 // ((V_LAST + 1 + 7) // 8 * 8))
     phi_cols = ", ".join(f"0x{c:04x}" for c in PHI)
     phi_inv_cols = ", ".join(f"0x{c:04x}" for c in PHI_INV)
     src = f"""// GENERATED by tools/codegen/gen_gf16_tw.py -- do not edit by hand.
@@ -761,15 +806,20 @@ def main():
 #include "bitslice.hpp"
 
 namespace nfec {{
-static_assert(kGf16TwRowsPerPass == {ROWS}u, "gen_gf16_tw.py and nfec_internal.hpp disagree on the rows per pass");
 namespace {{
 
+// kernel configurations: rows per wave and the relative cost of one pass
+constexpr uint32_t kTwRows[] = {{{cfg_rows}}};
+constexpr uint32_t kTwPassCost[] = {{{cfg_cost}}};
+constexpr uint32_t kTwConfigs = {len(CONFIGS)};
+
+template <int R>
 __device__ __forceinline__ uint32_t gf16_tw_passes_dev(uint32_t m)
 {{
-    return ((m + {ROWS - 1}u) / {ROWS}u + {NWAVES - 1}u) / {NWAVES}u * {NWAVES}u;
+    return ((m + R - 1u) / R + {NWAVES - 1}u) / {NWAVES}u * {NWAVES}u;
 }}
 
-template <int V>
+template <int R, int V>
 __device__ __forceinline__ void tw_body(const Gf16T3Args& a, uint32_t wg)
 {{
     // per lane, shared by the workgroup's waves (each writes the same values and reads only
@@ -816,7 +866,7 @@ __device__ __forceinline__ void tw_body(const Gf16T3Args& a, uint32_t wg)
     }}
     // the rows in play spread evenly over whole workgroups of four passes (the table holds any
     // row range); the launch sized the grid for a.m rows, so later workgroups may leave
-    const uint32_t npass = gf16_tw_passes_dev(rlim);
+    const uint32_t npass = gf16_tw_passes_dev<R>(rlim);
     if (rlim == 0u || kk == 0u || quad * {NWAVES}u >= npass) return;
     const uint32_t pass = quad * {NWAVES}u + wave;
     const uint32_t row0 = pass * rlim / npass, row1 = (pass + 1u) * rlim / npass;
@@ -859,29 +909,12 @@ __device__ __forceinline__ void tw_body(const Gf16T3Args& a, uint32_t wg)
 {asm_blocks}
 }}
 
-template <int V>
-__global__ __launch_bounds__({64 * NWAVES}, {WAVES_PER_SIMD}) void gf16_tw_encode_kernel(Gf16T3Args a)
-{{
-    tw_body<V>(a, bs::wg_index(1));
-}}
-
-// several independent products in one grid (the RS16 Toeplitz split, rs16_tmvp): workgroup
-// ranges [wg_end[i-1], wg_end[i]) run problem i, so their tails share one launch
-template <int V>
-__global__ __launch_bounds__({64 * NWAVES}, {WAVES_PER_SIMD}) void gf16_tw_multi_kernel(Gf16TwMulti mm)
-{{
-    const uint32_t wg = bs::wg_index(1);
-    // one body instance (one per problem would hold their argument sets live: more registers,
-    // fewer waves); the problem index is workgroup-uniform
-    uint32_t i = 0;
-    while (i + 1u < mm.n && wg >= mm.wg_end[i]) ++i;
-    tw_body<V>(mm.e[i], wg - (i ? mm.wg_end[i - 1] : 0u));
-}}
+{kernel_defs}
 
 {tw_variant}
 
 // checks the shape, fills the default output / accumulate layouts and the pass count
-int tw_prepare(const Gf16T3Args& a, Gf16T3Args& b, uint64_t& wgs)
+int tw_prepare(const Gf16T3Args& a, Gf16T3Args& b, uint64_t& wgs, uint32_t rows)
 {{
     // (numData masking is a flat-mode feature; the column map is the Toeplitz split's, unshortened)
     if ((a.vec_bytes & 7u) || a.vec_bytes == 0 || !a.tw || a.k == 0 || (a.num_data && (a.blk_rows || a.col_chunk)))
@@ -912,7 +945,7 @@ int tw_prepare(const Gf16T3Args& a, Gf16T3Args& b, uint64_t& wgs)
         nbg * b.acc_block_stride + aslots * b.acc_seg_stride >= (1ull << 31))
         return NFEC_ENOTSUP;
     const uint64_t total = (uint64_t)a.nblocks * a.vec_bytes;
-    b.passes = gf16_tw_passes(a.m);
+    b.passes = gf16_tw_passes(a.m, rows);
     // per-block mode: one table and one set of row offsets per block, no accumulate source
     if (a.blk_rows && (!a.row_off || !a.tw_block_stride || a.accumulate)) return NFEC_ENOTSUP;
     const uint64_t groups = a.blk_rows ? (uint64_t)a.nblocks * ((a.vec_bytes + {GROUP_BYTES - 1}u) / {GROUP_BYTES}u)
@@ -930,19 +963,28 @@ bool gf16_tw_covers(const Gf16T3Args& a)
 {{
     Gf16T3Args b;
     uint64_t wgs = 0;
-    return tw_prepare(a, b, wgs) == NFEC_OK;
+    return tw_prepare(a, b, wgs, kTwRows[0]) == NFEC_OK;
 }}
 
 int launch_gf16_tw_multi(const Gf16T3Args* e, uint32_t n, hipStream_t s)
 {{
     if (n == 0 || n > kTwMultiMax) return NFEC_EINVAL;
+    // one configuration for the launch: the lowest cost of all its products' passes
+    uint32_t rows = kTwRows[0];
+    uint64_t best = ~0ull;
+    for (uint32_t c = 0; c < kTwConfigs; ++c) {{
+        uint64_t cost = 0;
+        for (uint32_t i = 0; i < n; ++i)
+            cost += (uint64_t)kTwPassCost[c] * gf16_tw_passes(e[i].m, kTwRows[c]) * e[i].k * e[i].nblocks;
+        if (cost < best) best = cost, rows = kTwRows[c];
+    }}
     Gf16TwMulti mm;
     mm.n = n;
     uint64_t end = 0;
     for (uint32_t i = 0; i < n; ++i) {{
         uint64_t w = 0;
         if (e[i].nblocks) {{
-            const int rc = tw_prepare(e[i], mm.e[i], w);
+            const int rc = tw_prepare(e[i], mm.e[i], w, rows);
             if (rc) return rc;
         }}
         end += w;
@@ -950,7 +992,7 @@ int launch_gf16_tw_multi(const Gf16T3Args* e, uint32_t n, hipStream_t s)
         mm.wg_end[i] = (uint32_t)end;
     }}
     if (end == 0) return NFEC_OK;
-    switch (tw_variant()) {{
+    switch (rows) {{
 {multi_cases}
     }}
     const hipError_t err = hipGetLastError();
@@ -962,9 +1004,10 @@ int launch_gf16_tw_encode(const Gf16T3Args& a, hipStream_t s)
     if (a.nblocks == 0) return NFEC_OK;
     Gf16T3Args b;
     uint64_t wgs = 0;
-    const int rc = tw_prepare(a, b, wgs);
+    const uint32_t rows = gf16_tw_rows(a.m);
+    const int rc = tw_prepare(a, b, wgs, rows);
     if (rc) return rc;
-    switch (tw_variant()) {{
+    switch (rows) {{
 {enc_cases}
     }}
     const hipError_t e = hipGetLastError();
@@ -978,9 +1021,28 @@ void gf16_tw_field(uint16_t phi_cols[16], uint32_t* lam, uint16_t* phi_inv_cols)
     *lam = 0x{LAM:02x}u;
 }}
 
-uint32_t gf16_tw_passes(uint32_t m)
+uint32_t gf16_tw_passes(uint32_t m, uint32_t rows)
 {{
-    return ((m + {ROWS - 1}u) / {ROWS}u + {NWAVES - 1}u) / {NWAVES}u * {NWAVES}u;
+    return ((m + rows - 1u) / rows + {NWAVES - 1}u) / {NWAVES}u * {NWAVES}u;
+}}
+
+uint32_t gf16_tw_rows(uint32_t m)
+{{
+    uint32_t rows = kTwRows[0];
+    uint64_t best = ~0ull;
+    for (uint32_t c = 0; c < kTwConfigs; ++c) {{
+        const uint64_t cost = (uint64_t)kTwPassCost[c] * gf16_tw_passes(m, kTwRows[c]);
+        if (cost < best) best = cost, rows = kTwRows[c];
+    }}
+    return rows;
+}}
+
+uint64_t gf16_tw_cost(uint32_t m)
+{{
+    uint64_t best = ~0ull;
+    for (uint32_t c = 0; c < kTwConfigs; ++c)
+        best = std::min<uint64_t>(best, (uint64_t)kTwPassCost[c] * gf16_tw_passes(m, kTwRows[c]));
+    return best;
 }}
 
 size_t gf16_tw_table_elems(uint32_t k, uint32_t m)
