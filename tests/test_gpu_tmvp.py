@@ -3,8 +3,8 @@ the oracle on the GPU, bit-exact, at one Karatsuba level (three (m/2)-row produc
 (nine (m/4)-row products).  NFEC_OPT_RS16_TOEPLITZ_ON forces the split, at the most levels the
 shape allows, where it is not chosen by default (NFEC_OPT_RS16_TOEPLITZ_OFF: never;
 NFEC_OPT_RS16_TOEPLITZ_ONE_LEVEL: one level at most); by default the codec takes the form with the
-lowest pass cost (gf16_tw_cost: each product's rows on the cheaper of the tower kernel's 6-row and
-4-row configurations, a 4-row pass costing 0.73 of a 6-row one): one level for (128, 32), two for
+lowest pass cost (gf16_tw_cost: each product's rows on the cheapest of the tower kernel's 7-, 6-
+and 4-row configurations, a pass costing 1.2, 1 and 0.73): one level for (128, 32), two for
 (256, 64), (512, 128) and C4."""
 
 import numpy as np

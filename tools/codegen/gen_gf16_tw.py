@@ -60,11 +60,13 @@ GPR_MODE = 0x9000        # M0[15:12]: index SRC0 and DST
 # v0..v3: the asm's three inputs (lo, xl, lq; placed by the compiler below the first clobber)
 PREFETCH = True          # x1 / next x0 planes read into S while a sweep runs (--noprefetch: into W after it)
 # The library holds one kernel per configuration (rows per wave, prefetch) and each launch takes
-# the one with the lowest PASS_COST x passes: 6 rows fit 3 waves per SIMD (164 VGPRs), 4 rows 4
-# (125).  A pass of the 4-row kernel costs ~0.73 of a 6-row one (profiles/r05/tw_rows4_ab/: C4's
-# 64-row products 16 passes vs 12, 0.946x the time; RS16(400, 100) 28 vs 20, 1.044x).
-CONFIGS = [(6, True), (4, True)]
-PASS_COST = {6: 100, 4: 73}
+# the one with the lowest PASS_COST x passes: 7 rows without the prefetch and 6 rows with it fit
+# 3 waves per SIMD (166 / 158 VGPRs), 4 rows 4 (125).  Relative pass costs measured on one box
+# (profiles/r05/tw_rows4_ab/, tw_r7/): a 4-row pass ~0.73 of a 6-row one (C4's 64-row products
+# 16 passes vs 12, 0.946x the time; RS16(400, 100) 28 vs 20, 1.044x), a 7-row pass ~1.2 (RS16
+# encode m = 100: 16 passes vs 20, 0.957x; m = 50: 8 vs 16 4-row passes, 0.85x).
+CONFIGS = [(7, False), (6, True), (4, True)]
+PASS_COST = {7: 120, 6: 100, 4: 73}
 
 
 def layout():
@@ -724,13 +726,13 @@ def main():
     global FLAGS, CONFIGS
     diag = "--diag" in sys.argv
     args = [a for a in sys.argv[1:] if a != "--diag"]
-    prefetch = "--noprefetch" not in args
-    if not prefetch:
+    if "--noprefetch" in args:
         args.remove("--noprefetch")
-    CONFIGS = [(r, prefetch) for r, _ in CONFIGS]
+        CONFIGS = [(r, False) for r, _ in CONFIGS]
     if "--rows" in args:   # one configuration only (A/B builds)
         i = args.index("--rows")
-        CONFIGS = [(int(args[i + 1]), prefetch)]
+        r = int(args[i + 1])
+        CONFIGS = [(r, dict(CONFIGS).get(r, True) and PREFETCH)]
         del args[i:i + 2]
     if "--waves" in args:
         i = args.index("--waves")
@@ -830,7 +832,12 @@ __device__ __forceinline__ void tw_body(const Gf16T3Args& a, uint32_t wg)
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t quads = a.passes / {NWAVES}u;   // workgroups per item group
-    const uint32_t group = wg / quads, quad = wg - group * quads;
+    // the group's workgroups in a rotated order: when the rows in play leave some of its passes
+    // idle (decode stages: rows_lim, per-block e), the idle workgroups are spread over the
+    // dispatcher's round-robin instead of falling on the same shader engines every group (with
+    // 4 workgroups per group and 2 idle, half of them idled: 2x per pass, r05k)
+    const uint32_t group = wg / quads, slot = wg - group * quads;
+    const uint32_t quad = (slot + group) % quads;
     // flat mode: item groups run over the batch's bytes across blocks (one coefficient table);
     // per-block mode (blk_rows): each group lies in one block, which has its own table, row
     // count e, column count (blk_cols, else e) and output row offsets
