@@ -268,6 +268,18 @@ __global__ __launch_bounds__(kWave) void rs16_plan_cf_kernel(RsPlanArgs a)
     __shared__ uint16_t xs[kPlanCfMaxE], yt[kPlanCfMaxE];
     __shared__ int32_t lA[kPlanCfMaxE], lB[kPlanCfMaxE];
     __shared__ uint32_t np_s;
+    // lost parity rows as a bitmap and the stage-2 column -> substitute index map, for the
+    // usual sizes (ec, ncol <= kPlanCfScan); past them the serial scan / binary search below
+    constexpr uint32_t kPlanCfScan = 1024;
+    __shared__ uint32_t pbits[kPlanCfScan / 32];
+    __shared__ int16_t pinv[kPlanCfScan];
+    // e <= 64: the e x e logs lg[x_s ^ y_t] kept in LDS (each gathered once for the row sums of
+    // lA, the column sums of lB and the inverse's entries), the x-x and y-y log sums gathered
+    // for s < s' only (symmetric).  The kernel is bound by these random gathers through the
+    // vector memory path (~one cache line per lane).
+    constexpr uint32_t kPlanCfSmall = 64, kLxyStride = kPlanCfSmall + 1;
+    __shared__ uint16_t Lxy[kPlanCfSmall * kLxyStride];
+    __shared__ int32_t xxs[kPlanCfSmall], yys[kPlanCfSmall];
     const uint32_t lane = threadIdx.x;
     const uint32_t b = blockIdx.x;
     const uint16_t* ex = reinterpret_cast<const uint16_t*>(a.exp_tab);  // 2q entries
@@ -297,8 +309,29 @@ __global__ __launch_bounds__(kWave) void rs16_plan_cf_kernel(RsPlanArgs a)
     if (ok && es > kPlanCfMaxE) ok = false;  // launch_rs_plan only picks this kernel when e fits
     if (!ok) status = 0;
     if (ok && es > 0) {
-        // surviving parities in ascending slot order (reference scan normEncoderRS8.cpp:660-718)
-        if (lane == 0) {
+        // surviving parities in ascending slot order (reference scan normEncoderRS8.cpp:660-718);
+        // the es-th survivor lies before parity offset ec, so with ec <= kPlanCfScan the lanes
+        // scan 64 offsets at a time against a bitmap of the lost ones
+        if (ec <= kPlanCfScan) {
+            for (uint32_t i = lane; i < kPlanCfScan / 32; i += kWave) pbits[i] = 0;
+            __syncthreads();
+            for (uint32_t i = es + lane; i < ec; i += kWave) {
+                const uint32_t off = (uint32_t)locs[i] - nd;   // < m (checked above)
+                if (off < kPlanCfScan) atomicOr(&pbits[off >> 5], 1u << (off & 31u));
+            }
+            __syncthreads();
+            uint32_t np = 0;
+            const uint32_t lim = min(m, kPlanCfScan);
+            for (uint32_t base = 0; np < es && base < lim; base += kWave) {
+                const uint32_t off = base + lane;
+                const bool surv = off < lim && !((pbits[off >> 5] >> (off & 31u)) & 1u);
+                const uint64_t mask = __ballot(surv);
+                const uint32_t rank = (uint32_t)__popcll(mask & ((1ull << lane) - 1ull));
+                if (surv && np + rank < es) listP[np + rank] = (uint16_t)(nd + off);
+                np += (uint32_t)__popcll(mask);
+            }
+            if (lane == 0) np_s = min(np, es);
+        } else if (lane == 0) {
             uint32_t next = es, np = 0;
             for (uint32_t s = nd; s < nd + m && np < es; ++s) {
                 if (next < ec && locs[next] == s) { ++next; continue; }
@@ -358,48 +391,106 @@ __global__ __launch_bounds__(kWave) void rs16_plan_cf_kernel(RsPlanArgs a)
         yt[i] = ex[(k - 1 + (listP[i] - nd)) % (uint32_t)q];  // parity row p: point alpha^(k+p-1)
     }
     __syncthreads();
-    for (uint32_t i = lane; i < e; i += kWave) {
-        const uint32_t x = xs[i], y = yt[i];
-        int32_t acc = (int32_t)a.lwp[listE[i]], bcc = -(int32_t)a.lw[listP[i] - nd];
+    const bool small = e <= kPlanCfSmall;
+    if (small) {
+        if (lane < e) xxs[lane] = 0, yys[lane] = 0;
+        __syncthreads();
+        int32_t row = 0, sx = 0, sy = 0;
+        if (lane < e) {
+            const uint32_t x = xs[lane], y = yt[lane];
 #pragma unroll 4
-        for (uint32_t t = 0; t < e; ++t) {
-            acc += (int32_t)lg[x ^ yt[t]] - (int32_t)lg[x ^ xs[t]];
-            bcc += (int32_t)lg[y ^ xs[t]] - (int32_t)lg[y ^ yt[t]];
+            for (uint32_t t = 0; t < e; ++t) {
+                const uint32_t v = lg[x ^ yt[t]];
+                Lxy[lane * kLxyStride + t] = (uint16_t)v;
+                row += (int32_t)v;
+            }
+            for (uint32_t t = lane + 1; t < e; ++t) {
+                const int32_t vx = (int32_t)lg[x ^ xs[t]], vy = (int32_t)lg[y ^ yt[t]];
+                sx += vx;
+                sy += vy;
+                atomicAdd(&xxs[t], vx);
+                atomicAdd(&yys[t], vy);
+            }
         }
-        // the t == i terms subtract lg[0] = q (x ^ x, y ^ y), which is 0 mod q
-        acc %= q;
-        bcc %= q;
-        lA[i] = acc < 0 ? acc + q : acc;
-        lB[i] = bcc < 0 ? bcc + q : bcc;
+        __syncthreads();
+        if (lane < e) {
+            int32_t col = 0;
+            for (uint32_t t = 0; t < e; ++t) col += (int32_t)Lxy[t * kLxyStride + lane];
+            // (the s' == s terms of the original sums are lg[0] = q: 0 mod q, left out here)
+            int32_t acc = (int32_t)a.lwp[listE[lane]] + row - sx - xxs[lane];
+            int32_t bcc = -(int32_t)a.lw[listP[lane] - nd] + col - sy - yys[lane];
+            acc %= q;
+            bcc %= q;
+            lA[lane] = acc < 0 ? acc + q : acc;
+            lB[lane] = bcc < 0 ? bcc + q : bcc;
+        }
+    } else {
+        for (uint32_t i = lane; i < e; i += kWave) {
+            const uint32_t x = xs[i], y = yt[i];
+            int32_t acc = (int32_t)a.lwp[listE[i]], bcc = -(int32_t)a.lw[listP[i] - nd];
+#pragma unroll 4
+            for (uint32_t t = 0; t < e; ++t) {
+                acc += (int32_t)lg[x ^ yt[t]] - (int32_t)lg[x ^ xs[t]];
+                bcc += (int32_t)lg[y ^ xs[t]] - (int32_t)lg[y ^ yt[t]];
+            }
+            // the t == i terms subtract lg[0] = q (x ^ x, y ^ y), which is 0 mod q
+            acc %= q;
+            bcc %= q;
+            lA[i] = acc < 0 ? acc + q : acc;
+            lB[i] = bcc < 0 ? bcc + q : bcc;
+        }
     }
     __syncthreads();
+    // lg[x_s ^ y_t]: from LDS when small
+    auto lxy = [&](uint32_t s_, uint32_t t_) -> int32_t {
+        return small ? (int32_t)Lxy[s_ * kLxyStride + t_] : (int32_t)lg[xs[s_] ^ yt[t_]];
+    };
     uint16_t* coef2 = reinterpret_cast<uint16_t*>(a.coef2) + (uint64_t)b * (a.coef2_block ? a.coef2_block : (uint64_t)cs * cs);
     if (by_row) {
         // column = parity row P_t - nd (z row), rows s < e; the lost parity rows below P_last
-        // get zero columns
+        // get zero columns.  pinv[col] = t (or -1) when ncol <= kPlanCfScan, else a binary search
+        const bool map = ncol <= kPlanCfScan;
+        if (map) {
+            for (uint32_t c = lane; c < ncol; c += kWave) pinv[c] = -1;
+            __syncthreads();
+            for (uint32_t t = lane; t < e; t += kWave) pinv[(uint32_t)listP[t] - nd] = (int16_t)t;
+            __syncthreads();
+        }
+        uint32_t col = lane / e, s = lane - col * e;   // (col, s) of idx, stepped without a division
+        const uint32_t dcol = kWave / e, ds = kWave - dcol * e;
         for (uint32_t idx = lane; idx < ncol * e; idx += kWave) {
-            const uint32_t col = idx / e, s = idx - col * e;
-            uint32_t lo = 0, hi = e;  // first t with listP[t] - nd >= col
-            while (lo < hi) {
-                const uint32_t mid = (lo + hi) >> 1;
-                if ((uint32_t)listP[mid] - nd < col) lo = mid + 1;
-                else hi = mid;
+            uint32_t lo;
+            if (map) {
+                const int32_t t = pinv[col];
+                lo = t < 0 ? e : (uint32_t)t;
+            } else {
+                lo = 0;
+                uint32_t hi = e;  // first t with listP[t] - nd >= col
+                while (lo < hi) {
+                    const uint32_t mid = (lo + hi) >> 1;
+                    if ((uint32_t)listP[mid] - nd < col) lo = mid + 1;
+                    else hi = mid;
+                }
+                if (lo < e && (uint32_t)listP[lo] - nd != col) lo = e;
             }
             uint16_t v = 0;
-            if (lo < e && (uint32_t)listP[lo] - nd == col) {
-                int32_t l = lA[s] + lB[lo] - (int32_t)lg[xs[s] ^ yt[lo]];
+            if (lo < e) {
+                int32_t l = lA[s] + lB[lo] - lxy(s, lo);
                 l %= q;
                 if (l < 0) l += q;
                 v = ex[l];
             }
             coef2[(uint64_t)col * cs + s] = v;
+            col += dcol;
+            s += ds;
+            if (s >= e) s -= e, ++col;
         }
     } else {
         for (uint32_t idx = lane; idx < cs * cs; idx += kWave) {
             const uint32_t t = idx / cs, s = idx % cs;  // column t (input z_t), row s (output)
             uint16_t v = 0;
             if (t < e && s < e) {
-                int32_t l = lA[s] + lB[t] - (int32_t)lg[xs[s] ^ yt[t]];
+                int32_t l = lA[s] + lB[t] - lxy(s, t);
                 l %= q;
                 if (l < 0) l += q;
                 v = ex[l];
