@@ -324,7 +324,7 @@ int launch_gf16_tw_encode(const Gf16T3Args& a, hipStream_t s);  // NFEC_ENOTSUP:
 bool gf16_tw_covers(const Gf16T3Args& a);
 int launch_gf16_tw_multi(const Gf16T3Args* e, uint32_t n, hipStream_t s);  // n <= kTwMultiMax
 void gf16_tw_offsets(const std::vector<uint32_t>& parity_rows, uint32_t k, uint32_t m, uint16_t* out);
-// The library holds the kernel in several configurations (rows per wave: 6 at 3 waves per SIMD,
+// The library holds the kernel in several configurations (rows per wave: 7 and 6 at 3 waves per SIMD,
 // 4 at 4); each launch takes the cheapest for its rows (gen_gf16_tw.py CONFIGS / PASS_COST).
 uint32_t gf16_tw_passes(uint32_t m, uint32_t rows);  // passes for m rows at `rows` per wave (a multiple of 4)
 uint32_t gf16_tw_rows(uint32_t m);   // the configuration a launch of m rows takes

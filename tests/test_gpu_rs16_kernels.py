@@ -28,9 +28,9 @@ def _codecs(monkeypatch, tw, k, m, vec, tmvp=None):
 
 @pytest.mark.parametrize("tw", KERNELS)
 @pytest.mark.parametrize("k,m,vec,stride,nb,tmvp", [
-    (100, 20, 1400, 1400, 3, "0"),     # one product, two passes of 11 rows (tower) / one of 44
-    (64, 11, 64, 64, 9, "0"),          # exactly one full tower pass
-    (40, 12, 72, 80, 5, "0"),          # one row past a full pass, padded stride
+    (100, 20, 1400, 1400, 3, "0"),     # one product: four 5-row passes (tower, 6-row kernel) / one of 44 (shared tables)
+    (64, 11, 64, 64, 9, "0"),          # 11 rows: four passes of the 4-row kernel (the 11-row kernel's one full pass)
+    (40, 12, 72, 80, 5, "0"),          # 12 rows, padded stride
     (128, 32, 1408, 1416, 3, "1"),     # Toeplitz split, padded stride
     (512, 128, 64, 64, 2, "1"),        # Toeplitz split, several passes per product
 ])
