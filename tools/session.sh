@@ -16,7 +16,7 @@
 #              HBM bytes) -> pmc_tw_rs16_summary.json, which bench_extra's op roofline reads
 #   pmc_c4     PMC passes of C4 (tools/pmc_c4.sh)
 #   pmc_bench  PMC passes of the headline workload (tools/pmc_r03.sh: HBM bytes for bench.py)
-#   mdp        MDP(64,32) encode + 16-erasure repair line
+#   mdp        MDP(64,32) encode + 16-erasure repair line under a kernel trace
 #   rs8sweep   RS8 shape sweep (tools/bench_extra.py --workload rs8sweep) under a kernel trace
 #   c5         tools/bench_c5.py --steps 2 (the C5 mix's one-GPU share)
 #   percall    tools/percall per-call latencies (needs tools/percall/_build/percall)
@@ -88,8 +88,7 @@ PY
         TAG=${TAG}_bench timeout -k 10 900 bash tools/pmc_r03.sh > "$O/pmc_bench.log" 2>&1 || die pmc_bench $?
         cp "$R/gpurun_out/pmc_${TAG}_bench/summary.json" "$O/pmc_bench_summary.json" ;;
     mdp)
-        timeout -k 10 300 python3 tools/bench_extra.py --workload mdp > "$O/mdp.json" 2> "$O/mdp.err" || die mdp $?
-        cat "$O/mdp.json" ;;
+        prof mdp "$R/tools/bench_extra.py" --workload mdp || die mdp $? ;;
     rs8sweep)
         prof rs8sweep "$R/tools/bench_extra.py" --workload rs8sweep || die rs8sweep $? ;;
     c5)
