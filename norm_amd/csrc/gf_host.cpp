@@ -17,6 +17,8 @@
 
 #include "nfec_internal.hpp"
 
+#include <functional>
+
 namespace nfec {
 
 static thread_local std::string g_last_error;
@@ -222,25 +224,24 @@ bool rs16_tmvp_plan(uint32_t k, uint32_t m, const std::vector<uint32_t>& gen, st
     return rs16_tmvp_plan_levels(k, m, gen, 1, prod, cmat, wmat, gmat);
 }
 
-// levels = 1: the three products above.  levels = 2 (cw >= 2): each of them split again inside
-// every cw-wide chunk of its columns, whose cw x cw blocks N_q are Toeplitz, [[al, be], [ga, al]]
-// in halves of hw = cw/2 (al: top-left = bottom-right).  With the level-1 inputs z_0 = c_a d_a +
-// c_b d_b (the pair sums), z_1 = c_b d_b, z_2 = c_a d_a and z = (z0, z1) per chunk,
-//   N z = [al (z0 + z1) + (be - al) z1 ; al (z0 + z1) + (ga - al) z0],
-// nine hw-row products over k/4 columns (level-2 virtual column q*hw + i, chunk q, i < hw):
-//   prod[3X]     = al_X         over the scaled sums s_X = z_X0 + z_X1 (the prescale writes them)
-//   prod[3X + 1] = (be_X - al_X) over z_X1: the pair sums' second halves for X = 0, else the raw
-//                  source columns b1 = a1 + cw (X = 1) / a1 = 2q cw + hw + i (X = 2), their c
-//                  scaling folded into the coefficients
-//   prod[3X + 2] = (ga_X - al_X) over z_X0: the first halves, likewise (b0 / a0 = 2q cw + i)
-// tests/test_tmvp.py::test_two_karatsuba_levels_reproduce_product checks the identity.
+// levels = L in 1..3: the general form (tests/test_tmvp.py::_split_levels restates it).  The root
+// is the Toeplitz part T[p][q m + i] over the scaled source u_j = c_j d_j in chunks of m columns;
+// a node of width r (its r x r blocks Toeplitz) splits into three of r/2 rows, per chunk
+//   alpha = the top-left block      over (first half + second half of its input)
+//   beta  = top-right - top-left    over the second half
+//   gamma = bottom-left - top-left  over the first half,
+// and the 3^L leaves (path digits d_1..d_L, 0 alpha / 1 beta / 2 gamma; product index
+// sum d_l 3^(L-l)) have m >> L rows over k >> L virtual columns v = q (m >> L) + i.  A leaf
+// whose path holds no alpha reads raw source columns j = q m + i + (sum of m >> l over its beta
+// levels l), its c_j folded into the coefficients; the others read the alpha sums the prescale
+// writes (kernels_tmvp.hip).  L = 1: prod[0] = A, prod[1] = (B - A) c_b, prod[2] = (C - A) c_a.
 bool rs16_tmvp_plan_levels(uint32_t k, uint32_t m, const std::vector<uint32_t>& gen, int levels,
                            std::vector<uint32_t>* prod, std::vector<uint16_t>& cmat, std::vector<uint16_t>& wmat,
                            std::vector<uint16_t>& gmat)
 {
-    const uint32_t cw = m / 2, hw = cw / 2;
+    const uint32_t cw = m / 2;
     if (m < 2 || (m & 1u) || (cw & (cw - 1u)) || k % m || gen.size() != (size_t)m * k) return false;
-    if (levels != 1 && (levels != 2 || hw == 0)) return false;
+    if (levels < 1 || levels > 3 || (m >> levels) == 0) return false;
     const Field& f = gf16();
     const uint32_t q = f.q;
     std::vector<uint32_t> x(k);
@@ -266,39 +267,38 @@ bool rs16_tmvp_plan_levels(uint32_t k, uint32_t m, const std::vector<uint32_t>& 
     for (uint32_t p = 0; p < m; ++p)
         for (uint32_t j = 1; j < k; ++j)
             if (gen[(size_t)p * k + j] != f.mul(w[p], f.mul(h[k + p - j], c[j]))) return false;
-    const uint32_t half = k / 2;
-    if (levels == 1) {
-        for (int e = 0; e < 3; ++e) prod[e].assign((size_t)cw * half, 0);
-        for (uint32_t p = 0; p < cw; ++p)
-            for (uint32_t v = 0; v < half; ++v) {
-                const uint32_t a = 2 * (v / cw) * cw + v % cw, b = a + cw;
-                const uint32_t ta = h[k + p - a];
-                prod[0][(size_t)p * half + v] = ta;
-                prod[1][(size_t)p * half + v] = f.mul(h[k + p - b] ^ ta, c[b]);
-                prod[2][(size_t)p * half + v] = f.mul(h[k + p + cw - a] ^ ta, c[a]);
-            }
-    } else {
-        // N_X(p, q, i), p < cw, i < cw: the Toeplitz part of level-1 product X at chunk q
-        auto N = [&](int X, uint32_t p, uint32_t q, uint32_t i) -> uint32_t {
-            const uint32_t a = 2 * q * cw + i;
-            const uint32_t ta = h[k + p - a];
-            return X == 0 ? ta : X == 1 ? (h[k + p - a - cw] ^ ta) : (h[k + p + cw - a] ^ ta);
-        };
-        const uint32_t quarter = k / 4;
-        for (int e = 0; e < 9; ++e) prod[e].assign((size_t)hw * quarter, 0);
-        for (int X = 0; X < 3; ++X)
-            for (uint32_t p = 0; p < hw; ++p)
-                for (uint32_t v = 0; v < quarter; ++v) {
-                    const uint32_t q = v / hw, i = v % hw;
-                    const uint32_t al = N(X, p, q, i), be = N(X, p, q, hw + i), ga = N(X, hw + p, q, i);
-                    if (N(X, hw + p, q, hw + i) != al) return false;  // not Toeplitz: no split
-                    // the raw columns of z_X1 / z_X0 (X = 1: b1, b0; X = 2: a1, a0) and their c
-                    const uint32_t a0 = 2 * q * cw + i, off = X == 1 ? cw : 0u;
-                    const uint32_t c1 = X == 0 ? 1u : c[a0 + off + hw], c0 = X == 0 ? 1u : c[a0 + off];
-                    prod[3 * X][(size_t)p * quarter + v] = al;
-                    prod[3 * X + 1][(size_t)p * quarter + v] = f.mul(be ^ al, c1);
-                    prod[3 * X + 2][(size_t)p * quarter + v] = f.mul(ga ^ al, c0);
+    const int L = levels;
+    const uint32_t r = m >> L, cols = k >> L, nq = k / m;
+    // block entry (p, i) of the node with digits dg[0..l) in chunk qq
+    std::function<uint32_t(const int*, int, uint32_t, uint32_t, uint32_t)> M =
+        [&](const int* dg, int l, uint32_t qq, uint32_t p, uint32_t i) -> uint32_t {
+        if (l == 0) return h[k + p - qq * m - i];
+        const uint32_t hf = m >> l;
+        if (dg[l - 1] == 0) return M(dg, l - 1, qq, p, i);
+        if (dg[l - 1] == 1) return M(dg, l - 1, qq, p, i + hf) ^ M(dg, l - 1, qq, p, i);
+        return M(dg, l - 1, qq, p + hf, i) ^ M(dg, l - 1, qq, p, i);
+    };
+    uint32_t np = 1;
+    for (int l = 0; l < L; ++l) np *= 3;
+    for (uint32_t e = 0; e < np; ++e) {
+        int dg[3] = {0, 0, 0};
+        bool raw = true;
+        uint32_t off = 0;
+        for (int l = L, t = (int)e; l >= 1; --l, t /= 3) dg[l - 1] = t % 3;
+        for (int l = 1; l <= L; ++l) {
+            raw = raw && dg[l - 1] != 0;
+            if (dg[l - 1] == 1) off += m >> l;
+        }
+        prod[e].assign((size_t)r * cols, 0);
+        for (uint32_t qq = 0; qq < nq; ++qq)
+            for (uint32_t i = 0; i < r; ++i) {
+                const uint32_t v = qq * r + i, j = qq * m + i + off;
+                for (uint32_t p = 0; p < r; ++p) {
+                    uint32_t val = M(dg, L, qq, p, i);
+                    if (raw) val = f.mul(val, c[j]);
+                    prod[e][(size_t)p * cols + v] = val;
                 }
+            }
     }
     cmat.assign((size_t)k * 16, 0);
     wmat.assign((size_t)m * 16, 0);

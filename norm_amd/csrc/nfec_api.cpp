@@ -524,27 +524,50 @@ int build_codec(nfec_codec* c)
                                             : (c->opts & NFEC_OPT_RS16_TOEPLITZ_ON) ? 1
                                                                                     : -1,
                                             -1, 1);
-            const uint32_t cw = c->m / 2, hw = cw / 2;
+            const uint32_t cw = c->m / 2;
             const uint32_t rpp = kGf16T3RowsPerPass;
-            // column passes of each form (the products' cost is about one column step per pass;
-            // on the tower kernel weighted by the cost of a pass of the configuration a launch
-            // of that many rows takes, gf16_tw_cost)
-            const uint64_t l0 = c->tw ? gf16_tw_cost(c->m) * c->k : (uint64_t)((c->m + rpp - 1) / rpp) * c->k;
-            const uint64_t l1 = c->tw ? 3ull * gf16_tw_cost(cw) * (c->k / 2) : 3ull * ((cw + rpp - 1) / rpp) * (c->k / 2);
-            const bool two_ok = c->tw && hw >= 1 && !(c->opts & NFEC_OPT_RS16_TOEPLITZ_ONE_LEVEL);
-            const uint64_t l2 = two_ok ? 9ull * gf16_tw_cost(hw) * (c->k / 4) : ~0ull;
+            // cost of each form per block, in the products' units (about one column step per
+            // pass, weighted on the tower kernel by the cost of a pass of the configuration a
+            // launch of that many rows takes, gf16_tw_cost): the products (3^L of m >> L rows
+            // over k >> L columns, plus ~20 columns' worth of fixed work per pass), the prescale
+            // (~165 per column it moves: it is HBM-bound) and the postscale (per parity row ~460
+            // at one level, ~1,490 at two: its constant multiplies).  Fitted to the split forced
+            // at 0 / 1 / 2 levels on (128, 32), (256, 64), (512, 128) and C4
+            // (profiles/r05/tmvp_levels/: fastest at 0, 0, 1 and 2 levels).  A third level
+            // measured slower: its prescale moves 3.4 k columns per block against 2.25 k.
+            const int max_levels = (!c->tw || (c->opts & NFEC_OPT_RS16_TOEPLITZ_ONE_LEVEL)) ? 1 : 2;
+            uint64_t cost[3];
+            int top = 0;
+            for (int L = 0; L <= 2; ++L) {
+                cost[L] = ~0ull;
+                const uint32_t r = c->m >> L;
+                if (L > max_levels || r == 0 || (L && (c->m % (1u << L)))) continue;
+                top = L;
+                uint64_t np = 1;
+                for (int i = 0; i < L; ++i) np *= 3;
+                const uint64_t cols = (c->k >> L) + 20;
+                const uint64_t prod_cost = c->tw ? np * gf16_tw_cost(r) * cols : np * ((r + rpp - 1) / rpp) * cols;
+                // (the shared-table kernel keeps the round-2 rule: passes alone)
+                cost[L] = prod_cost + (!c->tw ? 0ull
+                                       : L == 1 ? 165ull * (c->k + c->k / 2) + 460ull * c->m
+                                       : L == 2 ? 165ull * (c->k + c->k / 2 + 3ull * (c->k / 4)) + 1490ull * c->m
+                                                : 0ull);
+            }
             int levels = 0;
-            if (mode == 1) levels = two_ok ? 2 : 1;
-            else if (mode != 0) levels = l2 < std::min(l0, l1) ? 2 : l1 < l0 ? 1 : 0;
-            const int nprod = levels == 2 ? 9 : 3;
+            if (mode == 1) levels = top;
+            else if (mode != 0)
+                for (int L = 1; L <= 2; ++L)
+                    if (cost[L] < cost[levels]) levels = L;
+            uint32_t nprod = 1;
+            for (int i = 0; i < levels; ++i) nprod *= 3;
             std::vector<uint32_t> prod[9];
             std::vector<uint16_t> cm, wm, gm;
             if (levels && rs16_tmvp_plan_levels(c->k, c->m, c->gen, levels, prod, cm, wm, gm)) {
-                const uint32_t cols = levels == 2 ? c->k / 4 : c->k / 2, rows = levels == 2 ? hw : cw;
+                const uint32_t cols = c->k >> levels, rows = c->m >> levels;
                 const uint32_t mp = gf16_t3_rows_padded(rows);
                 const size_t one = c->tw ? gf16_tw_table_elems(cols, rows) : (size_t)(cols + 1) * mp * 48;
                 std::vector<uint16_t> off(nprod * one);
-                for (int e = 0; e < nprod; ++e) {
+                for (uint32_t e = 0; e < nprod; ++e) {
                     if (c->tw) gf16_tw_offsets(prod[e], cols, rows, off.data() + e * one);
                     else gf16_t3_offsets(prod[e], cols, rows, off.data() + e * one);
                 }
@@ -654,16 +677,19 @@ static bool use_asm()
 // The sub-batch scratch is the codec's, so calls are ordered: each waits (on its stream) for
 // the previous one's end.
 // Two Karatsuba levels (tower kernel only): the level-2 prescale writes the pair sums and the
-// scaled sums into the block's scratch, one launch runs the nine (m/4)-row products (their alpha
-// parts over the scaled sums, the beta / gamma parts over the pair sums' halves (X = 0) or the
-// source columns themselves through column maps (X = 1, 2)) into the scratch, and the level-2
-// postscale combines them into the m parity rows (kernels_tmvp.hip; gf_host.cpp,
-// rs16_tmvp_plan_levels).
+// scaled sums into the block's scratch, launches of the nine (m/4)-row products run into the
+// scratch -- each reads, through a column map, the alpha input of its last alpha level (its later
+// beta level selects halves) or, with no alpha in its path, the source columns themselves (c
+// folded into its coefficients) -- and the level-2 postscale combines them into the m parity rows
+// (kernels_tmvp.hip; gf_host.cpp, rs16_tmvp_plan_levels, whose product paths index them).
 static int rs16_tmvp2_encode(nfec_codec* c, const nfec_block_batch* b, hipStream_t s)
 {
-    const uint32_t k = c->k, m = c->m, cw = m / 2, hw = cw / 2, half = k / 2, quarter = k / 4, vec = c->vec;
-    const uint32_t prow0 = half + 3 * quarter;                  // first product row in the scratch
-    const uint64_t per_block = (uint64_t)(prow0 + 9 * hw) * vec;
+    const int L = c->tmvp_levels;
+    const uint32_t k = c->k, m = c->m, r = m >> L, cols = k >> L, vec = c->vec;
+    uint32_t nprod = 1;
+    for (int i = 0; i < L; ++i) nprod *= 3;
+    const uint32_t prow0 = k / 2 + 3 * (k / 4);                 // first product row in the scratch
+    const uint64_t per_block = (uint64_t)(prow0 + nprod * r) * vec;
     std::lock_guard<std::mutex> lk(c->tmvp_mu);
     size_t free_b = 0, total_b = 0;
     if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) {
@@ -685,9 +711,9 @@ static int rs16_tmvp2_encode(nfec_codec* c, const nfec_block_batch* b, hipStream
             code = hip_fail(hipGetLastError(), "tmvp event");
         return code;
     };
-    const size_t one_tw = gf16_tw_table_elems(quarter, hw);
-    uint32_t hshift = 0;
-    while ((1u << hshift) < hw) ++hshift;
+    const size_t one_tw = gf16_tw_table_elems(cols, r);
+    uint32_t rshift = 0;
+    while ((1u << rshift) < r) ++rshift;
     int rc;
     for (uint32_t b0 = 0; b0 < b->nblocks; b0 += sb) {
         const uint32_t nb = std::min(sb, b->nblocks - b0);
@@ -699,63 +725,71 @@ static int rs16_tmvp2_encode(nfec_codec* c, const nfec_block_batch* b, hipStream
         a.nblocks = nb;
         a.vec = vec;
         a.k = k;
-        a.cw = cw;
-        a.hw = hw;
+        a.cw = m / 2;
+        a.hw = r;
         a.sc = c->w_tmvp.p;
         a.sc_block_stride = per_block;
         a.cmat = c->d_tmvp_mat.p;
         a.wmat = c->d_tmvp_mat.p + (size_t)k * 16;
         a.gmat = c->d_tmvp_mat.p + (size_t)(k + m) * 16;
-        Gf16T3Args e[9];
-        for (int X = 0; X < 3; ++X)
-            for (int t = 0; t < 3; ++t) {
-                Gf16T3Args& g = e[3 * X + t];
-                g.nblocks = nb;
-                g.k = quarter;
-                g.m = hw;
-                g.vec_bytes = vec;
-                g.tw = c->d_tmvp_tw.p + (3 * X + t) * one_tw;
-                g.out_base = a.sc;
-                g.out_block_stride = per_block;
-                g.out_seg_stride = vec;
-                g.out_slot0 = prow0 + (3 * X + t) * hw;
-                if (t == 0) {
-                    // alpha: the scaled sums s_X, plain columns of the scratch
-                    g.base = a.sc;
-                    g.block_stride = per_block;
-                    g.seg_stride = vec;
-                    g.col_base = half + X * quarter;
-                    g.in_slots = prow0;
-                    continue;
-                }
-                // beta (t = 1: second halves) / gamma (t = 2: first halves) through a column map:
-                // level-2 column q * hw + i -> slot (q * chunk) + base + i
-                g.col_shift = hshift;
-                g.col_mask = hw - 1;
-                if (X == 0) {  // the pair sums in the scratch, chunks of cw
-                    g.base = a.sc;
-                    g.block_stride = per_block;
-                    g.seg_stride = vec;
-                    g.col_chunk = cw;
-                    g.col_base = t == 1 ? hw : 0;
-                    g.in_slots = prow0;
-                } else {       // the source columns, chunk pairs of 2 cw: X = 1 the pairs' b halves
-                    g.base = blocks;
-                    g.block_stride = b->block_stride;
-                    g.seg_stride = b->seg_stride;
-                    g.col_chunk = 2 * cw;
-                    g.col_base = (X == 1 ? cw : 0) + (t == 1 ? hw : 0);
-                    g.in_slots = k + m;
-                }
+        std::vector<Gf16T3Args> e(nprod);
+        for (uint32_t pi = 0; pi < nprod; ++pi) {
+            int dg[3] = {0, 0, 0};
+            for (int l = L, t = (int)pi; l >= 1; --l, t /= 3) dg[l - 1] = t % 3;
+            int last_alpha = 0;
+            for (int l = 1; l <= L; ++l)
+                if (dg[l - 1] == 0) last_alpha = l;
+            uint32_t off = 0;  // the beta levels after the last alpha select second halves
+            for (int l = last_alpha + 1; l <= L; ++l)
+                if (dg[l - 1] == 1) off += m >> l;
+            Gf16T3Args& g = e[pi];
+            g.nblocks = nb;
+            g.k = cols;
+            g.m = r;
+            g.vec_bytes = vec;
+            g.tw = c->d_tmvp_tw.p + pi * one_tw;
+            g.out_base = a.sc;
+            g.out_block_stride = per_block;
+            g.out_seg_stride = vec;
+            g.out_slot0 = prow0 + pi * r;
+            if (last_alpha == 0) {  // the source columns q m + i + off, chunks of m
+                g.base = blocks;
+                g.block_stride = b->block_stride;
+                g.seg_stride = b->seg_stride;
+                g.col_shift = rshift;
+                g.col_mask = r - 1;
+                g.col_chunk = m;
+                g.col_base = off;
+                g.in_slots = k + m;
+                continue;
             }
+            // the alpha input of level last_alpha (block of prefix P' = the digits before it),
+            // column q (m >> last_alpha) + i + off
+            uint32_t pre = 0;
+            for (int l = 1; l < last_alpha; ++l) pre = pre * 3 + (uint32_t)dg[l - 1];
+            const uint32_t blk = (last_alpha == 1 ? 0u : k / 2) + pre * (k >> last_alpha);  // level 1: pair sums; 2: s_X
+            g.base = a.sc;
+            g.block_stride = per_block;
+            g.seg_stride = vec;
+            g.in_slots = prow0;
+            if (last_alpha == L) {
+                g.col_base = blk;  // plain columns
+            } else {
+                g.col_shift = rshift;
+                g.col_mask = r - 1;
+                g.col_chunk = m >> last_alpha;
+                g.col_base = blk + off;
+            }
+        }
         // a shape the kernels do not cover shows on the first sub-batch, before any parity byte
         // is written: NFEC_ENOTSUP then hands the batch to the one-product encode
         if ((rc = launch_tmvp2_prescale(a, s)))
-            return leave(rc == NFEC_ENOTSUP && b0 == 0 ? rc : fail(rc, "tmvp level-2 prescale"));
+            return leave(rc == NFEC_ENOTSUP && b0 == 0 ? rc : fail(rc, "tmvp multi-level prescale"));
         queued = true;
-        if ((rc = launch_gf16_tw_multi(e, 9, s)))
-            return leave(rc == NFEC_ENOTSUP && b0 == 0 ? rc : fail(rc, "tmvp level-2 products"));
-        if ((rc = launch_tmvp2_postscale(a, s))) return leave(fail(rc, "tmvp level-2 postscale"));
+        for (uint32_t e0 = 0; e0 < nprod; e0 += kTwMultiMax)
+            if ((rc = launch_gf16_tw_multi(e.data() + e0, std::min<uint32_t>(kTwMultiMax, nprod - e0), s)))
+                return leave(rc == NFEC_ENOTSUP && b0 == 0 && e0 == 0 ? rc : fail(rc, "tmvp multi-level products"));
+        if ((rc = launch_tmvp2_postscale(a, s))) return leave(fail(rc, "tmvp multi-level postscale"));
     }
     return leave(NFEC_OK);
 }

@@ -308,7 +308,7 @@ struct Rs16TmvpArgs {
 };
 bool rs16_tmvp_plan(uint32_t k, uint32_t m, const std::vector<uint32_t>& gen, std::vector<uint32_t> prod[3],
                     std::vector<uint16_t>& cmat, std::vector<uint16_t>& wmat, std::vector<uint16_t>& gmat);
-// levels 1 (prod[0..2], (m/2) x (k/2) each) or 2 (prod[0..8], (m/4) x (k/4) each; gf_host.cpp)
+// levels L = 1..3: prod[0 .. 3^L), (m >> L) x (k >> L) each (gf_host.cpp; the codec uses 1 or 2)
 bool rs16_tmvp_plan_levels(uint32_t k, uint32_t m, const std::vector<uint32_t>& gen, int levels,
                            std::vector<uint32_t>* prod, std::vector<uint16_t>& cmat, std::vector<uint16_t>& wmat,
                            std::vector<uint16_t>& gmat);

@@ -3,9 +3,10 @@ the oracle on the GPU, bit-exact, at one Karatsuba level (three (m/2)-row produc
 (nine (m/4)-row products).  NFEC_OPT_RS16_TOEPLITZ_ON forces the split, at the most levels the
 shape allows, where it is not chosen by default (NFEC_OPT_RS16_TOEPLITZ_OFF: never;
 NFEC_OPT_RS16_TOEPLITZ_ONE_LEVEL: one level at most); by default the codec takes the form with the
-lowest pass cost (gf16_tw_cost: each product's rows on the cheapest of the tower kernel's 7-, 6-
-and 4-row configurations, a pass costing 1.2, 1 and 0.73): one level for (128, 32), two for
-(256, 64), (512, 128) and C4."""
+lowest modelled cost (the products' passes on the cheapest of the tower kernel's 7-, 6- and 4-row
+configurations, plus the prescale's traffic and the postscale's multiplies, fitted to the split
+forced at each level, profiles/r05/tmvp_levels/): no split for (128, 32) and (256, 64), one level
+for (512, 128), two for C4."""
 
 import numpy as np
 import pytest
@@ -42,9 +43,9 @@ CASES = [
     (128, 32, 64, 64, 37, "1L1", 1),
     (128, 32, 1408, 1416, 3, "1", 2),     # padded segment stride
     # pass costs: 4 passes of 4 rows 292, 8 passes 584, 16 passes 1168, 6-row passes 100 each
-    (128, 32, 1400, 1400, 4, None, 1),    # one level by default (3 x 292 x 64 < 584 x 128 < 9 x 292 x 32)
-    (256, 64, 1400, 1400, 4, None, 2),    # two levels by default (9 x 292 x 64 < 3 x 584 x 128 < 1168 x 256)
-    (256, 64, 1400, 1400, 4, "L1", 1),    # at most one level: 3 x 584 x 128 < 1168 x 256
+    (128, 32, 1400, 1400, 4, None, 0),    # no split by default (measured 7.8 ms against 11.3 / 17.3 at one / two levels)
+    (256, 64, 1400, 1400, 4, None, 0),    # likewise (14.3 against 16.5 / 19.2 ms)
+    (256, 64, 1400, 1400, 4, "L1", 0),
     (256, 64, 1400, 1400, 4, "0", 0),
     (512, 128, 64, 64, 2, "1", 2),        # several passes per product
     (512, 128, 64, 64, 2, "1L1", 1),
@@ -54,7 +55,7 @@ CASES = [
     (96, 16, 72, 72, 5, "1", 2),          # three chunk pairs
     (1024, 64, 1400, 1400, 2, "1", 2),
     (2048, 128, 64, 64, 2, "1", 2),
-    (512, 128, 64, 64, 3, None, 2),       # two levels by default (9 x 584 x 128 < 3 x 1168 x 256 < 2336 x 512)
+    (512, 128, 64, 64, 3, None, 1),       # one level by default (26.1 ms against 27.9 / 27.0 at none / two)
     (96, 24, 1400, 1400, 3, "1", 0),      # m / 2 not a power of two: not allowed
     (100, 20, 1400, 1400, 3, "1", 0),     # k not a multiple of m
 ]

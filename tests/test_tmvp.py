@@ -182,3 +182,76 @@ def test_two_karatsuba_levels_reproduce_product(orc, gf, k, m):
             for s in range(2):
                 ref[p, s] ^= mul(int(G[p][j]), int(d[j, s]))
     assert np.array_equal(_level2(gf, k, m, d, G, w, c, t), ref)
+
+
+def _split_levels(gf, k, m, L, d, G, w, c, t):
+    """L Karatsuba levels of the Toeplitz split, as rs16_tmvp_plan_levels / the level-L kernels lay
+    them out (the general form of the two tests above).  A product is a path of L digits
+    (0 alpha, 1 beta, 2 gamma; product index sum d_l 3^(L-l)).  The root takes the Toeplitz part
+    T[p][q m + i] over the scaled source u_j = c_j d_j, chunk q of m columns; a node of width r
+    (its Toeplitz blocks r x r, input per chunk r values) splits into alpha = top-left block over
+    (input first half + second half), beta = top-right - top-left over the second half, gamma =
+    bottom-left - top-left over the first half, r/2 rows each.  Output row block b (L bits, level
+    1 the top bit) sums the products whose digits are alpha, or beta where b's bit is 0, or gamma
+    where it is 1; parity = W (sum) + G[p][0] d_0."""
+    _, _, _, mul = gf
+    r, nq, S = m >> L, k // m, d.shape[1]
+    u = [[mul(c[j], int(d[j, s])) for s in range(S)] for j in range(k)]
+
+    def inp(path, q, i, s):
+        if not path:
+            return u[q * m + i][s]
+        par, dg, half = path[:-1], path[-1], m >> len(path)
+        if dg == 0:
+            return inp(par, q, i, s) ^ inp(par, q, i + half, s)
+        return inp(par, q, i + half, s) if dg == 1 else inp(par, q, i, s)
+
+    def M(path, q, p, i):
+        if not path:
+            return t(p, q * m + i)
+        par, dg, half = path[:-1], path[-1], m >> len(path)
+        if dg == 0:
+            return M(par, q, p, i)
+        if dg == 1:
+            return M(par, q, p, i + half) ^ M(par, q, p, i)
+        return M(par, q, p + half, i) ^ M(par, q, p, i)
+
+    import itertools
+    paths = list(itertools.product(range(3), repeat=L))
+    P = {}
+    for path in paths:
+        acc = np.zeros((r, S), np.int64)
+        for q in range(nq):
+            for i in range(r):
+                x = [inp(path, q, i, s) for s in range(S)]
+                for p in range(r):
+                    co = M(path, q, p, i)
+                    for s in range(S):
+                        acc[p, s] ^= mul(co, x[s])
+        P[path] = acc
+    out = np.zeros((m, S), np.int64)
+    for b in range(1 << L):
+        R = np.zeros((r, S), np.int64)
+        for path in paths:
+            if all(dg == 0 or (dg == 1) == (((b >> (L - 1 - l)) & 1) == 0) for l, dg in enumerate(path)):
+                R ^= P[path]
+        for p in range(r):
+            row = b * r + p
+            for s in range(S):
+                out[row, s] = mul(w[row], int(R[p, s])) ^ mul(int(G[row][0]), int(d[0, s]))
+    return out
+
+
+@pytest.mark.parametrize("k,m,L", [(16, 8, 1), (16, 8, 2), (16, 8, 3), (32, 8, 3), (64, 16, 3), (32, 16, 2)])
+def test_karatsuba_levels_reproduce_product(orc, gf, k, m, L):
+    _, _, _, mul = gf
+    G = orc.generator(orc.RS16, k, m)[k:]
+    w, c, t = _factors(gf, k, m)
+    rng = np.random.default_rng(13 + L)
+    d = rng.integers(0, 65536, size=(k, 2))
+    ref = np.zeros((m, 2), np.int64)
+    for p in range(m):
+        for j in range(k):
+            for s in range(2):
+                ref[p, s] ^= mul(int(G[p][j]), int(d[j, s]))
+    assert np.array_equal(_split_levels(gf, k, m, L, d, G, w, c, t), ref)

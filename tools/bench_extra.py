@@ -39,6 +39,7 @@ def main():
     p.add_argument("--loss", default="source", choices=["source", "uniform"],
                    help="source: erasures among the source segments (the headline pattern); uniform: "
                         "drawn over all k + m segments, as NORM loses source and parity alike")
+    p.add_argument("--options", type=int, default=0, help="encoder options (NFEC_OPT_*, e.g. the Toeplitz split's levels)")
     a = p.parse_args()
     import torch
     import norm_amd as na
@@ -62,7 +63,7 @@ def main():
     dec_cls = {na.NFEC_RS8: na.NormDecoderRS8, na.NFEC_RS16: na.NormDecoderRS16, na.NFEC_MDP: na.NormDecoderMDP}[kind]
     torch.cuda.set_device(0)
     t0 = time.perf_counter()
-    enc = enc_cls()
+    enc = enc_cls(options=a.options) if a.options else enc_cls()
     assert enc.Init(k, m, vec)
     init_s = time.perf_counter() - t0
     dec = None
@@ -125,6 +126,10 @@ def main():
         "encode_ms": round(enc_ms, 3),
         "encode_GiBps": round(float(ndh.sum()) * vec / (enc_ms * 1e-3) / 2**30, 2),
     }
+    if kind == na.NFEC_RS16:
+        from norm_amd import _native as N
+        f = enc.features()
+        out["toeplitz_levels"] = (2 if f & N.NFEC_FEATURE_RS16_TOEPLITZ2 else 1 if f & N.NFEC_FEATURE_RS16_TOEPLITZ else 0)
     if kind == na.NFEC_RS16 and vec % 8 == 0 and not a.shortened:
         out["op_roofline"] = rs16_op_roofline(enc, k, m, nb, vec, enc_ms)
     if er:
@@ -177,8 +182,8 @@ def rs16_op_roofline(enc, k, m, nb, vec, enc_ms):
     out = {"kernel": name + form,
            "gf16_macs_per_s": float("%.4g" % (k * m * (vec // 2) * nb / (enc_ms * 1e-3))),
            "macs_note": "k*m*symbols of the generator product per second"
-                        + (" (the split computes 9/16 of them)" if two else " (the split computes 3/4 of them)" if split
-                           else "")}
+                        + (" (the split computes 9/16 of them)" if two
+                           else " (the split computes 3/4 of them)" if split else "")}
     src = None
     for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "r0*", "pmc_tw_*summary.json")), reverse=True):
         d = json.load(open(path))

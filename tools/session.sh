@@ -20,6 +20,7 @@
 #   rs8sweep   RS8 shape sweep (tools/bench_extra.py --workload rs8sweep) under a kernel trace
 #   c5         tools/bench_c5.py --steps 2 (the C5 mix's one-GPU share)
 #   percall    tools/percall per-call latencies (needs tools/percall/_build/percall)
+#   tmvp_levels RS16 encode with the Toeplitz split forced at 0..2 levels on four shapes
 #   ab         A/B of the product library against AB_LIBS (other builds of the same sources, e.g.
 #              tools/ab_build.sh with a generator option, loaded through NFEC_LIBRARY): the RS16 GPU
 #              tests on each (AB_K: a -k expression, e.g. to skip the split-level expectations of a
@@ -99,6 +100,18 @@ PY
         for args in "rs8 64 32 1408 16 2000" "rs8 64 16 1408 8 2000" "rs8 16 4 1408 4 2000" "rs16 400 100 1400 50 200" "mdp 64 32 1408 16 500"; do
             timeout -k 10 120 tools/percall/_build/percall $args >> "$O/percall.jsonl" || die percall $?
         done ;;
+    tmvp_levels)
+        # the Toeplitz split forced at 0 / 1 / 2 Karatsuba levels (NFEC_OPT_* 2 / 20 / 4) on
+        # shapes where the level choice is close, encode only; one JSON line each
+        : > "$O/tmvp_levels.jsonl"
+        for shape in "128 32 51200" "256 64 25600" "512 128 12800" "4096 256 4096"; do
+            set -- $shape
+            for opt in 2 20 4; do
+                timeout -k 10 300 python3 tools/bench_extra.py --workload rs16 --k $1 --m $2 --blocks $3 --erasures 0 \
+                    --options $opt >> "$O/tmvp_levels.jsonl" || die tmvp_levels $?
+            done
+        done
+        python3 -c "import json,sys; [print(d['k'], d['m'], d['toeplitz_levels'], d['encode_ms']) for d in map(json.loads, open(sys.argv[1]))]" "$O/tmvp_levels.jsonl" ;;
     ab)
         [ -n "$AB_LIBS" ] || die "ab (AB_LIBS unset)" 2
         for L in $AB_LIBS; do
