@@ -130,8 +130,10 @@ def sweep(rows, chain):
         for r in range(rows):
             for j in range(2):
                 op = "s_pack_lh_b32_b16" if j == 0 else "s_pack_hh_b32_b16"
-                L += [f"{op} s{S_TGT}, s{S_E + r}, s{S_SNIP}",
-                      f"s_mov_b32 m0, 0x{GPR_MODE | (16 * r + 8 * j):x}",
+                # movk: a 4-byte SOPK (M0's upper half gets the sign copies of bit 15)
+                mv = (f"s_movk_i32 m0, 0x{GPR_MODE | (16 * r + 8 * j):x}" if MODE == "movk"
+                      else f"s_mov_b32 m0, 0x{GPR_MODE | (16 * r + 8 * j):x}")
+                L += [f"{op} s{S_TGT}, s{S_E + r}, s{S_SNIP}", mv,
                       f"s_swappc_b64 s[{S_RET}:{S_RET + 1}], s[{S_TGT}:{S_TGT + 1}]"]
     L += ["s_set_gpr_idx_off", "s_nop 1"]
     return L
@@ -186,9 +188,9 @@ def main(path):
     entries = [(c0 << 7) | ((c1 << 7) << 16) for c0, c1 in coef]
     for rows in (7, 4):
         global IDX_MODE
-        for kind in ("plain", "chain", "empty", "noidx", "inline_idx", "inline_idx_once", "inline_reg",
-                     "inline_reg_mov", "inline_idxdst_once", "inline_idxsrc0_once"):
-            MODE = kind if kind in ("empty", "noidx") else ""
+        for kind in ("plain", "movk", "chain", "empty", "noidx", "inline_idx", "inline_idx_once", "inline_reg",
+                     "inline_reg_mov"):
+            MODE = kind if kind in ("empty", "noidx", "movk") else ""
             name = f"k_{kind}_r{rows}"
             IDX_MODE = {"inline_idxdst_once": "DST", "inline_idxsrc0_once": "SRC0"}.get(kind, "SRC0,DST")
             inline = kind[len("inline_"):] if kind.startswith("inline_") else None
