@@ -250,7 +250,7 @@ def fdec_asm(k, m, probe=None, e16=False):
                         S.extend([f"s_bfe_u32 s{S_T}, s{cur + sl // 2}, 0x{(16 << 16) | (16 * (sl % 2)):x}",
                                   f"s_add_u32 s{S_TAB + 2}, s{S_TAB}, s{S_T}",
                                   f"s_addc_u32 s{S_TAB + 3}, s{S_TAB + 1}, 0"])
-                    S.extend([f"s_mov_b32 m0, 0x{GPR_MODE | (16 * sl):x}",
+                    S.extend([f"s_movk_i32 m0, 0x{GPR_MODE | (16 * sl):x}",
                               f"s_swappc_b64 s[{S_RET}:{S_RET + 1}], s[{S_TAB + 2}:{S_TAB + 3}]"])
                 S.extend([f"Lsend{h}_{t}{x}_%=:", "s_set_gpr_idx_off"])
             S.append(f"Lrows{h}{x}_%=:")

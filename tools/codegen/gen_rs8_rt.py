@@ -165,7 +165,7 @@ def call(r, fast, ebuf):
         L = [f"s_bfe_u32 s{S_T1}, s{dw}, 0x{(16 << 16) | (16 * half):x}",
              f"s_add_u32 s{S_TGT}, s{S_SNIP}, s{S_T1}",
              f"s_addc_u32 s{S_TGT + 1}, s{S_SNIP + 1}, 0"]
-    return L + [f"s_mov_b32 m0, 0x{GPR_MODE | (16 * r):x}",
+    return L + [f"s_movk_i32 m0, 0x{GPR_MODE | (16 * r):x}",
                 f"s_swappc_b64 s[{S_RET}:{S_RET + 1}], s[{S_TGT}:{S_TGT + 1}]"]
 
 

@@ -182,7 +182,7 @@ def solve_asm():
                   f"s_lshl_b32 s{S_T}, s{S_T}, {SNIP_ALIGN}",
                   f"s_add_u32 s{S_TAB + 2}, s{S_TAB}, s{S_T}",
                   f"s_addc_u32 s{S_TAB + 3}, s{S_TAB + 1}, 0",
-                  f"s_mov_b32 m0, 0x{GPR_MODE | (16 * s):x}",
+                  f"s_movk_i32 m0, 0x{GPR_MODE | (16 * s):x}",
                   f"s_swappc_b64 s[{S_RET}:{S_RET + 1}], s[{S_TAB + 2}:{S_TAB + 3}]"]
         L += [f"Lsend{t}_%=:", "s_set_gpr_idx_off"]
     L.append("Lrows_%=:")
@@ -294,7 +294,7 @@ def mdp_solve_asm():
                   f"s_lshl_b32 s{S_T}, s{S_T}, {SNIP_ALIGN}",
                   f"s_add_u32 s{S_TAB + 2}, s{S_TAB}, s{S_T}",
                   f"s_addc_u32 s{S_TAB + 3}, s{S_TAB + 1}, 0",
-                  f"s_mov_b32 m0, 0x{GPR_MODE | (16 * s):x}",
+                  f"s_movk_i32 m0, 0x{GPR_MODE | (16 * s):x}",
                   f"s_swappc_b64 s[{S_RET}:{S_RET + 1}], s[{S_TAB + 2}:{S_TAB + 3}]"]
         L += [f"Lsend{t}_%=:", "s_set_gpr_idx_off"]
     L.append("Lrows_%=:")
