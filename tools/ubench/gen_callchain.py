@@ -91,11 +91,14 @@ def _explicit(b, off):
     return out
 
 
+ALIGN = 7   # snippet slot alignment (log2 bytes)
+
+
 def table(chain):
     out = [".p2align 16", "Lsnip0_%=:"]
     for c in range(257 if chain else 256):
         if c:
-            out.append(".p2align 7")
+            out.append(f".p2align {ALIGN}")
         if chain and c == 0:
             out.append(f"s_setpc_b64 s[{S_RET}:{S_RET + 1}]")   # slot 0: back to the caller
             continue
@@ -183,22 +186,23 @@ def main(path):
     rnd = random.Random(5)
     parts = ["#include <hip/hip_runtime.h>", "#include <cstdio>", "#include <vector>"]
     runs = []
-    global MODE
+    global MODE, ALIGN
     coef = [(rnd.randrange(1, 256), rnd.randrange(1, 256)) for _ in range(8)]
     entries = [(c0 << 7) | ((c1 << 7) << 16) for c0, c1 in coef]
     for rows in (7, 4):
         global IDX_MODE
-        for kind in ("plain", "movk", "chain", "empty", "noidx", "inline_idx", "inline_idx_once", "inline_reg",
-                     "inline_reg_mov"):
-            MODE = kind if kind in ("empty", "noidx", "movk") else ""
+        for kind in ("plain", "movk", "movk256", "chain", "empty", "noidx", "inline_idx", "inline_idx_once",
+                     "inline_reg", "inline_reg_mov"):
+            MODE = "movk" if kind == "movk256" else kind if kind in ("empty", "noidx", "movk") else ""
+            ALIGN = 8 if kind == "movk256" else 7
             name = f"k_{kind}_r{rows}"
             IDX_MODE = {"inline_idxdst_once": "DST", "inline_idxsrc0_once": "SRC0"}.get(kind, "SRC0,DST")
             inline = kind[len("inline_"):] if kind.startswith("inline_") else None
             inline = {"idxdst_once": "idx_once", "idxsrc0_once": "idx_once"}.get(inline, inline)
             waves, src = kernel(name, rows, kind == "chain", inline, coef)
             parts.append(src)
-            runs.append(f'    run("{name}", {name}, {rows}, {waves}, tab);')
-    MODE = ""
+            runs.append(f'    run("{name}", {name}, {rows}, {waves}, {"tab2" if kind == "movk256" else "tab"});')
+    MODE, ALIGN = "", 7
     ent = ", ".join(f"0x{e:08x}u" for e in entries)
     parts.append(r'''
 typedef void (*kfn)(unsigned*, const unsigned*, int);
@@ -234,6 +238,11 @@ int main()
     unsigned* tab;
     hipMalloc(&tab, 64);
     hipMemcpy(tab, h, 32, hipMemcpyHostToDevice);
+    unsigned h2[8];   // the same coefficients at 256-byte slots
+    for (int i = 0; i < 8; ++i) h2[i] = ((h[i] & 0xFFFFu) << 1) | (((h[i] >> 16) << 1) << 16);
+    unsigned* tab2;
+    hipMalloc(&tab2, 64);
+    hipMemcpy(tab2, h2, 32, hipMemcpyHostToDevice);
 ''' + "\n".join(runs) + r'''
     return 0;
 }
