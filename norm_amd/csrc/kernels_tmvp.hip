@@ -15,6 +15,9 @@
 // kernels are the elementwise steps around it: bit-sliced multiplies by wave-uniform constants.
 #include "nfec_internal.hpp"
 #include "gf16_bs.hpp"
+#include "bitslice.hpp"
+
+#include <algorithm>
 
 namespace nfec {
 namespace {
@@ -133,7 +136,63 @@ __device__ __forceinline__ uint32_t tmvp2_prow0(const Rs16TmvpArgs& a) { return 
 //   v at q cw + i = u_a0 + u_b0, at q cw + hw + i = u_a1 + u_b1   (the level-1 pair sums, halves)
 //   s_0 = both pair sums, s_1 = u_b0 + u_b1, s_2 = u_a0 + u_a1      (level 2's alpha inputs)
 // (the products are linear, so the sums are taken after transposing back to symbols)
-__global__ __launch_bounds__(256, 3) void tmvp2_prescale_kernel(Rs16TmvpArgs a)
+// buffer addressing for the level-2 prescale and postscale: descriptors over the wave's first block (of the
+// batch and of the scratch) and per item a 32-bit offset into each (0x80000000 outside the batch:
+// its loads read zeros, its stores drop, no branches).  With 64-bit addresses per item and
+// branches the postscale spilled (332 bytes per lane) and took 1.44 ms per 2,048 C4 blocks.
+struct ItemMapB {
+    uint32_t vs[8], vc[8];
+    __amdgpu_buffer_rsrc_t src, sc;
+};
+
+__device__ __forceinline__ void map_items_b(const Rs16TmvpArgs& a, uint32_t chunk, uint32_t lane, ItemMapB& m)
+{
+    const uint32_t ipb = a.vec / 8u, items = a.nblocks * ipb;
+    const uint32_t blk0 = __builtin_amdgcn_readfirstlane((chunk * 512u) / ipb);
+    m.src = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(a.base) + (uint64_t)blk0 * a.block_stride, (short)0,
+                                              (int)0x80000000u, 0x00020000);
+    m.sc = __builtin_amdgcn_make_buffer_rsrc(a.sc + (uint64_t)blk0 * a.sc_block_stride, (short)0, (int)0x80000000u,
+                                             0x00020000);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const uint32_t it = chunk * 512u + (uint32_t)j * 64u + lane;
+        const uint32_t b = it / ipb, off = (it - b * ipb) * 8u, db = b - blk0;
+        const bool ok = it < items;
+        m.vs[j] = ok ? db * (uint32_t)a.block_stride + off : 0x80000000u;
+        m.vc[j] = ok ? db * (uint32_t)a.sc_block_stride + off : 0x80000000u;
+    }
+}
+
+__device__ __forceinline__ void load16_b(uint32_t x[16], __amdgpu_buffer_rsrc_t rs, uint32_t soff, const uint32_t v[8])
+{
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const bs::u32x2 w = __builtin_amdgcn_raw_buffer_load_b64(rs, v[j], soff, 0);
+        x[2 * j] = w.x;
+        x[2 * j + 1] = w.y;
+    }
+}
+
+__device__ __forceinline__ void store16_b(const uint32_t x[16], __amdgpu_buffer_rsrc_t rs, uint32_t soff, const uint32_t v[8])
+{
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        bs::u32x2 w;
+        w.x = x[2 * j];
+        w.y = x[2 * j + 1];
+        __builtin_amdgcn_raw_buffer_store_b64(w, rs, v[j], soff, 0);
+    }
+}
+
+// the postscale's offsets fit 32 bits: a wave's 512 items span at most 512 / ipb + 2 blocks
+static bool tmvp2_offsets_fit(const Rs16TmvpArgs& a)
+{
+    const uint64_t ipb = a.vec / 8u, nb = 512u / std::max<uint64_t>(ipb, 1) + 2u;
+    const uint64_t slots = (uint64_t)a.k + 2u * a.cw;
+    return nb * a.block_stride + slots * a.seg_stride < (1ull << 31) && (nb + 1) * a.sc_block_stride < (1ull << 31);
+}
+
+__global__ __launch_bounds__(256, 4) void tmvp2_prescale_kernel(Rs16TmvpArgs a)
 {
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t wid = __builtin_amdgcn_readfirstlane(blockIdx.x * 4u + (threadIdx.x >> 6));
@@ -144,39 +203,45 @@ __global__ __launch_bounds__(256, 3) void tmvp2_prescale_kernel(Rs16TmvpArgs a)
     const uint32_t q = u / a.hw, i = u - q * a.hw;
     const uint32_t a0 = 2u * q * a.cw + i;
     const uint32_t col[4] = {a0, a0 + a.hw, a0 + a.cw, a0 + a.cw + a.hw};  // a0, a1, b0, b1
-    ItemMap m;
-    map_items(chunk, lane, items, ipb, m);
+    ItemMapB m;
+    map_items_b(a, chunk, lane, m);
+    // all four columns' loads in flight first, then each scaled in place
     uint32_t r[4][16];
 #pragma unroll
+    for (int t = 0; t < 4; ++t) load16_b(r[t], m.src, col[t] * a.seg_stride, m.vs);
+#pragma unroll
     for (int t = 0; t < 4; ++t) {
-        uint32_t x[16];
-        load16(x, a.base + (uint64_t)col[t] * a.seg_stride, a.block_stride, m);
-        bs16::transpose(x);
-#pragma unroll
-        for (int p = 0; p < 16; ++p) r[t][p] = 0;
-        bs16::mulc_acc(x, r[t], a.cmat + 16u * col[t]);
+        uint32_t o[16];
         bs16::transpose(r[t]);
+#pragma unroll
+        for (int p = 0; p < 16; ++p) o[p] = 0;
+        bs16::mulc_acc(r[t], o, a.cmat + 16u * col[t]);
+        bs16::transpose(o);
+#pragma unroll
+        for (int p = 0; p < 16; ++p) r[t][p] = o[p];
     }
-    uint32_t v0[16], v1[16], o[16];
+    uint32_t o[16];
 #pragma unroll
-    for (int p = 0; p < 16; ++p) v0[p] = r[0][p] ^ r[2][p], v1[p] = r[1][p] ^ r[3][p];
-    uint8_t* sc = a.sc;
-    store16(v0, sc + (uint64_t)(q * a.cw + i) * a.vec, a.sc_block_stride, m);
-    store16(v1, sc + (uint64_t)(q * a.cw + a.hw + i) * a.vec, a.sc_block_stride, m);
+    for (int p = 0; p < 16; ++p) o[p] = r[0][p] ^ r[2][p];
+    store16_b(o, m.sc, (q * a.cw + i) * a.vec, m.vc);
 #pragma unroll
-    for (int p = 0; p < 16; ++p) o[p] = v0[p] ^ v1[p];
-    store16(o, sc + (uint64_t)(a.k / 2u + u) * a.vec, a.sc_block_stride, m);
+    for (int p = 0; p < 16; ++p) o[p] = r[1][p] ^ r[3][p];
+    store16_b(o, m.sc, (q * a.cw + a.hw + i) * a.vec, m.vc);
+#pragma unroll
+    for (int p = 0; p < 16; ++p) o[p] = r[0][p] ^ r[1][p] ^ r[2][p] ^ r[3][p];
+    store16_b(o, m.sc, (a.k / 2u + u) * a.vec, m.vc);
 #pragma unroll
     for (int p = 0; p < 16; ++p) o[p] = r[2][p] ^ r[3][p];
-    store16(o, sc + (uint64_t)(a.k / 2u + quarter + u) * a.vec, a.sc_block_stride, m);
+    store16_b(o, m.sc, (a.k / 2u + quarter + u) * a.vec, m.vc);
 #pragma unroll
     for (int p = 0; p < 16; ++p) o[p] = r[0][p] ^ r[1][p];
-    store16(o, sc + (uint64_t)(a.k / 2u + 2u * quarter + u) * a.vec, a.sc_block_stride, m);
+    store16_b(o, m.sc, (a.k / 2u + 2u * quarter + u) * a.vec, m.vc);
 }
 
 // per p < hw: level-1 product X's rows p (top) and hw + p (bottom) are P_aX + P_bX and
 // P_aX + P_gX (products e = 3X, 3X + 1, 3X + 2); parity rows p and hw + p (R0) take X = 0, 1,
-// rows cw + p and cw + hw + p (R1) take X = 0, 2, then W(y_r) and G[r][0] d_0 as at one level
+// rows cw + p and cw + hw + p (R1) take X = 0, 2, then W(y_r) and G[r][0] d_0 as at one level.
+// The wave forms the four outputs one at a time (each the sum of four products).
 __global__ __launch_bounds__(256, 3) void tmvp2_postscale_kernel(Rs16TmvpArgs a)
 {
     const uint32_t lane = threadIdx.x & 63;
@@ -184,39 +249,34 @@ __global__ __launch_bounds__(256, 3) void tmvp2_postscale_kernel(Rs16TmvpArgs a)
     const uint32_t p = wid % a.hw, chunk = wid / a.hw;
     const uint32_t ipb = a.vec / 8u, items = a.nblocks * ipb;
     if (chunk * 512u >= items) return;
-    ItemMap m;
-    map_items(chunk, lane, items, ipb, m);
-    const uint8_t* pr = a.sc + (uint64_t)(tmvp2_prow0(a) + p) * a.vec;  // product e at + e * hw * vec
-    // sums over (R0 top, R0 bottom, R1 top, R1 bottom) of the nine products (e = 3X + {a, b, g})
+    ItemMapB m;
+    map_items_b(a, chunk, lane, m);
+    const uint32_t pr = (tmvp2_prow0(a) + p) * a.vec;  // product e's row p at pr + e hw vec
+    // output rows (R0 top, R0 bottom, R1 top, R1 bottom): bit t of uses[e] = product e feeds output t
     constexpr uint8_t uses[9] = {0xF, 0x5, 0xA, 0x3, 0x1, 0x2, 0xC, 0x4, 0x8};
-    uint32_t sum[4][16], x[16];
-#pragma unroll
-    for (int t = 0; t < 4; ++t)
-#pragma unroll
-        for (int j = 0; j < 16; ++j) sum[t][j] = 0;
-#pragma unroll
-    for (int e = 0; e < 9; ++e) {
-        load16(x, pr + (uint64_t)e * a.hw * a.vec, a.sc_block_stride, m);
-#pragma unroll
-        for (int t = 0; t < 4; ++t)
-            if (uses[e] & (1u << t))
-#pragma unroll
-                for (int j = 0; j < 16; ++j) sum[t][j] ^= x[j];
-    }
-    uint32_t d0[16];
-    load16(d0, a.base, a.block_stride, m);
-    bs16::transpose(d0);
-    const uint32_t rows[4] = {p, a.hw + p, a.cw + p, a.cw + a.hw + p};
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
-        bs16::transpose(sum[t]);
+        uint32_t sum[16], x[16];
+#pragma unroll
+        for (int j = 0; j < 16; ++j) sum[j] = 0;
+#pragma unroll
+        for (int e = 0; e < 9; ++e) {
+            if (!(uses[e] & (1u << t))) continue;
+            load16_b(x, m.sc, pr + (uint32_t)e * a.hw * a.vec, m.vc);
+#pragma unroll
+            for (int j = 0; j < 16; ++j) sum[j] ^= x[j];
+        }
+        const uint32_t row = (uint32_t)(t >> 1) * a.cw + (uint32_t)(t & 1) * a.hw + p;
+        bs16::transpose(sum);
         uint32_t o[16];
 #pragma unroll
         for (int j = 0; j < 16; ++j) o[j] = 0;
-        bs16::mulc_acc(sum[t], o, a.wmat + 16u * rows[t]);
-        bs16::mulc_acc(d0, o, a.gmat + 16u * rows[t]);
+        bs16::mulc_acc(sum, o, a.wmat + 16u * row);
+        load16_b(x, m.src, 0u, m.vs);
+        bs16::transpose(x);
+        bs16::mulc_acc(x, o, a.gmat + 16u * row);
         bs16::transpose(o);
-        store16(o, const_cast<uint8_t*>(a.base) + (uint64_t)(a.k + rows[t]) * a.seg_stride, a.block_stride, m);
+        store16_b(o, m.src, (a.k + row) * a.seg_stride, m.vs);
     }
 }
 
@@ -226,7 +286,8 @@ int launch_tmvp2_prescale(const Rs16TmvpArgs& a, hipStream_t s)
 {
     const uint64_t items = (uint64_t)a.nblocks * (a.vec / 8u);
     const uint64_t waves = (items + 511) / 512 * (a.k / 4);
-    if (!a.hw || !a.sc || items >= (1ull << 32) || waves >= (1ull << 32)) return NFEC_ENOTSUP;
+    // (the postscale's 32-bit offsets: checked here too, before anything is written)
+    if (!a.hw || !a.sc || items >= (1ull << 32) || waves >= (1ull << 32) || !tmvp2_offsets_fit(a)) return NFEC_ENOTSUP;
     if (waves == 0) return NFEC_OK;
     hipLaunchKernelGGL(tmvp2_prescale_kernel, dim3((uint32_t)((waves + 3) / 4)), dim3(256), 0, s, a);
     const hipError_t e = hipGetLastError();
@@ -237,7 +298,7 @@ int launch_tmvp2_postscale(const Rs16TmvpArgs& a, hipStream_t s)
 {
     const uint64_t items = (uint64_t)a.nblocks * (a.vec / 8u);
     const uint64_t waves = (items + 511) / 512 * a.hw;
-    if (!a.hw || !a.sc || items >= (1ull << 32) || waves >= (1ull << 32)) return NFEC_ENOTSUP;
+    if (!a.hw || !a.sc || items >= (1ull << 32) || waves >= (1ull << 32) || !tmvp2_offsets_fit(a)) return NFEC_ENOTSUP;
     if (waves == 0) return NFEC_OK;
     hipLaunchKernelGGL(tmvp2_postscale_kernel, dim3((uint32_t)((waves + 3) / 4)), dim3(256), 0, s, a);
     const hipError_t e = hipGetLastError();

@@ -524,16 +524,15 @@ int build_codec(nfec_codec* c)
                                             : (c->opts & NFEC_OPT_RS16_TOEPLITZ_ON) ? 1
                                                                                     : -1,
                                             -1, 1);
-            const uint32_t cw = c->m / 2;
             const uint32_t rpp = kGf16T3RowsPerPass;
             // cost of each form per block, in the products' units (about one column step per
             // pass, weighted on the tower kernel by the cost of a pass of the configuration a
             // launch of that many rows takes, gf16_tw_cost): the products (3^L of m >> L rows
             // over k >> L columns, plus ~20 columns' worth of fixed work per pass), the prescale
             // (~165 per column it moves: it is HBM-bound) and the postscale (per parity row ~460
-            // at one level, ~1,490 at two: its constant multiplies).  Fitted to the split forced
+            // at one level, ~700 at two: its constant multiplies).  Fitted to the split forced
             // at 0 / 1 / 2 levels on (128, 32), (256, 64), (512, 128) and C4
-            // (profiles/r05/tmvp_levels/: fastest at 0, 0, 1 and 2 levels).  A third level
+            // (profiles/r05/tmvp_levels/: fastest at 0, 0, 2 and 2 levels).  A third level
             // measured slower: its prescale moves 3.4 k columns per block against 2.25 k.
             const int max_levels = (!c->tw || (c->opts & NFEC_OPT_RS16_TOEPLITZ_ONE_LEVEL)) ? 1 : 2;
             uint64_t cost[3];
@@ -550,7 +549,7 @@ int build_codec(nfec_codec* c)
                 // (the shared-table kernel keeps the round-2 rule: passes alone)
                 cost[L] = prod_cost + (!c->tw ? 0ull
                                        : L == 1 ? 165ull * (c->k + c->k / 2) + 460ull * c->m
-                                       : L == 2 ? 165ull * (c->k + c->k / 2 + 3ull * (c->k / 4)) + 1490ull * c->m
+                                       : L == 2 ? 165ull * (c->k + c->k / 2 + 3ull * (c->k / 4)) + 700ull * c->m
                                                 : 0ull);
             }
             int levels = 0;
@@ -3178,7 +3177,6 @@ static int run_host_vectors(nfec_codec* c, void* const* vecs, uint32_t nblocks, 
         uint64_t dl = 0;  // decode: download length of the chunk's single piece
         bool busy = false;
     } jobs[kHostSlots];
-    const uint64_t blk_bytes = (uint64_t)n * c->vec;
     auto gather = [&](HostSlot& s, const Job& j) {
         // encode without accumulate reads the source only; everything else reads the whole
         // listed block (absent parity is zero, as MDP's decoder treats it)

@@ -5,8 +5,8 @@ shape allows, where it is not chosen by default (NFEC_OPT_RS16_TOEPLITZ_OFF: nev
 NFEC_OPT_RS16_TOEPLITZ_ONE_LEVEL: one level at most); by default the codec takes the form with the
 lowest modelled cost (the products' passes on the cheapest of the tower kernel's 7-, 6- and 4-row
 configurations, plus the prescale's traffic and the postscale's multiplies, fitted to the split
-forced at each level, profiles/r05/tmvp_levels/): no split for (128, 32) and (256, 64), one level
-for (512, 128), two for C4."""
+forced at each level, profiles/r05/tmvp_levels/): no split for (128, 32) and (256, 64), two levels
+for (512, 128) and C4."""
 
 import numpy as np
 import pytest
@@ -43,8 +43,8 @@ CASES = [
     (128, 32, 64, 64, 37, "1L1", 1),
     (128, 32, 1408, 1416, 3, "1", 2),     # padded segment stride
     # pass costs: 4 passes of 4 rows 292, 8 passes 584, 16 passes 1168, 6-row passes 100 each
-    (128, 32, 1400, 1400, 4, None, 0),    # no split by default (measured 7.8 ms against 11.3 / 17.3 at one / two levels)
-    (256, 64, 1400, 1400, 4, None, 0),    # likewise (14.3 against 16.5 / 19.2 ms)
+    (128, 32, 1400, 1400, 4, None, 0),    # no split by default (measured 7.8 ms against 11.4 / 14.1 at one / two levels)
+    (256, 64, 1400, 1400, 4, None, 0),    # likewise (14.2 against 16.4 / 15.9 ms)
     (256, 64, 1400, 1400, 4, "L1", 0),
     (256, 64, 1400, 1400, 4, "0", 0),
     (512, 128, 64, 64, 2, "1", 2),        # several passes per product
@@ -55,7 +55,8 @@ CASES = [
     (96, 16, 72, 72, 5, "1", 2),          # three chunk pairs
     (1024, 64, 1400, 1400, 2, "1", 2),
     (2048, 128, 64, 64, 2, "1", 2),
-    (512, 128, 64, 64, 3, None, 1),       # one level by default (26.1 ms against 27.9 / 27.0 at none / two)
+    (512, 128, 64, 64, 3, None, 2),       # two levels by default (23.5 ms against 27.6 / 26.0 at none / one)
+    (512, 128, 64, 64, 3, "L1", 1),
     (96, 24, 1400, 1400, 3, "1", 0),      # m / 2 not a power of two: not allowed
     (100, 20, 1400, 1400, 3, "1", 0),     # k not a multiple of m
 ]
