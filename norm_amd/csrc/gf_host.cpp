@@ -217,7 +217,8 @@ static void gf16_bitmatrix(const Field& f, uint32_t c, uint16_t* M)
 //   prod[2] = (C-A) c = (T[p+cw][a] + T[p][a]) c_a      (c_0 = 0)
 // and the row masks of c_j, W(y_p) and G[p][0].  Every G[p][j] is re-derived from the factors
 // and compared with the generator; false (and nothing used) on any mismatch or shape the split
-// does not cover (m even, m/2 a power of two, k a multiple of m).
+// does not cover (m even, k a multiple of m; the caller adds that the shared-table kernel's
+// column map needs m/2 a power of two, the tower kernel's takes any width).
 bool rs16_tmvp_plan(uint32_t k, uint32_t m, const std::vector<uint32_t>& gen, std::vector<uint32_t> prod[3],
                     std::vector<uint16_t>& cmat, std::vector<uint16_t>& wmat, std::vector<uint16_t>& gmat)
 {
@@ -239,9 +240,8 @@ bool rs16_tmvp_plan_levels(uint32_t k, uint32_t m, const std::vector<uint32_t>& 
                            std::vector<uint32_t>* prod, std::vector<uint16_t>& cmat, std::vector<uint16_t>& wmat,
                            std::vector<uint16_t>& gmat)
 {
-    const uint32_t cw = m / 2;
-    if (m < 2 || (m & 1u) || (cw & (cw - 1u)) || k % m || gen.size() != (size_t)m * k) return false;
-    if (levels < 1 || levels > 3 || (m >> levels) == 0) return false;
+    if (m < 2 || (m & 1u) || k % m || gen.size() != (size_t)m * k) return false;
+    if (levels < 1 || levels > 3 || (m >> levels) == 0 || m % (1u << levels)) return false;
     const Field& f = gf16();
     const uint32_t q = f.q;
     std::vector<uint32_t> x(k);

@@ -541,6 +541,8 @@ int build_codec(nfec_codec* c)
                 cost[L] = ~0ull;
                 const uint32_t r = c->m >> L;
                 if (L > max_levels || r == 0 || (L && (c->m % (1u << L)))) continue;
+                // (the shared-table kernel's column map needs chunks of a power of two)
+                if (L && !c->tw && ((c->m / 2) & (c->m / 2 - 1))) continue;
                 top = L;
                 uint64_t np = 1;
                 for (int i = 0; i < L; ++i) np *= 3;
@@ -711,8 +713,6 @@ static int rs16_tmvp2_encode(nfec_codec* c, const nfec_block_batch* b, hipStream
         return code;
     };
     const size_t one_tw = gf16_tw_table_elems(cols, r);
-    uint32_t rshift = 0;
-    while ((1u << rshift) < r) ++rshift;
     int rc;
     for (uint32_t b0 = 0; b0 < b->nblocks; b0 += sb) {
         const uint32_t nb = std::min(sb, b->nblocks - b0);
@@ -755,8 +755,7 @@ static int rs16_tmvp2_encode(nfec_codec* c, const nfec_block_batch* b, hipStream
                 g.base = blocks;
                 g.block_stride = b->block_stride;
                 g.seg_stride = b->seg_stride;
-                g.col_shift = rshift;
-                g.col_mask = r - 1;
+                g.col_div = r;
                 g.col_chunk = m;
                 g.col_base = off;
                 g.in_slots = k + m;
@@ -774,8 +773,7 @@ static int rs16_tmvp2_encode(nfec_codec* c, const nfec_block_batch* b, hipStream
             if (last_alpha == L) {
                 g.col_base = blk;  // plain columns
             } else {
-                g.col_shift = rshift;
-                g.col_mask = r - 1;
+                g.col_div = r;
                 g.col_chunk = m >> last_alpha;
                 g.col_base = blk + off;
             }
@@ -873,6 +871,7 @@ int rs16_tmvp_encode(nfec_codec* c, const nfec_block_batch* b, hipStream_t s)
         // P1 over the second column of every pair -> x rows
         e[1].col_shift = shift;
         e[1].col_mask = cw - 1;
+        e[1].col_div = c->tw ? cw : 0;  // (any chunk width on the tower kernel)
         e[1].col_chunk = 2 * cw;
         e[1].col_base = cw;
         e[1].in_slots = k + m;
@@ -883,6 +882,7 @@ int rs16_tmvp_encode(nfec_codec* c, const nfec_block_batch* b, hipStream_t s)
         // P2 over the first column of every pair -> parity rows [k + cw, k + m)
         e[2].col_shift = shift;
         e[2].col_mask = cw - 1;
+        e[2].col_div = c->tw ? cw : 0;
         e[2].col_chunk = 2 * cw;
         e[2].col_base = 0;
         e[2].in_slots = k + m;

@@ -254,8 +254,11 @@ struct Gf16T3Args {
     uint32_t out_after_data = 0, acc_after_data = 0;
     const uint32_t* rows_lim = nullptr;  // device word: rows needed (<= m), null: m
     // column map: column c is read from slot ((c >> col_shift) * col_chunk + (c & col_mask) +
-    // col_base) (identity by default); in_slots bounds the slots read (0: k + m)
+    // col_base) (identity by default); in_slots bounds the slots read (0: k + m).  The tower
+    // kernel also takes any chunk width: col_div != 0 reads slot (c / col_div) * col_chunk +
+    // c % col_div + col_base (col_magic: set by its launcher)
     uint32_t col_shift = 31, col_mask = 0xFFFFFFFFu, col_chunk = 0, col_base = 0, in_slots = 0;
+    uint32_t col_div = 0, col_magic = 0;
     const uint16_t* tw = nullptr;   // [k][2][m][2] snippet offsets (gf16_tw_offsets)
     // per-block mode (RS16 decode stage 2 on the tower kernel): item groups stay inside one
     // block; block b has its own table (tw + b * tw_block_stride), e = blk_rows[b] rows,

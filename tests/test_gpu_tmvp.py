@@ -6,7 +6,8 @@ NFEC_OPT_RS16_TOEPLITZ_ONE_LEVEL: one level at most); by default the codec takes
 lowest modelled cost (the products' passes on the cheapest of the tower kernel's 7-, 6- and 4-row
 configurations, plus the prescale's traffic and the postscale's multiplies, fitted to the split
 forced at each level, profiles/r05/tmvp_levels/): no split for (128, 32) and (256, 64), two levels
-for (512, 128) and C4."""
+for (512, 128), RS16(400, 100) and C4.  Chunk widths need not be powers of two on the tower kernel
+(its column map divides by a multiply-high)."""
 
 import numpy as np
 import pytest
@@ -57,8 +58,15 @@ CASES = [
     (2048, 128, 64, 64, 2, "1", 2),
     (512, 128, 64, 64, 3, None, 2),       # two levels by default (23.5 ms against 27.6 / 26.0 at none / one)
     (512, 128, 64, 64, 3, "L1", 1),
-    (96, 24, 1400, 1400, 3, "1", 0),      # m / 2 not a power of two: not allowed
-    (100, 20, 1400, 1400, 3, "1", 0),     # k not a multiple of m
+    (96, 24, 1400, 1400, 3, "1", 2),      # chunks of 12 and 6 columns (the column map's division)
+    (96, 24, 1400, 1400, 3, "1L1", 1),
+    (40, 10, 72, 72, 6, "1", 1),          # m / 4 not whole: one level at most, chunks of 5
+    (48, 12, 64, 64, 5, "1", 2),          # level-2 chunks of 3 columns
+    (400, 100, 1400, 1400, 3, None, 2),   # RS16(400, 100): two levels by default (chunks of 50 and 25)
+    (400, 100, 1400, 1400, 3, "L1", 1),
+    (400, 100, 1400, 1400, 3, "0", 0),
+    (100, 20, 1400, 1400, 3, "1", 2),     # level-2 chunks of 5 columns
+    (100, 24, 1400, 1400, 3, "1", 0),     # k not a multiple of m: not allowed
 ]
 
 

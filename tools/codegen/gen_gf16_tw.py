@@ -467,11 +467,14 @@ SPECIAL_ROWS = (6, 5, 4, 3, 2, 1)   # pass row counts with their own (unchecked)
 
 
 def col_offset():
-    """column index s[S_C] -> byte offset s[S_COL] through the column map
-    ((c >> csh) * cck + (c & cmk) * ss + cbb; identity: csh 31, cck 0, cmk ~0, cbb 0)"""
-    return [f"s_lshr_b32 s{S_T2}, s{S_C}, %[csh]", f"s_mul_i32 s{S_T2}, s{S_T2}, %[cck]",
-            f"s_and_b32 s{S_COL}, s{S_C}, %[cmk]", f"s_mul_i32 s{S_COL}, s{S_COL}, %[ss]",
-            f"s_add_u32 s{S_COL}, s{S_COL}, s{S_T2}", f"s_add_u32 s{S_COL}, s{S_COL}, %[cbb]"]
+    """column index s[S_C] -> byte offset s[S_COL] through the column map: q = c / d by the
+    multiply-high with cmg = ceil(2^32 / d) (exact for c, d < 2^16), then
+    q * cck + (c - q d) * crs + cbb.  Identity: cmg 0 (q = 0), crs = ss, cck = cbb = 0; d = 1:
+    cmg 0 with crs = the chunk stride (set up by the wrapper, chunk_map)"""
+    return [f"s_mul_hi_u32 s{S_T2}, s{S_C}, %[cmg]", f"s_mul_i32 s{S_COL}, s{S_T2}, %[cdv]",
+            f"s_sub_u32 s{S_COL}, s{S_C}, s{S_COL}", f"s_mul_i32 s{S_COL}, s{S_COL}, %[crs]",
+            f"s_mul_i32 s{S_T2}, s{S_T2}, %[cck]", f"s_add_u32 s{S_COL}, s{S_COL}, s{S_T2}",
+            f"s_add_u32 s{S_COL}, s{S_COL}, %[cbb]"]
 
 
 _uid = [0]
@@ -715,7 +718,7 @@ def asm_block(cond, text, last_s):
 
 
 ASM_INPUTS = """[wb] "s"(wb), [ss] "s"(a.seg_stride), [k] "s"(kk), [tw] "s"(tw), [tstep] "s"(tstep), [t1off] "s"(t1off), [nr] "s"(nr),
-              [csh] "s"(a.col_shift), [cmk] "s"(a.col_mask), [cck] "s"(cck), [cbb] "s"(cbb),
+              [cmg] "s"(cm.magic), [cdv] "s"(cm.div), [crs] "s"(cm.rem_stride), [cck] "s"(cck), [cbb] "s"(cbb),
               [acc] "s"(a.accumulate), [ob] "s"(ob), [ab] "s"(ab), [oslot] "s"(a.out_slot0 + row0),
               [oss] "s"(a.out_seg_stride), [aslot] "s"(a.acc_slot0 + row0), [ass] "s"(a.acc_seg_stride),
               [wv] "s"(wave), [rp] "s"(rp), [md] "s"(md), [lo] "v"(lo), [xl] "v"(xl), [lq] "v"(lq)"""
@@ -818,6 +821,17 @@ constexpr uint32_t kTwRows[] = {{{cfg_rows}}};
 constexpr uint32_t kTwPassCost[] = {{{cfg_cost}}};
 constexpr uint32_t kTwConfigs = {len(CONFIGS)};
 
+// the column map's scalars (col_offset): the multiply-high constant, the divisor and the stride of
+// the remainder (the segment stride; the chunk stride when the divisor is 1, cmg then 0)
+struct ChunkMap {{
+    uint32_t magic, div, rem_stride;
+}};
+
+__device__ __forceinline__ ChunkMap chunk_map(const Gf16T3Args& a, uint32_t cck)
+{{
+    return {{a.col_magic, a.col_div ? a.col_div : 1u, a.col_div == 1u ? cck : a.seg_stride}};
+}}
+
 template <int R>
 __device__ __forceinline__ uint32_t gf16_tw_passes_dev(uint32_t m)
 {{
@@ -916,6 +930,7 @@ __device__ __forceinline__ void tw_body(const Gf16T3Args& a, uint32_t wg)
     const uint8_t* ob = a.out_base + (uint64_t)b0 * a.out_block_stride;
     const uint8_t* ab = a.acc_base + (uint64_t)b0 * a.acc_block_stride;
     const uint32_t cck = a.col_chunk * a.seg_stride, cbb = a.col_base * a.seg_stride;
+    const ChunkMap cm = chunk_map(a, cck);
 {asm_blocks}
 }}
 
@@ -930,6 +945,14 @@ int tw_prepare(const Gf16T3Args& a, Gf16T3Args& b, uint64_t& wgs, uint32_t rows)
     if ((a.vec_bytes & 7u) || a.vec_bytes == 0 || !a.tw || a.k == 0 || (a.num_data && (a.blk_rows || a.col_chunk)))
         return NFEC_ENOTSUP;
     b = a;
+    // the column map: chunks of col_div columns (or 2^col_shift), q = c / d by a multiply-high
+    // with ceil(2^32 / d), exact for c, d < 2^16
+    if (!b.col_div && a.col_shift < 31) {{
+        if (a.col_mask != (1u << a.col_shift) - 1u) return NFEC_ENOTSUP;
+        b.col_div = 1u << a.col_shift;
+    }}
+    if (b.col_div && (b.col_div >= 65536u || a.k >= 65536u)) return NFEC_ENOTSUP;
+    b.col_magic = b.col_div >= 2u ? (uint32_t)((0xFFFFFFFFull + b.col_div) / b.col_div) : 0u;
     if (!b.out_base) {{  // encode: parity in place, slot k + r (numData + r when shortened); accumulate against it
         b.out_base = const_cast<uint8_t*>(a.base);
         b.out_block_stride = a.block_stride;
