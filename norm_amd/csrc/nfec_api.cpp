@@ -518,7 +518,9 @@ int build_codec(nfec_codec* c)
         // shape allows it, at the most levels allowed (tests), neither when it pays;
         // NFEC_OPT_RS16_TOEPLITZ_ONE_LEVEL caps it at one level (NFEC_RS16_TMVP=0/1/-1 overrides,
         // diagnostic library)
-        if (wide && use_gf16_t3() && (c->vec % 8) == 0) {
+        // (a vector size not a multiple of 8: the split over its 8-byte pieces, the tail kernel
+        // over the last 2-6 bytes with the whole generator; tower kernel only)
+        if (wide && use_gf16_t3() && ((c->vec % 8) == 0 || (c->tw && c->vec >= 8))) {
             const int mode = (int)diag_knob("NFEC_RS16_TMVP",
                                             (c->opts & NFEC_OPT_RS16_TOEPLITZ_OFF)  ? 0
                                             : (c->opts & NFEC_OPT_RS16_TOEPLITZ_ON) ? 1
@@ -686,7 +688,7 @@ static bool use_asm()
 static int rs16_tmvp2_encode(nfec_codec* c, const nfec_block_batch* b, hipStream_t s)
 {
     const int L = c->tmvp_levels;
-    const uint32_t k = c->k, m = c->m, r = m >> L, cols = k >> L, vec = c->vec;
+    const uint32_t k = c->k, m = c->m, r = m >> L, cols = k >> L, vec = c->vec & ~7u;
     uint32_t nprod = 1;
     for (int i = 0; i < L; ++i) nprod *= 3;
     const uint32_t prow0 = k / 2 + 3 * (k / 4);                 // first product row in the scratch
@@ -791,10 +793,32 @@ static int rs16_tmvp2_encode(nfec_codec* c, const nfec_block_batch* b, hipStream
     return leave(NFEC_OK);
 }
 
+static int rs16_tmvp1_encode(nfec_codec* c, const nfec_block_batch* b, hipStream_t s);
+
+// the split over the vector's 8-byte pieces, then (vec % 8 != 0) its last 2-6 bytes on the tail
+// kernel with the whole generator: the product is the same at every byte position, so the split
+// and the tail write disjoint bytes of the same parity
 int rs16_tmvp_encode(nfec_codec* c, const nfec_block_batch* b, hipStream_t s)
 {
-    if (c->tmvp_levels == 2) return rs16_tmvp2_encode(c, b, s);
-    const uint32_t k = c->k, m = c->m, cw = m / 2, half = k / 2, vec = c->vec;
+    const int rc = c->tmvp_levels == 2 ? rs16_tmvp2_encode(c, b, s) : rs16_tmvp1_encode(c, b, s);
+    const uint32_t even = c->vec & ~1u, body = even & ~7u;
+    if (rc || even == body) return rc;
+    Gf16T3Args t;
+    t.base = static_cast<const uint8_t*>(b->blocks);
+    t.block_stride = b->block_stride;
+    t.seg_stride = b->seg_stride;
+    t.nblocks = b->nblocks;
+    t.k = c->k;
+    t.m = c->m;
+    t.vec_bytes = even;
+    t.tw = c->d_twoff.p;
+    const int tr = launch_gf16_tw_tail(t, body, even - body, s);
+    return tr ? fail(tr, "tmvp vector tail") : NFEC_OK;
+}
+
+static int rs16_tmvp1_encode(nfec_codec* c, const nfec_block_batch* b, hipStream_t s)
+{
+    const uint32_t k = c->k, m = c->m, cw = m / 2, half = k / 2, vec = c->vec & ~7u;
     // sub-batches of at most 16 GiB of scratch (C4's 4,096 blocks: one, 12.5 GB) and at most
     // half of the device memory free now (plus the scratch this codec already holds), of equal
     // size so no launch runs a small tail batch

@@ -228,3 +228,20 @@ def test_entry_registers():
                 assert g.S_OFF + 12 * n <= dw < g.S_OFF + 12 * n + 12
                 seen.add(e)
     assert len(seen) == 4 * g.ROWS
+
+
+def test_column_map_division_is_exact():
+    """The column map's division (col_offset): q = mulhi(c, ceil(2^32 / d)), remainder c - q d,
+    as the generated launcher sets col_magic (d >= 2; d = 1 and the identity use magic 0).
+    Exact for every column c < 2^16 and chunk width d < 2^16 (tw_prepare rejects larger)."""
+    import numpy as np
+
+    c = np.arange(1 << 16, dtype=np.uint64)
+    widths = list(range(2, 1025)) + [3 << 10, 25 << 8, 65535]
+    for d in widths:
+        magic = ((1 << 32) - 1 + d) // d
+        assert magic < (1 << 32)
+        q = (c * np.uint64(magic)) >> np.uint64(32)
+        assert np.array_equal(q, c // np.uint64(d)), d
+    src = g.col_offset()
+    assert src[0].startswith("s_mul_hi_u32") and "%[cmg]" in src[0]

@@ -65,6 +65,11 @@ CASES = [
     (400, 100, 1400, 1400, 3, None, 2),   # RS16(400, 100): two levels by default (chunks of 50 and 25)
     (400, 100, 1400, 1400, 3, "L1", 1),
     (400, 100, 1400, 1400, 3, "0", 0),
+    # vec % 8 != 0: the split over the 8-byte pieces, the tail kernel over the last 2-6 bytes
+    (400, 100, 1460, 1464, 3, None, 2),   # NORM's 1452-byte segments (strides are multiples of 8)
+    (64, 16, 1402, 1408, 5, "1", 2),      # 2-byte tail, padded stride
+    (64, 16, 1406, 1408, 5, "1L1", 1),    # 6-byte tail at one level
+    (32, 8, 14, 16, 7, "1", 2),           # one 8-byte piece and a 6-byte tail per segment
     (100, 20, 1400, 1400, 3, "1", 2),     # level-2 chunks of 5 columns
     (100, 24, 1400, 1400, 3, "1", 0),     # k not a multiple of m: not allowed
 ]
