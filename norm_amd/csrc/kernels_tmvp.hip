@@ -11,8 +11,11 @@
 //   P0 = A (v_C0 + v_C1)  (v = c * d, the prescaled data: prescale_kernel)
 //   P1 = (B - A) c_C1 d_C1,  P2 = (C - A) c_C0 d_C0   (coefficients absorb c)
 //   parity_R0 = W (P0 + P1) + G[.][0] d_0,  parity_R1 = W (P0 + P2) + G[.][0] d_0  (postscale_kernel)
-// The three products run on the shared-table kernel (gen_gf16_t3.hip) in one launch; these two
-// kernels are the elementwise steps around it: bit-sliced multiplies by wave-uniform constants.
+// The products run in one launch of the tower kernel (gen_gf16_tw.hip; the shared-table kernel,
+// gen_gf16_t3.hip, in the diagnostic build); the kernels here are the elementwise steps around
+// them: bit-sliced multiplies by wave-uniform constants.  Two Karatsuba levels (nine products)
+// use the tmvp2_* pair below.  Any chunk width; vec % 8 != 0 runs over the 8-byte pieces and the
+// tail kernel takes the rest (rs16_tmvp_encode, nfec_api.cpp).
 #include "nfec_internal.hpp"
 #include "gf16_bs.hpp"
 #include "bitslice.hpp"
