@@ -12,7 +12,7 @@
 //   P1 = (B - A) c_C1 d_C1,  P2 = (C - A) c_C0 d_C0   (coefficients absorb c)
 //   parity_R0 = W (P0 + P1) + G[.][0] d_0,  parity_R1 = W (P0 + P2) + G[.][0] d_0  (postscale_kernel)
 // The products run in one launch of the tower kernel (gen_gf16_tw.hip; the shared-table kernel,
-// gen_gf16_t3.hip, in the diagnostic build); the kernels here are the elementwise steps around
+// gen_gf16_t3.hip, under NFEC_OPT_RS16_SHARED_TABLES, one level only); the kernels here are the elementwise steps around
 // them: bit-sliced multiplies by wave-uniform constants.  Two Karatsuba levels (nine products)
 // use the tmvp2_* pair below.  Any chunk width; vec % 8 != 0 runs over the 8-byte pieces and the
 // tail kernel takes the rest (rs16_tmvp_encode, nfec_api.cpp).
