@@ -25,110 +25,6 @@
 namespace nfec {
 namespace {
 
-// items of 8 bytes (4 symbols), 8 per lane, 512 per wave: item j of the lane is
-// chunk * 512 + j * 64 + lane, flat over (block, position in the segment)
-struct ItemMap {
-    uint32_t ok[8];
-    uint64_t blk[8];
-    uint32_t off[8];
-};
-
-__device__ __forceinline__ void map_items(uint32_t chunk, uint32_t lane, uint32_t items, uint32_t ipb, ItemMap& m)
-{
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-        const uint32_t it = chunk * 512u + (uint32_t)j * 64u + lane;
-        m.ok[j] = it < items;
-        const uint32_t b = it / ipb;
-        m.blk[j] = b;
-        m.off[j] = (it - b * ipb) * 8u;
-    }
-}
-
-__device__ __forceinline__ void load16(uint32_t x[16], const uint8_t* col, uint64_t block_stride, const ItemMap& m)
-{
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-        uint2 v = make_uint2(0u, 0u);
-        if (m.ok[j]) v = *reinterpret_cast<const uint2*>(col + m.blk[j] * block_stride + m.off[j]);
-        x[2 * j] = v.x;
-        x[2 * j + 1] = v.y;
-    }
-}
-
-__device__ __forceinline__ void store16(const uint32_t x[16], uint8_t* col, uint64_t block_stride, const ItemMap& m)
-{
-#pragma unroll
-    for (int j = 0; j < 8; ++j)
-        if (m.ok[j]) *reinterpret_cast<uint2*>(col + m.blk[j] * block_stride + m.off[j]) = make_uint2(x[2 * j], x[2 * j + 1]);
-}
-
-// v = c_a d_a + c_b d_b for every chunk pair: virtual column q*cw + i from columns
-// a = 2q*cw + i and b = a + cw (c_0 = 0: column 0 is added by the postscale)
-__global__ __launch_bounds__(256, 4) void tmvp_prescale_kernel(Rs16TmvpArgs a)
-{
-    const uint32_t lane = threadIdx.x & 63;
-    const uint32_t wid = __builtin_amdgcn_readfirstlane(blockIdx.x * 4u + (threadIdx.x >> 6));
-    const uint32_t half = a.k / 2;
-    const uint32_t v = wid % half, chunk = wid / half;
-    const uint32_t ipb = a.vec / 8u, items = a.nblocks * ipb;
-    if (chunk * 512u >= items) return;
-    const uint32_t q = v / a.cw, i = v - q * a.cw;
-    const uint32_t ca = 2u * q * a.cw + i, cb = ca + a.cw;
-    ItemMap m;
-    map_items(chunk, lane, items, ipb, m);
-    uint32_t x[16], y[16], z[16];
-    load16(x, a.base + (uint64_t)ca * a.seg_stride, a.block_stride, m);
-    load16(y, a.base + (uint64_t)cb * a.seg_stride, a.block_stride, m);
-    bs16::transpose(x);
-    bs16::transpose(y);
-#pragma unroll
-    for (int p = 0; p < 16; ++p) z[p] = 0;
-    bs16::mulc_acc(x, z, a.cmat + 16u * ca);
-    bs16::mulc_acc(y, z, a.cmat + 16u * cb);
-    bs16::transpose(z);
-    store16(z, a.s + (uint64_t)v * a.vec, a.s_block_stride, m);
-}
-
-// parity row p < cw and p + cw from P0 (parity row p), P1 (x row p), P2 (parity row cw + p)
-// and source column 0
-__global__ __launch_bounds__(256, 4) void tmvp_postscale_kernel(Rs16TmvpArgs a)
-{
-    const uint32_t lane = threadIdx.x & 63;
-    const uint32_t wid = __builtin_amdgcn_readfirstlane(blockIdx.x * 4u + (threadIdx.x >> 6));
-    const uint32_t p = wid % a.cw, chunk = wid / a.cw;
-    const uint32_t ipb = a.vec / 8u, items = a.nblocks * ipb;
-    if (chunk * 512u >= items) return;
-    ItemMap m;
-    map_items(chunk, lane, items, ipb, m);
-    uint8_t* r0 = const_cast<uint8_t*>(a.base) + (uint64_t)(a.k + p) * a.seg_stride;
-    uint8_t* r1 = const_cast<uint8_t*>(a.base) + (uint64_t)(a.k + a.cw + p) * a.seg_stride;
-    uint32_t t0[16], t1[16], d0[16], o[16];
-    load16(t0, r0, a.block_stride, m);
-    load16(d0, a.base, a.block_stride, m);
-    load16(t1, a.x + (uint64_t)p * a.vec, a.x_block_stride, m);
-#pragma unroll
-    for (int j = 0; j < 16; ++j) t1[j] ^= t0[j];  // P0 + P1
-    bs16::transpose(t1);
-    bs16::transpose(d0);
-#pragma unroll
-    for (int j = 0; j < 16; ++j) o[j] = 0;
-    bs16::mulc_acc(t1, o, a.wmat + 16u * p);
-    bs16::mulc_acc(d0, o, a.gmat + 16u * p);
-    bs16::transpose(o);
-    load16(t1, r1, a.block_stride, m);
-    store16(o, r0, a.block_stride, m);
-#pragma unroll
-    for (int j = 0; j < 16; ++j) t1[j] ^= t0[j];  // P0 + P2
-    bs16::transpose(t1);
-#pragma unroll
-    for (int j = 0; j < 16; ++j) o[j] = 0;
-    bs16::mulc_acc(t1, o, a.wmat + 16u * (a.cw + p));
-    bs16::mulc_acc(d0, o, a.gmat + 16u * (a.cw + p));
-    bs16::transpose(o);
-    store16(o, r1, a.block_stride, m);
-}
-
 // ---- two Karatsuba levels (rs16_tmvp_plan_levels, levels = 2) ----
 // Scratch per block (sc, sc_block_stride; columns of vec bytes): the level-1 pair sums v at
 // [0, k/2) (virtual column q*cw + i), the level-2 scaled sums s_0, s_1, s_2 at k/2 + X*k/4 + u
@@ -139,7 +35,7 @@ __device__ __forceinline__ uint32_t tmvp2_prow0(const Rs16TmvpArgs& a) { return 
 //   v at q cw + i = u_a0 + u_b0, at q cw + hw + i = u_a1 + u_b1   (the level-1 pair sums, halves)
 //   s_0 = both pair sums, s_1 = u_b0 + u_b1, s_2 = u_a0 + u_a1      (level 2's alpha inputs)
 // (the products are linear, so the sums are taken after transposing back to symbols)
-// buffer addressing for the level-2 prescale and postscale: descriptors over the wave's first block (of the
+// buffer addressing for the prescale and postscale kernels: descriptors over the wave's first block (of the
 // batch and of the scratch) and per item a 32-bit offset into each (0x80000000 outside the batch:
 // its loads read zeros, its stores drop, no branches).  With 64-bit addresses per item and
 // branches the postscale spilled (332 bytes per lane) and took 1.44 ms per 2,048 C4 blocks.
@@ -148,21 +44,22 @@ struct ItemMapB {
     __amdgpu_buffer_rsrc_t src, sc;
 };
 
-__device__ __forceinline__ void map_items_b(const Rs16TmvpArgs& a, uint32_t chunk, uint32_t lane, ItemMapB& m)
+// (sc, sc_stride: the scratch the kernel reads or writes -- level 2: a.sc; level 1: a.s or a.x)
+__device__ __forceinline__ void map_items_b(const Rs16TmvpArgs& a, uint32_t chunk, uint32_t lane, ItemMapB& m,
+                                            uint8_t* sc, uint64_t sc_stride)
 {
     const uint32_t ipb = a.vec / 8u, items = a.nblocks * ipb;
     const uint32_t blk0 = __builtin_amdgcn_readfirstlane((chunk * 512u) / ipb);
     m.src = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(a.base) + (uint64_t)blk0 * a.block_stride, (short)0,
                                               (int)0x80000000u, 0x00020000);
-    m.sc = __builtin_amdgcn_make_buffer_rsrc(a.sc + (uint64_t)blk0 * a.sc_block_stride, (short)0, (int)0x80000000u,
-                                             0x00020000);
+    m.sc = __builtin_amdgcn_make_buffer_rsrc(sc + (uint64_t)blk0 * sc_stride, (short)0, (int)0x80000000u, 0x00020000);
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
         const uint32_t it = chunk * 512u + (uint32_t)j * 64u + lane;
         const uint32_t b = it / ipb, off = (it - b * ipb) * 8u, db = b - blk0;
         const bool ok = it < items;
         m.vs[j] = ok ? db * (uint32_t)a.block_stride + off : 0x80000000u;
-        m.vc[j] = ok ? db * (uint32_t)a.sc_block_stride + off : 0x80000000u;
+        m.vc[j] = ok ? db * (uint32_t)sc_stride + off : 0x80000000u;
     }
 }
 
@@ -195,6 +92,82 @@ static bool tmvp2_offsets_fit(const Rs16TmvpArgs& a)
     return nb * a.block_stride + slots * a.seg_stride < (1ull << 31) && (nb + 1) * a.sc_block_stride < (1ull << 31);
 }
 
+// level 1's offsets fit 32 bits (its scratch: the pair sums a.s, the P1 rows a.x)
+static bool tmvp1_offsets_fit(const Rs16TmvpArgs& a)
+{
+    const uint64_t ipb = a.vec / 8u, nb = 512u / std::max<uint64_t>(ipb, 1) + 2u;
+    const uint64_t slots = (uint64_t)a.k + 2u * a.cw;
+    return nb * a.block_stride + slots * a.seg_stride < (1ull << 31) && (nb + 1) * a.s_block_stride < (1ull << 31) &&
+           (nb + 1) * a.x_block_stride < (1ull << 31);
+}
+
+// items of 8 bytes (4 symbols), 8 per lane, 512 per wave: item j of the lane is
+// chunk * 512 + j * 64 + lane, flat over (block, position in the segment), addressed as above.
+// v = c_a d_a + c_b d_b for every chunk pair: virtual column q*cw + i from columns
+// a = 2q*cw + i and b = a + cw (c_0 = 0: column 0 is added by the postscale)
+__global__ __launch_bounds__(256, 4) void tmvp_prescale_kernel(Rs16TmvpArgs a)
+{
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t wid = __builtin_amdgcn_readfirstlane(blockIdx.x * 4u + (threadIdx.x >> 6));
+    const uint32_t half = a.k / 2;
+    const uint32_t v = wid % half, chunk = wid / half;
+    const uint32_t ipb = a.vec / 8u, items = a.nblocks * ipb;
+    if (chunk * 512u >= items) return;
+    const uint32_t q = v / a.cw, i = v - q * a.cw;
+    const uint32_t ca = 2u * q * a.cw + i, cb = ca + a.cw;
+    ItemMapB m;
+    map_items_b(a, chunk, lane, m, a.s, a.s_block_stride);
+    uint32_t x[16], y[16], z[16];
+    load16_b(x, m.src, ca * a.seg_stride, m.vs);
+    load16_b(y, m.src, cb * a.seg_stride, m.vs);
+    bs16::transpose(x);
+    bs16::transpose(y);
+#pragma unroll
+    for (int p = 0; p < 16; ++p) z[p] = 0;
+    bs16::mulc_acc(x, z, a.cmat + 16u * ca);
+    bs16::mulc_acc(y, z, a.cmat + 16u * cb);
+    bs16::transpose(z);
+    store16_b(z, m.sc, v * a.vec, m.vc);
+}
+
+// parity row p < cw and p + cw from P0 (parity row p), P1 (x row p), P2 (parity row cw + p)
+// and source column 0
+__global__ __launch_bounds__(256, 4) void tmvp_postscale_kernel(Rs16TmvpArgs a)
+{
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t wid = __builtin_amdgcn_readfirstlane(blockIdx.x * 4u + (threadIdx.x >> 6));
+    const uint32_t p = wid % a.cw, chunk = wid / a.cw;
+    const uint32_t ipb = a.vec / 8u, items = a.nblocks * ipb;
+    if (chunk * 512u >= items) return;
+    ItemMapB m;
+    map_items_b(a, chunk, lane, m, a.x, a.x_block_stride);
+    const uint32_t r0 = (a.k + p) * a.seg_stride, r1 = (a.k + a.cw + p) * a.seg_stride;
+    uint32_t t0[16], t1[16], d0[16], o[16];
+    load16_b(t0, m.src, r0, m.vs);
+    load16_b(d0, m.src, 0u, m.vs);
+    load16_b(t1, m.sc, p * a.vec, m.vc);
+#pragma unroll
+    for (int j = 0; j < 16; ++j) t1[j] ^= t0[j];  // P0 + P1
+    bs16::transpose(t1);
+    bs16::transpose(d0);
+#pragma unroll
+    for (int j = 0; j < 16; ++j) o[j] = 0;
+    bs16::mulc_acc(t1, o, a.wmat + 16u * p);
+    bs16::mulc_acc(d0, o, a.gmat + 16u * p);
+    bs16::transpose(o);
+    load16_b(t1, m.src, r1, m.vs);
+    store16_b(o, m.src, r0, m.vs);
+#pragma unroll
+    for (int j = 0; j < 16; ++j) t1[j] ^= t0[j];  // P0 + P2
+    bs16::transpose(t1);
+#pragma unroll
+    for (int j = 0; j < 16; ++j) o[j] = 0;
+    bs16::mulc_acc(t1, o, a.wmat + 16u * (a.cw + p));
+    bs16::mulc_acc(d0, o, a.gmat + 16u * (a.cw + p));
+    bs16::transpose(o);
+    store16_b(o, m.src, r1, m.vs);
+}
+
 __global__ __launch_bounds__(256, 4) void tmvp2_prescale_kernel(Rs16TmvpArgs a)
 {
     const uint32_t lane = threadIdx.x & 63;
@@ -207,7 +180,7 @@ __global__ __launch_bounds__(256, 4) void tmvp2_prescale_kernel(Rs16TmvpArgs a)
     const uint32_t a0 = 2u * q * a.cw + i;
     const uint32_t col[4] = {a0, a0 + a.hw, a0 + a.cw, a0 + a.cw + a.hw};  // a0, a1, b0, b1
     ItemMapB m;
-    map_items_b(a, chunk, lane, m);
+    map_items_b(a, chunk, lane, m, a.sc, a.sc_block_stride);
     // all four columns' loads in flight first, then each scaled in place
     uint32_t r[4][16];
 #pragma unroll
@@ -255,7 +228,7 @@ __global__ __launch_bounds__(256, 3) void tmvp2_postscale_kernel(Rs16TmvpArgs a)
     const uint32_t ipb = a.vec / 8u, items = a.nblocks * ipb;
     if (chunk * 512u >= items) return;
     ItemMapB m;
-    map_items_b(a, chunk, lane, m);
+    map_items_b(a, chunk, lane, m, a.sc, a.sc_block_stride);
     const uint32_t pr = (tmvp2_prow0(a) + p) * a.vec;  // product e's row p at pr + e hw vec
     // output rows (R0 top, R0 bottom, R1 top, R1 bottom): bit t of uses[e] = product e feeds output t
     constexpr uint8_t uses[9] = {0xF, 0x5, 0xA, 0x3, 0x1, 0x2, 0xC, 0x4, 0x8};
@@ -318,7 +291,8 @@ int launch_tmvp_prescale(const Rs16TmvpArgs& a, hipStream_t s)
 {
     const uint64_t items = (uint64_t)a.nblocks * (a.vec / 8u);
     const uint64_t waves = (items + 511) / 512 * (a.k / 2);
-    if (items >= (1ull << 32) || waves >= (1ull << 32)) return NFEC_ENOTSUP;
+    // (the postscale's 32-bit offsets: checked here too, before anything is written)
+    if (items >= (1ull << 32) || waves >= (1ull << 32) || !tmvp1_offsets_fit(a)) return NFEC_ENOTSUP;
     if (waves == 0) return NFEC_OK;
     hipLaunchKernelGGL(tmvp_prescale_kernel, dim3((uint32_t)((waves + 3) / 4)), dim3(256), 0, s, a);
     const hipError_t e = hipGetLastError();
@@ -329,7 +303,7 @@ int launch_tmvp_postscale(const Rs16TmvpArgs& a, hipStream_t s)
 {
     const uint64_t items = (uint64_t)a.nblocks * (a.vec / 8u);
     const uint64_t waves = (items + 511) / 512 * a.cw;
-    if (items >= (1ull << 32) || waves >= (1ull << 32)) return NFEC_ENOTSUP;
+    if (items >= (1ull << 32) || waves >= (1ull << 32) || !tmvp1_offsets_fit(a)) return NFEC_ENOTSUP;
     if (waves == 0) return NFEC_OK;
     hipLaunchKernelGGL(tmvp_postscale_kernel, dim3((uint32_t)((waves + 3) / 4)), dim3(256), 0, s, a);
     const hipError_t e = hipGetLastError();
