@@ -19,7 +19,10 @@ value = k * vec * blocks_total / step_time  (source bytes through encode+decode,
 the same formula as the CPU baseline; SURVEY.md 8d's "combined" figure,
 2*k*vec*B / (t_enc + t_dec), counts each source byte twice and is exactly 2x this value.
 --strong splits a fixed total of --blocks over the ranks instead (norm_amd/dist.py shard).  roofline = the encode kernel's
-algorithmic HBM bytes ((k+m)*vec per block) / its measured launch time vs 8 TB/s.
+algorithmic HBM bytes per launch / its measured launch time vs 8 TB/s, for the step's dominant
+kernel (the longer of the encode, (k+m)*vec per block, and the repair call, (k+e)*vec per block);
+both halves are in the line.  After timing, one clean encode -> erase -> repair round trip from the
+pristine source is compared byte for byte ("verified"; --no-verify skips it).
 """
 import argparse
 import json
@@ -81,7 +84,10 @@ def parse():
                    help="CPU-baseline threads (0 = every core this process may run on: the affinity mask, "
                         "capped by a cgroup CPU quota when one is set)")
     p.add_argument("--no-cpu-baseline", action="store_true")
-    p.add_argument("--verify", action="store_true", help="check the round trip after timing")
+    p.add_argument("--no-verify", action="store_true",
+                   help="skip the clean round trip after timing (by default the line carries 'verified': one "
+                        "encode -> erase -> repair from the pristine source, every byte compared, as the "
+                        "reference's fecTest does, fecTest.cpp:121-129)")
     p.add_argument("--host-steps", type=int, default=2,
                    help="also time K steps with blocks in pinned host memory (PCIe-inclusive, reported "
                         "under 'host_resident'; never the headline value; 0: skip)")
@@ -187,7 +193,7 @@ def main():
         if dist is not None:
             dist.barrier()
 
-    orig = blocks[:, :k].clone() if a.verify else None
+    orig = None if a.no_verify else blocks[:, :k].clone()
     for _ in range(a.warmup):
         step()
     torch.cuda.synchronize(dev)
@@ -330,7 +336,7 @@ def main():
         del hblocks, hnp
 
     ok = None
-    if a.verify:
+    if not a.no_verify:
         from norm_amd import zero_erasures
 
         # One clean round trip from the pristine source: encode once, erase, repair once, and
@@ -344,7 +350,14 @@ def main():
         dec.decode_blocks(blocks, locs, counts, status=status, stream=stream)
         torch.cuda.synchronize(dev)
         ok = bool(torch.equal(blocks, keep)) and bool((status == a.erasures).all())
+        del keep
+        if dist is not None:  # every rank's blocks: the line says true only if all came back
+            t = torch.tensor([1 if ok else 0], dtype=torch.int32, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MIN)
+            ok = bool(t.item())
 
+    if orig is not None:
+        del orig
     total_blocks = a.blocks if a.strong else nb * world
     src_bytes = k * vec * total_blocks
     ms_per_step = elapsed / a.steps * 1e3
@@ -423,7 +436,7 @@ def main():
             "k": k, "m": m, "vec": vec, "blocks_per_gpu": nb, "blocks_total": total_blocks, "erasures": a.erasures,
             "parallelism": f"block-striped x{world} (no collective)",
         },
-        "roofline": {
+        "roofline_encode": {
             "bound": "hbm",
             "achieved": round(achieved, 1),
             "peak": HBM_PEAK_GBS,
@@ -453,6 +466,15 @@ def main():
         "kernels_ms": {"encode": round(enc_ms, 4), "decode": round(dec_ms, 4)},
         "cpu_baseline": cpu,
     }
+    # `roofline` is the step's dominant kernel: the one with the longer measured launch (the
+    # repair call, plan included, on most boxes); both halves stay under roofline_encode /
+    # roofline_decode
+    dom = "roofline_decode" if dec_ms > enc_ms else "roofline_encode"
+    out["roofline"] = dict(out[dom], dominant_of_step=dom.split("_")[1],
+                           share_of_step=round(max(enc_ms, dec_ms) / (enc_ms + dec_ms), 4))
+    out = {key: out[key] for key in ["metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step",
+                                     "higher_is_better", "scaling", "vs_baseline", "dtype", "data", "config",
+                                     "roofline", "roofline_encode", "roofline_decode", "kernels_ms", "cpu_baseline"]}
     if host is not None:
         out["host_resident"] = host
     if ok is not None:

@@ -168,6 +168,15 @@ int nfec_codec_get_info(const nfec_codec* codec, nfec_codec_info* out);
 /* ... at two Karatsuba levels: nine (m/4)-row products over k/4 columns (tower kernel) */
 #define NFEC_FEATURE_RS16_TOEPLITZ2 2
 int nfec_codec_features(const nfec_codec* codec);
+/* Device-batch encodes so far per path that took them (diagnostics: which kernel family a
+ * batch shape reaches).  counts[i] for i < n; returns NFEC_PATH_COUNT (< 0 on error). */
+#define NFEC_PATH_FIXED 0        /* bit-sliced kernels generated for the (k, m) generator (RS8, MDP; shortened RS8 too) */
+#define NFEC_PATH_RUNTIME 1      /* bit-sliced, runtime coefficients (any RS8 / MDP shape) */
+#define NFEC_PATH_RS16_SPLIT 2   /* RS16 Toeplitz split (shortened batches too, tower kernel) */
+#define NFEC_PATH_RS16_PRODUCT 3 /* RS16 one product over all k columns (tower or shared-table kernel) */
+#define NFEC_PATH_GENERIC 4      /* table-lookup kernels */
+#define NFEC_PATH_COUNT 5
+int nfec_codec_encode_paths(const nfec_codec* codec, uint64_t* counts, uint32_t n);
 /* Copies the m x k parity rows of the systematic generator (row p = generator row k+p),
  * row-major, elements of symbol_bytes each.  MDP: the m x k matrix of the LFSR code for a
  * full block of k source symbols.  bytes must be >= m*k*symbol_bytes. */
@@ -305,6 +314,12 @@ size_t nfec_dropin_sizeof(int kind, int decoder);
  * or NFEC_HOST_THREADS, at most 64), the usable and the visible cores.  All stripes of all codecs
  * share it; smaller copies run on the calling thread. */
 int nfec_host_threads(uint32_t* pool, uint32_t* usable_cores, uint32_t* visible_cores);
+/* Self-check of that pool (tests): runs `pieces` pieces on it.  mode 0: every piece counts once;
+ * 1: piece 1 throws std::bad_alloc; 2: piece 1 throws std::runtime_error.  Returns the pieces that
+ * ran to completion (mode 0: all of them), or the pool's error status (NFEC_ENOMEM / NFEC_EINVAL)
+ * once every piece has run -- a throwing piece neither ends the process nor leaves the call
+ * waiting.  Safe in a child forked after the pool started (its pieces then run inline). */
+int nfec_util_pool_check(uint32_t pieces, int mode);
 /* Host-side rate probe of the segment-list gather (no GPU): nstripes driver threads, one per
  * would-be device, each gather their contiguous block range [i*B/N, (i+1)*B/N) of the pointer
  * table vectors[b*slots + s] (slots vectors of vector_size bytes per block) into staging of their

@@ -21,6 +21,10 @@ NFEC_ACCUMULATE = 1
 NFEC_FEATURE_RS16_TOEPLITZ, NFEC_FEATURE_RS16_TOEPLITZ2 = 1, 2
 NFEC_OPT_RS16_SHARED_TABLES, NFEC_OPT_RS16_TOEPLITZ_OFF, NFEC_OPT_RS16_TOEPLITZ_ON, NFEC_OPT_HOST_ONLY = 1, 2, 4, 8
 NFEC_OPT_RS16_TOEPLITZ_ONE_LEVEL = 16
+# encode paths (nfec_codec_encode_paths)
+NFEC_PATH_FIXED, NFEC_PATH_RUNTIME, NFEC_PATH_RS16_SPLIT, NFEC_PATH_RS16_PRODUCT, NFEC_PATH_GENERIC = 0, 1, 2, 3, 4
+NFEC_PATH_COUNT = 5
+PATH_NAMES = ("fixed", "runtime", "rs16_split", "rs16_product", "generic")
 NFEC_HOST_GF_SCALAR, NFEC_HOST_GF_AVX2, NFEC_HOST_GF_GFNI = 0, 1, 2
 
 
@@ -126,6 +130,7 @@ _SIGS = {
     "nfec_codec_destroy": (None, [_P]),
     "nfec_codec_get_info": (_I, [_P, ctypes.POINTER(CodecInfo)]),
     "nfec_codec_features": (_I, [_P]),
+    "nfec_codec_encode_paths": (_I, [_P, ctypes.POINTER(_U64), _U32]),
     "nfec_codec_get_generator": (_I, [_P, _P, ctypes.c_size_t]),
     "nfec_encode": (_I, [_P, ctypes.POINTER(BlockBatch), _P]),
     "nfec_decode": (_I, [_P, ctypes.POINTER(BlockBatch), _P, _U32, _P, _P, _P]),
@@ -151,6 +156,7 @@ _SIGS = {
     "nfec_util_zero_slots": (_I, [ctypes.POINTER(BlockBatch), _P, _U32, _P, _U32, _P]),
     "nfec_util_stream_copy": (_I, [_P, _P, _U64, _P]),
     "nfec_host_threads": (_I, [ctypes.POINTER(_U32), ctypes.POINTER(_U32), ctypes.POINTER(_U32)]),
+    "nfec_util_pool_check": (_I, [_U32, _I]),
     "nfec_util_gather_probe": (_I, [_P, _U32, _U32, _U32, _U32, _U32, ctypes.POINTER(ctypes.c_double),
                                     ctypes.POINTER(_U32)]),
     "nfec_fti_write": (_I, [ctypes.POINTER(Fti), _P, ctypes.c_size_t]),

@@ -177,6 +177,15 @@ class _Codec:
         N.check(min(rc, 0), "nfec_codec_features")
         return rc
 
+    def encode_paths(self):
+        """Device-batch encodes so far per path that took them, {name: count} (NFEC_PATH_*,
+        include/nfec.h): which kernel family a batch shape reaches."""
+        self._need()
+        cnt = (ctypes.c_uint64 * N.NFEC_PATH_COUNT)()
+        rc = N.lib().nfec_codec_encode_paths(self._h, cnt, N.NFEC_PATH_COUNT)
+        N.check(min(rc, 0), "nfec_codec_encode_paths")
+        return {name: int(cnt[i]) for i, name in enumerate(N.PATH_NAMES)}
+
     def _need(self):
         if not self._h:
             raise RuntimeError("codec not initialised (call Init)")

@@ -13,12 +13,16 @@
 #include "nfec_internal.hpp"
 
 #include <sched.h>
+#include <unistd.h>
 
 #include <atomic>
 #include <condition_variable>
 #include <cstdio>
 #include <deque>
 #include <memory>
+#include <new>
+#include <stdexcept>
+#include <string>
 #include <thread>
 
 namespace nfec {
@@ -47,15 +51,37 @@ struct PoolJob {
     unsigned n = 0;
     std::mutex mu;
     std::condition_variable cv;
-    unsigned done = 0;  // pieces finished (under mu)
+    unsigned done = 0;  // pieces finished, thrown or not (under mu)
+    int err = NFEC_OK;  // the first piece that threw (under mu)
+    std::string what;
 };
+
+// runs piece i; an exception (std::bad_alloc in a piece's allocation, anything else a piece
+// throws) is caught here -- a worker thread must not terminate the process and the caller must
+// not wait forever -- and reported as a status: NFEC_ENOMEM for bad_alloc, NFEC_EINVAL otherwise
+int run_piece(const std::function<void(unsigned)>& fn, unsigned i, std::string& what)
+{
+    try {
+        fn(i);
+        return NFEC_OK;
+    } catch (const std::bad_alloc&) {
+        what = "host pool piece: out of memory";
+        return NFEC_ENOMEM;
+    } catch (const std::exception& e) {
+        what = std::string("host pool piece: ") + e.what();
+        return NFEC_EINVAL;
+    } catch (...) {
+        what = "host pool piece: unknown exception";
+        return NFEC_EINVAL;
+    }
+}
 
 thread_local bool tl_pool_worker = false;
 std::atomic<unsigned> g_active{0}, g_max_active{0};  // pool pieces running now / at most so far
 
 class HostPool {
   public:
-    explicit HostPool(unsigned workers)
+    explicit HostPool(unsigned workers) : pid_(getpid())
     {
         for (unsigned i = 0; i < workers; ++i) {
             try {
@@ -67,12 +93,22 @@ class HostPool {
     }
     unsigned workers() const { return (unsigned)th_.size(); }
 
-    void run(unsigned n, const std::function<void(unsigned)>& fn)
+    // NFEC_OK, or the status of the first piece that threw (every piece runs either way)
+    int run(unsigned n, const std::function<void(unsigned)>& fn)
     {
-        if (n == 0) return;
-        if (n == 1 || th_.empty() || tl_pool_worker) {
-            for (unsigned i = 0; i < n; ++i) fn(i);
-            return;
+        if (n == 0) return NFEC_OK;
+        // inline: one piece, no workers, a call from a worker, or a child forked after the pool
+        // started (it inherits the pool object but not its threads, and a queue lock a thread
+        // held at the fork would stay held: the child never touches the queue)
+        if (n == 1 || th_.empty() || tl_pool_worker || getpid() != pid_) {
+            int err = NFEC_OK;
+            std::string what;
+            for (unsigned i = 0; i < n; ++i) {
+                std::string w;
+                const int rc = run_piece(fn, i, w);
+                if (rc && !err) err = rc, what = w;
+            }
+            return err ? fail(err, what) : NFEC_OK;
         }
         auto job = std::make_shared<PoolJob>();
         job->fn = fn;
@@ -85,6 +121,7 @@ class HostPool {
         cv_.notify_all();
         std::unique_lock<std::mutex> lk(job->mu);
         job->cv.wait(lk, [&] { return job->done == job->n; });
+        return job->err ? fail(job->err, job->what) : NFEC_OK;
     }
 
   private:
@@ -106,13 +143,16 @@ class HostPool {
                 unsigned mx = g_max_active.load();
                 while (a > mx && !g_max_active.compare_exchange_weak(mx, a)) {
                 }
-                job->fn(i);
+                std::string what;
+                const int rc = run_piece(job->fn, i, what);
                 g_active.fetch_sub(1);
                 std::lock_guard<std::mutex> lk(job->mu);
+                if (rc && !job->err) job->err = rc, job->what = what;
                 if (++job->done == job->n) job->cv.notify_all();
             }
         }
     }
+    const pid_t pid_;  // the process that started the workers
     std::vector<std::thread> th_;
     std::mutex mu_;
     std::condition_variable cv_;
@@ -153,7 +193,7 @@ unsigned host_pool_size()
     return n;
 }
 
-void host_parallel_for(unsigned n, const std::function<void(unsigned)>& fn) { pool().run(n, fn); }
+int host_parallel_for(unsigned n, const std::function<void(unsigned)>& fn) { return pool().run(n, fn); }
 
 unsigned host_pool_workers() { return pool().workers(); }
 

@@ -45,8 +45,11 @@ struct ItemMapB {
 };
 
 // (sc, sc_stride: the scratch the kernel reads or writes -- level 2: a.sc; level 1: a.s or a.x)
+// SH (shortened batch, a.num_data): nd[j] = the numData of item j's block (k outside the batch);
+// an item whose block has numData 0 or past k is treated as outside the batch (left alone)
+template <bool SH>
 __device__ __forceinline__ void map_items_b(const Rs16TmvpArgs& a, uint32_t chunk, uint32_t lane, ItemMapB& m,
-                                            uint8_t* sc, uint64_t sc_stride)
+                                            uint8_t* sc, uint64_t sc_stride, uint32_t nd[8])
 {
     const uint32_t ipb = a.vec / 8u, items = a.nblocks * ipb;
     const uint32_t blk0 = __builtin_amdgcn_readfirstlane((chunk * 512u) / ipb);
@@ -57,10 +60,31 @@ __device__ __forceinline__ void map_items_b(const Rs16TmvpArgs& a, uint32_t chun
     for (int j = 0; j < 8; ++j) {
         const uint32_t it = chunk * 512u + (uint32_t)j * 64u + lane;
         const uint32_t b = it / ipb, off = (it - b * ipb) * 8u, db = b - blk0;
-        const bool ok = it < items;
+        bool ok = it < items;
+        nd[j] = a.k;
+        if (SH && ok) {
+            const uint32_t v = a.num_data[b];
+            ok = v >= 1u && v <= a.k;
+            nd[j] = ok ? v : a.k;
+        }
         m.vs[j] = ok ? db * (uint32_t)a.block_stride + off : 0x80000000u;
         m.vc[j] = ok ? db * (uint32_t)sc_stride + off : 0x80000000u;
     }
+}
+
+// item offsets for source column col (wave-uniform): bit 31 (reads zeros) where col is at or
+// past the item's numData
+__device__ __forceinline__ void col_offsets(uint32_t o[8], const uint32_t v[8], const uint32_t nd[8], uint32_t col)
+{
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = col < nd[j] ? v[j] : 0x80000000u;
+}
+
+// item offsets of the block's parity slot 0 (slot numData): stores past the batch drop
+__device__ __forceinline__ void parity_offsets(uint32_t o[8], const uint32_t v[8], const uint32_t nd[8], uint32_t ss)
+{
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = v[j] == 0x80000000u ? v[j] : v[j] + nd[j] * ss;
 }
 
 __device__ __forceinline__ void load16_b(uint32_t x[16], __amdgpu_buffer_rsrc_t rs, uint32_t soff, const uint32_t v[8])
@@ -105,6 +129,7 @@ static bool tmvp1_offsets_fit(const Rs16TmvpArgs& a)
 // chunk * 512 + j * 64 + lane, flat over (block, position in the segment), addressed as above.
 // v = c_a d_a + c_b d_b for every chunk pair: virtual column q*cw + i from columns
 // a = 2q*cw + i and b = a + cw (c_0 = 0: column 0 is added by the postscale)
+template <bool SH>
 __global__ __launch_bounds__(256, 4) void tmvp_prescale_kernel(Rs16TmvpArgs a)
 {
     const uint32_t lane = threadIdx.x & 63;
@@ -116,10 +141,19 @@ __global__ __launch_bounds__(256, 4) void tmvp_prescale_kernel(Rs16TmvpArgs a)
     const uint32_t q = v / a.cw, i = v - q * a.cw;
     const uint32_t ca = 2u * q * a.cw + i, cb = ca + a.cw;
     ItemMapB m;
-    map_items_b(a, chunk, lane, m, a.s, a.s_block_stride);
+    uint32_t nd[8];
+    map_items_b<SH>(a, chunk, lane, m, a.s, a.s_block_stride, nd);
     uint32_t x[16], y[16], z[16];
-    load16_b(x, m.src, ca * a.seg_stride, m.vs);
-    load16_b(y, m.src, cb * a.seg_stride, m.vs);
+    if (SH) {  // shortened blocks: source columns at or past numData read zeros
+        uint32_t o[8];
+        col_offsets(o, m.vs, nd, ca);
+        load16_b(x, m.src, ca * a.seg_stride, o);
+        col_offsets(o, m.vs, nd, cb);
+        load16_b(y, m.src, cb * a.seg_stride, o);
+    } else {
+        load16_b(x, m.src, ca * a.seg_stride, m.vs);
+        load16_b(y, m.src, cb * a.seg_stride, m.vs);
+    }
     bs16::transpose(x);
     bs16::transpose(y);
 #pragma unroll
@@ -131,7 +165,8 @@ __global__ __launch_bounds__(256, 4) void tmvp_prescale_kernel(Rs16TmvpArgs a)
 }
 
 // parity row p < cw and p + cw from P0 (parity row p), P1 (x row p), P2 (parity row cw + p)
-// and source column 0
+// and source column 0 (shortened blocks: the parity rows at slot numData + r)
+template <bool SH>
 __global__ __launch_bounds__(256, 4) void tmvp_postscale_kernel(Rs16TmvpArgs a)
 {
     const uint32_t lane = threadIdx.x & 63;
@@ -140,10 +175,17 @@ __global__ __launch_bounds__(256, 4) void tmvp_postscale_kernel(Rs16TmvpArgs a)
     const uint32_t ipb = a.vec / 8u, items = a.nblocks * ipb;
     if (chunk * 512u >= items) return;
     ItemMapB m;
-    map_items_b(a, chunk, lane, m, a.x, a.x_block_stride);
-    const uint32_t r0 = (a.k + p) * a.seg_stride, r1 = (a.k + a.cw + p) * a.seg_stride;
+    uint32_t nd[8], vp[8];
+    map_items_b<SH>(a, chunk, lane, m, a.x, a.x_block_stride, nd);
+    const uint32_t* pv = m.vs;  // parity rows: from slot k (vs) or slot numData (vp)
+    if (SH) {
+        parity_offsets(vp, m.vs, nd, a.seg_stride);
+        pv = vp;
+    }
+    const uint32_t pbase = SH ? 0u : a.k;
+    const uint32_t r0 = (pbase + p) * a.seg_stride, r1 = (pbase + a.cw + p) * a.seg_stride;
     uint32_t t0[16], t1[16], d0[16], o[16];
-    load16_b(t0, m.src, r0, m.vs);
+    load16_b(t0, m.src, r0, pv);
     load16_b(d0, m.src, 0u, m.vs);
     load16_b(t1, m.sc, p * a.vec, m.vc);
 #pragma unroll
@@ -155,8 +197,8 @@ __global__ __launch_bounds__(256, 4) void tmvp_postscale_kernel(Rs16TmvpArgs a)
     bs16::mulc_acc(t1, o, a.wmat + 16u * p);
     bs16::mulc_acc(d0, o, a.gmat + 16u * p);
     bs16::transpose(o);
-    load16_b(t1, m.src, r1, m.vs);
-    store16_b(o, m.src, r0, m.vs);
+    load16_b(t1, m.src, r1, pv);
+    store16_b(o, m.src, r0, pv);
 #pragma unroll
     for (int j = 0; j < 16; ++j) t1[j] ^= t0[j];  // P0 + P2
     bs16::transpose(t1);
@@ -165,9 +207,10 @@ __global__ __launch_bounds__(256, 4) void tmvp_postscale_kernel(Rs16TmvpArgs a)
     bs16::mulc_acc(t1, o, a.wmat + 16u * (a.cw + p));
     bs16::mulc_acc(d0, o, a.gmat + 16u * (a.cw + p));
     bs16::transpose(o);
-    store16_b(o, m.src, r1, m.vs);
+    store16_b(o, m.src, r1, pv);
 }
 
+template <bool SH>
 __global__ __launch_bounds__(256, 4) void tmvp2_prescale_kernel(Rs16TmvpArgs a)
 {
     const uint32_t lane = threadIdx.x & 63;
@@ -180,11 +223,21 @@ __global__ __launch_bounds__(256, 4) void tmvp2_prescale_kernel(Rs16TmvpArgs a)
     const uint32_t a0 = 2u * q * a.cw + i;
     const uint32_t col[4] = {a0, a0 + a.hw, a0 + a.cw, a0 + a.cw + a.hw};  // a0, a1, b0, b1
     ItemMapB m;
-    map_items_b(a, chunk, lane, m, a.sc, a.sc_block_stride);
-    // all four columns' loads in flight first, then each scaled in place
+    uint32_t nd[8];
+    map_items_b<SH>(a, chunk, lane, m, a.sc, a.sc_block_stride, nd);
+    // all four columns' loads in flight first, then each scaled in place (shortened blocks:
+    // columns at or past numData read zeros)
     uint32_t r[4][16];
 #pragma unroll
-    for (int t = 0; t < 4; ++t) load16_b(r[t], m.src, col[t] * a.seg_stride, m.vs);
+    for (int t = 0; t < 4; ++t) {
+        if (SH) {
+            uint32_t o[8];
+            col_offsets(o, m.vs, nd, col[t]);
+            load16_b(r[t], m.src, col[t] * a.seg_stride, o);
+        } else {
+            load16_b(r[t], m.src, col[t] * a.seg_stride, m.vs);
+        }
+    }
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
         uint32_t o[16];
@@ -220,6 +273,7 @@ __global__ __launch_bounds__(256, 4) void tmvp2_prescale_kernel(Rs16TmvpArgs a)
 // The wave loads each of the nine products once into four sums (143 VGPRs, no spill; one
 // output at a time, reloading the products, measured 1.82 against 1.56 ms per 16,384
 // RS16(400,100) blocks).
+template <bool SH>
 __global__ __launch_bounds__(256, 3) void tmvp2_postscale_kernel(Rs16TmvpArgs a)
 {
     const uint32_t lane = threadIdx.x & 63;
@@ -228,7 +282,8 @@ __global__ __launch_bounds__(256, 3) void tmvp2_postscale_kernel(Rs16TmvpArgs a)
     const uint32_t ipb = a.vec / 8u, items = a.nblocks * ipb;
     if (chunk * 512u >= items) return;
     ItemMapB m;
-    map_items_b(a, chunk, lane, m, a.sc, a.sc_block_stride);
+    uint32_t nd[8];
+    map_items_b<SH>(a, chunk, lane, m, a.sc, a.sc_block_stride, nd);
     const uint32_t pr = (tmvp2_prow0(a) + p) * a.vec;  // product e's row p at pr + e hw vec
     // output rows (R0 top, R0 bottom, R1 top, R1 bottom): bit t of uses[e] = product e feeds output t
     constexpr uint8_t uses[9] = {0xF, 0x5, 0xA, 0x3, 0x1, 0x2, 0xC, 0x4, 0x8};
@@ -248,6 +303,14 @@ __global__ __launch_bounds__(256, 3) void tmvp2_postscale_kernel(Rs16TmvpArgs a)
     }
     load16_b(x, m.src, 0u, m.vs);
     bs16::transpose(x);  // d_0, bit-sliced
+    // parity rows at slot k + row, or numData + row for shortened blocks
+    uint32_t vp[8];
+    const uint32_t* pv = m.vs;
+    if (SH) {
+        parity_offsets(vp, m.vs, nd, a.seg_stride);
+        pv = vp;
+    }
+    const uint32_t pbase = SH ? 0u : a.k;
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
         const uint32_t row = (uint32_t)(t >> 1) * a.cw + (uint32_t)(t & 1) * a.hw + p;
@@ -258,7 +321,7 @@ __global__ __launch_bounds__(256, 3) void tmvp2_postscale_kernel(Rs16TmvpArgs a)
         bs16::mulc_acc(sum[t], o, a.wmat + 16u * row);
         bs16::mulc_acc(x, o, a.gmat + 16u * row);
         bs16::transpose(o);
-        store16_b(o, m.src, (a.k + row) * a.seg_stride, m.vs);
+        store16_b(o, m.src, (pbase + row) * a.seg_stride, pv);
     }
 }
 
@@ -271,7 +334,8 @@ int launch_tmvp2_prescale(const Rs16TmvpArgs& a, hipStream_t s)
     // (the postscale's 32-bit offsets: checked here too, before anything is written)
     if (!a.hw || !a.sc || items >= (1ull << 32) || waves >= (1ull << 32) || !tmvp2_offsets_fit(a)) return NFEC_ENOTSUP;
     if (waves == 0) return NFEC_OK;
-    hipLaunchKernelGGL(tmvp2_prescale_kernel, dim3((uint32_t)((waves + 3) / 4)), dim3(256), 0, s, a);
+    if (a.num_data) hipLaunchKernelGGL(tmvp2_prescale_kernel<true>, dim3((uint32_t)((waves + 3) / 4)), dim3(256), 0, s, a);
+    else hipLaunchKernelGGL(tmvp2_prescale_kernel<false>, dim3((uint32_t)((waves + 3) / 4)), dim3(256), 0, s, a);
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? NFEC_OK : hip_fail(e, "tmvp level-2 prescale launch");
 }
@@ -282,7 +346,8 @@ int launch_tmvp2_postscale(const Rs16TmvpArgs& a, hipStream_t s)
     const uint64_t waves = (items + 511) / 512 * a.hw;
     if (!a.hw || !a.sc || items >= (1ull << 32) || waves >= (1ull << 32) || !tmvp2_offsets_fit(a)) return NFEC_ENOTSUP;
     if (waves == 0) return NFEC_OK;
-    hipLaunchKernelGGL(tmvp2_postscale_kernel, dim3((uint32_t)((waves + 3) / 4)), dim3(256), 0, s, a);
+    if (a.num_data) hipLaunchKernelGGL(tmvp2_postscale_kernel<true>, dim3((uint32_t)((waves + 3) / 4)), dim3(256), 0, s, a);
+    else hipLaunchKernelGGL(tmvp2_postscale_kernel<false>, dim3((uint32_t)((waves + 3) / 4)), dim3(256), 0, s, a);
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? NFEC_OK : hip_fail(e, "tmvp level-2 postscale launch");
 }
@@ -294,7 +359,8 @@ int launch_tmvp_prescale(const Rs16TmvpArgs& a, hipStream_t s)
     // (the postscale's 32-bit offsets: checked here too, before anything is written)
     if (items >= (1ull << 32) || waves >= (1ull << 32) || !tmvp1_offsets_fit(a)) return NFEC_ENOTSUP;
     if (waves == 0) return NFEC_OK;
-    hipLaunchKernelGGL(tmvp_prescale_kernel, dim3((uint32_t)((waves + 3) / 4)), dim3(256), 0, s, a);
+    if (a.num_data) hipLaunchKernelGGL(tmvp_prescale_kernel<true>, dim3((uint32_t)((waves + 3) / 4)), dim3(256), 0, s, a);
+    else hipLaunchKernelGGL(tmvp_prescale_kernel<false>, dim3((uint32_t)((waves + 3) / 4)), dim3(256), 0, s, a);
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? NFEC_OK : hip_fail(e, "tmvp prescale launch");
 }
@@ -305,7 +371,8 @@ int launch_tmvp_postscale(const Rs16TmvpArgs& a, hipStream_t s)
     const uint64_t waves = (items + 511) / 512 * a.cw;
     if (items >= (1ull << 32) || waves >= (1ull << 32) || !tmvp1_offsets_fit(a)) return NFEC_ENOTSUP;
     if (waves == 0) return NFEC_OK;
-    hipLaunchKernelGGL(tmvp_postscale_kernel, dim3((uint32_t)((waves + 3) / 4)), dim3(256), 0, s, a);
+    if (a.num_data) hipLaunchKernelGGL(tmvp_postscale_kernel<true>, dim3((uint32_t)((waves + 3) / 4)), dim3(256), 0, s, a);
+    else hipLaunchKernelGGL(tmvp_postscale_kernel<false>, dim3((uint32_t)((waves + 3) / 4)), dim3(256), 0, s, a);
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? NFEC_OK : hip_fail(e, "tmvp postscale launch");
 }

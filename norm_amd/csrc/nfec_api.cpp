@@ -13,6 +13,7 @@
 #include <cstring>
 #include <map>
 #include <memory>
+#include <stdexcept>
 #include <thread>
 #include <chrono>
 #include <vector>
@@ -233,6 +234,8 @@ struct nfec_codec {
     std::mutex tmvp_mu;            // one Toeplitz encode at a time per codec: they share w_tmvp
     DevBuf<uint8_t> w_tmvp;        // prescaled pair sums + P1 rows of a sub-batch
     hipEvent_t tmvp_done = nullptr;  // the last Toeplitz encode's end, on its stream
+    // device-batch encodes per path that took them (NFEC_PATH_*, nfec_codec_encode_paths)
+    std::atomic<uint64_t> enc_paths[NFEC_PATH_COUNT] = {};
 
     // decode workspace (guarded by mu)
     std::mutex mu;
@@ -733,6 +736,7 @@ static int rs16_tmvp2_encode(nfec_codec* c, const nfec_block_batch* b, hipStream
         a.cmat = c->d_tmvp_mat.p;
         a.wmat = c->d_tmvp_mat.p + (size_t)k * 16;
         a.gmat = c->d_tmvp_mat.p + (size_t)(k + m) * 16;
+        a.num_data = b->num_data ? b->num_data + b0 : nullptr;
         std::vector<Gf16T3Args> e(nprod);
         for (uint32_t pi = 0; pi < nprod; ++pi) {
             int dg[3] = {0, 0, 0};
@@ -761,6 +765,9 @@ static int rs16_tmvp2_encode(nfec_codec* c, const nfec_block_batch* b, hipStream
                 g.col_chunk = m;
                 g.col_base = off;
                 g.in_slots = k + m;
+                // shortened blocks: a source slot at or past the block's numData reads zeros
+                g.num_data = a.num_data;
+                g.nd_limit = k;
                 continue;
             }
             // the alpha input of level last_alpha (block of prefix P' = the digits before it),
@@ -812,6 +819,7 @@ int rs16_tmvp_encode(nfec_codec* c, const nfec_block_batch* b, hipStream_t s)
     t.m = c->m;
     t.vec_bytes = even;
     t.tw = c->d_twoff.p;
+    t.num_data = b->num_data;
     const int tr = launch_gf16_tw_tail(t, body, even - body, s);
     return tr ? fail(tr, "tmvp vector tail") : NFEC_OK;
 }
@@ -871,6 +879,7 @@ static int rs16_tmvp1_encode(nfec_codec* c, const nfec_block_batch* b, hipStream
         a.cmat = c->d_tmvp_mat.p;
         a.wmat = c->d_tmvp_mat.p + (size_t)k * 16;
         a.gmat = c->d_tmvp_mat.p + (size_t)(k + m) * 16;
+        a.num_data = b->num_data ? b->num_data + b0 : nullptr;
         Gf16T3Args e[3];
         for (int i = 0; i < 3; ++i) {
             e[i].nblocks = nb;
@@ -911,6 +920,20 @@ static int rs16_tmvp1_encode(nfec_codec* c, const nfec_block_batch* b, hipStream
         e[2].col_base = 0;
         e[2].in_slots = k + m;
         e[2].out_slot0 = k + cw;
+        if (a.num_data) {
+            // shortened blocks (tower kernel only): P1 and P2 mask the source slots at or past
+            // the block's numData; P0 (over the pair sums) and P2 write the parity rows after
+            // it, slot numData + r
+            for (int i = 0; i < 3; ++i) {
+                e[i].num_data = a.num_data;
+                e[i].nd_limit = k;
+            }
+            e[0].nd_outputs_only = 1;
+            e[0].out_slot0 = 0;
+            e[0].out_after_data = 1;
+            e[2].out_slot0 = cw;
+            e[2].out_after_data = 1;
+        }
         // a shape the kernels do not cover shows on the first sub-batch, before any parity byte
         // is written: NFEC_ENOTSUP then hands the batch to the one-product encode
         if ((rc = launch_tmvp_prescale(a, s)))
@@ -961,7 +984,7 @@ int launch_rt_encode(nfec_codec* c, const nfec_block_batch* b, hipStream_t s)
     return launch_rs8_rt(a, s);
 }
 
-int encode_device(nfec_codec* c, const nfec_block_batch* b, hipStream_t s)
+static int encode_device_impl(nfec_codec* c, const nfec_block_batch* b, hipStream_t s, int& path)
 {
     const bool acc = b->flags & NFEC_ACCUMULATE;
     if (c->kind == NFEC_RS8 && !force_generic()) {
@@ -980,6 +1003,7 @@ int encode_device(nfec_codec* c, const nfec_block_batch* b, hipStream_t s)
         // hand-allocated assembly kernels first (NFEC_ASM=0 disables them for A/B runs): the
         // 4-role-wave kernels sharing each column's transpose, then the 2-role kernels
         if (use_asm() && use_q4()) {
+            path = NFEC_PATH_FIXED;
             const int rc = launch_rs8_q4_encode(c->k, c->m, e, s);
             if (rc != NFEC_ENOTSUP) return rc == NFEC_OK ? NFEC_OK : fail(rc, "q4 encode launch failed");
         }
@@ -989,15 +1013,18 @@ int encode_device(nfec_codec* c, const nfec_block_batch* b, hipStream_t s)
             if (rc != NFEC_ENOTSUP) return rc == NFEC_OK ? NFEC_OK : fail(rc, "assembly encode launch failed");
         }
 #endif
+        path = NFEC_PATH_FIXED;
         const int rc = launch_rs8_bitsliced_encode(c->k, c->m, e, s);
         if (rc != NFEC_ENOTSUP) return rc == NFEC_OK ? NFEC_OK : fail(rc, "bit-sliced encode launch failed");
     }
     if (c->kind == NFEC_RS8 && !force_generic()) {
         // any other shape, and shortened batches (per-block mode: the block's numData columns,
         // parity at slot numData + r): bit-sliced with runtime coefficients
+        path = NFEC_PATH_RUNTIME;
         const int rc = launch_rt_encode(c, b, s);
         if (rc != NFEC_ENOTSUP) return rc;
     }
+    path = NFEC_PATH_GENERIC;
     if (c->kind == NFEC_RS8) {
         Gf8MatmulArgs a;
         a.in_base = static_cast<const uint8_t*>(b->blocks);
@@ -1020,7 +1047,11 @@ int encode_device(nfec_codec* c, const nfec_block_batch* b, hipStream_t s)
     }
     if (c->kind == NFEC_RS16) {
         static const bool use_bs16 = diag_knob("NFEC_GF16_BS", 1) != 0;
-        if (c->tmvp && !b->num_data && !acc) {
+        // (shortened batches: on the tower kernel, whose products mask each block's source
+        // slots at its numData; the prescale masks them too and the postscale writes slot
+        // numData + r)
+        if (c->tmvp && !acc && (!b->num_data || c->tw)) {
+            path = NFEC_PATH_RS16_SPLIT;
             const int rc = rs16_tmvp_encode(c, b, s);
             if (rc != NFEC_ENOTSUP) return rc;
         }
@@ -1041,10 +1072,12 @@ int encode_device(nfec_codec* c, const nfec_block_batch* b, hipStream_t s)
             t.offs = c->d_t3off.p;
             t.tw = c->d_twoff.p;
             t.accumulate = acc;
+            path = NFEC_PATH_RS16_PRODUCT;
             const int rc = !c->tw ? launch_rs16_product(c, t, s)
                            : rs16_tw_full_covers(t) ? launch_rs16_tw_full(t, s) : NFEC_ENOTSUP;
             if (rc != NFEC_ENOTSUP) return rc;
         }
+        path = NFEC_PATH_GENERIC;
         if (use_bs16 && c->d_sel16.p) {
             Gf16BsEncArgs e;
             e.base = static_cast<const uint8_t*>(b->blocks);
@@ -1101,6 +1134,7 @@ int encode_device(nfec_codec* c, const nfec_block_batch* b, hipStream_t s)
         e.xcd_remap = bs_flags() & 1u;
         e.nt_store = (bs_flags() >> 1) & 1u;
         if (use_q4()) {
+            path = NFEC_PATH_FIXED;
             const int rc = launch_mdp_q4_encode(c->k, c->m, e, s);
             if (rc != NFEC_ENOTSUP) return rc == NFEC_OK ? NFEC_OK : fail(rc, "MDP q4 encode launch failed");
         }
@@ -1111,9 +1145,11 @@ int encode_device(nfec_codec* c, const nfec_block_batch* b, hipStream_t s)
     }
     if (!force_generic()) {
         // other shapes and shortened blocks (the block map of each block length as a table)
+        path = NFEC_PATH_RUNTIME;
         const int rc = launch_rt_encode(c, b, s);
         if (rc != NFEC_ENOTSUP) return rc;
     }
+    path = NFEC_PATH_GENERIC;
     Gf8MatmulArgs a;
     a.in_base = static_cast<const uint8_t*>(b->blocks);
     a.in_block_stride = b->block_stride;
@@ -1133,6 +1169,15 @@ int encode_device(nfec_codec* c, const nfec_block_batch* b, hipStream_t s)
     a.nblocks = b->nblocks;
     a.vec_bytes = c->vec;
     return launch_gf8_matmul(a, false, s);
+}
+
+// counts each batch encode by the path that took it (nfec_codec_encode_paths)
+int encode_device(nfec_codec* c, const nfec_block_batch* b, hipStream_t s)
+{
+    int path = NFEC_PATH_GENERIC;
+    const int rc = encode_device_impl(c, b, s, path);
+    if (rc == NFEC_OK) c->enc_paths[path].fetch_add(1, std::memory_order_relaxed);
+    return rc;
 }
 
 // ---- RS16 decode on the tower kernel, every block ----
@@ -2106,6 +2151,17 @@ int nfec_codec_features(const nfec_codec* c)
     return (p->tmvp ? NFEC_FEATURE_RS16_TOEPLITZ : 0) | (p->tmvp_levels == 2 ? NFEC_FEATURE_RS16_TOEPLITZ2 : 0);
 }
 
+int nfec_codec_encode_paths(const nfec_codec* c, uint64_t* counts, uint32_t n)
+{
+    if (!c || (!counts && n)) return fail(NFEC_EINVAL, "null argument");
+    for (uint32_t i = 0; i < n; ++i) {
+        uint64_t v = i < NFEC_PATH_COUNT ? c->enc_paths[i].load(std::memory_order_relaxed) : 0;
+        for (const auto& st : c->stripes) v += i < NFEC_PATH_COUNT ? st->enc_paths[i].load(std::memory_order_relaxed) : 0;
+        counts[i] = v;
+    }
+    return NFEC_PATH_COUNT;
+}
+
 int nfec_codec_get_generator(const nfec_codec* c, void* host_out, size_t bytes)
 {
     if (!c || !host_out) return fail(NFEC_EINVAL, "null argument");
@@ -2302,8 +2358,8 @@ unsigned host_copy_threads();
 // or symbols (GF(2^16)), row dot products over pieces of the vectors, so a piece of every column
 // stays in cache while all rows take it; a repair of more than 8 MiB of products splits the
 // vectors over host threads (disjoint element ranges, no sharing).
-static void host_rows_apply(bool wide, void* const* dst, uint32_t nrows, const void* const* srcs, uint32_t ncol,
-                            const uint16_t* coef, size_t nelem, bool acc)
+static int host_rows_apply(bool wide, void* const* dst, uint32_t nrows, const void* const* srcs, uint32_t ncol,
+                           const uint16_t* coef, size_t nelem, bool acc)
 {
     const int isa = host_gf8_isa();
     const uint64_t work = (uint64_t)nrows * ncol * nelem * (wide ? 2 : 1);
@@ -2327,11 +2383,11 @@ static void host_rows_apply(bool wide, void* const* dst, uint32_t nrows, const v
                             : 1u;
     if (nt <= 1) {
         run(0, nelem);
-        return;
+        return NFEC_OK;
     }
     // ranges in multiples of 128 elements, on the process's host pool
     const size_t per = ((nelem + nt - 1) / nt + 127) & ~(size_t)127;
-    host_parallel_for(nt, [&](unsigned t) {
+    return host_parallel_for(nt, [&](unsigned t) {
         const size_t e0 = std::min(nelem, t * per), e1 = std::min(nelem, e0 + per);
         if (e0 < e1) run(e0, e1);
     });
@@ -2342,7 +2398,7 @@ static void host_rows_apply(bool wide, void* const* dst, uint32_t nrows, const v
 // Lambda(1 / gamma_v)] / (gamma_v beta_r + 1) over the surviving slots v, written over the erased
 // source (the reference's syndrome decode, normEncoderMDP.cpp:333-430, reads erased source as
 // zeros and missing parity as absent).  The list is already validated and es > 0.
-static void mdp_decode_host(const nfec_codec* c, void* const* vectors, uint32_t nd, uint32_t ec,
+static int mdp_decode_host(const nfec_codec* c, void* const* vectors, uint32_t nd, uint32_t ec,
                             const uint32_t* locs, uint32_t es)
 {
     const Field& f = gf8();
@@ -2390,7 +2446,7 @@ static void mdp_decode_host(const nfec_codec* c, void* const* vectors, uint32_t 
             coef[(size_t)r * ncol + j] = (uint16_t)f.exp[(lrow[r] + lcols[j] + 255u - f.log[w1]) % 255u];
         }
     }
-    host_rows_apply(false, dst.data(), es, srcs.data(), ncol, coef.data(), c->vec, false);
+    return host_rows_apply(false, dst.data(), es, srcs.data(), ncol, coef.data(), c->vec, false);
 }
 
 int nfec_decode_vectors_host(nfec_codec* c, void* const* vectors, uint32_t num_data, uint32_t erasure_count,
@@ -2412,8 +2468,8 @@ int nfec_decode_vectors_host(nfec_codec* c, void* const* vectors, uint32_t num_d
     }
     if (es == 0) return (int)erasure_count;  // only parity lost: nothing is filled (:732)
     if (c->kind == NFEC_MDP) {
-        mdp_decode_host(c, vectors, nd, erasure_count, erasure_locs, es);
-        return (int)erasure_count;
+        const int rc = mdp_decode_host(c, vectors, nd, erasure_count, erasure_locs, es);
+        return rc ? rc : (int)erasure_count;
     }
     const bool wide = c->kind == NFEC_RS16;
     const Field& f = wide ? gf16() : gf8();
@@ -2482,8 +2538,8 @@ int nfec_decode_vectors_host(nfec_codec* c, void* const* vectors, uint32_t num_d
             coef[(size_t)s * ncol + j] = (uint16_t)f.exp[md(lA[s] + lcol[j] - L(xs[s] ^ pts[j]))];
     }
     // RS16: an odd last byte is never touched
-    host_rows_apply(wide, dst.data(), es, srcs.data(), ncol, coef.data(), wide ? c->vec / 2 : c->vec, true);
-    return (int)erasure_count;
+    const int rc = host_rows_apply(wide, dst.data(), es, srcs.data(), ncol, coef.data(), wide ? c->vec / 2 : c->vec, true);
+    return rc ? rc : (int)erasure_count;
 }
 
 // Repair products up to which one-block Decode stays on the host, from tools/percall
@@ -2622,9 +2678,9 @@ uint8_t* host_device_ptr(const void* p)
 unsigned host_copy_threads() { return host_pool_size(); }
 
 // rows x width bytes, strided on both sides, split over host threads for large copies
-void copy2d(uint8_t* dst, uint64_t dpitch, const uint8_t* src, uint64_t spitch, uint64_t width, uint32_t rows)
+int copy2d(uint8_t* dst, uint64_t dpitch, const uint8_t* src, uint64_t spitch, uint64_t width, uint32_t rows)
 {
-    if (rows == 0 || width == 0) return;
+    if (rows == 0 || width == 0) return NFEC_OK;
     auto run = [=](uint32_t r0, uint32_t r1) {
         if (dpitch == width && spitch == width) {
             std::memcpy(dst + r0 * width, src + r0 * width, (size_t)(r1 - r0) * width);
@@ -2637,10 +2693,10 @@ void copy2d(uint8_t* dst, uint64_t dpitch, const uint8_t* src, uint64_t spitch, 
                                                       std::max<uint64_t>(1, bytes >> 22));
     if (nt <= 1) {
         run(0, rows);
-        return;
+        return NFEC_OK;
     }
     const uint32_t per = (rows + nt - 1) / nt;
-    host_parallel_for(nt, [&](unsigned t) {
+    return host_parallel_for(nt, [&](unsigned t) {
         const uint32_t r0 = std::min<uint32_t>(rows, t * per), r1 = std::min<uint32_t>(rows, r0 + per);
         if (r0 < r1) run(r0, r1);
     });
@@ -2824,7 +2880,7 @@ static int host_decode_zc(nfec_codec* c, const nfec_block_batch* hb, HostSlot& s
         mv.src_block_stride = hbs;
     } else {
         if (!s.pin_dev) return fail(NFEC_EDEVICE, "pinned staging is not device-mapped");
-        copy2d(s.pin, dbs, hsrc, hbs, ul, nb);
+        if (const int rc = copy2d(s.pin, dbs, hsrc, hbs, ul, nb)) return rc;
         mv.src = s.pin_dev;
         mv.src_block_stride = dbs;
     }
@@ -3017,7 +3073,9 @@ static int run_host_batch(nfec_codec* c, const nfec_block_batch* hb, const uint1
         NFEC_HIP(hipEventSynchronize(s.done));
         if (!pinned)
             for (const auto& pc : dn)
-                copy2d(hbase + (uint64_t)j.b0 * hbs + pc.first, hbs, s.pin + pc.first, dbs, decode ? j.dl : pc.second, j.nb);
+                if (const int rc = copy2d(hbase + (uint64_t)j.b0 * hbs + pc.first, hbs, s.pin + pc.first, dbs,
+                                          decode ? j.dl : pc.second, j.nb))
+                    return rc;
         if (decode && status) std::memcpy(status + j.b0, s.hstat, (size_t)j.nb * 4);
         return NFEC_OK;
     };
@@ -3050,7 +3108,7 @@ static int run_host_batch(nfec_codec* c, const nfec_block_batch* hb, const uint1
         if (pinned) {
             ae = hipMemcpy2DAsync(s.dev + up_off, dbs, hsrc + up_off, hbs, ul, j.nb, hipMemcpyHostToDevice, s.st);
         } else {
-            copy2d(s.pin + up_off, dbs, hsrc + up_off, hbs, ul, j.nb);
+            if ((rc = copy2d(s.pin + up_off, dbs, hsrc + up_off, hbs, ul, j.nb))) return bail(rc);
             ae = hipMemcpyAsync(s.dev, s.pin, (size_t)(j.nb - 1) * dbs + up_off + ul, hipMemcpyHostToDevice, s.st);
         }
         uint16_t* dnd = nullptr;
@@ -3120,16 +3178,16 @@ static int run_host_batch(nfec_codec* c, const nfec_block_batch* hb, const uint1
 namespace {
 
 extern "C++" template <typename F>
-void parallel_blocks(uint32_t nb, uint64_t bytes, F fn)
+int parallel_blocks(uint32_t nb, uint64_t bytes, F fn)
 {
     const unsigned nt = (unsigned)std::min<uint64_t>(std::min<uint64_t>(host_copy_threads(), nb),
                                                       std::max<uint64_t>(1, bytes >> 22));
     if (nt <= 1) {
         fn(0u, nb);
-        return;
+        return NFEC_OK;
     }
     const uint32_t per = (nb + nt - 1) / nt;
-    host_parallel_for(nt, [&](unsigned t) {
+    return host_parallel_for(nt, [&](unsigned t) {
         const uint32_t b0 = std::min<uint32_t>(nb, t * per), b1 = std::min<uint32_t>(nb, b0 + per);
         if (b0 < b1) fn(b0, b1);
     });
@@ -3138,10 +3196,10 @@ void parallel_blocks(uint32_t nb, uint64_t bytes, F fn)
 // the segment-list gather of blocks [b0, b0 + nb): block b's slots [0, numData_b + extra) from
 // its pointer list (vecs[b * n + s]; NULL: zero) into dst + (b - b0) * dbs + s * ss, on the host
 // pool.  extra: m when the parity is read too (decode, accumulate), else 0.
-void gather_segments(uint8_t* dst, uint64_t dbs, uint64_t ss, void* const* vecs, uint32_t n, uint32_t b0, uint32_t nb,
+int gather_segments(uint8_t* dst, uint64_t dbs, uint64_t ss, void* const* vecs, uint32_t n, uint32_t b0, uint32_t nb,
                      const uint16_t* num_data, uint32_t k, uint32_t extra, uint32_t vec)
 {
-    parallel_blocks(nb, (uint64_t)nb * n * vec, [&](uint32_t i0, uint32_t i1) {
+    return parallel_blocks(nb, (uint64_t)nb * n * vec, [&](uint32_t i0, uint32_t i1) {
         for (uint32_t i = i0; i < i1; ++i) {
             const uint32_t b = b0 + i;
             const uint32_t up = (num_data ? num_data[b] : k) + extra;
@@ -3204,10 +3262,11 @@ static int run_host_vectors(nfec_codec* c, void* const* vecs, uint32_t nblocks, 
     auto gather = [&](HostSlot& s, const Job& j) {
         // encode without accumulate reads the source only; everything else reads the whole
         // listed block (absent parity is zero, as MDP's decoder treats it)
-        gather_segments(s.pin, dbs, ss, vecs, n, j.b0, j.nb, num_data, c->k, (!decode && !acc) ? 0u : c->m, c->vec);
+        return gather_segments(s.pin, dbs, ss, vecs, n, j.b0, j.nb, num_data, c->k, (!decode && !acc) ? 0u : c->m,
+                               c->vec);
     };
     auto scatter = [&](HostSlot& s, const Job& j) {
-        parallel_blocks(j.nb, (uint64_t)j.nb * (uint64_t)c->m * c->vec, [&](uint32_t i0, uint32_t i1) {
+        return parallel_blocks(j.nb, (uint64_t)j.nb * (uint64_t)c->m * c->vec, [&](uint32_t i0, uint32_t i1) {
             for (uint32_t i = i0; i < i1; ++i) {
                 const uint32_t b = j.b0 + i;
                 const uint32_t nd = num_data ? num_data[b] : c->k;
@@ -3230,7 +3289,7 @@ static int run_host_vectors(nfec_codec* c, void* const* vecs, uint32_t nblocks, 
         if (!j.busy) return NFEC_OK;
         j.busy = false;
         NFEC_HIP(hipEventSynchronize(sl[i]->done));
-        scatter(*sl[i], j);
+        if (const int rc = scatter(*sl[i], j)) return rc;
         if (decode && status) std::memcpy(status + j.b0, sl[i]->hstat, (size_t)j.nb * 4);
         return NFEC_OK;
     };
@@ -3246,7 +3305,7 @@ static int run_host_vectors(nfec_codec* c, void* const* vecs, uint32_t nblocks, 
         Job& j = jobs[i];
         j.b0 = b0;
         j.nb = std::min(chunk, nblocks - b0);
-        gather(s, j);
+        if ((rc = gather(s, j))) return bail(rc);
         // decode: the staged slots the decode reads go up by the zero-copy gather kernel (the
         // erased source and unused parity stay on the host), the repaired ones come down by
         // the scatter kernel (launch_slot_move, as in run_host_batch)
@@ -3478,6 +3537,18 @@ int nfec_host_threads(uint32_t* pool, uint32_t* usable_cores, uint32_t* visible_
     return NFEC_OK;
 }
 
+int nfec_util_pool_check(uint32_t pieces, int mode)
+{
+    if (mode < 0 || mode > 2 || (mode && pieces < 2)) return fail(NFEC_EINVAL, "bad argument");
+    std::atomic<uint32_t> ran{0};
+    const int rc = host_parallel_for(pieces, [&](unsigned i) {
+        if (mode == 1 && i == 1) throw std::bad_alloc();
+        if (mode == 2 && i == 1) throw std::runtime_error("pool check");
+        ran.fetch_add(1);
+    });
+    return rc ? rc : (int)ran.load();
+}
+
 int nfec_util_gather_probe(void* const* vectors, uint32_t nblocks, uint32_t slots, uint32_t vector_size,
                            uint32_t nstripes, uint32_t reps, double* seconds, uint32_t* max_active)
 {
@@ -3498,8 +3569,8 @@ int nfec_util_gather_probe(void* const* vectors, uint32_t nblocks, uint32_t slot
     auto stripe = [&](uint32_t i) {
         const uint32_t lo = (uint32_t)((uint64_t)nblocks * i / nstripes), hi = (uint32_t)((uint64_t)nblocks * (i + 1) / nstripes);
         for (uint32_t b0 = lo; b0 < hi; b0 += chunk)
-            gather_segments(stage[i].get(), dbs, ss, vectors, slots, b0, std::min(chunk, hi - b0), nullptr, slots, 0,
-                            vector_size);
+            (void)gather_segments(stage[i].get(), dbs, ss, vectors, slots, b0, std::min(chunk, hi - b0), nullptr, slots,
+                                  0, vector_size);
     };
     auto pass = [&] {
         std::vector<std::thread> th;

@@ -8,6 +8,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <functional>
+#include <atomic>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -59,7 +60,9 @@ unsigned host_usable_cores();
 unsigned host_pool_size();
 unsigned host_pool_workers();  // workers actually running (starts the pool)
 unsigned host_pool_max_active(bool reset);  // most pool pieces that ran at once (since the last reset)
-void host_parallel_for(unsigned n, const std::function<void(unsigned)>& fn);
+// returns NFEC_OK, or the status of the first piece that threw (NFEC_ENOMEM for std::bad_alloc,
+// NFEC_EINVAL for anything else; nfec_last_error names it) after every piece has run
+[[nodiscard]] int host_parallel_for(unsigned n, const std::function<void(unsigned)>& fn);
 
 // ---------------------------------------------------------------------------------
 // Host field arithmetic (gf_host.cpp).  GF(2^8) on 0x11d and GF(2^16) on 0x1100B with
@@ -233,9 +236,14 @@ struct Gf16T3Args {
     uint64_t block_stride = 0;
     uint32_t seg_stride = 0;
     uint32_t nblocks = 0;
-    // per block numData (tower kernel, flat mode only: columns at or past it read as zeros; the
-    // shared-table kernel takes unshortened batches only)
+    // per block numData (tower kernel, flat mode only: columns whose source slot -- through the
+    // column map -- is at or past it read as zeros; the shared-table kernel takes unshortened
+    // batches only).  nd_limit: the largest valid numData (0: k; the Toeplitz split's products
+    // have k >> L columns but mask the codec's k source slots); nd_outputs_only: numData only
+    // places the output / accumulate rows (out_after_data), the loads are not masked (products
+    // over scratch columns)
     const uint16_t* num_data = nullptr;
+    uint32_t nd_limit = 0, nd_outputs_only = 0;
     uint32_t k = 0, m = 0, m_pad = 0;    // m_pad = gf16_t3_rows_padded(m)
     uint32_t vec_bytes = 0;              // multiple of 8
     const uint16_t* offs = nullptr;      // [k + 1][m_pad][48] LDS offsets (gf16_t3_offsets)
@@ -308,6 +316,10 @@ struct Rs16TmvpArgs {
     uint32_t hw = 0;
     uint8_t* sc = nullptr;
     uint64_t sc_block_stride = 0;
+    // shortened blocks (null: every block has k sources): block b's source columns at or past
+    // num_data[b] read as zeros in the prescale, and the postscale reads and writes its parity
+    // at slot num_data[b] + p; a block whose numData is 0 or past k is left alone
+    const uint16_t* num_data = nullptr;
 };
 bool rs16_tmvp_plan(uint32_t k, uint32_t m, const std::vector<uint32_t>& gen, std::vector<uint32_t> prod[3],
                     std::vector<uint16_t>& cmat, std::vector<uint16_t>& wmat, std::vector<uint16_t>& gmat);

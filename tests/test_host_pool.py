@@ -71,3 +71,61 @@ def test_pool_respects_host_threads_override():
     r = subprocess.run([sys.executable, "-c", code], cwd=ROOT, capture_output=True, text=True, timeout=120,
                        env=dict(os.environ, NFEC_HOST_THREADS="3"))
     assert r.returncode == 0 and r.stdout.strip() == "3", r.stderr
+
+
+def test_throwing_piece_returns_an_error():
+    """a piece that throws (std::bad_alloc in a gather's allocation, anything else) neither ends
+    the process nor leaves the caller waiting: every piece runs and the call returns a status"""
+    L = N.lib()
+    assert L.nfec_util_pool_check(64, 0) == 64
+    assert L.nfec_util_pool_check(64, 1) == N.NFEC_ENOMEM
+    assert "out of memory" in N.last_error()
+    assert L.nfec_util_pool_check(64, 2) == N.NFEC_EINVAL
+    assert "pool check" in N.last_error()
+    assert L.nfec_util_pool_check(2, 1) == N.NFEC_ENOMEM
+    assert L.nfec_util_pool_check(64, 0) == 64  # the pool still works afterwards
+
+
+def _wait_child(pid, seconds=60):
+    import time
+
+    t0 = time.time()
+    while time.time() - t0 < seconds:
+        done, status = os.waitpid(pid, os.WNOHANG)
+        if done:
+            return os.waitstatus_to_exitcode(status)
+        time.sleep(0.05)
+    os.kill(pid, 9)
+    os.waitpid(pid, 0)
+    return None
+
+
+def test_pool_after_fork_runs_inline():
+    """a child forked after the pool started inherits the pool object but not its workers: its
+    pool calls (and a large host repair, which splits over the pool) run inline instead of
+    queueing for threads that do not exist"""
+    from norm_amd import NFEC_RS8, NormDecoderRS8, NormEncoderRS8
+
+    L = N.lib()
+    assert L.nfec_util_pool_check(32, 0) == 32  # the pool's workers run in this process
+    k, m, vec, e = 128, 127, 16384, 100         # 200 MB of products: past the 8 MiB split
+    enc, dec = NormEncoderRS8(options=N.NFEC_OPT_HOST_ONLY), NormDecoderRS8(options=N.NFEC_OPT_HOST_ONLY)
+    assert enc.Init(k, m, vec) and dec.Init(k, m, vec)
+    blk = np.random.default_rng(3).integers(0, 256, (k + m, vec), dtype=np.uint8)
+    blk[k:] = 0
+    for s in range(k):
+        enc.Encode(s, blk[s], [blk[k + p] for p in range(m)])
+    want = blk.copy()
+    locs = list(range(1, k, k // e))[:e]  # source erasures only (parity is never filled)
+    for s in locs:
+        blk[s] = 0
+    pid = os.fork()
+    if pid == 0:  # child: no pytest machinery, exit code only
+        code = 1
+        try:
+            if L.nfec_util_pool_check(32, 0) == 32 and L.nfec_util_pool_check(8, 1) == N.NFEC_ENOMEM:
+                n = dec.Decode([blk[s] for s in range(k + m)], k, e, locs, host=True)
+                code = 0 if n == e and np.array_equal(blk, want) else 2
+        finally:
+            os._exit(code)
+    assert _wait_child(pid) == 0

@@ -34,7 +34,10 @@ def main():
     p.add_argument("--vec", type=int, default=1400)
     p.add_argument("--erasures", type=int, default=-1)
     p.add_argument("--shortened", action="store_true",
-                   help="numData drawn per block from [k/2, k] (every NORM object's last block is shortened)")
+                   help="numData drawn per block (--nd-dist; every NORM object's last block is shortened)")
+    p.add_argument("--nd-dist", default="half", choices=["half", "rfc"],
+                   help="half: numData uniform over [k/2, k]; rfc: k or k - 1 (RFC 5052 large and small "
+                        "blocks, NORM's block partition, normObject.cpp:203-231)")
     p.add_argument("--accumulate", action="store_true", help="decode with NFEC_ACCUMULATE (erased source zeroed)")
     p.add_argument("--loss", default="source", choices=["source", "uniform"],
                    help="source: erasures among the source segments (the headline pattern); uniform: "
@@ -78,7 +81,7 @@ def main():
     nd = None
     ndh = np.full(nb, k, np.int64)
     if a.shortened:
-        ndh = rng.integers(k // 2, k + 1, nb)
+        ndh = rng.integers(k // 2, k + 1, nb) if a.nd_dist == "half" else k - rng.integers(0, 2, nb)
         nd = torch.from_numpy(ndh.astype(np.uint16).view(np.int16)).cuda()
         na.fill_blocks(blocks, k, vec, 0x4E4F524D, per_block_num_data=nd)
     else:
@@ -121,6 +124,7 @@ def main():
         "codec": {na.NFEC_RS8: "RS8", na.NFEC_RS16: "RS16", na.NFEC_MDP: "MDP"}[kind],
         "k": k, "m": m, "vec": vec, "blocks": nb, "erasures": er, "loss": a.loss,
         "shortened": a.shortened, "accumulate": a.accumulate,
+        "nd_dist": a.nd_dist if a.shortened else None,
         "source_GB": round(float(ndh.sum()) * vec / 1e9, 3),
         "init_s": round(init_s, 3),
         "encode_ms": round(enc_ms, 3),
@@ -130,6 +134,7 @@ def main():
         from norm_amd import _native as N
         f = enc.features()
         out["toeplitz_levels"] = (2 if f & N.NFEC_FEATURE_RS16_TOEPLITZ2 else 1 if f & N.NFEC_FEATURE_RS16_TOEPLITZ else 0)
+    out["encode_paths"] = {n: c for n, c in enc.encode_paths().items() if c}
     if kind == na.NFEC_RS16 and vec % 8 == 0 and not a.shortened:
         out["op_roofline"] = rs16_op_roofline(enc, k, m, nb, vec, enc_ms)
     if er:
@@ -196,12 +201,18 @@ def rs16_op_roofline(enc, k, m, nb, vec, enc_ms):
         out["note"] = "no committed tower-kernel PMC summary for this shape (tools/pmc_r03.sh, PMC_SCRIPT=tools/bench_extra.py)"
         return out
     path, d = src
+    meta = d.get("_workload", {})
     kern = [v for kk, v in d.items() if kk != "_workload" and name in kk]
     if not kern:
         out["pmc"] = None
         return out
     c = kern[0]
     cycles = c["GRBM_GUI_ACTIVE"] / 8.0
+    # a large batch runs as several sub-batches (C4: two, each ~12.5 GB of split scratch), each
+    # with its own product launch: the PMC summary holds per-launch averages over `dispatches`
+    # launches of a run of `encodes` encodes (the pmc scripts run --warmup 1 --steps 1)
+    encodes = meta.get("encodes", 2)
+    launches = max(1, round(c.get("dispatches", encodes) / encodes))
     out.update({
         "pmc": os.path.relpath(path, ROOT),
         "cycles_per_launch": round(cycles),
@@ -210,9 +221,11 @@ def rs16_op_roofline(enc, k, m, nb, vec, enc_ms):
         "valu_issue_frac": round(c["SQ_INSTS_VALU"] * 2 / (1024 * cycles), 4),
         "salu_issue_frac": round(c["SQ_INSTS_SALU"] / (256 * cycles), 4),
         "branch_issue_frac": round(c.get("SQ_INSTS_BRANCH", 0) / (256 * cycles), 4),
-        "valu_lane_ops_frac_of_peak": round(c["SQ_INSTS_VALU"] * 64 / (enc_ms * 1e-3) / VALU_PEAK, 4),
+        "launches_per_encode": launches,
+        "valu_lane_ops_frac_of_peak": round(c["SQ_INSTS_VALU"] * launches * 64 / (enc_ms * 1e-3) / VALU_PEAK, 4),
         "note": "counters per launch of the product kernel; issue fractions against its own cycles "
-                "(VALU 2 cycles per wave64 instruction per SIMD, SALU / branch 1 per cycle per CU)",
+                "(VALU 2 cycles per wave64 instruction per SIMD, SALU / branch 1 per cycle per CU); "
+                "lane-op fraction: all product launches of one encode over the whole encode time",
     })
     return out
 

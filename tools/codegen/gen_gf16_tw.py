@@ -483,8 +483,11 @@ _uid = [0]
 def loads():
     """column s[S_C]'s 8 pieces -> the slot.  The pieces' byte offsets come from LDS (%[lo] + 80,
     shared by the workgroup's waves).  Flat shortened mode (bit 0 of %[md]): a piece whose block
-    has numData <= c reads zeros (its offset gets bit 31: past num_records; q = the piece's
-    numData - 1, u16 pairs at %[lq]), so each piece's block stops at its own numData"""
+    has numData <= the column's source slot reads zeros (its offset gets bit 31: past
+    num_records; q = the piece's numData - 1, u16 pairs at %[lq]), so each piece's block stops at
+    its own numData.  The slot is the column map's (s[S_COL] = slot * seg_stride, so the sign of
+    q * seg_stride - s[S_COL] decides): the Toeplitz split's products that read source columns
+    through the map (chunks, halves) mask the source slot, not their own column index"""
     x = slot()
     if "noload" in FLAGS:
         return []
@@ -502,7 +505,8 @@ def loads():
     for i in range(8):
         src = q[i // 2]
         masked += [f"v_lshrrev_b32 v{t}, 16, v{src}" if i & 1 else f"v_and_b32 v{t}, 0xffff, v{src}",
-                   f"v_subrev_u32 v{t}, s{S_C}, v{t}",                          # numData - 1 - c
+                   f"v_mul_u32_u24 v{t}, %[ss], v{t}",
+                   f"v_subrev_u32 v{t}, s{S_COL}, v{t}",                        # (numData - 1 - slot) ss
                    f"v_and_or_b32 v{o[i]}, v{t}, s{S_DESC + 2}, v{o[i]}",       # sign -> bit 31
                    f"buffer_load_dwordx2 v[{x[2 * i]}:{x[2 * i + 1]}], v{o[i]}, s[{S_DESC}:{S_DESC + 3}], s{S_COL} offen"]
     return (L + [f"s_bitcmp1_b32 %[md], 0", f"s_cbranch_scc0 Lldp{u}_%="] + masked +
@@ -864,11 +868,15 @@ __device__ __forceinline__ void tw_body(const Gf16T3Args& a, uint32_t wg)
     const uint64_t total = pb ? (uint64_t)a.vec_bytes : (uint64_t)a.nblocks * a.vec_bytes;
     const uint64_t f0 = pb ? (uint64_t)(group - pblk * chunks) * {GROUP_BYTES}u : (uint64_t)group * {GROUP_BYTES}u;
     if ((pb && pblk >= a.nblocks) || f0 >= total) return;  // workgroup-uniform, as the next exits
-    // flat shortened mode (num_data): every piece's block has its own numData; columns at or
-    // past it read zeros, and the output / accumulate rows may sit after it (out_after_data /
-    // acc_after_data: slot numData + r).  The item group runs to the largest numData among its
-    // blocks; a block whose numData is 0 or past k is left alone.
+    // flat shortened mode (num_data): every piece's block has its own numData; columns whose
+    // source slot is at or past it read zeros, and the output / accumulate rows may sit after it
+    // (out_after_data / acc_after_data: slot numData + r).  The item group runs to the largest
+    // numData among its blocks (the column map never maps a column below its own index); a
+    // block whose numData is 0 or past nd_limit (0: k) is left alone.  nd_outputs_only: numData
+    // places the rows but the loads are not masked (a Toeplitz product over scratch columns)
     const uint32_t lnd = !pb && a.num_data ? 1u : 0u;
+    const uint32_t lmask = lnd && !a.nd_outputs_only ? 1u : 0u;
+    const uint32_t ndk = a.nd_limit ? a.nd_limit : a.k;
     // rows actually needed (decode stage 1: the last substitute-parity row among the blocks it
     // serves, written by the plan; per-block mode: the block's e); workgroups past them leave
     // at once, waves past them only load, transpose and share their columns
@@ -878,15 +886,15 @@ __device__ __forceinline__ void tw_body(const Gf16T3Args& a, uint32_t wg)
         const int32_t e = (int32_t)__builtin_amdgcn_readfirstlane((uint32_t)a.blk_rows[pblk]);
         rlim = e > 0 ? min(rlim, (uint32_t)e) : 0u;
         kk = a.blk_cols ? min(kk, (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)a.blk_cols[pblk])) : min(kk, rlim);
-    }} else if (lnd) {{
+    }} else if (lmask) {{
         const uint32_t bf = (uint32_t)(f0 / a.vec_bytes), bl = (uint32_t)((min(f0 + {GROUP_BYTES}u, total) - 1u) / a.vec_bytes);
         uint32_t mx = 0;
         for (uint32_t b = bf + lane; b <= bl; b += 64u) {{
             const uint32_t v = a.num_data[b];
-            if (v >= 1u && v <= a.k) mx = max(mx, v);
+            if (v >= 1u && v <= ndk) mx = max(mx, v);
         }}
         for (int off = 32; off > 0; off >>= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, off));
-        kk = __builtin_amdgcn_readfirstlane(mx);
+        kk = __builtin_amdgcn_readfirstlane(min(kk, mx));
     }}
     // the rows in play spread evenly over whole workgroups of four passes (the table holds any
     // row range); the launch sized the grid for a.m rows, so later workgroups may leave
@@ -904,8 +912,8 @@ __device__ __forceinline__ void tw_body(const Gf16T3Args& a, uint32_t wg)
         const uint64_t f = f0 + (uint64_t)i * 512u + lane * 8u;
         const uint32_t b = pb ? b0 : (uint32_t)(f / a.vec_bytes);
         const uint32_t p = (uint32_t)(f - (uint64_t)(pb ? 0u : b) * a.vec_bytes);
-        const uint32_t raw = lnd && f < total ? (uint32_t)a.num_data[b] : a.k;
-        const bool ok = f < total && raw >= 1u && raw <= a.k;
+        const uint32_t raw = lnd && f < total ? (uint32_t)a.num_data[b] : ndk;
+        const bool ok = f < total && raw >= 1u && raw <= ndk;
         const uint32_t pnd = ok ? raw : 1u;
         q[i] = pnd - 1u;
         po[20 + i] = ok ? (uint32_t)((uint64_t)(b - b0) * a.block_stride) + p : 0x80000000u;
@@ -918,7 +926,7 @@ __device__ __forceinline__ void tw_body(const Gf16T3Args& a, uint32_t wg)
     }}
 #pragma unroll
     for (int i = 0; i < 4; ++i) po[16 + i] = (q[2 * i] & 0xFFFFu) | (q[2 * i + 1] << 16);
-    const uint32_t md = __builtin_amdgcn_readfirstlane(lnd);
+    const uint32_t md = __builtin_amdgcn_readfirstlane(lmask);
     const uint32_t lo = bs::lds_addr(po);
     const uint32_t lq = lo + 64u;
     const uint32_t xl = bs::lds_addr(xch) + lane * 8u;
@@ -941,9 +949,12 @@ __device__ __forceinline__ void tw_body(const Gf16T3Args& a, uint32_t wg)
 // checks the shape, fills the default output / accumulate layouts and the pass count
 int tw_prepare(const Gf16T3Args& a, Gf16T3Args& b, uint64_t& wgs, uint32_t rows)
 {{
-    // (numData masking is a flat-mode feature; the column map is the Toeplitz split's, unshortened)
-    if ((a.vec_bytes & 7u) || a.vec_bytes == 0 || !a.tw || a.k == 0 || (a.num_data && (a.blk_rows || a.col_chunk)))
+    // (numData masking is a flat-mode feature; with a column map it masks the mapped source slot,
+    // whose byte offset it compares with numData x seg_stride in 24-bit multiplies)
+    if ((a.vec_bytes & 7u) || a.vec_bytes == 0 || !a.tw || a.k == 0 || (a.num_data && a.blk_rows) ||
+        (a.num_data && (a.seg_stride >= (1u << 24) || a.nd_limit >= (1u << 16))))
         return NFEC_ENOTSUP;
+    const uint64_t ndk = a.nd_limit ? a.nd_limit : a.k;
     b = a;
     // the column map: chunks of col_div columns (or 2^col_shift), q = c / d by a multiply-high
     // with ceil(2^32 / d), exact for c, d < 2^16
@@ -971,8 +982,8 @@ int tw_prepare(const Gf16T3Args& a, Gf16T3Args& b, uint64_t& wgs, uint32_t rows)
     // every piece offset of a group ({GROUP_BYTES} bytes of flat positions) plus slot offsets within 2^31
     const uint64_t nbg = {GROUP_BYTES}u / a.vec_bytes + 2u;
     const uint64_t in_slots = a.in_slots ? a.in_slots : (uint64_t)a.k + a.m;
-    const uint64_t oslots = (uint64_t)b.out_slot0 + (b.out_after_data ? a.k : 0u) + a.m;
-    const uint64_t aslots = (uint64_t)b.acc_slot0 + (b.acc_after_data ? a.k : 0u) + a.m;
+    const uint64_t oslots = (uint64_t)b.out_slot0 + (b.out_after_data ? ndk : 0u) + a.m;
+    const uint64_t aslots = (uint64_t)b.acc_slot0 + (b.acc_after_data ? ndk : 0u) + a.m;
     if (nbg * a.block_stride + in_slots * a.seg_stride >= (1ull << 31) ||
         nbg * b.out_block_stride + oslots * b.out_seg_stride >= (1ull << 31) ||
         nbg * b.acc_block_stride + aslots * b.acc_seg_stride >= (1ull << 31))

@@ -290,8 +290,18 @@ def ab_off(c, i):
     return (c * 15 + i) * 512
 
 
-def role_asm(G, k, m, w, probe=None, cfg=DEFAULT):
+# shortened batches (per-block numData, RFC 5052 small blocks / an object's last block): the
+# lane's four items' numData as bytes in one input VGPR (%[nd], k <= 64); per load of column c
+# an item whose numData <= c reads zeros (offset | sign(numData - 1 - c) -> bit 31, past the
+# descriptor's num_records), and the parity of an item's block goes to slot numData + r.  Four
+# otherwise unused VGPRs of the default register map hold the masked offsets.
+SHORT_TMP = [120, 121, 124, 125]
+SHORT_ND = 9
+
+
+def role_asm(G, k, m, w, probe=None, cfg=DEFAULT, short=False):
     noload, nocompute, nolds = probe == "noload", probe == "nocompute", probe == "nolds"
+    assert not short or (k <= 64 and cfg is DEFAULT and probe is None)
     NS = cfg.nslot
     rows = m // NW
     r0 = w * rows
@@ -314,7 +324,14 @@ def role_asm(G, k, m, w, probe=None, cfg=DEFAULT):
         rs = cfg.ring_slot(step % NS)
         out = [f"s_mul_i32 s{S_COL}, %[ss], {col}"]
         for q in range(4):
-            out.append(f"buffer_load_dwordx2 v[{rs[2 * q]}:{rs[2 * q + 1]}], {offs[q]}, s[{S_LRS}:{S_LRS + 3}], s{S_COL} offen{cfg.lpol}")
+            addr = offs[q]
+            if short:
+                t = SHORT_TMP[q]
+                out += [f"v_bfe_u32 v{t}, %[nd], {8 * q}, 8",
+                        f"v_subrev_u32 v{t}, {col + 1}, v{t}",                     # numData - 1 - c
+                        f"v_and_or_b32 v{t}, v{t}, s{S_LRS + 2}, {offs[q]}"]       # sign -> bit 31
+                addr = f"v{t}"
+            out.append(f"buffer_load_dwordx2 v[{rs[2 * q]}:{rs[2 * q + 1]}], {addr}, s[{S_LRS}:{S_LRS + 3}], s{S_COL} offen{cfg.lpol}")
         return out
 
     for s in range(min(NS, steps)):
@@ -366,11 +383,17 @@ def role_asm(G, k, m, w, probe=None, cfg=DEFAULT):
             L += column_code(G, r0, rows, NW * s + c, pbuf(buf), first=False, cfg=cfg)
             if t + 2 < len(others):
                 L += reads(others[t + 2], buf)
-    # epilogue: planes back to bytes, optional accumulate, store
+    # epilogue: planes back to bytes, optional accumulate, store (shortened: the items' parity
+    # slot 0 is numData, so the row offsets are the items' offsets + numData * seg_stride)
+    if short:
+        for q in range(4):
+            t = SHORT_TMP[q]
+            L += [f"v_bfe_u32 v{t}, %[nd], {8 * q}, 8", f"v_mad_u32_u24 v{t}, v{t}, %[ss], {offs[q]}"]
+        offs = [f"v{t}" for t in SHORT_TMP]
     for r in range(rows):
         acc = [acc_reg(r, i) for i in range(8)]
         L += transpose(acc, epi_temps(cfg))
-        L.append(f"s_mul_i32 s{S_ROW}, %[ss], {k + r0 + r}")
+        L.append(f"s_mul_i32 s{S_ROW}, %[ss], {(0 if short else k) + r0 + r}")
         tmp = cfg.ring_slot(0)
         L.append("s_cmp_eq_u32 %[acc], 0")
         L.append(f"s_cbranch_scc1 Lnoacc_{r}_%=")
@@ -458,8 +481,9 @@ def shared_step(G, r0, rows, s, w, own, others, cfg):
     return L
 
 
-def clobbers(cfg):
-    v = [f'"v{i}"' for i in range(4 * NQUAD) if i not in cfg.in_regs]
+def clobbers(cfg, short=False):
+    keep = cfg.in_regs + ([SHORT_ND] if short else [])
+    v = [f'"v{i}"' for i in range(4 * NQUAD) if i not in keep]
     s = [f'"s{i}"' for i in range(S_LRS, S_ROW + 1)]
     return ", ".join(v + s + ['"scc"', '"memory"'])
 
@@ -472,23 +496,24 @@ def lds_bytes(cfg):
     return 2 * SLOT_BYTES
 
 
-def gen_kernel(k, m, G=None, prefix="rs8_q4_enc", probe=None, suffix="", cfg=DEFAULT):
+def gen_kernel(k, m, G=None, prefix="rs8_q4_enc", probe=None, suffix="", cfg=DEFAULT, short=False):
     assert k % NW == 0 and m % NW == 0
     G = G if G is not None else generator(k, m)
-    K = f"{prefix}{suffix}_k{k}_m{m}"
+    K = f"{prefix}{suffix}{'_sh' if short else ''}_k{k}_m{m}"
     out = []
     la4 = ', [la4] "v"(la4)' if cfg.share == "A" else ""
+    nd_in = ', [nd] "v"(ndp)' if short else ""
     for w in range(NW):
-        body = role_asm(G, k, m, w, probe, cfg)
+        body = role_asm(G, k, m, w, probe, cfg, short)
         s = "\\n\"\n        \"".join(body)
-        out.append(f"""__device__ __forceinline__ void {K}_role{w}(const bs::EncArgs& a, const bs::Items& it, const uint32_t o[4], uint32_t la, uint32_t la4)
+        out.append(f"""__device__ __forceinline__ void {K}_role{w}(const bs::EncArgs& a, const bs::Items& it, const uint32_t o[4], uint32_t la, uint32_t la4, uint32_t ndp)
 {{
     asm volatile(
         "{s}\\n"
         :
         : [ib] "s"(it.wbase), [ob] "s"(it.obase), [ss] "s"(a.seg_stride), [acc] "s"(a.accumulate),
-          [o0] "v"(o[0]), [o1] "v"(o[1]), [o2] "v"(o[2]), [o3] "v"(o[3]), [la] "v"(la){la4}
-        : {clobbers(cfg)});
+          [o0] "v"(o[0]), [o1] "v"(o[1]), [o2] "v"(o[2]), [o3] "v"(o[3]), [la] "v"(la){la4}{nd_in}
+        : {clobbers(cfg, short)});
 }}""")
     body = [f"__global__ __launch_bounds__({64 * NW}, {NW}) void {K}(bs::EncArgs a)", "{"]
     body.append(f"    __shared__ uint32_t lds[{lds_bytes(cfg) // 4}];")
@@ -500,18 +525,33 @@ def gen_kernel(k, m, G=None, prefix="rs8_q4_enc", probe=None, suffix="", cfg=DEF
     body.append("    uint32_t o[4];")
     body.append("#pragma unroll")
     body.append("    for (int i = 0; i < 4; ++i) o[i] = it.nbytes[i] == 8 ? it.off[i] : 0x80000000u;")
+    body.append("    uint32_t ndp = 0;")
+    if short:
+        body.append(f"    // the items' numData as bytes (a block with numData 0 or past {k} is left alone)")
+        body.append("    const uint32_t ips = a.vec >> 3, ib = bs::wg_index(a.xcd_remap) * 256u;")
+        body.append("#pragma unroll")
+        body.append("    for (int i = 0; i < 4; ++i) {")
+        body.append("        const uint32_t g = ib + (uint32_t)i * 64u + lane;")
+        body.append(f"        uint32_t nd = {k}u;")
+        body.append("        if (g < a.nblocks * ips) {")
+        body.append("            const uint32_t v = a.num_data[g / ips];")
+        body.append(f"            if (v >= 1u && v <= {k}u) nd = v;")
+        body.append("            else o[i] = 0x80000000u;")
+        body.append("        }")
+        body.append("        ndp |= nd << (8 * i);")
+        body.append("    }")
     body.append("    const uint32_t la = bs::lds_addr(lds) + lane * 8u;   // b64 rows: 8 bytes per lane")
     body.append("    const uint32_t la4 = bs::lds_addr(lds) + lane * 4u;  // b32 rows")
     for w in range(NW):
         kw = "if" if w == 0 else "else if"
-        body.append(f"    {kw} (wave == {w}) {K}_role{w}(a, it, o, la, la4);")
+        body.append(f"    {kw} (wave == {w}) {K}_role{w}(a, it, o, la, la4, ndp);")
     body.append("}")
     out.append("\n".join(body))
     out.append(f"""
 static int launch_{K}(const bs::EncArgs& a, hipStream_t s)
 {{
     const uint64_t items = (uint64_t)a.nblocks * ((a.vec + 7) / 8);
-    if (a.num_data || (a.vec & 7u) || a.nt_store || items >= (1ull << 31) ||
+    if ({"!a.num_data" if short else "a.num_data"} || (a.vec & 7u) || a.nt_store || items >= (1ull << 31) ||
         !bs::offsets_fit(a.block_stride, a.seg_stride))
         return NFEC_ENOTSUP;
     const uint64_t wgs = (items + 255) / 256;
@@ -538,6 +578,7 @@ def main():
     ]
     for k, m in SHAPES:
         parts.append(gen_kernel(k, m))
+        parts.append(gen_kernel(k, m, short=True))
         if diag and (k, m) == (64, 32):
             for v, probe in PROBES.items():
                 parts.append(gen_kernel(k, m, probe=probe, suffix=f"_probe_{probe}"))
@@ -562,7 +603,7 @@ def main():
     for v in (VARIANTS if diag else ()):
         parts.append(f"    if (k == 64 && m == 32 && q4_variant() == {v}) return launch_rs8_q4_enc_v{v}_k64_m32(a, s);")
     for k, m in SHAPES:
-        parts.append(f"    if (k == {k} && m == {m}) return launch_rs8_q4_enc_k{k}_m{m}(a, s);")
+        parts.append(f"    if (k == {k} && m == {m}) return a.num_data ? launch_rs8_q4_enc_sh_k{k}_m{m}(a, s) : launch_rs8_q4_enc_k{k}_m{m}(a, s);")
     parts.append("    return NFEC_ENOTSUP;")
     parts.append("}")
     parts.append("")

@@ -13,7 +13,7 @@ python3 - gpurun_out/pmc_$TAG/summary.json <<'PY'
 import json, sys
 p = sys.argv[1]
 d = json.load(open(p))
-d["_workload"] = {"workload": "c4", "k": 4096, "m": 256, "vec": 1400, "blocks": 4096,
+d["_workload"] = {"workload": "c4", "k": 4096, "m": 256, "vec": 1400, "blocks": 4096, "encodes": 2,
                   "counters": "rocprofv3 --pmc, one group per pass (tools/pmc_c4.sh); per-launch averages"}
 json.dump(d, open(p, "w"), indent=1, sort_keys=True)
 print(json.dumps({k: {c: v.get(c) for c in ("SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_BRANCH", "GRBM_GUI_ACTIVE")}

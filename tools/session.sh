@@ -12,6 +12,8 @@
 #              source loss, uniform loss over all k + m segments, shortened batches (numData in
 #              [k/2, k]), accumulate, and vec 1460 (vec % 8 != 0); one JSON line each
 #   c4         C4 RS16(4096,256) encode line (with its op roofline) under a kernel trace
+#   short      shortened batches (numData in {k, k-1} and in [k/2, k]) beside unshortened ones for
+#              RS16(400,100), C4 and RS8(64,32)/(64,16), under kernel traces
 #   pmc_rs16   PMC passes of the RS16(400,100) encode (tools/pmc_r03.sh; instruction mix, cycles,
 #              HBM bytes) -> pmc_tw_rs16_summary.json, which bench_extra's op roofline reads
 #   pmc_c4     PMC passes of C4 (tools/pmc_c4.sh)
@@ -69,6 +71,22 @@ for task in "$@"; do
         prof rs16_vec1460_uniform "$X" --workload rs16 --vec 1460 --loss uniform || die rs16_vec1460_uniform $? ;;
     c4)
         prof c4 "$R/tools/bench_extra.py" --workload c4 || die c4 $? ;;
+    short)
+        # shortened batches on the fast kernels (round 6): per shape the unshortened encode beside
+        # numData in {k, k - 1} (RFC 5052 large / small blocks) and numData over [k/2, k]; the lines
+        # carry encode_GiBps per source byte and the encode path that took the batches
+        X=$R/tools/bench_extra.py
+        prof short_rs16_full "$X" --workload rs16 --erasures 0 || die short $?
+        prof short_rs16_rfc "$X" --workload rs16 --erasures 0 --shortened --nd-dist rfc || die short $?
+        prof short_rs16_half "$X" --workload rs16 --shortened || die short $?
+        prof short_rs16_rfc_dec "$X" --workload rs16 --shortened --nd-dist rfc --loss uniform || die short $?
+        prof short_c4_full "$X" --workload c4 || die short $?
+        prof short_c4_rfc "$X" --workload c4 --shortened --nd-dist rfc || die short $?
+        prof short_rs8_full "$X" --workload rs8 || die short $?
+        prof short_rs8_rfc "$X" --workload rs8 --shortened --nd-dist rfc || die short $?
+        prof short_rs8_half "$X" --workload rs8 --shortened || die short $?
+        prof short_rs8_16_full "$X" --workload rs8 --m 16 --erasures 8 || die short $?
+        prof short_rs8_16_rfc "$X" --workload rs8 --m 16 --erasures 8 --shortened --nd-dist rfc || die short $? ;;
     pmc_rs16)
         # the encode alone (--erasures 0), so the tower kernel's counters are the encode's
         PMC_SCRIPT=tools/bench_extra.py PMC_ARGS="--workload rs16 --erasures 0 --steps 1 --warmup 1" \
@@ -77,7 +95,7 @@ for task in "$@"; do
         python3 - "$R/gpurun_out/pmc_${TAG}_rs16/summary.json" "$O/pmc_tw_rs16_summary.json" <<'PY' || die pmc_rs16 $?
 import json, sys
 d = json.load(open(sys.argv[1]))
-d["_workload"] = {"workload": "rs16", "k": 400, "m": 100, "vec": 1400, "blocks": 16384,
+d["_workload"] = {"workload": "rs16", "k": 400, "m": 100, "vec": 1400, "blocks": 16384, "encodes": 2,
                   "counters": "rocprofv3 --pmc, one group per pass (tools/session.sh pmc_rs16); encode only; per-launch averages"}
 json.dump(d, open(sys.argv[2], "w"), indent=1, sort_keys=True)
 PY
