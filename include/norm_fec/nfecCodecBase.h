@@ -13,9 +13,9 @@
 class NfecCodecBase
 {
   public:
-    // GPU used by codecs created afterwards in this process (one process per GPU); clears a
-    // device list set by SetDevices
-    static void SetDevice(int device) { default_device = device; num_devices = 0; }
+    // GPU used by codecs created afterwards in this process; clears a device list set by
+    // SetDevices (which spreads one codec over several GPUs from one process)
+    static void SetDevice(int device) { default_device = device; num_devices = 0; devices_chosen = true; }
     static int GetDevice() { return default_device; }
     // Several GPUs for codecs created afterwards (at most kMaxDevices; a device may repeat):
     // Init creates one codec striped over them (nfec_codec_create_ex), so a single-process
@@ -24,9 +24,12 @@ class NfecCodecBase
     enum { kMaxDevices = 64 };
     static bool SetDevices(const int* devices, int count);
     static int GetDevices(int* devices, int cap);  // the list (count returned; 1: the one device)
-    // With no usable gfx950 device, Init still succeeds when both per-call paths are on the host
-    // (the defaults): the codec is host-only (NFEC_OPT_HOST_ONLY), Encode / Decode run on the CPU
-    // and the batch calls return NFEC_EDEVICE.  SetHostFallback(false) makes Init fail instead.
+    // With no usable gfx950 device in the process (nfec_device_count() == 0) and no device
+    // chosen by SetDevice / SetDevices, Init still succeeds when both per-call paths are on the
+    // host (the defaults): the codec is host-only (NFEC_OPT_HOST_ONLY, a one-line notice on
+    // stderr), Encode / Decode run on the CPU and the batch calls return NFEC_EDEVICE.  Any other
+    // device failure (a bad ordinal or device list, an allocation failure on a present GPU) makes
+    // Init fail, as does SetHostFallback(false).
     static void SetHostFallback(bool on) { host_fallback = on; }
     static bool GetHostFallback() { return host_fallback; }
     bool IsHostOnly() const;
@@ -62,6 +65,7 @@ class NfecCodecBase
     static bool segment_on_host;
     static bool decode_on_host;
     static bool host_fallback;
+    static bool devices_chosen;  // SetDevice / SetDevices called: no host-only fallback
 };
 
 #endif  // NFEC_CODEC_BASE_H

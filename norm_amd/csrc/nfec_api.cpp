@@ -263,6 +263,9 @@ struct nfec_codec {
     ~nfec_codec()
     {
         async.shutdown();  // outstanding async requests complete before the codec goes away
+        // a host-only codec (device -1) holds no device state and never starts the HIP runtime
+        // (hipSetDevice(-1) would also leave an error in this thread's last-error slot)
+        if (host_only || device < 0) return;
         DeviceGuard g(device);
         stage.release();
         for (auto* b : {&d_coef, &d_gen, &d_exp, &w_coef1, &w_coef2, &w_z, &w_work, &s_block, &d_mdp_step, &w_tmvp})
@@ -378,22 +381,36 @@ static int launch_rs16_tw_full(const Gf16T3Args& t, hipStream_t s)
 // ---- codec construction ----
 // log W'(x_j) over the k source points and log W(y_p) at the parity points: the constants of
 // the closed-form plans (rs_plan2_kernel for RS8, rs16_plan_cf_kernel for RS16, the host repair)
+// The closed-form plans' constants: log W'(x_j) = sum_{l != j, l < k} log(x_j + x_l) over the
+// source points and log W(y_p) = sum_{l < k} log(y_p + x_l) at the parity points, with x_0 = 0,
+// x_l = alpha^(l-1), y_p = alpha^(k+p-1) (normEncoderRS8.cpp:432-439).  Since
+// alpha^a + alpha^b = alpha^a (1 + alpha^(b-a)), with g(d) = log(1 + alpha^d):
+//   log W'(x_0)  = sum_{l=1}^{k-1} (l - 1) = (k-1)(k-2)/2
+//   log W'(x_j)  = (k-1)(j-1) + sum_{d=1-j, d != 0}^{k-1-j} g(d)          (j >= 1)
+//   log W(y_p)   = (k+p-1) + (k-1)(k-2)/2 + sum_{d=p+1}^{k+p-1} g(d)
+// so one prefix sum of g over d in [-(k-2), k+m-2] gives all of them in O(k + m) (the direct
+// sums are O(k^2 + mk): seconds at RS16's largest k).  Every d stays inside (-q, q) and is never
+// 0 mod q, so 1 + alpha^d is never zero.
 static void plan_constants(nfec_codec* c, const Field& f)
 {
+    const int64_t k = c->k, m = c->m, q = f.q;
+    const int64_t lo = -(k - 2), hi = k + m - 2;  // the d range (lo <= 0 <= hi for k >= 2)
+    std::vector<int64_t> pre((size_t)std::max<int64_t>(0, hi - lo + 2), 0);  // pre[i] = sum of g over [lo, lo + i)
+    for (int64_t d = lo, i = 0; d <= hi; ++d, ++i) {
+        const int64_t g = d == 0 ? 0 : (int64_t)f.log[1u ^ f.exp[(uint32_t)(((d % q) + q) % q)]];
+        pre[(size_t)i + 1] = pre[(size_t)i] + g;
+    }
+    auto sum = [&](int64_t a, int64_t b) -> int64_t {  // g over [a, b] (d = 0 counts 0)
+        if (b < a) return 0;
+        return pre[(size_t)(b - lo + 1)] - pre[(size_t)(a - lo)];
+    };
     std::vector<uint16_t> lwp(c->k), lw(c->m);
-    std::vector<uint32_t> pt(c->k + c->m);
-    for (uint32_t j = 0; j < c->k + c->m; ++j) pt[j] = rs_point(f, j);
-    for (uint32_t j = 0; j < c->k; ++j) {
-        uint64_t acc = 0;
-        for (uint32_t l = 0; l < c->k; ++l)
-            if (l != j) acc += f.log[pt[j] ^ pt[l]];
-        lwp[j] = (uint16_t)(acc % f.q);
+    const int64_t tri = (k - 1) * (k - 2) / 2;
+    for (int64_t j = 0; j < k; ++j) {
+        const int64_t v = j == 0 ? tri : (k - 1) * (j - 1) + sum(1 - j, k - 1 - j);
+        lwp[(size_t)j] = (uint16_t)(v % q);
     }
-    for (uint32_t p = 0; p < c->m; ++p) {
-        uint64_t acc = 0;
-        for (uint32_t l = 0; l < c->k; ++l) acc += f.log[pt[c->k + p] ^ pt[l]];
-        lw[p] = (uint16_t)(acc % f.q);
-    }
+    for (int64_t p = 0; p < m; ++p) lw[(size_t)p] = (uint16_t)(((k + p - 1) + tri + sum(p + 1, k + p - 1)) % q);
     c->h_lwp = lwp;
     c->h_lw = lw;
 }
@@ -416,7 +433,7 @@ int build_codec(nfec_codec* c)
             return NFEC_OK;
         }
         if (rs_generator(wide ? 16 : 8, c->k, c->m, c->gen)) return fail(NFEC_ERANGE, "RS: numData/numParity exceeds code limits");
-        if (!wide || std::min(c->k, c->m) <= kPlanCfMaxE) plan_constants(c, f);
+        plan_constants(c, f);  // any shape: the host repair's closed form has no size limit
         return NFEC_OK;
     }
     if (c->kind == NFEC_MDP) {
@@ -591,8 +608,8 @@ int build_codec(nfec_codec* c)
                 c->tmvp_levels = levels;
             }
         }
+        plan_constants(c, f);  // the host repair (nfec_decode_vectors_host) takes any shape
         if (!wide || std::min(c->k, c->m) <= kPlanCfMaxE) {
-            plan_constants(c, f);
             if ((rc = c->d_lwp.reserve(c->k))) return rc;
             if ((rc = c->d_lw.reserve(c->m))) return rc;
             NFEC_HIP(hipMemcpy(c->d_lwp.p, c->h_lwp.data(), c->h_lwp.size() * 2, hipMemcpyHostToDevice));
@@ -2024,14 +2041,21 @@ nfec_codec* primary(nfec_codec* c) { return c->stripes.empty() ? c : c->stripes[
 // know runs on the first stripe, so a codec's device list does not change which batches it takes.
 nfec_codec* stripe_for(nfec_codec* c, const void* dev_ptr)
 {
-    if (c->stripes.empty()) return c;
     hipPointerAttribute_t at;
     std::memset(&at, 0, sizeof(at));
+    // memory HIP does not know (plain pageable malloc: the query fails or reports it
+    // unregistered) is refused -- a kernel dereferencing unmapped host memory faults the GPU
+    // (no XNACK); pinned / registered host and managed memory runs on stripe 0
     if (hipPointerGetAttributes(&at, dev_ptr) != hipSuccess) {
         (void)hipGetLastError();
-        return c->stripes[0].get();
+        return nullptr;
     }
-    if (at.type != hipMemoryTypeDevice) return c->stripes[0].get();
+    if (at.type != hipMemoryTypeHost && at.type != hipMemoryTypeManaged && at.type != hipMemoryTypeUnified &&
+        at.type != hipMemoryTypeDevice && at.type != hipMemoryTypeArray)
+        return nullptr;
+    // a one-device codec runs any memory HIP maps (its own device's, a peer's, pinned host)
+    if (c->stripes.empty()) return c;
+    if (at.type != hipMemoryTypeDevice && at.type != hipMemoryTypeArray) return c->stripes[0].get();
     for (auto& st : c->stripes)
         if (st->device == at.device) return st.get();
     return nullptr;
@@ -2455,7 +2479,7 @@ int nfec_decode_vectors_host(nfec_codec* c, void* const* vectors, uint32_t num_d
     if (!c || !vectors || (erasure_count && !erasure_locs)) return fail(NFEC_EINVAL, "null argument");
     c = primary(c);
     if (c->kind != NFEC_MDP && c->h_lwp.empty())
-        return fail(NFEC_ENOTSUP, "host decode: RS8, MDP, or RS16 with min(k, m) <= 64");
+        return fail(NFEC_ENOTSUP, "host decode: the codec has no closed-form plan constants");
     if (num_data == 0 || num_data > c->k) return fail(NFEC_EINVAL, "numData out of range");
     const uint32_t k = c->k, m = c->m, nd = num_data;
     // the reference's undefined cases (more erasures than parity, unsorted or out-of-range lists)

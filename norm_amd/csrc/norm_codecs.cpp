@@ -18,12 +18,14 @@ int NfecCodecBase::num_devices = 0;
 bool NfecCodecBase::segment_on_host = true;
 bool NfecCodecBase::decode_on_host = true;
 bool NfecCodecBase::host_fallback = true;
+bool NfecCodecBase::devices_chosen = false;
 
 bool NfecCodecBase::SetDevices(const int* devices, int count)
 {
     if (count < 1 || count > kMaxDevices || !devices) return false;
     default_device = devices[0];
     num_devices = count > 1 ? count : 0;
+    devices_chosen = true;
     for (int i = 0; i < count; ++i) device_list[i] = devices[i];
     return true;
 }
@@ -57,12 +59,19 @@ bool NfecCodecBase::InitCodec(int kind, unsigned int numData, unsigned int numPa
     cfg.num_devices = (uint32_t)n;
     cfg.flags = 0;
     int rc = nfec_codec_create_ex(&cfg, &c);
-    if (rc == NFEC_EDEVICE && host_fallback && segment_on_host && decode_on_host) {
-        // no usable gfx950: a host-only codec still serves NORM's per-call Encode / Decode
+    if (rc == NFEC_EDEVICE && host_fallback && segment_on_host && decode_on_host && !devices_chosen &&
+        nfec_device_count() == 0) {
+        // no usable gfx950 in this process and none asked for: a host-only codec still serves
+        // NORM's per-call Encode / Decode (a bad device choice or a failure on a present GPU is
+        // an Init failure instead, below)
         cfg.devices = 0;
         cfg.num_devices = 0;
         cfg.flags = NFEC_OPT_HOST_ONLY;
         rc = nfec_codec_create_ex(&cfg, &c);
+        if (rc == NFEC_OK)
+            std::fprintf(stderr, "nfec: no usable gfx950 device: Init(%u, %u, %u) built a host-only codec "
+                                 "(per-call Encode / Decode on the CPU)\n",
+                         numData, numParity, (unsigned)vectorSize);
     }
     if (rc != NFEC_OK) {
         // the reference logs PL_FATAL and returns false (normEncoderRS8.cpp:405-409)

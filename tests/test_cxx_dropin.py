@@ -162,3 +162,22 @@ def _run_fectest(orc, tmp_path, kind, k, m, vec, nd, locs, nullpar, src, env_ext
         nbytes = vec & ~1 if kind == "rs16" else vec  # RS16 never repairs an odd last byte
         assert np.array_equal(rx[:nd, :nbytes], data[:, :nbytes])
     return r.stderr
+
+
+def test_fectest_explicit_device_list_is_not_a_host_fallback(tmp_path):
+    """The host-only fallback is for a process with no usable gfx950 and no device chosen: a
+    device list given through NfecCodecBase::SetDevices that cannot be opened makes Init fail
+    (the reference's Init-returns-false path), here (no GPU) and on a box with a bad ordinal."""
+    if not _no_gpu():
+        pytest.skip("needs a process without a usable gfx950")
+    inp = tmp_path / "in.bin"
+    np.zeros((16, 64), np.uint8).tofile(inp)
+    env = dict(os.environ, NFEC_FECTEST_GPU="0", NFEC_FECTEST_DEVICES="0,0")
+    r = subprocess.run([EXE, "rs8", "16", "4", "64", "16", str(inp), str(tmp_path / "out.bin"), "0", "1"],
+                       capture_output=True, text=True, timeout=120, env=env)
+    assert r.returncode != 0 and "Init(16, 4, 64) failed" in r.stderr, r.stderr
+    # and the default (no device chosen) still falls back, with its notice
+    env.pop("NFEC_FECTEST_DEVICES")
+    r = subprocess.run([EXE, "rs8", "16", "4", "64", "16", str(inp), str(tmp_path / "out.bin"), "0", "1"],
+                       capture_output=True, text=True, timeout=120, env=env)
+    assert r.returncode == 0 and "built a host-only codec" in r.stderr, r.stderr

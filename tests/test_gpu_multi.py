@@ -143,3 +143,18 @@ def test_multi_device_codec_takes_host_mapped_batches(orc):
         enc.encode_blocks(pinned)
         torch.cuda.synchronize()
         assert np.array_equal(pinned.numpy(), ref), devices
+
+
+def test_multi_device_codec_refuses_pageable_batches():
+    """plain pageable host memory (numpy) is no device batch: HIP does not know it, and a kernel
+    dereferencing it would fault the GPU (no XNACK).  A striped codec refuses it with NFEC_EINVAL
+    before any launch; pinned memory (above) and device memory run."""
+    import ctypes
+
+    k, m, vec, nb = 16, 4, 64, 3
+    blk = np.zeros((nb, k + m, vec), np.uint8)
+    enc, _ = _codecs(N.NFEC_RS8, k, m, vec, [0, 0])
+    b = N.BlockBatch()
+    b.blocks, b.block_stride, b.seg_stride, b.nblocks = blk.ctypes.data, (k + m) * vec, vec, nb
+    assert N.lib().nfec_encode(enc._h, ctypes.byref(b), None) == N.NFEC_EINVAL
+    assert "not on a device" in N.last_error()

@@ -71,6 +71,11 @@ CASES = [
     (NFEC_RS16, 60, 13, 1461, 45, 8, 5),
     (NFEC_MDP, 64, 32, 1408, 64, 16, 0),
     (NFEC_MDP, 40, 20, 1401, 30, 8, 6),
+    # min(k, m) > 256: past the GPU plan's closed form (kPlanCfMaxE); the host repair takes any
+    # size (the reference decodes any k + m <= 65535, normEncoderRS16.cpp:650-755)
+    (NFEC_RS16, 600, 300, 1400, 600, 260, 20),
+    (NFEC_RS16, 600, 300, 64, 550, 280, 0),
+    (NFEC_RS16, 1000, 400, 32, 900, 400, 0),
 ]
 
 

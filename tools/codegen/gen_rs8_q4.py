@@ -290,13 +290,54 @@ def ab_off(c, i):
     return (c * 15 + i) * 512
 
 
-# shortened batches (per-block numData, RFC 5052 small blocks / an object's last block): the
-# lane's four items' numData as bytes in one input VGPR (%[nd], k <= 64); per load of column c
-# an item whose numData <= c reads zeros (offset | sign(numData - 1 - c) -> bit 31, past the
-# descriptor's num_records), and the parity of an item's block goes to slot numData + r.  Four
-# otherwise unused VGPRs of the default register map hold the masked offsets.
+# shortened batches (per-block numData, RFC 5052 small blocks / an object's last block): every
+# piece's block has its own numData; source column c of a piece whose numData <= c counts as
+# zero and the parity goes to slot numData + r.  The column loads are issued unmasked (so no
+# load waits on the numData fetch: a masked load offset would put a dependent memory round trip
+# in front of every workgroup's first column, measured +13 % at RS8(64,32)); the loaded
+# dwords of a masked piece are zeroed before the transpose (one SDWA compare of c with the
+# piece's numData byte, two v_cndmask).  A column at or past numData lies inside the block (its
+# parity or unused slots), read but never used.  The four pieces' numData are fetched inside the
+# asm (buffer_load_ushort through a descriptor over num_data + the wave's first block, the
+# pieces' block deltas packed in %[nd]) and packed as bytes into SHORT_TMP[0] (k <= 64; an
+# invalid numData -- 0 or past k -- packs as 0: every column masked, every store dropped).
 SHORT_TMP = [120, 121, 124, 125]
 SHORT_ND = 9
+S_NDD = 80                   # numData descriptor (shortened kernels)
+
+
+def short_fetch_nd(k):
+    """the four pieces' numData (block deltas in %[nd]) -> SHORT_TMP (issued before any column load)"""
+    L = [f"s_mov_b64 s[{S_NDD}:{S_NDD + 1}], %[ndb]", f"s_mov_b32 s{S_NDD + 2}, 0x80000000",
+         f"s_mov_b32 s{S_NDD + 3}, 0x00020000"]
+    for q, t in enumerate(SHORT_TMP):
+        L += [f"v_bfe_u32 v{t}, %[nd], {8 * q}, 8", f"v_lshlrev_b32 v{t}, 1, v{t}",
+              f"buffer_load_ushort v{t}, v{t}, s[{S_NDD}:{S_NDD + 3}], 0 offen"]
+    return L
+
+
+def short_pack_nd(k):
+    """after the first column wait (the numData loads are older): SHORT_TMP[0] = the four
+    numData as bytes, 0 for a value outside [1, k]"""
+    L = []
+    for q, t in enumerate(SHORT_TMP):
+        L += [f"v_subrev_u32 v{t}, 1, v{t}",                                         # numData - 1
+              f"v_cmp_gt_u32 vcc, {k}, v{t}",
+              f"v_add_u32 v{t}, 1, v{t}",
+              f"v_cndmask_b32 v{t}, 0, v{t}, vcc"]
+        if q:
+            L.append(f"v_lshl_or_b32 v{SHORT_TMP[0]}, v{t}, {8 * q}, v{SHORT_TMP[0]}")
+    return L
+
+
+def short_mask(col, w):
+    """zero the loaded dwords w[2q], w[2q+1] of every piece q whose numData <= col"""
+    L = []
+    for q in range(4):
+        L += [f"v_cmp_lt_u32_sdwa vcc, {col}, v{SHORT_TMP[0]} src0_sel:DWORD src1_sel:BYTE_{q}",
+              f"v_cndmask_b32 v{w[2 * q]}, 0, v{w[2 * q]}, vcc",
+              f"v_cndmask_b32 v{w[2 * q + 1]}, 0, v{w[2 * q + 1]}, vcc"]
+    return L
 
 
 def role_asm(G, k, m, w, probe=None, cfg=DEFAULT, short=False):
@@ -324,16 +365,11 @@ def role_asm(G, k, m, w, probe=None, cfg=DEFAULT, short=False):
         rs = cfg.ring_slot(step % NS)
         out = [f"s_mul_i32 s{S_COL}, %[ss], {col}"]
         for q in range(4):
-            addr = offs[q]
-            if short:
-                t = SHORT_TMP[q]
-                out += [f"v_bfe_u32 v{t}, %[nd], {8 * q}, 8",
-                        f"v_subrev_u32 v{t}, {col + 1}, v{t}",                     # numData - 1 - c
-                        f"v_and_or_b32 v{t}, v{t}, s{S_LRS + 2}, {offs[q]}"]       # sign -> bit 31
-                addr = f"v{t}"
-            out.append(f"buffer_load_dwordx2 v[{rs[2 * q]}:{rs[2 * q + 1]}], {addr}, s[{S_LRS}:{S_LRS + 3}], s{S_COL} offen{cfg.lpol}")
+            out.append(f"buffer_load_dwordx2 v[{rs[2 * q]}:{rs[2 * q + 1]}], {offs[q]}, s[{S_LRS}:{S_LRS + 3}], s{S_COL} offen{cfg.lpol}")
         return out
 
+    if short:
+        L += short_fetch_nd(k)
     for s in range(min(NS, steps)):
         L += loads(s)
     for s in range(steps):
@@ -342,6 +378,10 @@ def role_asm(G, k, m, w, probe=None, cfg=DEFAULT, short=False):
         pending = min(steps, s + NS) - (s + 1)  # later steps' loads in flight behind ours
         if not noload:
             L.append(f"s_waitcnt vmcnt({4 * pending})")
+        if short:
+            if s == 0:
+                L += short_pack_nd(k)
+            L += short_mask(NW * s + w, own)
         if nocompute:
             for i in range(8):  # keep the loaded data live
                 L.append(f"v_xor_b32 v{acc_reg(0, i)}, v{own[i]}, v{acc_reg(0, i)}")
@@ -386,9 +426,13 @@ def role_asm(G, k, m, w, probe=None, cfg=DEFAULT, short=False):
     # epilogue: planes back to bytes, optional accumulate, store (shortened: the items' parity
     # slot 0 is numData, so the row offsets are the items' offsets + numData * seg_stride)
     if short:
-        for q in range(4):
+        # piece offset + numData * seg_stride; numData 0 (invalid) sets bit 31: the stores drop
+        # (the packed numData sit in SHORT_TMP[0], so piece 0's offset goes there last)
+        x = pbuf(1)[-1]  # (free until the first row's transpose)
+        for q in (1, 2, 3, 0):
             t = SHORT_TMP[q]
-            L += [f"v_bfe_u32 v{t}, %[nd], {8 * q}, 8", f"v_mad_u32_u24 v{t}, v{t}, %[ss], {offs[q]}"]
+            L += [f"v_bfe_u32 v{x}, v{SHORT_TMP[0]}, {8 * q}, 8", f"v_mad_u32_u24 v{t}, v{x}, %[ss], {offs[q]}",
+                  f"v_subrev_u32 v{x}, 1, v{x}", f"v_and_or_b32 v{t}, v{x}, s{S_LRS + 2}, v{t}"]
         offs = [f"v{t}" for t in SHORT_TMP]
     for r in range(rows):
         acc = [acc_reg(r, i) for i in range(8)]
@@ -484,8 +528,8 @@ def shared_step(G, r0, rows, s, w, own, others, cfg):
 def clobbers(cfg, short=False):
     keep = cfg.in_regs + ([SHORT_ND] if short else [])
     v = [f'"v{i}"' for i in range(4 * NQUAD) if i not in keep]
-    s = [f'"s{i}"' for i in range(S_LRS, S_ROW + 1)]
-    return ", ".join(v + s + ['"scc"', '"memory"'])
+    s = [f'"s{i}"' for i in range(S_LRS, (S_NDD + 3 if short else S_ROW) + 1)]
+    return ", ".join(v + s + (['"vcc"'] if short else []) + ['"scc"', '"memory"'])
 
 
 def lds_bytes(cfg):
@@ -502,15 +546,16 @@ def gen_kernel(k, m, G=None, prefix="rs8_q4_enc", probe=None, suffix="", cfg=DEF
     K = f"{prefix}{suffix}{'_sh' if short else ''}_k{k}_m{m}"
     out = []
     la4 = ', [la4] "v"(la4)' if cfg.share == "A" else ""
-    nd_in = ', [nd] "v"(ndp)' if short else ""
+    nd_in = ', [ndb] "s"(ndb), [nd] "v"(ndp)' if short else ""
+    nd_out = ""
     for w in range(NW):
         body = role_asm(G, k, m, w, probe, cfg, short)
         s = "\\n\"\n        \"".join(body)
-        out.append(f"""__device__ __forceinline__ void {K}_role{w}(const bs::EncArgs& a, const bs::Items& it, const uint32_t o[4], uint32_t la, uint32_t la4, uint32_t ndp)
+        out.append(f"""__device__ __forceinline__ void {K}_role{w}(const bs::EncArgs& a, const bs::Items& it, const uint32_t o[4], uint32_t la, uint32_t la4, uint32_t ndp, const uint16_t* ndb)
 {{
     asm volatile(
         "{s}\\n"
-        :
+        : {nd_out}
         : [ib] "s"(it.wbase), [ob] "s"(it.obase), [ss] "s"(a.seg_stride), [acc] "s"(a.accumulate),
           [o0] "v"(o[0]), [o1] "v"(o[1]), [o2] "v"(o[2]), [o3] "v"(o[3]), [la] "v"(la){la4}{nd_in}
         : {clobbers(cfg, short)});
@@ -520,31 +565,35 @@ def gen_kernel(k, m, G=None, prefix="rs8_q4_enc", probe=None, suffix="", cfg=DEF
     body.append("    const uint32_t lane = threadIdx.x & 63;")
     body.append("    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);")
     body.append("    bs::Items it;")
-    body.append("    bs::make_items(a, bs::wg_index(a.xcd_remap) * 256u, lane, it);")
-    body.append("    // out-of-range items: loads read zero, stores are dropped (bit 31 past num_records)")
     body.append("    uint32_t o[4];")
-    body.append("#pragma unroll")
-    body.append("    for (int i = 0; i < 4; ++i) o[i] = it.nbytes[i] == 8 ? it.off[i] : 0x80000000u;")
     body.append("    uint32_t ndp = 0;")
-    if short:
-        body.append(f"    // the items' numData as bytes (a block with numData 0 or past {k} is left alone)")
-        body.append("    const uint32_t ips = a.vec >> 3, ib = bs::wg_index(a.xcd_remap) * 256u;")
+    body.append("    const uint16_t* ndb = nullptr;")
+    if not short:
+        body.append("    bs::make_items(a, bs::wg_index(a.xcd_remap) * 256u, lane, it);")
+        body.append("    // out-of-range items: loads read zero, stores are dropped (bit 31 past num_records)")
+        body.append("#pragma unroll")
+        body.append("    for (int i = 0; i < 4; ++i) o[i] = it.nbytes[i] == 8 ? it.off[i] : 0x80000000u;")
+    else:
+        body.append("    // make_items' geometry (vec % 8 == 0), plus the pieces' block deltas from the wave's first")
+        body.append("    // block as bytes (a workgroup's 256 pieces span at most 256 blocks): the asm fetches their")
+        body.append("    // numData from ndb = num_data + that block")
+        body.append("    const uint32_t ips = a.vec >> 3, ib = bs::wg_index(a.xcd_remap) * 256u, total = a.nblocks * ips;")
+        body.append("    const uint32_t b0 = __builtin_amdgcn_readfirstlane(min(ib, total - 1u) / ips);")
+        body.append("    it.wbase = a.base + (uint64_t)b0 * a.block_stride;")
+        body.append("    it.obase = a.out + (uint64_t)b0 * a.block_stride;")
+        body.append("    ndb = a.num_data + b0;")
         body.append("#pragma unroll")
         body.append("    for (int i = 0; i < 4; ++i) {")
-        body.append("        const uint32_t g = ib + (uint32_t)i * 64u + lane;")
-        body.append(f"        uint32_t nd = {k}u;")
-        body.append("        if (g < a.nblocks * ips) {")
-        body.append("            const uint32_t v = a.num_data[g / ips];")
-        body.append(f"            if (v >= 1u && v <= {k}u) nd = v;")
-        body.append("            else o[i] = 0x80000000u;")
-        body.append("        }")
-        body.append("        ndp |= nd << (8 * i);")
+        body.append("        const uint32_t g = ib + (uint32_t)i * 64u + lane, gg = g < total ? g : ib;")
+        body.append("        const uint32_t db = gg / ips - b0;")
+        body.append("        o[i] = g < total ? db * (uint32_t)a.block_stride + (gg - (db + b0) * ips) * 8u : 0x80000000u;")
+        body.append("        ndp |= db << (8 * i);")
         body.append("    }")
     body.append("    const uint32_t la = bs::lds_addr(lds) + lane * 8u;   // b64 rows: 8 bytes per lane")
     body.append("    const uint32_t la4 = bs::lds_addr(lds) + lane * 4u;  // b32 rows")
     for w in range(NW):
         kw = "if" if w == 0 else "else if"
-        body.append(f"    {kw} (wave == {w}) {K}_role{w}(a, it, o, la, la4, ndp);")
+        body.append(f"    {kw} (wave == {w}) {K}_role{w}(a, it, o, la, la4, ndp, ndb);")
     body.append("}")
     out.append("\n".join(body))
     out.append(f"""
