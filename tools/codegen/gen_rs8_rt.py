@@ -165,7 +165,8 @@ def call(r, fast, ebuf):
         L = [f"s_bfe_u32 s{S_T1}, s{dw}, 0x{(16 << 16) | (16 * half):x}",
              f"s_add_u32 s{S_TGT}, s{S_SNIP}, s{S_T1}",
              f"s_addc_u32 s{S_TGT + 1}, s{S_SNIP + 1}, 0"]
-    return L + [f"s_movk_i32 m0, 0x{GPR_MODE | (16 * r):x}",
+    m0 = "s_mov_b32" if M0_LITERAL else "s_movk_i32"   # (--m0-literal: the round-4 8-byte form, A/B only)
+    return L + [f"{m0} m0, 0x{GPR_MODE | (16 * r):x}",
                 f"s_swappc_b64 s[{S_RET}:{S_RET + 1}], s[{S_TGT}:{S_TGT + 1}]"]
 
 
@@ -422,7 +423,14 @@ def clobbers():
     return ", ".join(v + s + ['"m0"', '"scc"', '"memory"'])
 
 
+M0_LITERAL = False
+
+
 def main():
+    global M0_LITERAL
+    if "--m0-literal" in sys.argv:   # A/B builds (tools/ab_build.sh): M0 written with a 32-bit literal
+        sys.argv.remove("--m0-literal")
+        M0_LITERAL = True
     path = sys.argv[1]
     asms = {G: "\\n\"\n            \"".join(body(G)) for G in GS}
     ins = ", ".join([f'[o{i}] "v"(o[{i}])' for i in range(4)] + [f'[q{i}] "v"(q[{i}])' for i in range(4)])

@@ -23,6 +23,8 @@
 #   c5         tools/bench_c5.py --steps 2 (the C5 mix's one-GPU share)
 #   percall    tools/percall per-call latencies (needs tools/percall/_build/percall)
 #   tmvp_levels RS16 encode with the Toeplitz split forced at 0..2 levels on four shapes
+#   ab_mdp     MDP(64,32) encode + repair lines from the product library and each of AB_LIBS,
+#              alternating on one box (AB_REPS rounds, default 3)
 #   ab         A/B of the product library against AB_LIBS (other builds of the same sources, e.g.
 #              tools/ab_build.sh with a generator option, loaded through NFEC_LIBRARY): the RS16 GPU
 #              tests on each (AB_K: a -k expression, e.g. to skip the split-level expectations of a
@@ -151,6 +153,20 @@ PY
         for f in "$O"/rs16_*_[0-9].json "$O"/c4_*_[0-9].json; do
             python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print(sys.argv[1].rsplit('/',1)[1], d.get('encode_ms'), d.get('decode_ms'))" "$f"
         done ;;
+    ab_mdp)
+        # MDP(64,32) encode + 16-erasure repair on the product library and each of AB_LIBS,
+        # alternating on one box, AB_REPS times (default 3): one JSON line per run
+        [ -n "$AB_LIBS" ] || die "ab_mdp (AB_LIBS unset)" 2
+        : > "$O/ab_mdp.jsonl"
+        for i in $(seq 1 "${AB_REPS:-3}"); do
+            timeout -k 10 300 python3 tools/bench_extra.py --workload mdp --steps 10 | sed 's/^{/{"lib": "product", /' >> "$O/ab_mdp.jsonl" || die ab_mdp $?
+            for L in $AB_LIBS; do
+                n=$(basename "$L" .so)
+                NFEC_LIBRARY=$R/$L timeout -k 10 300 python3 tools/bench_extra.py --workload mdp --steps 10 \
+                    | sed "s/^{/{\"lib\": \"$n\", /" >> "$O/ab_mdp.jsonl" || die ab_mdp $?
+            done
+        done
+        python3 -c "import json,sys; [print(d['lib'], d['encode_ms'], d['decode_ms'], d['verified']) for d in map(json.loads, open(sys.argv[1]))]" "$O/ab_mdp.jsonl" ;;
     *)
         echo "session: unknown task $task"; exit 2 ;;
     esac
