@@ -327,17 +327,27 @@ def short_pack_nd(k):
               f"v_cndmask_b32 v{t}, 0, v{t}, vcc"]
         if q:
             L.append(f"v_lshl_or_b32 v{SHORT_TMP[0]}, v{t}, {8 * q}, v{SHORT_TMP[0]}")
+    # the lane's smallest numData (SHORT_TMP[1]): a step whose column is below it in every lane
+    # skips the masking (RFC 5052 blocks of k and k - 1 mask in the last step only)
+    t0, t1, t2, t3 = SHORT_TMP
+    L += [f"v_min3_u32 v{t1}, v{t1}, v{t2}, v{t3}", f"v_and_b32 v{t2}, 0xff, v{t0}", f"v_min_u32 v{t1}, v{t1}, v{t2}"]
     return L
 
 
+_mask_id = [0]
+
+
 def short_mask(col, w):
-    """zero the loaded dwords w[2q], w[2q+1] of every piece q whose numData <= col"""
-    L = []
+    """zero the loaded dwords w[2q], w[2q+1] of every piece q whose numData <= col (skipped when
+    no lane holds such a piece)"""
+    _mask_id[0] += 1
+    skip = f"Lnomask{_mask_id[0]}_%="
+    L = [f"v_cmp_gt_u32 vcc, {col + 1}, v{SHORT_TMP[1]}", f"s_cbranch_vccz {skip}"]
     for q in range(4):
         L += [f"v_cmp_lt_u32_sdwa vcc, {col}, v{SHORT_TMP[0]} src0_sel:DWORD src1_sel:BYTE_{q}",
               f"v_cndmask_b32 v{w[2 * q]}, 0, v{w[2 * q]}, vcc",
               f"v_cndmask_b32 v{w[2 * q + 1]}, 0, v{w[2 * q + 1]}, vcc"]
-    return L
+    return L + [f"{skip}:"]
 
 
 def role_asm(G, k, m, w, probe=None, cfg=DEFAULT, short=False):
