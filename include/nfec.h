@@ -177,6 +177,13 @@ int nfec_codec_features(const nfec_codec* codec);
 #define NFEC_PATH_GENERIC 4      /* table-lookup kernels */
 #define NFEC_PATH_COUNT 5
 int nfec_codec_encode_paths(const nfec_codec* codec, uint64_t* counts, uint32_t n);
+/* The same for device-batch decodes (NFEC_DPATH_*). */
+#define NFEC_DPATH_FIXED 0        /* RS8 closed-form plan + fused / bit-sliced repair for the (k, m) generator (shortened too) */
+#define NFEC_DPATH_RUNTIME 1      /* one-pass repair on the runtime-coefficient kernel (any RS8 shape, MDP) */
+#define NFEC_DPATH_RS16_TOWER 2   /* RS16 closed-form plan, both stages on the tower kernel */
+#define NFEC_DPATH_GENERIC 3      /* Gauss-Jordan plan and table-lookup kernels */
+#define NFEC_DPATH_COUNT 4
+int nfec_codec_decode_paths(const nfec_codec* codec, uint64_t* counts, uint32_t n);
 /* Copies the m x k parity rows of the systematic generator (row p = generator row k+p),
  * row-major, elements of symbol_bytes each.  MDP: the m x k matrix of the LFSR code for a
  * full block of k source symbols.  bytes must be >= m*k*symbol_bytes. */

@@ -25,6 +25,8 @@ NFEC_OPT_RS16_TOEPLITZ_ONE_LEVEL = 16
 NFEC_PATH_FIXED, NFEC_PATH_RUNTIME, NFEC_PATH_RS16_SPLIT, NFEC_PATH_RS16_PRODUCT, NFEC_PATH_GENERIC = 0, 1, 2, 3, 4
 NFEC_PATH_COUNT = 5
 PATH_NAMES = ("fixed", "runtime", "rs16_split", "rs16_product", "generic")
+NFEC_DPATH_COUNT = 4
+DPATH_NAMES = ("fixed", "runtime", "rs16_tower", "generic")
 NFEC_HOST_GF_SCALAR, NFEC_HOST_GF_AVX2, NFEC_HOST_GF_GFNI = 0, 1, 2
 
 
@@ -131,6 +133,7 @@ _SIGS = {
     "nfec_codec_get_info": (_I, [_P, ctypes.POINTER(CodecInfo)]),
     "nfec_codec_features": (_I, [_P]),
     "nfec_codec_encode_paths": (_I, [_P, ctypes.POINTER(_U64), _U32]),
+    "nfec_codec_decode_paths": (_I, [_P, ctypes.POINTER(_U64), _U32]),
     "nfec_codec_get_generator": (_I, [_P, _P, ctypes.c_size_t]),
     "nfec_encode": (_I, [_P, ctypes.POINTER(BlockBatch), _P]),
     "nfec_decode": (_I, [_P, ctypes.POINTER(BlockBatch), _P, _U32, _P, _P, _P]),

@@ -186,6 +186,14 @@ class _Codec:
         N.check(min(rc, 0), "nfec_codec_encode_paths")
         return {name: int(cnt[i]) for i, name in enumerate(N.PATH_NAMES)}
 
+    def decode_paths(self):
+        """Device-batch decodes so far per path that took them, {name: count} (NFEC_DPATH_*)."""
+        self._need()
+        cnt = (ctypes.c_uint64 * N.NFEC_DPATH_COUNT)()
+        rc = N.lib().nfec_codec_decode_paths(self._h, cnt, N.NFEC_DPATH_COUNT)
+        N.check(min(rc, 0), "nfec_codec_decode_paths")
+        return {name: int(cnt[i]) for i, name in enumerate(N.DPATH_NAMES)}
+
     def _need(self):
         if not self._h:
             raise RuntimeError("codec not initialised (call Init)")

@@ -147,6 +147,7 @@ struct DecArgs {
     uint32_t xcd_remap = 0;
     const uint32_t* gate = nullptr;   // non-null: skip the launch unless *gate == gate_gen
     uint32_t gate_gen = 0;            // (RsPlan2Args::gate)
+    const uint16_t* num_data = nullptr;  // per block (null: k): parity row p at slot numData + p
 };
 
 // Workgroup -> work index.  The dispatcher deals workgroups round-robin over the 8 XCDs

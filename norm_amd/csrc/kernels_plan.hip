@@ -756,10 +756,12 @@ __global__ __launch_bounds__(64 * kPlan2Waves) void rs_plan2_kernel(RsPlan2Args 
     const uint32_t b = blockIdx.x * kPlan2Waves + w;
     const bool live = b < a.nblocks;
     const uint32_t k = a.k, m = a.m;
-    // the erasure list is fetched first so its two dependent loads overlap the table staging
+    // the erasure list is fetched first so its two dependent loads overlap the table staging;
+    // a shortened block (numData < k, normEncoderRS8.cpp:675-693) has its parity at slot nd + p
     const uint32_t ec = live ? uni(a.erasure_counts[b]) : 0u;
+    const uint32_t nd = live && a.num_data ? uni(a.num_data[b]) : k;
     const uint16_t* locs = a.erasure_locs + (uint64_t)b * a.erasure_stride;
-    bool ok = ec <= m && ec <= a.erasure_stride;   // then ec <= 64: one entry per lane
+    bool ok = ec <= m && ec <= a.erasure_stride && nd >= 1 && nd <= k;   // then ec <= 64: one entry per lane
     const uint32_t myl = (live && ok && lane < ec) ? (uint32_t)locs[lane] : 0u;
     for (uint32_t i = threadIdx.x; i < 510; i += 64 * kPlan2Waves) ex[i] = a.exp_tab[i];
     for (uint32_t i = threadIdx.x; i < 256; i += 64 * kPlan2Waves) lg[i] = a.log_tab[i];
@@ -771,17 +773,17 @@ __global__ __launch_bounds__(64 * kPlan2Waves) void rs_plan2_kernel(RsPlan2Args 
     // source entries are a prefix); a valid list marks its slots in ers
     if (ok) {
         const uint32_t prev = __shfl_up(myl, 1);
-        const bool bad = lane < ec && (myl >= k + m || (lane > 0 && myl <= prev));
-        es = (uint32_t)__popcll(__ballot(lane < ec && myl < k));
+        const bool bad = lane < ec && (myl >= nd + m || (lane > 0 && myl <= prev));
+        es = (uint32_t)__popcll(__ballot(lane < ec && myl < nd));
         ok = !__any(bad);
     }
     wave_lds_sync();
     if (ok && lane < ec) ers[myl] = 1;
     wave_lds_sync();
-    // surviving parity rows: lane p tests slot k+p
+    // surviving parity rows: lane p tests slot nd + p
     uint64_t surv = 0;
     if (ok) {
-        surv = __ballot(lane < m && !ers[k + lane]);
+        surv = __ballot(lane < m && !ers[nd + lane]);
         if ((uint32_t)__popcll(surv) < es) ok = false;
     }
     const uint32_t e = ok ? es : 0;
@@ -799,8 +801,10 @@ __global__ __launch_bounds__(64 * kPlan2Waves) void rs_plan2_kernel(RsPlan2Args 
     const uint64_t pused = __ballot(used);
     const bool fused = a.fused_rows && e > 0 && e <= 16 && (pused >> a.fused_rows) == 0ull;
     if (lane < m) a.pmap[(uint64_t)b * m + lane] = used ? (uint8_t)rank : (uint8_t)0xff;
-    // erased-source bitmap (k <= 64 for the specialised kernels; others ignore it)
-    const uint64_t em = e > 0 ? __ballot(lane < k && ers[lane]) : 0ull;
+    // erased-source bitmap (k <= 64 for the specialised kernels; others ignore it), plus the
+    // columns [nd, k) of a shortened block: the repair kernels skip both (read and compute
+    // nothing), which is what a shortened block's absent columns need
+    const uint64_t em = e > 0 ? __ballot((lane < nd && ers[lane]) || (lane >= nd && lane < k)) : 0ull;
     if (lane == 0) {
         emask[0] = (uint32_t)em;
         emask[1] = (uint32_t)(em >> 32);

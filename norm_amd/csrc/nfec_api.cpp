@@ -236,6 +236,7 @@ struct nfec_codec {
     hipEvent_t tmvp_done = nullptr;  // the last Toeplitz encode's end, on its stream
     // device-batch encodes per path that took them (NFEC_PATH_*, nfec_codec_encode_paths)
     std::atomic<uint64_t> enc_paths[NFEC_PATH_COUNT] = {};
+    std::atomic<uint64_t> dec_paths[NFEC_DPATH_COUNT] = {};  // ... and decodes (NFEC_DPATH_*)
 
     // decode workspace (guarded by mu)
     std::mutex mu;
@@ -1379,15 +1380,18 @@ static int decode_rs16_tw(nfec_codec* c, const nfec_block_batch* b, const uint16
 // ---- decode on a device batch ----
 // caller_locked: the caller already holds c->mu (nfec_decode_vectors keeps it for the whole
 // per-call decode, staging included)
-int decode_device(nfec_codec* c, const nfec_block_batch* b, const uint16_t* locs, uint32_t lstride,
-                  const uint16_t* counts, int32_t* status, hipStream_t s, bool caller_locked = false)
+static int decode_device_impl(nfec_codec* c, const nfec_block_batch* b, const uint16_t* locs, uint32_t lstride,
+                              const uint16_t* counts, int32_t* status, hipStream_t s, bool caller_locked, int& path)
 {
     if (!locs || !counts) return fail(NFEC_EINVAL, "null erasure arrays");
     const bool acc = b->flags & NFEC_ACCUMULATE;
     if (c->kind == NFEC_MDP && acc) return fail(NFEC_ENOTSUP, "MDP decode requires zero-filled erased segments");
     std::unique_lock<std::mutex> lk(c->mu, std::defer_lock);
     if (!caller_locked) lk.lock();
-    if (rs16_twdec_covers(c, b)) return decode_rs16_tw(c, b, locs, lstride, counts, status, s);
+    if (rs16_twdec_covers(c, b)) {
+        path = NFEC_DPATH_RS16_TOWER;
+        return decode_rs16_tw(c, b, locs, lstride, counts, status, s);
+    }
     const uint32_t n = c->k + c->m;
     const uint32_t zstride = round_up(c->vec, 8);
     // RS decode rows: at most min(k, m) source erasures are solved per block, so the plan's
@@ -1400,7 +1404,9 @@ int decode_device(nfec_codec* c, const nfec_block_batch* b, const uint16_t* locs
     // computes the erased source from the received columns
     // (NFEC_RT_DEC=1: the one-pass runtime-coefficient repair for those shapes too, for A/B)
     static const bool rt_first = diag_knob("NFEC_RT_DEC", 0) != 0;
-    const bool fast = !rt_first && c->kind == NFEC_RS8 && !b->num_data && c->m <= 32 && c->k <= 64 && !force_generic() &&
+    // (shortened batches too: the plan marks each block's columns past its numData like erased
+    // ones, and the repair kernels read its parity at slot numData + t)
+    const bool fast = !rt_first && c->kind == NFEC_RS8 && c->m <= 32 && c->k <= 64 && !force_generic() &&
                       has_bitsliced(c->k, c->m) && bs::offsets_fit(b->block_stride, b->seg_stride);
     static const bool use_rt = diag_knob("NFEC_RT", 1) != 0;
     const bool rt_dec = use_rt && !fast && c->kind == NFEC_RS8 && (c->vec % 8) == 0 && c->d_rt.p && c->d_lwp.p &&
@@ -1440,6 +1446,7 @@ int decode_device(nfec_codec* c, const nfec_block_batch* b, const uint16_t* locs
     };
     const bool mdp_rt = c->kind == NFEC_MDP && use_mdp_rt && (c->vec % 8) == 0 && !force_generic() &&
                         rs8_rt_covers(mdp_rt_args(static_cast<uint8_t*>(b->blocks), 1));
+    path = fast ? NFEC_DPATH_FIXED : (rt_dec || mdp_rt) ? NFEC_DPATH_RUNTIME : NFEC_DPATH_GENERIC;
     const uint32_t rt_np = rs8_rt_passes(std::min(c->k, c->m));  // RS8 repair table passes
     const uint64_t ws_per_block = c->kind == NFEC_MDP ? (mdp_rt ? (uint64_t)mdp_np * n * 16 : (uint64_t)n * c->cs)
                                   : rt_dec            ? (uint64_t)rt_np * c->k * 16
@@ -1619,6 +1626,7 @@ int decode_device(nfec_codec* c, const nfec_block_batch* b, const uint16_t* locs
             p2.k = c->k;
             p2.m = c->m;
             p2.nblocks = nb;
+            p2.num_data = nd;
             p2.erasure_locs = l;
             p2.erasure_stride = lstride;
             p2.erasure_counts = cnt;
@@ -1654,6 +1662,7 @@ int decode_device(nfec_codec* c, const nfec_block_batch* b, const uint16_t* locs
             f.out_slots = c->w_oslots.p;
             f.slots_stride = c->k;
             f.accumulate = acc;
+            f.num_data = nd;
             // 2 (default) = compact lane-major items, idle lanes out of EXEC (1.981-1.985 vs
             // 1.989-1.998 ms, r02g); 0 = item q*64 + lane; 1 = lane L holds items 4L..4L+3
             // (strided loads: 2.16 vs 2.02 ms).  NFEC_FDEC_LANEMAJOR overrides (diagnostic library).
@@ -1690,6 +1699,7 @@ int decode_device(nfec_codec* c, const nfec_block_batch* b, const uint16_t* locs
             d.xcd_remap = bs_flags() & 1u;
             d.gate = gate;
             d.gate_gen = gen;
+            d.num_data = nd;
             if ((rc = launch_rs8_bitsliced_reencode(c->k, c->m, d, s))) return fail(rc, "bit-sliced re-encode launch failed");
             static const bool use_solve = diag_knob("NFEC_SOLVE", 1) != 0;
             if (!use_solve) {
@@ -1957,6 +1967,16 @@ int decode_device(nfec_codec* c, const nfec_block_batch* b, const uint16_t* locs
     return NFEC_OK;
 }
 
+// counts each batch decode by the path that took it (nfec_codec_decode_paths)
+int decode_device(nfec_codec* c, const nfec_block_batch* b, const uint16_t* locs, uint32_t lstride,
+                  const uint16_t* counts, int32_t* status, hipStream_t s, bool caller_locked = false)
+{
+    int path = NFEC_DPATH_GENERIC;
+    const int rc = decode_device_impl(c, b, locs, lstride, counts, status, s, caller_locked, path);
+    if (rc == NFEC_OK) c->dec_paths[path].fetch_add(1, std::memory_order_relaxed);
+    return rc;
+}
+
 }  // namespace
 
 // =====================================================================================
@@ -2184,6 +2204,17 @@ int nfec_codec_encode_paths(const nfec_codec* c, uint64_t* counts, uint32_t n)
         counts[i] = v;
     }
     return NFEC_PATH_COUNT;
+}
+
+int nfec_codec_decode_paths(const nfec_codec* c, uint64_t* counts, uint32_t n)
+{
+    if (!c || (!counts && n)) return fail(NFEC_EINVAL, "null argument");
+    for (uint32_t i = 0; i < n; ++i) {
+        uint64_t v = i < NFEC_DPATH_COUNT ? c->dec_paths[i].load(std::memory_order_relaxed) : 0;
+        for (const auto& st : c->stripes) v += i < NFEC_DPATH_COUNT ? st->dec_paths[i].load(std::memory_order_relaxed) : 0;
+        counts[i] = v;
+    }
+    return NFEC_DPATH_COUNT;
 }
 
 int nfec_codec_get_generator(const nfec_codec* c, void* host_out, size_t bytes)

@@ -509,6 +509,7 @@ int launch_rs8_plan_rt(const RsPlanArgs& a, uint32_t npass, hipStream_t s);
 // elimination; the inverse is unique, so the bytes equal the reference's.
 struct RsPlan2Args {
     uint32_t k = 0, m = 0, nblocks = 0;
+    const uint16_t* num_data = nullptr;  // per block (null: k); parity p at slot numData + p
     const uint16_t* erasure_locs = nullptr;
     uint32_t erasure_stride = 0;
     const uint16_t* erasure_counts = nullptr;
@@ -521,7 +522,7 @@ struct RsPlan2Args {
     int32_t* rows = nullptr;            // e_s per block (0: nothing to repair)
     uint16_t* cols2 = nullptr;          // e_s per block
     uint16_t* out_slots2 = nullptr;     // [b][k]: erased source slots E_s
-    uint32_t* emask = nullptr;          // [b][2]: bit j set = source column j erased
+    uint32_t* emask = nullptr;          // [b][2]: bit j set = source column j erased or past numData
     uint32_t* psel = nullptr;           // [b][2]: bit p set = parity row p used (P)
     uint8_t* pmap = nullptr;            // [b][m]: index t of parity row p in P
     uint32_t coef_stride = 0;
@@ -559,6 +560,7 @@ struct FdecArgs {
     uint32_t slots_stride = 0;
     uint32_t accumulate = 0;
     uint32_t lane_major = 0;             // lane L holds items 4L..4L+3; lanes without one exit
+    const uint16_t* num_data = nullptr;  // per block (null: k): parity row t read at slot numData + t
 };
 int launch_rs8_fused_decode(uint32_t k, uint32_t m, const FdecArgs& a, hipStream_t s);
 bool rs8_fused_decode_covers(uint32_t k, uint32_t m, const FdecArgs& a);

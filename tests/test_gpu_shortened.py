@@ -11,8 +11,10 @@ These batches now stay on the fast kernels:
     source column at or past the block's numData, the products that read source columns through
     their column map mask the mapped slot, and the postscale writes slot numData + r;
   * RS8 (64, 32) / (64, 16) / (64, 8): the fixed-generator q4 kernels with each 8-byte piece's
-    loads masked at its own block's numData.
-nfec_codec_encode_paths() tells which kernel family took each batch.  A block whose numData is 0
+    source data masked at its own block's numData; and their repair on the closed-form plan and
+    the fused / bit-sliced repair kernels (a shortened block's columns past numData are skipped
+    like erased ones, its parity read at slot numData + t).
+nfec_codec_encode_paths() / decode_paths() tell which kernel family took each batch.  A block whose numData is 0
 or past k (undefined in the reference) is left untouched."""
 import numpy as np
 import pytest
@@ -21,7 +23,7 @@ pytestmark = pytest.mark.gpu
 
 torch = pytest.importorskip("torch")
 
-from norm_amd import (NFEC_RS8, NFEC_RS16, NormEncoderRS8, NormEncoderRS16)  # noqa: E402
+from norm_amd import (NFEC_RS8, NFEC_RS16, NormDecoderRS8, NormEncoderRS8, NormEncoderRS16)  # noqa: E402
 from norm_amd._native import (NFEC_FEATURE_RS16_TOEPLITZ, NFEC_FEATURE_RS16_TOEPLITZ2,  # noqa: E402
                               NFEC_OPT_RS16_TOEPLITZ_ON, NFEC_OPT_RS16_TOEPLITZ_ONE_LEVEL)
 
@@ -169,3 +171,90 @@ def test_rs8_shortened_other_shapes_stay_on_the_runtime_kernel(orc):
     assert enc.Init(k, m, vec)
     nd = _num_data(k, nb, 5)
     _check(orc, NFEC_RS8, k, m, vec, vec, nb, nd, enc, "runtime")
+
+
+def _i16a(a):
+    return torch.from_numpy(np.ascontiguousarray(a).astype(np.int16)).cuda()
+
+
+@pytest.mark.parametrize("k,m,vec,nb,acc", [(64, 32, 1400, 48, False), (64, 16, 1408, 40, False),
+                                             (64, 8, 64, 40, False), (64, 32, 1400, 24, True)])
+def test_rs8_shortened_decode_on_the_fixed_kernels(orc, k, m, vec, nb, acc):
+    """Shortened blocks (numData < k) repaired by the closed-form plan and the fused / bit-sliced
+    repair kernels (normEncoderRS8.cpp:652-757 with :675-693): source erasures only (the fused
+    kernel), source and parity erasures (substitute rows past 16: the unfused stage 1 + solve),
+    more than 16 erasures, none, too many (status 0, untouched) and invalid numData (left alone)"""
+    rng = np.random.default_rng(k + m + nb + int(acc))
+    nd = _num_data(k, nb, 17 * m + nb, invalid=True)
+    valid = (nd >= 1) & (nd <= k)
+    host = orc.make_blocks(k, m, vec, nb, num_data=np.clip(nd, 1, k))
+    enc = NormEncoderRS8()
+    assert enc.Init(k, m, vec)
+    clean = host.copy()
+    clean[valid] = orc.encode_blocks(NFEC_RS8, k, m, vec, host[valid].copy(), num_data=nd[valid])
+    ls = m + 1
+    locs = np.zeros((nb, ls), np.uint16)
+    counts = np.zeros(nb, np.uint16)
+    for b in range(nb):
+        n = int(np.clip(nd[b], 1, k))
+        kind = b % 6
+        if kind == 0:      # source erasures only, e <= 16: the fused kernel
+            es, ep = min(n, int(rng.integers(1, 17))), 0
+        elif kind == 1:    # source + parity: substitute parity rows shift upward
+            es, ep = min(n, int(rng.integers(1, 9))), int(rng.integers(1, m // 2 + 1))
+        elif kind == 2:    # more than 16 source erasures (m = 32): unfused
+            es, ep = min(n, m // 2 + 4 if m > 16 else m), 0
+        elif kind == 3:    # nothing lost
+            es, ep = 0, 0
+        elif kind == 4:    # lost parity only
+            es, ep = 0, int(rng.integers(1, m + 1))
+        else:              # everything a block can lose and still decode
+            es = min(n, m // 2)
+            ep = m - es
+        es = min(es, n)
+        ep = min(ep, m - es)
+        e = np.sort(np.concatenate([rng.choice(n, es, replace=False), n + rng.choice(m, ep, replace=False)]))
+        if b == 7:         # one past the parity count: undecodable, the block stays as it is
+            e = np.sort(rng.choice(n + m, min(n + m, m + 1), replace=False))
+        locs[b, :len(e)] = e
+        counts[b] = len(e)
+    rx = clean.copy()
+    for b in range(nb):
+        for s in locs[b, :counts[b]]:
+            # erased source: zero (NORM's zero-fill), or junk under accumulate (XORed into)
+            rx[b, s] = rng.integers(0, 256, rx.shape[2], dtype=np.uint8) if acc else 0
+    want = rx.copy()
+    st_ref = np.zeros(nb, np.int32)
+    if valid.any():
+        sub = want[valid].copy()
+        st_ref[valid] = _oracle_decode(orc, k, m, vec, sub, locs[valid], counts[valid], nd[valid])
+        want[valid] = sub
+    dec = NormDecoderRS8()
+    assert dec.Init(k, m, vec)
+    dev = torch.from_numpy(rx).cuda()
+    before = dec.decode_paths()
+    st = dec.decode_blocks(dev, _i16a(locs), _i16a(counts), num_data=_i16(nd), accumulate=acc)
+    torch.cuda.synchronize()
+    after = dec.decode_paths()
+    assert {p: after[p] - before[p] for p in after if after[p] != before[p]} == {"fixed": 1}
+    got = dev.cpu().numpy()
+    stg = st.cpu().numpy()
+    assert np.array_equal(stg, st_ref), (stg, st_ref)
+    assert np.array_equal(got, want)
+    for b in np.nonzero(~valid)[0]:
+        assert stg[b] == 0 and np.array_equal(got[b], rx[b])
+
+
+def _oracle_decode(orc, k, m, vec, blocks, locs, counts, nd):
+    """the oracle's Decode per block; a list longer than m (undecodable) gives status 0 and
+    leaves the block alone, as the reference's dec_matrix build fails (normEncoderRS8.cpp:721-725)"""
+    st = np.zeros(len(blocks), np.int32)
+    for i in range(len(blocks)):
+        if counts[i] > m:
+            continue
+        one = blocks[i:i + 1].copy()
+        l1 = np.zeros((1, m), np.uint16)
+        l1[0, :counts[i]] = locs[i, :counts[i]]
+        st[i] = orc.decode_blocks(NFEC_RS8, k, m, vec, one, l1, counts[i:i + 1], nd[i:i + 1])[0]
+        blocks[i] = one[0]
+    return st

@@ -146,7 +146,10 @@ def fdec_asm(k, m, probe=None, e16=False):
             out = [f"s_bitcmp1_b64 s[{S_EM}:{S_EM + 1}], {c}", f"s_cselect_b32 s{S_LRS + 2}, 0, 0x80000000"]
         else:  # parity row c - k: read when the block uses it (bit of the parity-row mask)
             out = [f"s_bitcmp1_b32 %[ps], {c - k}", f"s_cselect_b32 s{S_LRS + 2}, 0x80000000, 0"]
-        out.append(f"s_mul_i32 s{S_COL}, %[ss], {c}")
+        if c < k:
+            out.append(f"s_mul_i32 s{S_COL}, %[ss], {c}")
+        else:  # (slot numData + t: a shortened block's parity follows its numData sources)
+            out += [f"s_add_u32 s{S_COL}, %[pk], {c - k}", f"s_mul_i32 s{S_COL}, s{S_COL}, %[ss]"]
         for q in range(4):
             out.append(f"buffer_load_dwordx2 v[{w[2 * q]}:{w[2 * q + 1]}], {offs[q]}, s[{S_LRS}:{S_LRS + 3}], s{S_COL} offen")
         return out
@@ -319,7 +322,7 @@ PROBES = {1: "nos2", 2: "nos1", 3: "noload", 4: "gen", 5: "sync4", 6: "sync8", 7
 # and prologue per block, no tail of partly filled workgroups)
 
 
-def persist_kernel(K, nr, body):
+def persist_kernel(K, nr, body, k):
     """the fused repair as a persistent loop: each wave walks blocks w, w + 4 * gridDim.x, ...;
     the item offsets are the same for every block (o doubles as the store offsets)"""
     return f"""__global__ __launch_bounds__(256, 2) void {K}(FdecArgs a)
@@ -344,6 +347,7 @@ def persist_kernel(K, nr, body):
         const uint32_t tmax = 32u - (uint32_t)__builtin_clz(ps0);
         const uint64_t em = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane(a.emask[2 * (uint64_t)blk]) |
                             ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane(a.emask[2 * (uint64_t)blk + 1]) << 32);
+        const uint32_t pk = a.num_data ? __builtin_amdgcn_readfirstlane((uint32_t)a.num_data[blk]) : {k}u;
         if (lane == 0) {{
             a.rows[blk] = 0;
             a.psel[2 * (uint64_t)blk] = 0;
@@ -355,7 +359,7 @@ def persist_kernel(K, nr, body):
             "{body}\\n"
             :
             : [base] "s"(base), [em] "s"(em), [cp] "s"(cp), [sp] "s"(sp), [e] "s"(e), [ss] "s"(a.seg_stride),
-              [acc] "s"(a.accumulate), [ps] "s"(ps0), [tmax] "s"(tmax),
+              [acc] "s"(a.accumulate), [ps] "s"(ps0), [tmax] "s"(tmax), [pk] "s"(pk),
               [o0] "v"(o[0]), [o1] "v"(o[1]), [o2] "v"(o[2]), [o3] "v"(o[3]),
               [s0] "v"(o[0]), [s1] "v"(o[1]), [s2] "v"(o[2]), [s3] "v"(o[3])
             : {clobbers()});
@@ -380,7 +384,7 @@ def gen_kernel(k, m, probe=None):
                f"        for (int i = 0; i < {nsleep}; ++i) __builtin_amdgcn_s_sleep(127);\n") if nsleep else ""
     body = "\\n\"\n        \"".join(asm)
     if probe == "persist":
-        return persist_kernel(K, nr, body)
+        return persist_kernel(K, nr, body, k)
     return f"""__global__ __launch_bounds__(256, 2) void {K}(FdecArgs a)
 {{
     const uint32_t lane = threadIdx.x & 63;
@@ -398,6 +402,9 @@ def gen_kernel(k, m, probe=None):
     // high word)
     const uint64_t em = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane(a.emask[2 * (uint64_t)blk]) |
                         ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane(a.emask[2 * (uint64_t)blk + 1]) << 32);
+    // the block's parity slot 0: numData (a shortened block; the plan put its columns
+    // [numData, k) into em, so they are neither read nor computed), else k
+    const uint32_t pk = a.num_data ? __builtin_amdgcn_readfirstlane((uint32_t)a.num_data[blk]) : {k}u;
     // hand the block off: the unfused stage 1 and solve that follow on the stream skip it
     if (lane == 0) {{
         a.rows[blk] = 0;
@@ -426,7 +433,7 @@ def gen_kernel(k, m, probe=None):
         "{body}\\n"
         :
         : [base] "s"(base), [em] "s"(em), [cp] "s"(cp), [sp] "s"(sp), [e] "s"(e), [ss] "s"(a.seg_stride),
-          [acc] "s"(a.accumulate), [ps] "s"(ps0), [tmax] "s"(tmax),
+          [acc] "s"(a.accumulate), [ps] "s"(ps0), [tmax] "s"(tmax), [pk] "s"(pk),
           [o0] "v"(o[0]), [o1] "v"(o[1]), [o2] "v"(o[2]), [o3] "v"(o[3]),
           [s0] "v"(so[0]), [s1] "v"(so[1]), [s2] "v"(so[2]), [s3] "v"(so[3])
         : {clobbers()});

@@ -248,9 +248,12 @@ def gen_dec_role(k, m, role, r0, rows, cfg):
     L.append("    // t = rank of row p among the used rows (P is the first e surviving parity rows in")
     L.append("    // ascending order), so no table lookup; received parity is prefetched 4 rows ahead.")
     ahead = min(4, rows)
+    # parity slot 0 of each item's block: numData (shortened blocks), else k
+    L.append("    uint32_t " + ", ".join(f"p{i} = o{i} + (a.num_data ? (uint32_t)a.num_data[tl.blk[{i}]] : {k}u) * sstride"
+                                       for i in range(4)) + ";")
     for r in range(ahead):
         p = r0 + r
-        L.append(f"    uint2 " + ", ".join(f"q{r}_{i} = bs::bld8(it.rs, o{i}, {k + p}u * sstride)" for i in range(4)) + ";")
+        L.append(f"    uint2 " + ", ".join(f"q{r}_{i} = bs::bld8(it.rs, p{i}, {p}u * sstride)" for i in range(4)) + ";")
     for r in range(rows):
         p = r0 + r
         q = r % ahead
@@ -258,7 +261,7 @@ def gen_dec_role(k, m, role, r0, rows, cfg):
         L.append(f"        const uint2 c0 = q{q}_0, c1 = q{q}_1, c2 = q{q}_2, c3 = q{q}_3;")
         if r + ahead < rows:
             pn = r0 + r + ahead
-            L.append("        " + "; ".join(f"q{q}_{i} = bs::bld8(it.rs, o{i}, {k + pn}u * sstride)" for i in range(4)) + ";")
+            L.append("        " + "; ".join(f"q{q}_{i} = bs::bld8(it.rs, p{i}, {pn}u * sstride)" for i in range(4)) + ";")
         L.append(f"        bs::transpose8(a{r}_0, a{r}_1, a{r}_2, a{r}_3, a{r}_4, a{r}_5, a{r}_6, a{r}_7);")
         for i in range(4):
             L.append(f"        if ((tl.sel[{i}] >> {p}) & 1u) {{")

@@ -337,17 +337,20 @@ def short_pack_nd(k):
 _mask_id = [0]
 
 
-def short_mask(col, w):
-    """zero the loaded dwords w[2q], w[2q+1] of every piece q whose numData <= col (skipped when
-    no lane holds such a piece)"""
+def short_mask(col, w, tail):
+    """zero the loaded dwords w[2q], w[2q+1] of every piece q whose numData <= col.  The common
+    case -- no lane holds such a piece -- falls through a not-taken branch; the masking itself
+    sits out of line (appended to `tail`, placed after the epilogue) and jumps back"""
     _mask_id[0] += 1
-    skip = f"Lnomask{_mask_id[0]}_%="
-    L = [f"v_cmp_gt_u32 vcc, {col + 1}, v{SHORT_TMP[1]}", f"s_cbranch_vccz {skip}"]
+    i = _mask_id[0]
+    L = [f"v_cmp_gt_u32 vcc, {col + 1}, v{SHORT_TMP[1]}", f"s_cbranch_vccnz Lmask{i}_%=", f"Lback{i}_%=:"]
+    tail.append(f"Lmask{i}_%=:")
     for q in range(4):
-        L += [f"v_cmp_lt_u32_sdwa vcc, {col}, v{SHORT_TMP[0]} src0_sel:DWORD src1_sel:BYTE_{q}",
-              f"v_cndmask_b32 v{w[2 * q]}, 0, v{w[2 * q]}, vcc",
-              f"v_cndmask_b32 v{w[2 * q + 1]}, 0, v{w[2 * q + 1]}, vcc"]
-    return L + [f"{skip}:"]
+        tail += [f"v_cmp_lt_u32_sdwa vcc, {col}, v{SHORT_TMP[0]} src0_sel:DWORD src1_sel:BYTE_{q}",
+                 f"v_cndmask_b32 v{w[2 * q]}, 0, v{w[2 * q]}, vcc",
+                 f"v_cndmask_b32 v{w[2 * q + 1]}, 0, v{w[2 * q + 1]}, vcc"]
+    tail.append(f"s_branch Lback{i}_%=")
+    return L
 
 
 def role_asm(G, k, m, w, probe=None, cfg=DEFAULT, short=False):
@@ -356,6 +359,7 @@ def role_asm(G, k, m, w, probe=None, cfg=DEFAULT, short=False):
     NS = cfg.nslot
     rows = m // NW
     r0 = w * rows
+    tail = []  # out-of-line blocks (shortened masking), after the epilogue
     steps = k // NW
     L = []
     L.append(f"s_mov_b64 s[{S_LRS}:{S_LRS + 1}], %[ib]")
@@ -391,7 +395,7 @@ def role_asm(G, k, m, w, probe=None, cfg=DEFAULT, short=False):
         if short:
             if s == 0:
                 L += short_pack_nd(k)
-            L += short_mask(NW * s + w, own)
+            L += short_mask(NW * s + w, own, tail)
         if nocompute:
             for i in range(8):  # keep the loaded data live
                 L.append(f"v_xor_b32 v{acc_reg(0, i)}, v{own[i]}, v{acc_reg(0, i)}")
@@ -460,6 +464,8 @@ def role_asm(G, k, m, w, probe=None, cfg=DEFAULT, short=False):
         L.append(f"Lnoacc_{r}_%=:")
         for q in range(4):
             L.append(f"buffer_store_dwordx2 v[{acc[2 * q]}:{acc[2 * q + 1]}], {offs[q]}, s[{S_SRS}:{S_SRS + 3}], s{S_ROW} offen{cfg.spol}")
+    if tail:
+        L += ["s_branch Lroleend_%="] + tail + ["Lroleend_%=:"]
     return L
 
 
