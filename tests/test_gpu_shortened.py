@@ -211,8 +211,8 @@ def test_rs8_shortened_decode_on_the_fixed_kernels(orc, k, m, vec, nb, acc):
         else:              # everything a block can lose and still decode
             es = min(n, m // 2)
             ep = m - es
-        es = min(es, n)
-        ep = min(ep, m - es)
+        es = min(es, n, m)
+        ep = max(0, min(ep, m - es))
         e = np.sort(np.concatenate([rng.choice(n, es, replace=False), n + rng.choice(m, ep, replace=False)]))
         if b == 7:         # one past the parity count: undecodable, the block stays as it is
             e = np.sort(rng.choice(n + m, min(n + m, m + 1), replace=False))
