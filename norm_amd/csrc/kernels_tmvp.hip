@@ -45,8 +45,9 @@ struct ItemMapB {
 };
 
 // (sc, sc_stride: the scratch the kernel reads or writes -- level 2: a.sc; level 1: a.s or a.x)
-// SH (shortened batch, a.num_data): nd[j] = the numData of item j's block (k outside the batch);
-// an item whose block has numData 0 or past k is treated as outside the batch (left alone)
+// SH (the shortened-capable form; a.num_data may be null: every block has k): nd[j] = the
+// numData of item j's block (k outside the batch); an item whose block has numData 0 or past k
+// is treated as outside the batch (left alone)
 template <bool SH>
 __device__ __forceinline__ void map_items_b(const Rs16TmvpArgs& a, uint32_t chunk, uint32_t lane, ItemMapB& m,
                                             uint8_t* sc, uint64_t sc_stride, uint32_t nd[8])
@@ -62,7 +63,7 @@ __device__ __forceinline__ void map_items_b(const Rs16TmvpArgs& a, uint32_t chun
         const uint32_t b = it / ipb, off = (it - b * ipb) * 8u, db = b - blk0;
         bool ok = it < items;
         nd[j] = a.k;
-        if (SH && ok) {
+        if (SH && ok && a.num_data) {
             const uint32_t v = a.num_data[b];
             ok = v >= 1u && v <= a.k;
             nd[j] = ok ? v : a.k;
@@ -210,8 +211,8 @@ __global__ __launch_bounds__(256, 4) void tmvp_postscale_kernel(Rs16TmvpArgs a)
     store16_b(o, m.src, r1, pv);
 }
 
-template <bool SH>
-__global__ __launch_bounds__(256, 4) void tmvp2_prescale_kernel(Rs16TmvpArgs a)
+template <bool SH, int W>
+__global__ __launch_bounds__(256, W) void tmvp2_prescale_kernel(Rs16TmvpArgs a)
 {
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t wid = __builtin_amdgcn_readfirstlane(blockIdx.x * 4u + (threadIdx.x >> 6));
@@ -327,6 +328,18 @@ __global__ __launch_bounds__(256, 3) void tmvp2_postscale_kernel(Rs16TmvpArgs a)
 
 }  // namespace
 
+static bool tmvp_sh_always()
+{
+    static const bool v = diag_knob("NFEC_TMVP_SH", 0) != 0;
+    return v;
+}
+
+static int tmvp_pre_waves()
+{
+    static const int v = (int)diag_knob("NFEC_TMVP_PRE_W", 4, 4, 5);
+    return v;
+}
+
 int launch_tmvp2_prescale(const Rs16TmvpArgs& a, hipStream_t s)
 {
     const uint64_t items = (uint64_t)a.nblocks * (a.vec / 8u);
@@ -334,8 +347,16 @@ int launch_tmvp2_prescale(const Rs16TmvpArgs& a, hipStream_t s)
     // (the postscale's 32-bit offsets: checked here too, before anything is written)
     if (!a.hw || !a.sc || items >= (1ull << 32) || waves >= (1ull << 32) || !tmvp2_offsets_fit(a)) return NFEC_ENOTSUP;
     if (waves == 0) return NFEC_OK;
-    if (a.num_data) hipLaunchKernelGGL(tmvp2_prescale_kernel<true>, dim3((uint32_t)((waves + 3) / 4)), dim3(256), 0, s, a);
-    else hipLaunchKernelGGL(tmvp2_prescale_kernel<false>, dim3((uint32_t)((waves + 3) / 4)), dim3(256), 0, s, a);
+    // A/B knobs (diagnostic library): NFEC_TMVP_SH=1 takes the shortened-capable kernels for
+    // unshortened batches too; NFEC_TMVP_PRE_W=5 bounds the prescale for 5 waves per SIMD
+    const dim3 g((uint32_t)((waves + 3) / 4));
+    if (a.num_data || tmvp_sh_always()) {
+        if (tmvp_pre_waves() == 5) hipLaunchKernelGGL((tmvp2_prescale_kernel<true, 5>), g, dim3(256), 0, s, a);
+        else hipLaunchKernelGGL((tmvp2_prescale_kernel<true, 4>), g, dim3(256), 0, s, a);
+    } else {
+        if (tmvp_pre_waves() == 5) hipLaunchKernelGGL((tmvp2_prescale_kernel<false, 5>), g, dim3(256), 0, s, a);
+        else hipLaunchKernelGGL((tmvp2_prescale_kernel<false, 4>), g, dim3(256), 0, s, a);
+    }
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? NFEC_OK : hip_fail(e, "tmvp level-2 prescale launch");
 }
@@ -346,7 +367,7 @@ int launch_tmvp2_postscale(const Rs16TmvpArgs& a, hipStream_t s)
     const uint64_t waves = (items + 511) / 512 * a.hw;
     if (!a.hw || !a.sc || items >= (1ull << 32) || waves >= (1ull << 32) || !tmvp2_offsets_fit(a)) return NFEC_ENOTSUP;
     if (waves == 0) return NFEC_OK;
-    if (a.num_data) hipLaunchKernelGGL(tmvp2_postscale_kernel<true>, dim3((uint32_t)((waves + 3) / 4)), dim3(256), 0, s, a);
+    if (a.num_data || tmvp_sh_always()) hipLaunchKernelGGL(tmvp2_postscale_kernel<true>, dim3((uint32_t)((waves + 3) / 4)), dim3(256), 0, s, a);
     else hipLaunchKernelGGL(tmvp2_postscale_kernel<false>, dim3((uint32_t)((waves + 3) / 4)), dim3(256), 0, s, a);
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? NFEC_OK : hip_fail(e, "tmvp level-2 postscale launch");
@@ -359,7 +380,7 @@ int launch_tmvp_prescale(const Rs16TmvpArgs& a, hipStream_t s)
     // (the postscale's 32-bit offsets: checked here too, before anything is written)
     if (items >= (1ull << 32) || waves >= (1ull << 32) || !tmvp1_offsets_fit(a)) return NFEC_ENOTSUP;
     if (waves == 0) return NFEC_OK;
-    if (a.num_data) hipLaunchKernelGGL(tmvp_prescale_kernel<true>, dim3((uint32_t)((waves + 3) / 4)), dim3(256), 0, s, a);
+    if (a.num_data || tmvp_sh_always()) hipLaunchKernelGGL(tmvp_prescale_kernel<true>, dim3((uint32_t)((waves + 3) / 4)), dim3(256), 0, s, a);
     else hipLaunchKernelGGL(tmvp_prescale_kernel<false>, dim3((uint32_t)((waves + 3) / 4)), dim3(256), 0, s, a);
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? NFEC_OK : hip_fail(e, "tmvp prescale launch");
@@ -371,7 +392,7 @@ int launch_tmvp_postscale(const Rs16TmvpArgs& a, hipStream_t s)
     const uint64_t waves = (items + 511) / 512 * a.cw;
     if (items >= (1ull << 32) || waves >= (1ull << 32) || !tmvp1_offsets_fit(a)) return NFEC_ENOTSUP;
     if (waves == 0) return NFEC_OK;
-    if (a.num_data) hipLaunchKernelGGL(tmvp_postscale_kernel<true>, dim3((uint32_t)((waves + 3) / 4)), dim3(256), 0, s, a);
+    if (a.num_data || tmvp_sh_always()) hipLaunchKernelGGL(tmvp_postscale_kernel<true>, dim3((uint32_t)((waves + 3) / 4)), dim3(256), 0, s, a);
     else hipLaunchKernelGGL(tmvp_postscale_kernel<false>, dim3((uint32_t)((waves + 3) / 4)), dim3(256), 0, s, a);
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? NFEC_OK : hip_fail(e, "tmvp postscale launch");
