@@ -37,7 +37,7 @@ int hip_fail(hipError_t e, const char* what);
 // what it runs.  Values outside [lo, hi] fall back to the default.
 inline long diag_knob(const char* name, long def, long lo = 0, long hi = 1)
 {
-#ifdef NFEC_DIAG
+#if defined(NFEC_DIAG) || defined(NFEC_KNOBS)  // (NFEC_KNOBS: an A/B build of the product kernels, tools/ab_build.sh)
     const char* e = std::getenv(name);
     if (!e || !*e) return def;
     const long v = std::strtol(e, nullptr, 0);

@@ -1,6 +1,6 @@
 #!/bin/bash
 # A/B of diag_knob switches on one box: the knob library (tools/ab_build.sh with
-# AB_FLAGS=-DNFEC_DIAG) under each environment setting of AB_ENVS (';'-separated, e.g.
+# AB_FLAGS=-DNFEC_KNOBS) under each environment setting of AB_ENVS (';'-separated, e.g.
 # "NFEC_TMVP_SH=0;NFEC_TMVP_SH=1"), alternating AB_REPS times (default 2), each run of
 # tools/bench_extra.py $AB_ARGS under a rocprofv3 kernel trace; one JSON line per run plus its
 # kernel stats under gpurun_out/$TAG/.
