@@ -45,10 +45,12 @@ struct ItemMapB {
 };
 
 // (sc, sc_stride: the scratch the kernel reads or writes -- level 2: a.sc; level 1: a.s or a.x)
-// SH (the shortened-capable form; a.num_data may be null: every block has k): nd[j] = the
-// numData of item j's block (k outside the batch); an item whose block has numData 0 or past k
-// is treated as outside the batch (left alone)
-template <bool SH>
+// nd[j] = the numData of item j's block (k without a.num_data, and outside the batch); an item
+// whose block has numData 0 or past k is treated as outside the batch (left alone).  Unshortened
+// batches take the same code with nd = k: the parity addressed as the item offset + k x stride
+// and a small slot offset measured 2 % faster over the whole RS16(400,100) encode than the item
+// offset + (k + row) x stride (postscale 138 -> 126 VGPRs, 4 waves per SIMD instead of 3;
+// profiles/r06/tmvp_sh_ab.jsonl)
 __device__ __forceinline__ void map_items_b(const Rs16TmvpArgs& a, uint32_t chunk, uint32_t lane, ItemMapB& m,
                                             uint8_t* sc, uint64_t sc_stride, uint32_t nd[8])
 {
@@ -63,7 +65,7 @@ __device__ __forceinline__ void map_items_b(const Rs16TmvpArgs& a, uint32_t chun
         const uint32_t b = it / ipb, off = (it - b * ipb) * 8u, db = b - blk0;
         bool ok = it < items;
         nd[j] = a.k;
-        if (SH && ok && a.num_data) {
+        if (ok && a.num_data) {
             const uint32_t v = a.num_data[b];
             ok = v >= 1u && v <= a.k;
             nd[j] = ok ? v : a.k;
@@ -130,7 +132,6 @@ static bool tmvp1_offsets_fit(const Rs16TmvpArgs& a)
 // chunk * 512 + j * 64 + lane, flat over (block, position in the segment), addressed as above.
 // v = c_a d_a + c_b d_b for every chunk pair: virtual column q*cw + i from columns
 // a = 2q*cw + i and b = a + cw (c_0 = 0: column 0 is added by the postscale)
-template <bool SH>
 __global__ __launch_bounds__(256, 4) void tmvp_prescale_kernel(Rs16TmvpArgs a)
 {
     const uint32_t lane = threadIdx.x & 63;
@@ -143,17 +144,14 @@ __global__ __launch_bounds__(256, 4) void tmvp_prescale_kernel(Rs16TmvpArgs a)
     const uint32_t ca = 2u * q * a.cw + i, cb = ca + a.cw;
     ItemMapB m;
     uint32_t nd[8];
-    map_items_b<SH>(a, chunk, lane, m, a.s, a.s_block_stride, nd);
+    map_items_b(a, chunk, lane, m, a.s, a.s_block_stride, nd);
     uint32_t x[16], y[16], z[16];
-    if (SH) {  // shortened blocks: source columns at or past numData read zeros
+    {  // shortened blocks: source columns at or past numData read zeros
         uint32_t o[8];
         col_offsets(o, m.vs, nd, ca);
         load16_b(x, m.src, ca * a.seg_stride, o);
         col_offsets(o, m.vs, nd, cb);
         load16_b(y, m.src, cb * a.seg_stride, o);
-    } else {
-        load16_b(x, m.src, ca * a.seg_stride, m.vs);
-        load16_b(y, m.src, cb * a.seg_stride, m.vs);
     }
     bs16::transpose(x);
     bs16::transpose(y);
@@ -167,7 +165,6 @@ __global__ __launch_bounds__(256, 4) void tmvp_prescale_kernel(Rs16TmvpArgs a)
 
 // parity row p < cw and p + cw from P0 (parity row p), P1 (x row p), P2 (parity row cw + p)
 // and source column 0 (shortened blocks: the parity rows at slot numData + r)
-template <bool SH>
 __global__ __launch_bounds__(256, 4) void tmvp_postscale_kernel(Rs16TmvpArgs a)
 {
     const uint32_t lane = threadIdx.x & 63;
@@ -176,15 +173,10 @@ __global__ __launch_bounds__(256, 4) void tmvp_postscale_kernel(Rs16TmvpArgs a)
     const uint32_t ipb = a.vec / 8u, items = a.nblocks * ipb;
     if (chunk * 512u >= items) return;
     ItemMapB m;
-    uint32_t nd[8], vp[8];
-    map_items_b<SH>(a, chunk, lane, m, a.x, a.x_block_stride, nd);
-    const uint32_t* pv = m.vs;  // parity rows: from slot k (vs) or slot numData (vp)
-    if (SH) {
-        parity_offsets(vp, m.vs, nd, a.seg_stride);
-        pv = vp;
-    }
-    const uint32_t pbase = SH ? 0u : a.k;
-    const uint32_t r0 = (pbase + p) * a.seg_stride, r1 = (pbase + a.cw + p) * a.seg_stride;
+    uint32_t nd[8], pv[8];
+    map_items_b(a, chunk, lane, m, a.x, a.x_block_stride, nd);
+    parity_offsets(pv, m.vs, nd, a.seg_stride);  // parity rows from slot numData (k unshortened)
+    const uint32_t r0 = p * a.seg_stride, r1 = (a.cw + p) * a.seg_stride;
     uint32_t t0[16], t1[16], d0[16], o[16];
     load16_b(t0, m.src, r0, pv);
     load16_b(d0, m.src, 0u, m.vs);
@@ -211,8 +203,7 @@ __global__ __launch_bounds__(256, 4) void tmvp_postscale_kernel(Rs16TmvpArgs a)
     store16_b(o, m.src, r1, pv);
 }
 
-template <bool SH, int W>
-__global__ __launch_bounds__(256, W) void tmvp2_prescale_kernel(Rs16TmvpArgs a)
+__global__ __launch_bounds__(256, 4) void tmvp2_prescale_kernel(Rs16TmvpArgs a)
 {
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t wid = __builtin_amdgcn_readfirstlane(blockIdx.x * 4u + (threadIdx.x >> 6));
@@ -225,19 +216,15 @@ __global__ __launch_bounds__(256, W) void tmvp2_prescale_kernel(Rs16TmvpArgs a)
     const uint32_t col[4] = {a0, a0 + a.hw, a0 + a.cw, a0 + a.cw + a.hw};  // a0, a1, b0, b1
     ItemMapB m;
     uint32_t nd[8];
-    map_items_b<SH>(a, chunk, lane, m, a.sc, a.sc_block_stride, nd);
+    map_items_b(a, chunk, lane, m, a.sc, a.sc_block_stride, nd);
     // all four columns' loads in flight first, then each scaled in place (shortened blocks:
     // columns at or past numData read zeros)
     uint32_t r[4][16];
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
-        if (SH) {
-            uint32_t o[8];
-            col_offsets(o, m.vs, nd, col[t]);
-            load16_b(r[t], m.src, col[t] * a.seg_stride, o);
-        } else {
-            load16_b(r[t], m.src, col[t] * a.seg_stride, m.vs);
-        }
+        uint32_t o[8];
+        col_offsets(o, m.vs, nd, col[t]);
+        load16_b(r[t], m.src, col[t] * a.seg_stride, o);
     }
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
@@ -274,7 +261,6 @@ __global__ __launch_bounds__(256, W) void tmvp2_prescale_kernel(Rs16TmvpArgs a)
 // The wave loads each of the nine products once into four sums (143 VGPRs, no spill; one
 // output at a time, reloading the products, measured 1.82 against 1.56 ms per 16,384
 // RS16(400,100) blocks).
-template <bool SH>
 __global__ __launch_bounds__(256, 3) void tmvp2_postscale_kernel(Rs16TmvpArgs a)
 {
     const uint32_t lane = threadIdx.x & 63;
@@ -284,7 +270,7 @@ __global__ __launch_bounds__(256, 3) void tmvp2_postscale_kernel(Rs16TmvpArgs a)
     if (chunk * 512u >= items) return;
     ItemMapB m;
     uint32_t nd[8];
-    map_items_b<SH>(a, chunk, lane, m, a.sc, a.sc_block_stride, nd);
+    map_items_b(a, chunk, lane, m, a.sc, a.sc_block_stride, nd);
     const uint32_t pr = (tmvp2_prow0(a) + p) * a.vec;  // product e's row p at pr + e hw vec
     // output rows (R0 top, R0 bottom, R1 top, R1 bottom): bit t of uses[e] = product e feeds output t
     constexpr uint8_t uses[9] = {0xF, 0x5, 0xA, 0x3, 0x1, 0x2, 0xC, 0x4, 0x8};
@@ -304,14 +290,9 @@ __global__ __launch_bounds__(256, 3) void tmvp2_postscale_kernel(Rs16TmvpArgs a)
     }
     load16_b(x, m.src, 0u, m.vs);
     bs16::transpose(x);  // d_0, bit-sliced
-    // parity rows at slot k + row, or numData + row for shortened blocks
-    uint32_t vp[8];
-    const uint32_t* pv = m.vs;
-    if (SH) {
-        parity_offsets(vp, m.vs, nd, a.seg_stride);
-        pv = vp;
-    }
-    const uint32_t pbase = SH ? 0u : a.k;
+    // parity rows at slot numData + row (k unshortened)
+    uint32_t pv[8];
+    parity_offsets(pv, m.vs, nd, a.seg_stride);
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
         const uint32_t row = (uint32_t)(t >> 1) * a.cw + (uint32_t)(t & 1) * a.hw + p;
@@ -322,23 +303,11 @@ __global__ __launch_bounds__(256, 3) void tmvp2_postscale_kernel(Rs16TmvpArgs a)
         bs16::mulc_acc(sum[t], o, a.wmat + 16u * row);
         bs16::mulc_acc(x, o, a.gmat + 16u * row);
         bs16::transpose(o);
-        store16_b(o, m.src, (pbase + row) * a.seg_stride, pv);
+        store16_b(o, m.src, row * a.seg_stride, pv);
     }
 }
 
 }  // namespace
-
-static bool tmvp_sh_always()
-{
-    static const bool v = diag_knob("NFEC_TMVP_SH", 0) != 0;
-    return v;
-}
-
-static int tmvp_pre_waves()
-{
-    static const int v = (int)diag_knob("NFEC_TMVP_PRE_W", 4, 4, 5);
-    return v;
-}
 
 int launch_tmvp2_prescale(const Rs16TmvpArgs& a, hipStream_t s)
 {
@@ -347,16 +316,7 @@ int launch_tmvp2_prescale(const Rs16TmvpArgs& a, hipStream_t s)
     // (the postscale's 32-bit offsets: checked here too, before anything is written)
     if (!a.hw || !a.sc || items >= (1ull << 32) || waves >= (1ull << 32) || !tmvp2_offsets_fit(a)) return NFEC_ENOTSUP;
     if (waves == 0) return NFEC_OK;
-    // A/B knobs (diagnostic library): NFEC_TMVP_SH=1 takes the shortened-capable kernels for
-    // unshortened batches too; NFEC_TMVP_PRE_W=5 bounds the prescale for 5 waves per SIMD
-    const dim3 g((uint32_t)((waves + 3) / 4));
-    if (a.num_data || tmvp_sh_always()) {
-        if (tmvp_pre_waves() == 5) hipLaunchKernelGGL((tmvp2_prescale_kernel<true, 5>), g, dim3(256), 0, s, a);
-        else hipLaunchKernelGGL((tmvp2_prescale_kernel<true, 4>), g, dim3(256), 0, s, a);
-    } else {
-        if (tmvp_pre_waves() == 5) hipLaunchKernelGGL((tmvp2_prescale_kernel<false, 5>), g, dim3(256), 0, s, a);
-        else hipLaunchKernelGGL((tmvp2_prescale_kernel<false, 4>), g, dim3(256), 0, s, a);
-    }
+    hipLaunchKernelGGL(tmvp2_prescale_kernel, dim3((uint32_t)((waves + 3) / 4)), dim3(256), 0, s, a);
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? NFEC_OK : hip_fail(e, "tmvp level-2 prescale launch");
 }
@@ -367,8 +327,7 @@ int launch_tmvp2_postscale(const Rs16TmvpArgs& a, hipStream_t s)
     const uint64_t waves = (items + 511) / 512 * a.hw;
     if (!a.hw || !a.sc || items >= (1ull << 32) || waves >= (1ull << 32) || !tmvp2_offsets_fit(a)) return NFEC_ENOTSUP;
     if (waves == 0) return NFEC_OK;
-    if (a.num_data || tmvp_sh_always()) hipLaunchKernelGGL(tmvp2_postscale_kernel<true>, dim3((uint32_t)((waves + 3) / 4)), dim3(256), 0, s, a);
-    else hipLaunchKernelGGL(tmvp2_postscale_kernel<false>, dim3((uint32_t)((waves + 3) / 4)), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(tmvp2_postscale_kernel, dim3((uint32_t)((waves + 3) / 4)), dim3(256), 0, s, a);
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? NFEC_OK : hip_fail(e, "tmvp level-2 postscale launch");
 }
@@ -380,8 +339,7 @@ int launch_tmvp_prescale(const Rs16TmvpArgs& a, hipStream_t s)
     // (the postscale's 32-bit offsets: checked here too, before anything is written)
     if (items >= (1ull << 32) || waves >= (1ull << 32) || !tmvp1_offsets_fit(a)) return NFEC_ENOTSUP;
     if (waves == 0) return NFEC_OK;
-    if (a.num_data || tmvp_sh_always()) hipLaunchKernelGGL(tmvp_prescale_kernel<true>, dim3((uint32_t)((waves + 3) / 4)), dim3(256), 0, s, a);
-    else hipLaunchKernelGGL(tmvp_prescale_kernel<false>, dim3((uint32_t)((waves + 3) / 4)), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(tmvp_prescale_kernel, dim3((uint32_t)((waves + 3) / 4)), dim3(256), 0, s, a);
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? NFEC_OK : hip_fail(e, "tmvp prescale launch");
 }
@@ -392,8 +350,7 @@ int launch_tmvp_postscale(const Rs16TmvpArgs& a, hipStream_t s)
     const uint64_t waves = (items + 511) / 512 * a.cw;
     if (items >= (1ull << 32) || waves >= (1ull << 32) || !tmvp1_offsets_fit(a)) return NFEC_ENOTSUP;
     if (waves == 0) return NFEC_OK;
-    if (a.num_data || tmvp_sh_always()) hipLaunchKernelGGL(tmvp_postscale_kernel<true>, dim3((uint32_t)((waves + 3) / 4)), dim3(256), 0, s, a);
-    else hipLaunchKernelGGL(tmvp_postscale_kernel<false>, dim3((uint32_t)((waves + 3) / 4)), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(tmvp_postscale_kernel, dim3((uint32_t)((waves + 3) / 4)), dim3(256), 0, s, a);
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? NFEC_OK : hip_fail(e, "tmvp postscale launch");
 }
