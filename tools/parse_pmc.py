@@ -13,6 +13,7 @@ from collections import defaultdict
 
 
 def main(root):
+    root = root.rstrip('/')
     # counter rows can come per XCD/SE instance: sum the rows of one dispatch, then average
     # over dispatches (per-launch totals)
     per = defaultdict(lambda: defaultdict(lambda: defaultdict(float)))
@@ -56,6 +57,19 @@ def main(root):
             "method": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE in separate passes; read = 2 x FETCH_SIZE KiB "
                       "(gfx950 correction, MI355X_MICROARCH.md HBM), write = WRITE_SIZE KiB",
         }
+        # the repair kernel of the same workload (the fused per-block repair, 16 source erasures)
+        dec = [n for n, v in out.items() if "fdec" in n and "k64_m32" in n and "FETCH_SIZE" in v]
+        if dec:
+            d = out[dec[0]]
+            traffic.update({
+                "decode_kernel": dec[0],
+                "decode_hbm_bytes_per_launch": round(d["hbm_read_bytes_corrected"] + d["hbm_write_bytes"]),
+                "decode_read_bytes_corrected": round(d["hbm_read_bytes_corrected"]),
+                "decode_write_bytes": round(d["hbm_write_bytes"]),
+                "decode_valu_insts_per_launch": round(d["SQ_INSTS_VALU"]) if "SQ_INSTS_VALU" in d else None,
+                "decode_salu_insts_per_launch": round(d["SQ_INSTS_SALU"]) if "SQ_INSTS_SALU" in d else None,
+            })
+        traffic["source"] = os.path.relpath(root) if not os.path.isabs(root) else root
         with open(sys.argv[2], "w") as f:
             json.dump(traffic, f, indent=1)
             f.write("\n")
