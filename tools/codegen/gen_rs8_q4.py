@@ -382,8 +382,10 @@ def role_asm(G, k, m, w, probe=None, cfg=DEFAULT, short=False):
             out.append(f"buffer_load_dwordx2 v[{rs[2 * q]}:{rs[2 * q + 1]}], {offs[q]}, s[{S_LRS}:{S_LRS + 3}], s{S_COL} offen{cfg.lpol}")
         return out
 
-    if short:
+    if short and SH_PROBE != "nofetch":
         L += short_fetch_nd(k)
+    elif short:  # (A/B probe: every piece numData k, no fetch, no masking -- timing only)
+        L += [f"v_mov_b32 v{SHORT_TMP[0]}, 0x{k:02x}{k:02x}{k:02x}{k:02x}", f"v_mov_b32 v{SHORT_TMP[1]}, {k}"]
     for s in range(min(NS, steps)):
         L += loads(s)
     for s in range(steps):
@@ -392,10 +394,11 @@ def role_asm(G, k, m, w, probe=None, cfg=DEFAULT, short=False):
         pending = min(steps, s + NS) - (s + 1)  # later steps' loads in flight behind ours
         if not noload:
             L.append(f"s_waitcnt vmcnt({4 * pending})")
-        if short:
+        if short and SH_PROBE != "nofetch":
             if s == 0:
                 L += short_pack_nd(k)
-            L += short_mask(NW * s + w, own, tail)
+            if SH_PROBE != "nomask":
+                L += short_mask(NW * s + w, own, tail)
         if nocompute:
             for i in range(8):  # keep the loaded data live
                 L.append(f"v_xor_b32 v{acc_reg(0, i)}, v{own[i]}, v{acc_reg(0, i)}")
@@ -626,9 +629,17 @@ static int launch_{K}(const bs::EncArgs& a, hipStream_t s)
     return "\n\n".join(out)
 
 
+SH_PROBE = None   # A/B timing probes of the shortened kernels (wrong bytes for masked pieces): --sh-probe nomask|nofetch
+
+
 def main():
     # --diag: also emit the A/B variants and probes and their NFEC_Q4_VARIANT switch (the
     # diagnostic library, make -C norm_amd diag); the product library ships the defaults only
+    global SH_PROBE
+    if "--sh-probe" in sys.argv:
+        i = sys.argv.index("--sh-probe")
+        SH_PROBE = sys.argv[i + 1]
+        del sys.argv[i:i + 2]
     diag = "--diag" in sys.argv
     path = [a for a in sys.argv if a != "--diag"][1]
     parts = [
