@@ -190,3 +190,40 @@ def test_c5_mixed_stream_two_host_threads(orc, pinned):
         assert j["parity_ok"], f"{name} parity"
         assert (j["st"] == j["er"]).all(), f"{name} status"
         assert np.array_equal(j["rx"], j["ref"]), f"{name} repair"
+
+
+@pytest.mark.gpu
+def test_c5_full_share_device_resident(orc):
+    """One GPU's whole C5 share (131,072 stream blocks: 114,726 RS8(64,32) + 16,346
+    RS16(400,100), vec 1400, 26.8 GB in HBM, tools/bench_c5.py's device-resident step): encode
+    both sub-streams, sampled blocks against the oracle's per-segment Encode, then erase 16 / 50
+    source symbols per block and repair: every source byte of every block comes back."""
+    torch = _gpu()
+    import norm_amd as na
+
+    total = 1 << 17
+    ids = np.arange(total, dtype=np.uint64)
+    is16 = (_splitmix64(np.uint64(SEED) ^ ids) % np.uint64(8)) == 0
+    subs = [("RS8", orc.RS8, 64, 32, 16, na.NormEncoderRS8, na.NormDecoderRS8, int((~is16).sum()), SEED ^ 0x8),
+            ("RS16", orc.RS16, 400, 100, 50, na.NormEncoderRS16, na.NormDecoderRS16, int(is16.sum()), SEED ^ 0x16)]
+    assert (subs[0][7], subs[1][7]) == (114726, 16346)
+    for name, kind, k, m, er, E, D, n, seed in subs:
+        enc, dec = E(), D()
+        assert enc.Init(k, m, VEC) and dec.Init(k, m, VEC)
+        d = torch.zeros((n, k + m, VEC), dtype=torch.uint8, device="cuda")
+        na.fill_blocks(d, k, VEC, seed)
+        enc.encode_blocks(d)
+        torch.cuda.synchronize()
+        for b in (0, n // 2 + 3, n - 1):
+            host = orc.make_blocks(k, m, VEC, 1, seed=seed, first_block=b)
+            ref = orc.encode_blocks(kind, k, m, VEC, host)
+            assert np.array_equal(d[b].cpu().numpy(), ref[0]), f"{name} block {b}"
+        keep = d[:, :k].clone()
+        locs, cnts = na.make_erasures(n, k, er, SEED, m)
+        na.zero_erasures(d, locs, cnts, VEC)
+        st = dec.decode_blocks(d, locs, cnts)
+        torch.cuda.synchronize()
+        assert bool((st == er).all()), name
+        assert torch.equal(d[:, :k], keep), name
+        del d, keep, st, locs, cnts
+        torch.cuda.empty_cache()
