@@ -90,16 +90,18 @@ __device__ __forceinline__ void parity_offsets(uint32_t o[8], const uint32_t v[8
     for (int j = 0; j < 8; ++j) o[j] = v[j] == 0x80000000u ? v[j] : v[j] + nd[j] * ss;
 }
 
+template <int AUX = 0>
 __device__ __forceinline__ void load16_b(uint32_t x[16], __amdgpu_buffer_rsrc_t rs, uint32_t soff, const uint32_t v[8])
 {
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-        const bs::u32x2 w = __builtin_amdgcn_raw_buffer_load_b64(rs, v[j], soff, 0);
+        const bs::u32x2 w = __builtin_amdgcn_raw_buffer_load_b64(rs, v[j], soff, AUX);
         x[2 * j] = w.x;
         x[2 * j + 1] = w.y;
     }
 }
 
+template <int AUX = 0>
 __device__ __forceinline__ void store16_b(const uint32_t x[16], __amdgpu_buffer_rsrc_t rs, uint32_t soff, const uint32_t v[8])
 {
 #pragma unroll
@@ -107,7 +109,7 @@ __device__ __forceinline__ void store16_b(const uint32_t x[16], __amdgpu_buffer_
         bs::u32x2 w;
         w.x = x[2 * j];
         w.y = x[2 * j + 1];
-        __builtin_amdgcn_raw_buffer_store_b64(w, rs, v[j], soff, 0);
+        __builtin_amdgcn_raw_buffer_store_b64(w, rs, v[j], soff, AUX);
     }
 }
 
@@ -203,6 +205,8 @@ __global__ __launch_bounds__(256, 4) void tmvp_postscale_kernel(Rs16TmvpArgs a)
     store16_b(o, m.src, r1, pv);
 }
 
+// (SP / LP: cache policy of the scratch stores / source loads, NFEC_TMVP_POLICY A/B, knob library)
+template <int SP, int LP>
 __global__ __launch_bounds__(256, 4) void tmvp2_prescale_kernel(Rs16TmvpArgs a)
 {
     const uint32_t lane = threadIdx.x & 63;
@@ -224,7 +228,7 @@ __global__ __launch_bounds__(256, 4) void tmvp2_prescale_kernel(Rs16TmvpArgs a)
     for (int t = 0; t < 4; ++t) {
         uint32_t o[8];
         col_offsets(o, m.vs, nd, col[t]);
-        load16_b(r[t], m.src, col[t] * a.seg_stride, o);
+        load16_b<LP>(r[t], m.src, col[t] * a.seg_stride, o);
     }
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
@@ -240,19 +244,19 @@ __global__ __launch_bounds__(256, 4) void tmvp2_prescale_kernel(Rs16TmvpArgs a)
     uint32_t o[16];
 #pragma unroll
     for (int p = 0; p < 16; ++p) o[p] = r[0][p] ^ r[2][p];
-    store16_b(o, m.sc, (q * a.cw + i) * a.vec, m.vc);
+    store16_b<SP>(o, m.sc, (q * a.cw + i) * a.vec, m.vc);
 #pragma unroll
     for (int p = 0; p < 16; ++p) o[p] = r[1][p] ^ r[3][p];
-    store16_b(o, m.sc, (q * a.cw + a.hw + i) * a.vec, m.vc);
+    store16_b<SP>(o, m.sc, (q * a.cw + a.hw + i) * a.vec, m.vc);
 #pragma unroll
     for (int p = 0; p < 16; ++p) o[p] = r[0][p] ^ r[1][p] ^ r[2][p] ^ r[3][p];
-    store16_b(o, m.sc, (a.k / 2u + u) * a.vec, m.vc);
+    store16_b<SP>(o, m.sc, (a.k / 2u + u) * a.vec, m.vc);
 #pragma unroll
     for (int p = 0; p < 16; ++p) o[p] = r[2][p] ^ r[3][p];
-    store16_b(o, m.sc, (a.k / 2u + quarter + u) * a.vec, m.vc);
+    store16_b<SP>(o, m.sc, (a.k / 2u + quarter + u) * a.vec, m.vc);
 #pragma unroll
     for (int p = 0; p < 16; ++p) o[p] = r[0][p] ^ r[1][p];
-    store16_b(o, m.sc, (a.k / 2u + 2u * quarter + u) * a.vec, m.vc);
+    store16_b<SP>(o, m.sc, (a.k / 2u + 2u * quarter + u) * a.vec, m.vc);
 }
 
 // per p < hw: level-1 product X's rows p (top) and hw + p (bottom) are P_aX + P_bX and
@@ -261,6 +265,7 @@ __global__ __launch_bounds__(256, 4) void tmvp2_prescale_kernel(Rs16TmvpArgs a)
 // The wave loads each of the nine products once into four sums (143 VGPRs, no spill; one
 // output at a time, reloading the products, measured 1.82 against 1.56 ms per 16,384
 // RS16(400,100) blocks).
+template <int SP, int LP>
 __global__ __launch_bounds__(256, 3) void tmvp2_postscale_kernel(Rs16TmvpArgs a)
 {
     const uint32_t lane = threadIdx.x & 63;
@@ -281,7 +286,7 @@ __global__ __launch_bounds__(256, 3) void tmvp2_postscale_kernel(Rs16TmvpArgs a)
         for (int j = 0; j < 16; ++j) sum[t][j] = 0;
 #pragma unroll
     for (int e = 0; e < 9; ++e) {
-        load16_b(x, m.sc, pr + (uint32_t)e * a.hw * a.vec, m.vc);
+        load16_b<LP>(x, m.sc, pr + (uint32_t)e * a.hw * a.vec, m.vc);
 #pragma unroll
         for (int t = 0; t < 4; ++t)
             if (uses[e] & (1u << t))
@@ -303,8 +308,16 @@ __global__ __launch_bounds__(256, 3) void tmvp2_postscale_kernel(Rs16TmvpArgs a)
         bs16::mulc_acc(sum[t], o, a.wmat + 16u * row);
         bs16::mulc_acc(x, o, a.gmat + 16u * row);
         bs16::transpose(o);
-        store16_b(o, m.src, row * a.seg_stride, pv);
+        store16_b<SP>(o, m.src, row * a.seg_stride, pv);
     }
+}
+
+// cache policy of the level-2 scale kernels' scratch traffic (A/B, knob library; 0 in the product
+// library): 1 nontemporal stores, 2 nontemporal stores and loads, 3 nontemporal loads
+static int tmvp_policy()
+{
+    static const int v = (int)diag_knob("NFEC_TMVP_POLICY", 0, 0, 3);
+    return v;
 }
 
 }  // namespace
@@ -316,7 +329,13 @@ int launch_tmvp2_prescale(const Rs16TmvpArgs& a, hipStream_t s)
     // (the postscale's 32-bit offsets: checked here too, before anything is written)
     if (!a.hw || !a.sc || items >= (1ull << 32) || waves >= (1ull << 32) || !tmvp2_offsets_fit(a)) return NFEC_ENOTSUP;
     if (waves == 0) return NFEC_OK;
-    hipLaunchKernelGGL(tmvp2_prescale_kernel, dim3((uint32_t)((waves + 3) / 4)), dim3(256), 0, s, a);
+    const dim3 g((uint32_t)((waves + 3) / 4));
+    switch (tmvp_policy()) {
+    case 1: hipLaunchKernelGGL((tmvp2_prescale_kernel<2, 0>), g, dim3(256), 0, s, a); break;
+    case 2: hipLaunchKernelGGL((tmvp2_prescale_kernel<2, 2>), g, dim3(256), 0, s, a); break;
+    case 3: hipLaunchKernelGGL((tmvp2_prescale_kernel<0, 2>), g, dim3(256), 0, s, a); break;
+    default: hipLaunchKernelGGL((tmvp2_prescale_kernel<0, 0>), g, dim3(256), 0, s, a); break;
+    }
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? NFEC_OK : hip_fail(e, "tmvp level-2 prescale launch");
 }
@@ -327,7 +346,13 @@ int launch_tmvp2_postscale(const Rs16TmvpArgs& a, hipStream_t s)
     const uint64_t waves = (items + 511) / 512 * a.hw;
     if (!a.hw || !a.sc || items >= (1ull << 32) || waves >= (1ull << 32) || !tmvp2_offsets_fit(a)) return NFEC_ENOTSUP;
     if (waves == 0) return NFEC_OK;
-    hipLaunchKernelGGL(tmvp2_postscale_kernel, dim3((uint32_t)((waves + 3) / 4)), dim3(256), 0, s, a);
+    const dim3 g((uint32_t)((waves + 3) / 4));
+    switch (tmvp_policy()) {
+    case 1: hipLaunchKernelGGL((tmvp2_postscale_kernel<2, 0>), g, dim3(256), 0, s, a); break;
+    case 2: hipLaunchKernelGGL((tmvp2_postscale_kernel<2, 2>), g, dim3(256), 0, s, a); break;
+    case 3: hipLaunchKernelGGL((tmvp2_postscale_kernel<0, 2>), g, dim3(256), 0, s, a); break;
+    default: hipLaunchKernelGGL((tmvp2_postscale_kernel<0, 0>), g, dim3(256), 0, s, a); break;
+    }
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? NFEC_OK : hip_fail(e, "tmvp level-2 postscale launch");
 }
