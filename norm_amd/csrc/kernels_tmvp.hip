@@ -312,11 +312,14 @@ __global__ __launch_bounds__(256, 3) void tmvp2_postscale_kernel(Rs16TmvpArgs a)
     }
 }
 
-// cache policy of the level-2 scale kernels' scratch traffic (A/B, knob library; 0 in the product
-// library): 1 nontemporal stores, 2 nontemporal stores and loads, 3 nontemporal loads
+// cache policy of the level-2 scale kernels (NFEC_TMVP_POLICY, knob library A/B): 0 none,
+// 1 non-temporal stores (the product library), 2 non-temporal stores and loads, 3 non-temporal
+// loads.  One box, alternating twice (profiles/r06/tmvp_policy_ab/): RS16(400,100) prescale 4.98 ->
+// 4.71 ms with non-temporal stores (encode 19.65 -> 19.38 ms), postscale 1.65 -> 1.62 ms; C4
+// encode unchanged (95.5-96.0 ms either way); non-temporal loads slower (prescale 5.5 ms)
 static int tmvp_policy()
 {
-    static const int v = (int)diag_knob("NFEC_TMVP_POLICY", 0, 0, 3);
+    static const int v = (int)diag_knob("NFEC_TMVP_POLICY", 1, 0, 3);
     return v;
 }
 

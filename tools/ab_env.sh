@@ -26,7 +26,7 @@ st = glob.glob(sys.argv[3] + "/**/*_kernel_stats.csv", recursive=True)
 ks = {}
 if st:
     for r in csv.DictReader(open(st[0])):
-        ks[r["Name"].split("(")[0].replace("nfec::(anonymous namespace)::", "").replace("void ", "")] = round(float(r["AverageNs"]) / 1e3, 1)
+        ks[r["Name"].replace("nfec::(anonymous namespace)::", "").replace("void ", "").split("(")[0]] = round(float(r["AverageNs"]) / 1e3, 1)
 d = {"env": sys.argv[2], "encode_ms": d.get("encode_ms"), "decode_ms": d.get("decode_ms"), "verified": d.get("verified"),
      "kernels_us": {k: v for k, v in ks.items() if "tmvp" in k or "gf16" in k or "rs8" in k}}
 open(sys.argv[4], "a").write(json.dumps(d) + "\n")

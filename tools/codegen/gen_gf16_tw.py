@@ -126,6 +126,7 @@ def set_rows(n):
 VARIANTS = {0: ()}
 DIAG_VARIANTS = {0: (), 1: ("nosweep",), 2: ("noload",), 3: ("empty",)}
 FLAGS = ()
+NT_STORES = False        # --nt-stores: the rows' stores non-temporal (A/B builds)
 
 
 # ---------------------------------------------------------------- field
@@ -687,7 +688,8 @@ def epilogue():
             L.append(f"v_xor_b32 v{x[i]}, v{x[i]}, v{tmp[i]}")
         L.append(f"Lna{r}_%=:")
         for i in range(8):
-            L.append(f"buffer_store_dwordx2 v[{x[2 * i]}:{x[2 * i + 1]}], v{V_W + i}, s[{S_ODESC}:{S_ODESC + 3}], s{S_T1} offen")
+            L.append(f"buffer_store_dwordx2 v[{x[2 * i]}:{x[2 * i + 1]}], v{V_W + i}, s[{S_ODESC}:{S_ODESC + 3}], s{S_T1} offen"
+                     + (" nt" if NT_STORES else ""))
     L += ["Lepi_%=:", "s_branch Lend_%="]
     L += snippets()
     L.append("Lend_%=:")
@@ -733,7 +735,7 @@ def main():
         lam, beta, _, _ = choose_tower()
         print(f"LAM, BETA = 0x{lam:02X}, 0x{beta:04X}")
         return
-    global FLAGS, CONFIGS
+    global FLAGS, CONFIGS, NT_STORES
     diag = "--diag" in sys.argv
     args = [a for a in sys.argv[1:] if a != "--diag"]
     if "--noprefetch" in args:
@@ -744,6 +746,9 @@ def main():
         r = int(args[i + 1])
         CONFIGS = [(r, dict(CONFIGS).get(r, True) and PREFETCH)]
         del args[i:i + 2]
+    if "--nt-stores" in args:
+        args.remove("--nt-stores")
+        NT_STORES = True
     if "--waves" in args:
         i = args.index("--waves")
         set_waves(int(args[i + 1]))
