@@ -151,7 +151,7 @@ def fdec_asm(k, m, probe=None, e16=False):
         else:  # (slot numData + t: a shortened block's parity follows its numData sources)
             out += [f"s_add_u32 s{S_COL}, %[pk], {c - k}", f"s_mul_i32 s{S_COL}, s{S_COL}, %[ss]"]
         for q in range(4):
-            out.append(f"buffer_load_dwordx2 v[{w[2 * q]}:{w[2 * q + 1]}], {offs[q]}, s[{S_LRS}:{S_LRS + 3}], s{S_COL} offen")
+            out.append(f"buffer_load_dwordx2 v[{w[2 * q]}:{w[2 * q + 1]}], {offs[q]}, s[{S_LRS}:{S_LRS + 3}], s{S_COL} offen{LPOL}")
         return out
 
     for r in range(16):
@@ -280,7 +280,7 @@ def fdec_asm(k, m, probe=None, e16=False):
                     S.append(f"v_xor_b32 v{w[2 * q + 1]}, v{tmp[2 * q + 1]}, v{w[2 * q + 1]}")
                 S.append(f"Lna{s}{x}_%=:")
                 for q in range(4):
-                    S.append(f"buffer_store_dwordx2 v[{w[2 * q]}:{w[2 * q + 1]}], {soffs[q]}, s[{S_SRS}:{S_SRS + 3}], s{S_T} offen")
+                    S.append(f"buffer_store_dwordx2 v[{w[2 * q]}:{w[2 * q + 1]}], {soffs[q]}, s[{S_SRS}:{S_SRS + 3}], s{S_T} offen{SPOL}")
             if h == 0:
                 S.append(f"Lhalf{h}{x}_%=:")
         return S
@@ -441,11 +441,18 @@ def gen_kernel(k, m, probe=None):
 """
 
 
+LPOL = SPOL = ""   # cache-policy suffixes (main: --nt-loads / --nt-stores)
+
+
 def main():
     # --diag: also emit the A/B probes and their NFEC_FDEC_VARIANT switch (the diagnostic
-    # library, make -C norm_amd diag); the product library ships the default kernels only
+    # library, make -C norm_amd diag); the product library ships the default kernels only.
+    # --nt-loads / --nt-stores: non-temporal column loads / repaired-row stores (A/B builds)
+    global LPOL, SPOL
     diag = "--diag" in sys.argv
-    argv = [a for a in sys.argv if a != "--diag"]
+    LPOL = " nt" if "--nt-loads" in sys.argv else ""
+    SPOL = " nt" if "--nt-stores" in sys.argv else ""
+    argv = [a for a in sys.argv if a not in ("--diag", "--nt-loads", "--nt-stores")]
     path = argv[1]
     shapes = DEFAULT_SHAPES
     if len(argv) > 2:
