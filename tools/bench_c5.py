@@ -15,7 +15,9 @@ codec's pinned-staging pipeline (nfec_encode_host / nfec_decode_host).
 
 Reported as one JSON line in bench.py's schema: value = host-resident GiB/s (source bytes
 through encode + decode, all ranks / max-over-ranks time), plus the device-resident GiB/s of the
-same mix with the blocks already in HBM.
+same mix with the blocks already in HBM (the two sub-streams on two HIP streams: 43.2 ms per
+one-GPU step against 44.0 on one stream, profiles/r06/c5_streams/), and a device round trip
+after the timing (erased source zeroed, repaired, compared).
 
 Page-locked memory: a rank's whole share is 26.8 GB (114,726 RS8 x 96 x 1400 + 16,346 RS16 x
 500 x 1400), 215 GB over 8 ranks.  At N = 1 the whole share is pinned; at N > 1 the host-resident
@@ -163,17 +165,29 @@ def main():
         st = j["dec"].decode_blocks_host(rx, j["locs"][:n].copy(), j["cnts"][:n].copy())
         sample_ok &= bool(np.array_equal(rx, keep)) and bool((st == j["er"]).all())
 
-    # device-resident rate of the same mix (blocks in HBM)
+    # device-resident rate of the same mix (blocks in HBM): the RS8 and RS16 sub-streams on two
+    # HIP streams, as the host-resident step runs them from two threads (--serial: one stream,
+    # one sub-stream after the other)
     dev_jobs = []
-    for j in jobs:
+    main_s = torch.cuda.current_stream(dev)
+    for i, j in enumerate(jobs):
         del j["host"], j["hnp"]  # the pinned copies are done with
-        dev_jobs.append((j, j["dev"], torch.empty(j["n"], dtype=torch.int32, device=dev)))
-    stream = torch.cuda.current_stream(dev)
+        s = main_s if (i == 0 or a.serial) else torch.cuda.Stream(dev)
+        dev_jobs.append((j, j["dev"], torch.empty(j["n"], dtype=torch.int32, device=dev), s))
 
     def dev_step():
-        for j, d, st in dev_jobs:
-            j["enc"].encode_blocks(d, stream=stream)
-            j["dec"].decode_blocks(d, j["dlocs"], j["dcnts"], status=st, stream=stream)
+        start = torch.cuda.Event()
+        start.record(main_s)
+        for j, d, st, s in dev_jobs:
+            if s is not main_s:
+                s.wait_event(start)
+            j["enc"].encode_blocks(d, stream=s)
+            j["dec"].decode_blocks(d, j["dlocs"], j["dcnts"], status=st, stream=s)
+        for j, d, st, s in dev_jobs:
+            if s is not main_s:
+                done = torch.cuda.Event()
+                done.record(s)
+                main_s.wait_event(done)
 
     dev_step()
     torch.cuda.synchronize(dev)
@@ -184,6 +198,20 @@ def main():
     torch.cuda.synchronize(dev)
     barrier()
     dev_s = max_time((time.perf_counter() - t0) / a.steps)
+
+    # device round trip after the timed steps: every sub-stream's erased source zeroed, repaired on
+    # its own stream (concurrently, as timed), compared with the bytes before
+    dev_ok = True
+    for j, d, st, s in dev_jobs:
+        j["keep"] = d[:, :j["k"]].clone()
+        na.zero_erasures(d, j["dlocs"], j["dcnts"], j["vec"], stream=main_s)
+    torch.cuda.synchronize(dev)
+    for j, d, st, s in dev_jobs:
+        j["dec"].decode_blocks(d, j["dlocs"], j["dcnts"], status=st, stream=s)
+    torch.cuda.synchronize(dev)
+    for j, d, st, s in dev_jobs:
+        dev_ok &= bool(torch.equal(d[:, :j["k"]], j["keep"])) and bool((st == j["er"]).all())
+        del j["keep"]
 
     def sum_ranks(v):
         t = torch.tensor([float(v)], dtype=torch.float64, device=dev)
@@ -209,8 +237,9 @@ def main():
                        "note": "host-resident timing on these first blocks of each sub-stream (page-locked); "
                                "device-resident timing on every block of the share"},
             "device_resident": {"value": round(src_all / dev_s / 2**30, 2), "unit": "GiB/s",
-                                "ms_per_step": round(dev_s * 1e3, 2)},
-            "status_ok": host_ok, "sample_round_trip_ok": sample_ok,
+                                "ms_per_step": round(dev_s * 1e3, 2),
+                                "streams": 1 if a.serial else len(dev_jobs)},
+            "status_ok": host_ok, "sample_round_trip_ok": sample_ok, "device_round_trip_ok": dev_ok,
             "rank0_host_s": {j["name"]: [round(j["host_enc_s"], 3), round(j["host_dec_s"], 3)] for j in jobs},
             "note": "one step = encode + 16 (RS8) / 50 (RS16) source-erasure repair of every block; "
                     "GiB/s counts source bytes, all ranks / max-over-ranks time",
