@@ -199,19 +199,21 @@ def main():
     torch.cuda.synchronize(dev)
 
     # ---- timed region: exactly K steps, barrier + sync on both sides ----
-    # HIP events on the launch stream around each half of every step (recording one costs
-    # microseconds): the per-kernel durations of the roofline come from the timed steps
-    # themselves, encode and repair interleaved as the step runs them
-    marks = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(a.steps)]
+    # HIP events on the launch stream around each half of every step: the per-kernel durations
+    # of the roofline come from the timed steps themselves, encode and repair interleaved as the
+    # step runs them.  Recording one costs the stream ~5 us (a gap before the next kernel in the
+    # kernel trace), so a step's end event is also the next step's start: 2K + 1 events, not 3K
+    bounds = [torch.cuda.Event(enable_timing=True) for _ in range(a.steps + 1)]
+    mids = [torch.cuda.Event(enable_timing=True) for _ in range(a.steps)]
     barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
+    bounds[0].record(stream)
     for i in range(a.steps):
-        marks[i][0].record(stream)
         enc.encode_blocks(blocks, stream=stream)
-        marks[i][1].record(stream)
+        mids[i].record(stream)
         dec.decode_blocks(blocks, locs, counts, status=status, stream=stream)
-        marks[i][2].record(stream)
+        bounds[i + 1].record(stream)
     torch.cuda.synchronize(dev)
     t1 = time.perf_counter()
     barrier()
@@ -231,8 +233,8 @@ def main():
         e1.synchronize()
         return e0.elapsed_time(e1) / n  # ms per launch
 
-    enc_ms = sum(mk[0].elapsed_time(mk[1]) for mk in marks) / a.steps  # ms per launch
-    dec_ms = sum(mk[1].elapsed_time(mk[2]) for mk in marks) / a.steps
+    enc_ms = sum(bounds[i].elapsed_time(mids[i]) for i in range(a.steps)) / a.steps  # ms per launch
+    dec_ms = sum(mids[i].elapsed_time(bounds[i + 1]) for i in range(a.steps)) / a.steps
 
     # achievable HBM rate on this box (report it beside the 8 TB/s spec): a 4 GiB
     # device-to-device copy by the library's streaming kernel (16 B per lane, non-temporal),
