@@ -69,6 +69,9 @@ def parse():
                    help="GPUs = ranks (default 1, or WORLD_SIZE under a launcher)")
     p.add_argument("--dry-run", action="store_true",
                    help="CPU rehearsal of the multi-rank launch and reporting (gloo; no GPU, no FEC work)")
+    p.add_argument("--share-gpu", action="store_true",
+                   help="one-GPU rehearsal of the N-rank path: every rank runs the real workload on cuda:0 and "
+                        "the collectives go over gloo (the line says so; never a scaling number)")
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--blocks", type=int, default=65536,
@@ -158,17 +161,26 @@ def main():
         return dry_run(a, world, rank)
     import torch
 
-    if world > torch.cuda.device_count():
+    share = a.share_gpu and world > 1
+    if world > torch.cuda.device_count() and not share:
         raise SystemExit(f"{world} ranks but {torch.cuda.device_count()} visible GPUs: one rank per GPU")
     dist = None
-    if world > 1:
+    if share:
+        # rehearsal: the ranks share cuda:0, so RCCL (one rank per device) is out; gloo carries
+        # the barrier and the max / min reductions on host tensors
+        import torch.distributed as dist
+
+        torch.cuda.set_device(0)
+        dist.init_process_group("gloo")
+    elif world > 1:
         import torch.distributed as dist
 
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     else:
         torch.cuda.set_device(0)
-    dev = torch.device("cuda", local if world > 1 else 0)
+    dev = torch.device("cuda", local if world > 1 and not share else 0)
+    cdev = torch.device("cpu") if share else dev  # where the collectives' tensors live
 
     from norm_amd import NormDecoderRS8, NormEncoderRS8, fill_blocks, make_erasures, stream_copy
     from norm_amd.dist import shard
@@ -219,7 +231,7 @@ def main():
     barrier()
     elapsed = t1 - t0
     if dist is not None:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed], dtype=torch.float64, device=cdev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
@@ -281,7 +293,7 @@ def main():
         barrier()
         he = h1 - h0
         if dist is not None:
-            t = torch.tensor([he], dtype=torch.float64, device=dev)
+            t = torch.tensor([he], dtype=torch.float64, device=cdev)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             he = float(t.item())
         # the link's own rate on this box: pinned -> device DMA of 1 GiB (and back), the
@@ -360,7 +372,7 @@ def main():
         ok = bool(torch.equal(blocks, keep)) and bool((status == a.erasures).all())
         del keep
         if dist is not None:  # every rank's blocks: the line says true only if all came back
-            t = torch.tensor([1 if ok else 0], dtype=torch.int32, device=dev)
+            t = torch.tensor([1 if ok else 0], dtype=torch.int32, device=cdev)
             dist.all_reduce(t, op=dist.ReduceOp.MIN)
             ok = bool(t.item())
 
@@ -487,6 +499,9 @@ def main():
         out["host_resident"] = host
     if ok is not None:
         out["verified"] = ok
+    if share:
+        out["rehearsal"] = (f"{world} ranks sharing cuda:0 over gloo (--share-gpu): the N-rank code path on one "
+                            "GPU, not a scaling number")
     print(json.dumps(out))
     if dist is not None:
         dist.destroy_process_group()
