@@ -66,6 +66,8 @@ def main():
                         "4 GB at N > 1)")
     p.add_argument("--dry-run", action="store_true",
                    help="CPU rehearsal: launch, per-rank plan and pinned budget (gloo; no GPU, no FEC work)")
+    p.add_argument("--share-gpu", action="store_true",
+                   help="one-GPU rehearsal of the N-rank path (bench.py's): every rank on cuda:0, gloo collectives")
     a = p.parse_args()
     from norm_amd.dist import launch_local_ranks, plan_launch
 
@@ -80,13 +82,20 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if a.dry_run:
         return dry_run(a, world, rank)
+    share = a.share_gpu and world > 1
+    if share:
+        local = 0  # every rank on cuda:0; RCCL wants one rank per device, so gloo carries the reductions
     torch.cuda.set_device(local)
     dist = None
     if world > 1:
         import torch.distributed as dist
 
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if share:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
+    cdev = torch.device("cpu") if share else dev  # the collectives' tensors
     import norm_amd as na
 
     pl = plan(a, world, rank)
@@ -139,7 +148,7 @@ def main():
     def max_time(t):
         if dist is None:
             return t
-        x = torch.tensor([t], dtype=torch.float64, device=dev)
+        x = torch.tensor([t], dtype=torch.float64, device=cdev)
         dist.all_reduce(x, op=dist.ReduceOp.MAX)
         return float(x.item())
 
@@ -214,7 +223,7 @@ def main():
         del j["keep"]
 
     def sum_ranks(v):
-        t = torch.tensor([float(v)], dtype=torch.float64, device=dev)
+        t = torch.tensor([float(v)], dtype=torch.float64, device=cdev)
         if dist is not None:
             dist.all_reduce(t)
         return float(t.item())
@@ -243,6 +252,8 @@ def main():
             "rank0_host_s": {j["name"]: [round(j["host_enc_s"], 3), round(j["host_dec_s"], 3)] for j in jobs},
             "note": "one step = encode + 16 (RS8) / 50 (RS16) source-erasure repair of every block; "
                     "GiB/s counts source bytes, all ranks / max-over-ranks time",
+            **({"rehearsal": f"{world} ranks sharing cuda:0 over gloo (--share-gpu), not a scaling number"}
+               if share else {}),
         }), flush=True)
     if dist is not None:
         dist.destroy_process_group()
