@@ -740,6 +740,7 @@ __global__ __launch_bounds__(64 * kPlan2Waves) void rs_plan2_kernel(RsPlan2Args 
 {
     __shared__ uint8_t ex[512];
     __shared__ uint16_t lg[256];
+    __shared__ uint16_t lwp_s[256], lw_s[256];     // the codec's log W'(x_j), log W(y_p) (k + m <= 255)
     __shared__ uint8_t xs_w[kPlan2Waves][64], yt_w[kPlan2Waves][64];   // points of E and P
     __shared__ uint16_t sP_w[kPlan2Waves][64], sE_w[kPlan2Waves][64];
     __shared__ int32_t lA_w[kPlan2Waves][64], lB_w[kPlan2Waves][64];   // per-s / per-t log factors
@@ -756,15 +757,22 @@ __global__ __launch_bounds__(64 * kPlan2Waves) void rs_plan2_kernel(RsPlan2Args 
     const uint32_t b = blockIdx.x * kPlan2Waves + w;
     const bool live = b < a.nblocks;
     const uint32_t k = a.k, m = a.m;
-    // the erasure list is fetched first so its two dependent loads overlap the table staging;
-    // a shortened block (numData < k, normEncoderRS8.cpp:675-693) has its parity at slot nd + p
+    // the erasure count and list are fetched first and together (the list's first min(stride,
+    // 64) entries, whatever the count: one round trip instead of two dependent ones), so they
+    // overlap the table staging; a shortened block (numData < k, normEncoderRS8.cpp:675-693) has
+    // its parity at slot nd + p
+    const uint16_t* locs = a.erasure_locs + (uint64_t)b * a.erasure_stride;
+    const uint32_t rawl = (live && lane < a.erasure_stride) ? (uint32_t)locs[lane] : 0u;
     const uint32_t ec = live ? uni(a.erasure_counts[b]) : 0u;
     const uint32_t nd = live && a.num_data ? uni(a.num_data[b]) : k;
-    const uint16_t* locs = a.erasure_locs + (uint64_t)b * a.erasure_stride;
     bool ok = ec <= m && ec <= a.erasure_stride && nd >= 1 && nd <= k;   // then ec <= 64: one entry per lane
-    const uint32_t myl = (live && ok && lane < ec) ? (uint32_t)locs[lane] : 0u;
+    const uint32_t myl = (live && ok && lane < ec) ? rawl : 0u;
     for (uint32_t i = threadIdx.x; i < 510; i += 64 * kPlan2Waves) ex[i] = a.exp_tab[i];
     for (uint32_t i = threadIdx.x; i < 256; i += 64 * kPlan2Waves) lg[i] = a.log_tab[i];
+    // (the closed form's per-point constants: staged with the tables instead of gathered from
+    // global memory after the erasure list, another dependent round trip)
+    for (uint32_t i = threadIdx.x; i < k; i += 64 * kPlan2Waves) lwp_s[i] = a.lwp[i];
+    for (uint32_t i = threadIdx.x; i < m; i += 64 * kPlan2Waves) lw_s[i] = a.lw[i];
     for (uint32_t i = lane; i < 256; i += 64) ers[i] = 0;
     __syncthreads();  // the only workgroup barrier: tables staged
     if (!live) return;
@@ -826,27 +834,37 @@ __global__ __launch_bounds__(64 * kPlan2Waves) void rs_plan2_kernel(RsPlan2Args 
         xs[lane] = s == 0 ? 0 : ex[(s - 1) % 255u];
     }
     wave_lds_sync();
-    // per-s: lA[s] = lWp(x_s) + lPP(s) - lQp(s);  per-t: lB[t] = lQ(t) - lW(t) - lD(t)
-    if (lane < e) {
-        const uint32_t x = xs[lane];
-        // unrolled so the (uniform-address) point reads and the table reads they feed are
-        // issued in batches instead of one dependent LDS round trip per term; the s2 == lane
-        // and t2 == lane terms are lg[0] (x ^ x), subtracted back out instead of branched on
-        const uint32_t y = yt[lane];
-        int32_t acc = (int32_t)a.lwp[sE[lane]], bcc = -(int32_t)a.lw[sP[lane]];
-#pragma unroll 8
-        for (uint32_t t = 0; t < e; ++t) {
-            acc += (int32_t)lg[x ^ yt[t]] - (int32_t)lg[x ^ xs[t]];
-            bcc += (int32_t)lg[y ^ xs[t]] - (int32_t)lg[y ^ yt[t]];
+    // per-s: lA[s] = lWp(x_s) + lPP(s) - lQp(s);  per-t: lB[t] = lQ(t) - lW(t) - lD(t).
+    // The e x e terms are spread over the whole wave: lane (s, q) of W = e rounded up to 16 / 32 /
+    // 64 lanes per group and Q = 64 / W groups sums the terms t = q, q + Q, ..., then the groups
+    // are summed across lanes (the plan is bound by its LDS instruction count: with one lane per s
+    // the wave issued e rounds of six table reads at e of 64 lanes).  The s2 == s and t2 == t terms
+    // are lg[0] (x ^ x), subtracted back out instead of branched on
+    {
+        const uint32_t W = e <= 16 ? 16u : e <= 32 ? 32u : 64u, Q = 64u / W;
+        const uint32_t si = lane & (W - 1u), q = lane / W;
+        int32_t acc = 0, bcc = 0;
+        if (si < e) {
+            const uint32_t x = xs[si], y = yt[si];
+            for (uint32_t t = q; t < e; t += Q) {
+                acc += (int32_t)lg[x ^ yt[t]] - (int32_t)lg[x ^ xs[t]];
+                bcc += (int32_t)lg[y ^ xs[t]] - (int32_t)lg[y ^ yt[t]];
+            }
         }
-        acc += (int32_t)lg[0];
-        bcc += (int32_t)lg[0];
-        // reduced to [0, 255) once here, so a coefficient's exponent lA + lB - log(x ^ y) lies in
-        // (-255, 510) and needs one conditional add before the doubled exp table, not a modulo
-        acc %= 255;
-        bcc %= 255;
-        lA[lane] = acc < 0 ? acc + 255 : acc;
-        lB[lane] = bcc < 0 ? bcc + 255 : bcc;
+        for (uint32_t off = W; off < 64u; off <<= 1) {
+            acc += __shfl_xor(acc, (int)off);
+            bcc += __shfl_xor(bcc, (int)off);
+        }
+        if (q == 0 && si < e) {
+            acc += (int32_t)lwp_s[sE[si]] + (int32_t)lg[0];
+            bcc += (int32_t)lg[0] - (int32_t)lw_s[sP[si]];
+            // reduced to [0, 255) once here, so a coefficient's exponent lA + lB - log(x ^ y) lies
+            // in (-255, 510) and needs one conditional add before the doubled exp table, not a modulo
+            acc %= 255;
+            bcc %= 255;
+            lA[si] = acc < 0 ? acc + 255 : acc;
+            lB[si] = bcc < 0 ? bcc + 255 : bcc;
+        }
     }
     wave_lds_sync();
     uint8_t* coef = a.coef2 + (uint64_t)b * cs * cs;
@@ -855,12 +873,15 @@ __global__ __launch_bounds__(64 * kPlan2Waves) void rs_plan2_kernel(RsPlan2Args 
         // as the fused kernel's snippet byte offsets (c << 7), unused rows zero (the fused kernel
         // applies rows 0..max used row; a zero coefficient's snippet is empty)
         uint16_t* coef16 = reinterpret_cast<uint16_t*>(coef);
-        for (uint32_t idx = lane; idx < 16 * 16; idx += 64) {
-            const uint32_t row = idx >> 4, s = idx & 15;
+        // a lane's output s = lane & 15 is the same in every round: its lA and point read once
+        const uint32_t s = lane & 15u;
+        const int32_t las = s < e ? lA[s] : 0;
+        const uint32_t xss = s < e ? xs[s] : 0u;
+        for (uint32_t row = lane >> 4; row < 16u; row += 4u) {
             const uint32_t t = (uint32_t)__popcll(pused & ((1ull << row) - 1ull));  // rank of row
             uint32_t v = 0;
             if (((pused >> row) & 1ull) && s < e) {
-                int32_t l = lA[s] + lB[t] - (int32_t)lg[xs[s] ^ yt[t]];
+                int32_t l = las + lB[t] - (int32_t)lg[xss ^ yt[t]];
                 if (l < 0) l += 255;
                 v = ex[l];
             }
