@@ -234,6 +234,10 @@ struct nfec_codec {
     std::mutex tmvp_mu;            // one Toeplitz encode at a time per codec: they share w_tmvp
     DevBuf<uint8_t> w_tmvp;        // prescaled pair sums + P1 rows of a sub-batch
     hipEvent_t tmvp_done = nullptr;  // the last Toeplitz encode's end, on its stream
+    // two-level encode pipeline (rs16_tmvp2_encode): a second stream of the codec's own and the
+    // events that fork it from the caller's stream, stagger the sub-batches' prescales and join
+    hipStream_t tmvp_s2 = nullptr;
+    hipEvent_t tmvp_ev[4] = {};      // fork, join, prescale done (two, alternating)
     // device-batch encodes per path that took them (NFEC_PATH_*, nfec_codec_encode_paths)
     std::atomic<uint64_t> enc_paths[NFEC_PATH_COUNT] = {};
     std::atomic<uint64_t> dec_paths[NFEC_DPATH_COUNT] = {};  // ... and decodes (NFEC_DPATH_*)
@@ -279,6 +283,12 @@ struct nfec_codec {
         d_tmvp_off.release();
         d_tmvp_mat.release();
         if (tmvp_done) (void)hipEventDestroy(tmvp_done);
+        if (tmvp_s2) {
+            (void)hipStreamSynchronize(tmvp_s2);
+            (void)hipStreamDestroy(tmvp_s2);
+        }
+        for (hipEvent_t ev : tmvp_ev)
+            if (ev) (void)hipEventDestroy(ev);
         d_vtab.release();
         d_log.release();
         d_lwp.release();
@@ -721,25 +731,67 @@ static int rs16_tmvp2_encode(nfec_codec* c, const nfec_block_batch* b, hipStream
         free_b = 0;
     }
     const uint64_t budget = std::min<uint64_t>(16ull << 30, ((uint64_t)free_b + c->w_tmvp.n) / 2);
-    const uint64_t cap = std::max<uint64_t>(1, budget / per_block);
-    const uint64_t nsub = (b->nblocks + cap - 1) / cap;
+    // pipeline: the batch runs as sub-batches whose products launch has about 3,072 workgroups
+    // (12 per CU), alternating between the caller's stream and the codec's second one, each
+    // stream with its own half of the scratch, each prescale after the previous sub-batch's.  A
+    // launch's tail (its last workgroups leave CUs idle) then fills with the other stream's
+    // kernels, and the HBM-bound scale kernels run beside the issue-bound products.  Measured
+    // (profiles/r06/tmvp_pipe/, one box): RS16(400,100) encode 19.6-19.8 -> 19.1 ms at 16
+    // sub-batches (8: 19.2, 32: 19.3, 2-4: no gain), C4 96.3 -> 91.9 ms at 16.
+    // NFEC_TMVP_PIPE (knob library): 0 this rule, 1 off, N >= 2 at least N sub-batches
+    static const long pipe = diag_knob("NFEC_TMVP_PIPE", 0, 0, 64);
+    uint64_t want = 1;
+    if (pipe == 0) {
+        const uint64_t wg_x4096 = (uint64_t)nprod * (gf16_tw_passes(r, gf16_tw_rows(r)) / 4u) * vec;  // x 4096 per block
+        const uint64_t target = std::max<uint64_t>(1, 3072ull * 4096ull / std::max<uint64_t>(wg_x4096, 1));
+        want = (b->nblocks + target - 1) / target;
+    } else if (pipe >= 2) {
+        want = (uint64_t)pipe;
+    }
+    const bool piped = want >= 2 && b->nblocks >= 2;
+    const uint32_t nbuf = piped ? 2u : 1u;
+    const uint64_t cap = std::max<uint64_t>(1, budget / nbuf / per_block);
+    const uint64_t nsub = std::max<uint64_t>((b->nblocks + cap - 1) / cap, piped ? want : 1u);
     const uint32_t sb = (uint32_t)std::max<uint64_t>(1, (b->nblocks + nsub - 1) / std::max<uint64_t>(nsub, 1));
-    if (c->w_tmvp.reserve((size_t)sb * per_block) != NFEC_OK) {
+    if (c->w_tmvp.reserve((size_t)nbuf * sb * per_block) != NFEC_OK) {
         (void)hipGetLastError();
         return NFEC_ENOTSUP;  // no room for the scratch: the one-product encode takes the batch
     }
+    if (piped && !c->tmvp_s2) {
+        if (hipStreamCreateWithFlags(&c->tmvp_s2, hipStreamNonBlocking) != hipSuccess)
+            return hip_fail(hipGetLastError(), "tmvp pipeline stream");
+        for (hipEvent_t& ev : c->tmvp_ev)
+            NFEC_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    }
     NFEC_HIP(hipStreamWaitEvent(s, c->tmvp_done, 0));
-    bool queued = false;
+    bool queued = false, forked = false;
     auto leave = [&](int code) {
+        // the second stream's work joins the caller's before tmvp_done, so the next encode (any
+        // stream) waits for both halves of the scratch
+        if (forked && (hipEventRecord(c->tmvp_ev[1], c->tmvp_s2) != hipSuccess ||
+                       hipStreamWaitEvent(s, c->tmvp_ev[1], 0) != hipSuccess) && code == NFEC_OK)
+            code = hip_fail(hipGetLastError(), "tmvp pipeline join");
         if (queued && hipEventRecord(c->tmvp_done, s) != hipSuccess && code == NFEC_OK)
             code = hip_fail(hipGetLastError(), "tmvp event");
         return code;
     };
     const size_t one_tw = gf16_tw_table_elems(cols, r);
     int rc;
-    for (uint32_t b0 = 0; b0 < b->nblocks; b0 += sb) {
+    uint32_t sub = 0;
+    for (uint32_t b0 = 0; b0 < b->nblocks; b0 += sb, ++sub) {
         const uint32_t nb = std::min(sb, b->nblocks - b0);
         uint8_t* blocks = static_cast<uint8_t*>(b->blocks) + (uint64_t)b0 * b->block_stride;
+        hipStream_t st = s;
+        if (piped && (sub & 1u)) {
+            if (!forked) {  // the second stream starts after everything before on the caller's
+                NFEC_HIP(hipEventRecord(c->tmvp_ev[0], s));
+                NFEC_HIP(hipStreamWaitEvent(c->tmvp_s2, c->tmvp_ev[0], 0));
+                forked = true;
+            }
+            st = c->tmvp_s2;
+        }
+        // the previous sub-batch's prescale first (the other stream)
+        if (piped && sub > 0 && forked) NFEC_HIP(hipStreamWaitEvent(st, c->tmvp_ev[2 + ((sub - 1) & 1u)], 0));
         Rs16TmvpArgs a;
         a.base = blocks;
         a.block_stride = b->block_stride;
@@ -749,7 +801,7 @@ static int rs16_tmvp2_encode(nfec_codec* c, const nfec_block_batch* b, hipStream
         a.k = k;
         a.cw = m / 2;
         a.hw = r;
-        a.sc = c->w_tmvp.p;
+        a.sc = c->w_tmvp.p + (piped ? (uint64_t)(sub & 1u) * sb * per_block : 0u);
         a.sc_block_stride = per_block;
         a.cmat = c->d_tmvp_mat.p;
         a.wmat = c->d_tmvp_mat.p + (size_t)k * 16;
@@ -807,13 +859,15 @@ static int rs16_tmvp2_encode(nfec_codec* c, const nfec_block_batch* b, hipStream
         }
         // a shape the kernels do not cover shows on the first sub-batch, before any parity byte
         // is written: NFEC_ENOTSUP then hands the batch to the one-product encode
-        if ((rc = launch_tmvp2_prescale(a, s)))
+        if ((rc = launch_tmvp2_prescale(a, st)))
             return leave(rc == NFEC_ENOTSUP && b0 == 0 ? rc : fail(rc, "tmvp multi-level prescale"));
         queued = true;
+        if (piped && hipEventRecord(c->tmvp_ev[2 + (sub & 1u)], st) != hipSuccess)
+            return leave(hip_fail(hipGetLastError(), "tmvp pipeline event"));
         for (uint32_t e0 = 0; e0 < nprod; e0 += kTwMultiMax)
-            if ((rc = launch_gf16_tw_multi(e.data() + e0, std::min<uint32_t>(kTwMultiMax, nprod - e0), s)))
+            if ((rc = launch_gf16_tw_multi(e.data() + e0, std::min<uint32_t>(kTwMultiMax, nprod - e0), st)))
                 return leave(rc == NFEC_ENOTSUP && b0 == 0 && e0 == 0 ? rc : fail(rc, "tmvp multi-level products"));
-        if ((rc = launch_tmvp2_postscale(a, s))) return leave(fail(rc, "tmvp multi-level postscale"));
+        if ((rc = launch_tmvp2_postscale(a, st))) return leave(fail(rc, "tmvp multi-level postscale"));
     }
     return leave(NFEC_OK);
 }
