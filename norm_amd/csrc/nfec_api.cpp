@@ -784,14 +784,17 @@ static int rs16_tmvp2_encode(nfec_codec* c, const nfec_block_batch* b, hipStream
         hipStream_t st = s;
         if (piped && (sub & 1u)) {
             if (!forked) {  // the second stream starts after everything before on the caller's
-                NFEC_HIP(hipEventRecord(c->tmvp_ev[0], s));
-                NFEC_HIP(hipStreamWaitEvent(c->tmvp_s2, c->tmvp_ev[0], 0));
+                if (hipEventRecord(c->tmvp_ev[0], s) != hipSuccess ||
+                    hipStreamWaitEvent(c->tmvp_s2, c->tmvp_ev[0], 0) != hipSuccess)
+                    return leave(hip_fail(hipGetLastError(), "tmvp pipeline fork"));
                 forked = true;
             }
             st = c->tmvp_s2;
         }
-        // the previous sub-batch's prescale first (the other stream)
-        if (piped && sub > 0 && forked) NFEC_HIP(hipStreamWaitEvent(st, c->tmvp_ev[2 + ((sub - 1) & 1u)], 0));
+        // the previous sub-batch's prescale first (the other stream); an error leaves through
+        // leave(), so tmvp_done still covers what both streams already hold
+        if (piped && sub > 0 && forked && hipStreamWaitEvent(st, c->tmvp_ev[2 + ((sub - 1) & 1u)], 0) != hipSuccess)
+            return leave(hip_fail(hipGetLastError(), "tmvp pipeline wait"));
         Rs16TmvpArgs a;
         a.base = blocks;
         a.block_stride = b->block_stride;
