@@ -191,7 +191,10 @@ int nfec_codec_get_generator(const nfec_codec* codec, void* host_out, size_t byt
 
 /* ---- batched device-resident path (the performance path) ----
  * stream is a hipStream_t (NULL = legacy default stream).  Calls are asynchronous with
- * respect to the host; results are ready when the stream reaches them. */
+ * respect to the host; results are ready when the stream reaches them.  (A large RS16 encode on
+ * the two-level Toeplitz split runs half of its sub-batches on a second stream of the codec's
+ * own; that stream starts after the caller's stream and joins it before the call's end, so the
+ * ordering the caller sees is the same.) */
 int nfec_encode(nfec_codec* codec, const nfec_block_batch* batch, void* stream);
 
 /* erasure_locs: device [nblocks][erasure_stride] sorted slot indices (source erasures
