@@ -173,3 +173,76 @@ def test_toeplitz_host_pipeline_chunks(orc, pinned, monkeypatch):
     monkeypatch.setenv("NFEC_HOST_CHUNK_BLOCKS", "3")
     enc.encode_blocks_host(arr)
     assert np.array_equal(arr, ref)
+
+
+def test_toeplitz_pipeline_sub_batches(orc):
+    """A large batch runs the two-level split as sub-batches pipelined over the caller's stream
+    and the codec's second stream (rs16_tmvp2_encode: about 3,072 product workgroups per
+    sub-batch, i.e. ~1,000 RS16(400, 100) blocks, so 2,100 blocks make three).  The bytes equal
+    the one-product encode of the same blocks, unshortened and with RFC 5052 numData in
+    {k, k - 1}; the blocks at the sub-batch seams equal the oracle; and two batches encoded at once
+    from two threads on two streams of one codec both come out right (the pipeline's fork, join
+    and scratch hand-over between calls)."""
+    import threading
+
+    from norm_amd import fill_blocks
+
+    k, m, vec, nb = 400, 100, 1400, 2100
+    enc = _encoder(k, m, vec, None)
+    assert _levels(enc) == 2
+    one = _encoder(k, m, vec, "0")
+    assert _levels(one) == 0
+
+    def batch(first, nd=None):
+        t = torch.zeros((nb, k + m, vec), dtype=torch.uint8, device="cuda")
+        fill_blocks(t, k, vec, 0x4E4F524D, first_block=first, per_block_num_data=nd)
+        t[:, k:] = 0xA5  # stale parity must not survive (the split overwrites)
+        return t
+
+    # unshortened: the split (pipelined) against the one-product kernel, and the seams against the oracle
+    a = batch(0)
+    ref = a.clone()
+    enc.encode_blocks(a)
+    one.encode_blocks(ref)
+    torch.cuda.synchronize()
+    assert torch.equal(a, ref)
+    seams = [0, 699, 700, 1399, 1400, nb - 1]
+    host = a[seams].cpu().numpy()
+    want = orc.encode_blocks(orc.RS16, k, m, vec, host.copy())
+    assert np.array_equal(host, want)
+
+    # RFC 5052 shortened blocks through the pipeline (each sub-batch's numData slice)
+    rng = np.random.default_rng(7)
+    ndh = rng.integers(k - 1, k + 1, nb).astype(np.uint16)
+    nd = torch.from_numpy(ndh.view(np.int16)).cuda()
+    s = batch(0, nd)
+    s_ref = s.clone()
+    enc.encode_blocks(s, num_data=nd)
+    one.encode_blocks(s_ref, num_data=nd)
+    torch.cuda.synchronize()
+    assert torch.equal(s, s_ref)
+
+    # two batches at once on one codec, two host threads and two streams
+    x, y = batch(5000), batch(9000)
+    x_ref, y_ref = x.clone(), y.clone()
+    one.encode_blocks(x_ref)
+    one.encode_blocks(y_ref)
+    torch.cuda.synchronize()
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    errs = []
+
+    def run(t, st):
+        try:
+            for _ in range(3):
+                enc.encode_blocks(t, stream=st)
+        except Exception as e:  # pragma: no cover - reported below
+            errs.append(e)
+
+    th = [threading.Thread(target=run, args=(t, st)) for t, st in ((x, streams[0]), (y, streams[1]))]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    torch.cuda.synchronize()
+    assert not errs
+    assert torch.equal(x, x_ref) and torch.equal(y, y_ref)
