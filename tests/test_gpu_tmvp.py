@@ -222,6 +222,19 @@ def test_toeplitz_pipeline_sub_batches(orc):
     torch.cuda.synchronize()
     assert torch.equal(s, s_ref)
 
+    # NORM's 1452-byte segments (vec 1460 = segmentSize + 8, % 8 != 0): the pipelined split over the
+    # 8-byte pieces, then the tail kernel over the last 4 bytes, against the one-product path
+    v2 = 1460
+    enc2, one2 = _encoder(k, m, v2, None), _encoder(k, m, v2, "0")
+    t = torch.zeros((nb, k + m, 1464), dtype=torch.uint8, device="cuda")
+    fill_blocks(t, k, v2, 0x4E4F524D, first_block=3000)
+    t_ref = t.clone()
+    enc2.encode_blocks(t)
+    one2.encode_blocks(t_ref)
+    torch.cuda.synchronize()
+    assert torch.equal(t, t_ref)
+    del t, t_ref
+
     # two batches at once on one codec, two host threads and two streams
     x, y = batch(5000), batch(9000)
     x_ref, y_ref = x.clone(), y.clone()
