@@ -259,3 +259,21 @@ def test_toeplitz_pipeline_sub_batches(orc):
     torch.cuda.synchronize()
     assert not errs
     assert torch.equal(x, x_ref) and torch.equal(y, y_ref)
+
+
+def test_toeplitz_pipeline_c4_shape():
+    """C4's code at 600 blocks: the pipelined two-level split (about 250 C4 blocks per sub-batch,
+    so three, over two streams and two scratch halves) against the one-product encode of the same
+    blocks, every byte."""
+    from norm_amd import fill_blocks
+
+    k, m, vec, nb = 4096, 256, 1400, 600
+    enc, one = _encoder(k, m, vec, None), _encoder(k, m, vec, "0")
+    assert _levels(enc) == 2 and _levels(one) == 0
+    t = torch.zeros((nb, k + m, vec), dtype=torch.uint8, device="cuda")
+    fill_blocks(t, k, vec, 0x4E4F524D, first_block=77)
+    t_ref = t.clone()
+    enc.encode_blocks(t)
+    one.encode_blocks(t_ref)
+    torch.cuda.synchronize()
+    assert torch.equal(t, t_ref)
